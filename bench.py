@@ -1,0 +1,202 @@
+"""Benchmark: particle-steps/s (B*N*T / s) of DPF.filtering_pos on synthetic disk tracking.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--no-cpu-baseline]
+
+A "step" is one filtering_pos pass over one batch (B, N, T) -- the hot path of
+BASELINE.json, with the frame encoder replaced by precomputed encodings exactly as the
+reference CPU path was timed.  Default workload = BASELINE configs[1]
+(C2: CNF-DPF, --NF-dyn --NF-cond, RealNVP, cos measurement, soft resampling, N=1000, B=64,
+T=50), device-RNG mode, ESS-gated as the reference.
+
+Multi-GPU (torch.distributed.run, one process per GPU, RCCL): weak scaling, B rows per rank;
+the only per-step exchange is an all-gather of the B per-row ESS terms so the batch-global
+resampling gate of DPFs.py:163-165 is taken identically on every rank.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "normalizing-flows-dpfs_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (flags, B, N, T, algorithmic FLOP per particle-step)
+    "c1": (dict(NF_dyn=False, NF_cond=False, measurement="cos", resampler_type="soft"), 16, 100, 24, 3.3e3),
+    "c2": (dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="soft"), 64, 1000, 50, 13.1e3),
+    "c3": (dict(NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler_type="ot"), 64, 1000, 50, 12.7e3),
+}
+B_ALG = 52.0            # algorithmic HBM bytes per particle-step
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
+PEAK_HBM_GBS = 8000.0
+
+
+def make_args(flags, B, N, T, extra):
+    from arguments import parse_args
+    a = parse_args([])
+    a.num_particles, a.batchsize, a.sequence_length = N, B, T
+    for k, v in {**flags, **extra}.items():
+        setattr(a, k, v)
+    return a
+
+
+def synthetic_disk(B, T, seed, E):
+    """Disk trajectories from the reference's process model (create_dataset.py:197-216):
+    spring 0.1, drag 0.0075, position noise 2.0, init pos U[-64,64]^2, vel N(0,1)*3; the
+    control input is the true velocity + N(0, 4^2) (DPFs.py:105); frame encodings N(0,1)."""
+    g = np.random.default_rng(seed)
+    pos = g.uniform(-64, 64, size=(B, 2))
+    vel = g.normal(size=(B, 2)) * 3
+    start = np.concatenate([pos, vel], -1)
+    states = []
+    for _ in range(T):
+        pull, drag = -0.1 * pos, -0.0075 * vel ** 2 * np.sign(vel)
+        pos = pos + vel + g.normal(scale=2.0, size=(B, 2))
+        vel = vel + pull + drag
+        states.append(np.concatenate([pos, vel], -1))
+    state = np.stack(states, 1).astype(np.float32)
+    vel_in = state[:, :, 2:] + g.normal(scale=4.0, size=(B, T, 2)).astype(np.float32)
+    enc = g.normal(size=(B, T, E)).astype(np.float32)
+    return (torch.from_numpy(start.astype(np.float32)), torch.from_numpy(state), torch.from_numpy(vel_in),
+            torch.from_numpy(enc))
+
+
+def cpu_baseline(cfg_name, seconds_budget=25.0):
+    """The oracle (PyTorch-CPU restatement, timing-faithful: O(N^2) marker matching, FP64
+    Sinkhorn, torch.cat history) on the host cores, on a bounded sample of the workload."""
+    from oracle import dpf_oracle as O
+    flags, B, N, T, _ = CONFIGS[cfg_name]
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    torch.manual_seed(2)
+    a = make_args(flags, B, N, T, {})
+    from DPFs import DPF
+    dpf = DPF(a)
+    params = {k: v.detach().float() for k, v in dpf.state_dict().items()}
+    start, state, vel, enc = synthetic_disk(B, T, 2, a.hiddensize)
+    Bs, Ts = B, T
+    if flags["resampler_type"] == "ot":
+        Bs, Ts = max(1, B // 16), min(T, 10)   # one FP64 OT call is tens of seconds at B=64
+    cfg = dict(N=N, NF_dyn=flags["NF_dyn"], NF_cond=flags["NF_cond"], measurement=flags["measurement"],
+               resampler=flags["resampler_type"], alpha=0.5, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100,
+               pos_noise=20.0, vel_noise=20.0, width=128, n_flows=2)
+    run = lambda: O.filtering(cfg, params, enc[:Bs, :Ts], start[:Bs], vel[:Bs, :Ts], rng=O.HostRNG())
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        run()  # warm-up
+        one = time.perf_counter() - t0
+        reps = max(1, min(3, int(seconds_budget / max(one, 1e-3)) - 1))
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            run()
+            times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": Bs * N * Ts / med, "unit": "particle-steps/s", "cores": cores, "kind": "port",
+            "sample": f"oracle filtering B={Bs} N={N} T={Ts} (ESS-gated), median of {reps} after 1 warm-up; "
+                      f"host {platform.processor() or platform.machine()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--force-resample", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from DPFs import DPF
+    from nfdpf.engine import FilterEngine, ShardInfo
+    flags, B, N, T, F_ALG = CONFIGS[args.config]
+    torch.manual_seed(2)
+    a = make_args(flags, B, N, T, {"force_resample": args.force_resample})
+    dpf = DPF(a).to(dev).eval()
+    start, state, vel_in, enc = synthetic_disk(B * world, T, 2, a.hiddensize)
+    sl = slice(rank * B, (rank + 1) * B)
+    start, state, vel_in, enc = (t[sl].to(dev) for t in (start, state, vel_in, enc))
+    shard = ShardInfo.from_env(B)
+    eng = FilterEngine(dpf.filter_config(), dpf)
+
+    def step():
+        return eng.run(enc, start, vel_in, shard=shard)
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.step_events = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    evs = eng.step_events
+    eng.step_events = None
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
+    se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
+    cnt = torch.tensor(float(res.pred.numel()), device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(se)
+        dist.all_reduce(cnt)
+    rmse = float(torch.sqrt(se / cnt))
+
+    if rank == 0:
+        units = B * world * N * T * args.steps
+        value = units / elapsed
+        per_launch_units = B * N
+        achieved_tf = F_ALG * per_launch_units / (kernel_ms * 1e-3) / 1e12
+        hbm_gbs = B_ALG * per_launch_units / (kernel_ms * 1e-3) / 1e9
+        out = {
+            "metric": "particle-steps/sec (batch x N x T / s) + filtering RMSE, disk-tracking task",
+            "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: DPF.filtering_pos, " + ", ".join(f"{k}={v}" for k, v in flags.items())
+                       + f", N={N}, batch={B} per GPU, seq_len={T}, state_dim=4 (2-D particles), "
+                         f"{'forced' if args.force_resample else 'ESS-gated'} resampling, device RNG",
+                       "global_batch": B * world, "num_particles": N, "seq_len": T,
+                       "parallelism": f"batch-sharded x{world}"},
+            "rmse": rmse,
+            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+                         "kernel": "filter_step_kernel", "kernel_avg_ms": kernel_ms,
+                         "flop_per_unit": F_ALG, "units_per_launch": per_launch_units,
+                         "hbm_achieved_GBs": hbm_gbs, "hbm_frac": hbm_gbs / PEAK_HBM_GBS},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.config)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

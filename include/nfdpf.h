@@ -1,0 +1,175 @@
+/*
+ * nfdpf.h -- C ABI of libnfdpf.so, the MI355X (gfx950) particle-update hot path of
+ * normalizing-flow differentiable particle filters.
+ *
+ * The reference (xiongjiechen/Normalizing-Flows-DPFs) is pure Python/PyTorch and has no
+ * FFI layer: its boundary for this path is the Python module API.  Each
+ * entry point below replaces the PyTorch op chain of the reference function cited in its
+ * comment; the Python mirror of the reference API (normalizing-flows-dpfs_amd/nf, model,
+ * resamplers, utils, DPFs) binds them through ctypes (nfdpf/_lib.py).
+ *
+ * Conventions
+ *   - every buffer is a DEVICE pointer owned by the caller; nothing is allocated inside,
+ *     so every call is stream-ordered and capturable into a hipGraph;
+ *   - fp32, row-major, contiguous unless a *_rs (row stride, in elements) says otherwise;
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream);
+ *   - return 0 on success, NFDPF_EINVAL for bad arguments (nothing launched),
+ *     NFDPF_ELAUNCH if the launch failed; nfdpf_last_error() gives the message.
+ *
+ * Packed parameter blobs (fp32, concatenated in this order, each tensor row-major as
+ * nn.Linear stores it):
+ *   FCNN(in,out,H)          : W1[H,in] b1[H] W2[H,H] b2[H] W3[out,H] b3[out]   (nf/flows.py:101-114)
+ *   RealNVP(_cond) flow     : FCNN t1, s1, t2, s2 with in = dim/2 + obser_dim   (nf/flows.py:181-190)
+ *   stack of n flows        : flow 0, flow 1, ... (model order, i.e. nf_dyn.flows[i])
+ *   MAF flow (dim d)        : initial_param[2], then FCNN(i, 2, H) for i = 1..d-1 (nf/flows.py:247-254)
+ *   particle encoder        : Linear(2,16) Linear(16,32) Linear(32,E): W,b each  (model/models.py:130-150)
+ *   likelihood_est (NN)     : Linear(2E,64) Linear(64,64) Linear(64,1): W,b each (model/models.py:119-128)
+ */
+#ifndef NFDPF_H
+#define NFDPF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#define NFDPF_API __attribute__((visibility("default")))
+#else
+#define NFDPF_API
+#endif
+
+#define NFDPF_OK 0
+#define NFDPF_EINVAL 1
+#define NFDPF_ELAUNCH 2
+
+/* measurement kinds (arguments.py:24 --measurement) */
+#define NFDPF_MEAS_COS 0
+#define NFDPF_MEAS_CRNVP 1
+#define NFDPF_MEAS_NN 2
+#define NFDPF_MEAS_GAUSSIAN 3
+#define NFDPF_MEAS_EXTERNAL 4 /* raw likelihood supplied in lik_ext (e.g. CGLOW kernel) */
+
+/* resampler kinds (arguments.py:32 --resampler_type) */
+#define NFDPF_RESAMPLE_SOFT 0
+#define NFDPF_RESAMPLE_OT 1
+
+/* RNG modes: DEVICE = counter-based Philox4x32-10 keyed by (seed, step, global row,
+ * particle), shard invariant; HOST = caller uploads the draws of the reference's CPU
+ * generator (parity mode) */
+#define NFDPF_RNG_DEVICE 0
+#define NFDPF_RNG_HOST 1
+
+NFDPF_API int nfdpf_version(void);
+NFDPF_API const char *nfdpf_last_error(void);
+
+/* NormalizingFlowModel_cond.forward / .inverse over RealNVP_cond flows
+ * (nf/models.py:45-61, nf/flows.py:215-239).  obser_dim = 0 gives the unconditional
+ * RealNVP stack (nf/models.py:13-30, nf/flows.py:155-179).
+ *   x       [rows, dim]
+ *   cond    [ceil(rows / cond_group), obser_dim]: row r uses cond row r / cond_group
+ *           (cond_group = 1 is the reference's materialised per-row obser; = N broadcasts a
+ *           per-batch context without materialising (B*N, O))
+ *   out     [rows, dim]; logdet [rows]; prior_logprob [rows] or NULL (forward only:
+ *           log N(z; prior_mean, prior_std^2 I), nf/models.py:51)                        */
+NFDPF_API int nfdpf_cond_stack(const float *params, int n_flows, int dim, int obser_dim, int hidden,
+                     const float *x, const float *cond, int64_t rows, int64_t cond_group,
+                     int inverse, float prior_mean, float prior_std,
+                     float *out, float *logdet, float *prior_logprob, void *stream);
+
+/* NormalizingFlowModel.forward / .inverse over MAF flows (nf/models.py:13-30,
+ * nf/flows.py:259-284; forward flips the output).  x/out [rows, dim], logdet [rows]. */
+NFDPF_API int nfdpf_maf_stack(const float *params, int n_flows, int dim, int hidden, const float *x,
+                    int64_t rows, int inverse, float *out, float *logdet, void *stream);
+
+/* soft_resampler (resamplers.py:20-60), bit-exact indices vs. the reference on CPU:
+ *   x [B,N,D], p [B,N], lin [N] = torch.linspace(0,(N-1)/N,N) (host constant),
+ *   offsets [B] (CPU-generator draw uniform_(0,1/N), resamplers.py:43)
+ *   -> x_out [B,N,D], w_out [B,N], idx_out [B,N] int64 = local index + N*(row_base + b) */
+NFDPF_API int nfdpf_soft_resample(const float *x, const float *p, const float *lin, const float *offsets,
+                        int B, int N, int D, float alpha, int64_t row_base, float *x_out,
+                        float *w_out, int64_t *idx_out, void *stream);
+
+/* resampler_ot (resamplers.py:62-277): entropy-regularised OT, Sinkhorn in fp32 with the
+ * reference's batch-coupled stop rule (the loop ends when ANY row converges, :126-129).
+ *   x [B,N,2], w [B,N] -> x_out [B,N,2], w_out [B,N] (= 1/N), idx_out [B,N] (identity)
+ *   iters_out [1] int32: the reference's returned count (total_iter + 2, :179)
+ *   workspace: nfdpf_ot_workspace_bytes(B,N) bytes, 256-B aligned                   */
+NFDPF_API int64_t nfdpf_ot_workspace_bytes(int B, int N);
+NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps, float scaling,
+                      float threshold, int max_iter, int64_t row_base, float *x_out,
+                      float *w_out, int64_t *idx_out, int32_t *iters_out, void *workspace,
+                      const int32_t *gate, void *stream);
+/*   gate: optional device flag; when non-NULL and *gate == 0 every kernel is a no-op (the
+ *         ESS gate of DPFs.py:165 decided not to resample this step, without a host sync) */
+
+/* ESS gate of DPFs.py:163-165: gate = mean_b(inv_ess[b]) < 0.5 N (or force) -> int32 [1] */
+NFDPF_API int nfdpf_ess_gate(const float *inv_ess, int B, int N, int force, int32_t *gate,
+                   void *stream);
+
+/* normalize_log_probs (utils.py:39-44) + add, and the per-row inverse ESS term
+ * 1/sum(p^2) of DPFs.py:163.  logw [B,N] -> p [B,N]; inv_ess [B] or NULL */
+NFDPF_API int nfdpf_normalize_log_probs(const float *logw, int B, int N, float add, float *p,
+                              float *inv_ess, void *stream);
+
+/* Measurement models (model/models.py:206-278): enc [B,E] frame encodings,
+ * x [B,N,2] particles -> lik [B,N].  kind = NFDPF_MEAS_*; meas_params: CRNVP stack
+ * (2 flows, dim E, obser E) or likelihood_est (NN); prior_std: CRNVP prior (2.5). */
+NFDPF_API int nfdpf_measurement(int kind, const float *pe_params, const float *meas_params, int n_flows,
+                      const float *enc, const float *x, int B, int N, int E, float prior_std,
+                      float *lik, void *stream);
+
+/* particle_initialization (utils.py:46-62) in DEVICE rng mode:
+ * uniform on [-width/2, width/2)^2 (or start + N(0,1) when true_state)        */
+NFDPF_API int nfdpf_particle_init(const float *start_xy, int B, int N, float width, int true_state,
+                        uint64_t seed, int64_t row_base, float *x, float *logw, void *stream);
+
+/* One iteration of the T loop of DPF.filtering_pos (DPFs.py:160-214), fused:
+ * ESS gate (batch-global, read from ess_all) -> [soft resample | OT result] -> motion ->
+ * nf_dyn inverse -> NF proposal -> nf_dyn forward -> densities -> measurement ->
+ * weight update -> normalise(+1e-12) -> inverse-ESS term, writing history slot t.
+ * One workgroup per batch row.                                                    */
+typedef struct nfdpf_filter_desc {
+  /* sizes */
+  int32_t B, N, T, E;       /* local rows, particles, history length, frame-encoding width */
+  int32_t B_global;         /* rows whose inverse-ESS terms gate resampling (all ranks) */
+  int32_t t;                /* step index */
+  int32_t phase;            /* 0 = whole step; 1 = up to the proposal (EXTERNAL measurement
+                               runs next on hist_x slot t); 2 = from the likelihood on */
+  int64_t row_base;         /* global row of local row 0 (flat index base = N*row_base) */
+  /* configuration */
+  int32_t nf_dyn, nf_cond, measurement, resampler, rng_mode, force_resample, n_flows,
+      hidden;
+  float alpha, pos_noise, dens_const, meas_prior_std;
+  uint64_t seed;
+  /* packed parameters */
+  const float *dyn_params, *cond_params, *pe_params, *meas_params;
+  /* inputs */
+  const float *enc;         /* [B,T,E] frame encodings */
+  const float *vel;         /* [B,2] velocity used by this step's motion */
+  const float *lin;         /* [N] soft-resampler markers base (host torch.linspace) */
+  const float *host_noise;  /* [B,N,2] parity-mode noise of this step (rng_mode HOST) */
+  const float *host_offsets;/* [B] parity-mode offsets (rng_mode HOST, soft) */
+  const float *x_prev;      /* particles after the previous step, rows of x_prev_rs */
+  const float *p_prev;      /* probabilities after the previous step, rows of p_prev_rs */
+  int64_t x_prev_rs, p_prev_rs;
+  const float *ess_all;     /* [B_global] 1/sum(p_prev^2) per row */
+  const int32_t *gate;      /* optional [1]: precomputed gate (OT path), NULL = compute */
+  const float *ot_x;        /* [B,N,2] OT-resampled particles (resampler OT, gate on) */
+  const float *lik_ext;     /* [B,N] raw likelihood (measurement EXTERNAL) */
+  /* outputs: history [B,T,...] slot t, plus per-step reductions */
+  float *hist_x, *hist_p, *hist_noise, *hist_lik, *hist_jac, *hist_prior;
+  int64_t *hist_idx;
+  float *ess_out;           /* [B] 1/sum(p^2) of this step */
+  float *lw_sum;            /* [B,T] row sums of the unnormalised log-weights (obs likelihood) */
+  float *pred;              /* [B,T,2] sum_n p*x (losses.py:18-31 prediction) */
+  float *scratch;           /* [B,N,2] phase 1 -> 2 hand-off (log p_resampled, log proposal) */
+} nfdpf_filter_desc;
+
+NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NFDPF_H */

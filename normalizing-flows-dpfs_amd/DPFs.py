@@ -1,0 +1,335 @@
+"""DPF -- the reference's DPFs.py class, same constructor / attributes / methods / returns,
+with the particle-update hot path on MI355X.
+
+``filtering_pos`` (DPFs.py:144-216) runs one fused HIP kernel per time step
+(nfdpf.engine.FilterEngine, csrc/filter_step.hip) whenever autograd is not recording --
+evaluation, testing, benchmarking.  With autograd active (``e2e_train``) it runs the
+reference's loop over this package's modules: each flow / measurement / resampler call is
+a HIP forward whose backward is recomputed with PyTorch ops (nfdpf.autograd; HIP backward
+kernels are SURVEY.md §8f1 "next").  Epoch loops, logging and checkpoint IO around the hot
+path keep the reference's behaviour (DPFs.py:218-451).
+"""
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from losses import autoencoder_loss, pseudolikelihood_loss, pseudolikelihood_loss_nf, supervised_loss
+from model.models import (build_conditional_glow, build_conditional_nf, build_decoder, build_decoder_cglow,
+                          build_encoder, build_encoder_cglow, build_likelihood, build_maf_dyn,
+                          build_particle_encoder, build_particle_encoder_cglow, build_transition_model,
+                          measurement_model_cglow, measurement_model_cnf, measurement_model_cosine_distance,
+                          measurement_model_Gaussian, measurement_model_NN, motion_update, nf_dynamic_model,
+                          proposal_likelihood)
+from nfdpf.engine import FilterConfig, FilterEngine, ShardInfo
+from resamplers.resamplers import resampler
+from utils import (checkpoint_state, compute_normal_density, load_model, normalize_log_probs,
+                   particle_initialization)
+
+device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+class _NullLogger:
+    def add_scalar(self, *a, **k):
+        pass
+
+
+def _summary_writer(path):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(path)
+    except Exception:  # tensorboard is optional
+        return _NullLogger()
+
+
+class DPF(nn.Module):
+
+    def __init__(self, args):
+        super().__init__()
+        self.param = args
+        self.NF = args.NF_dyn
+        self.NFcond = args.NF_cond
+        self.measurement = args.measurement
+        self.hidden_size = args.hiddensize
+        self.state_dim = 2  # particles are 2-D positions (DPFs.py:31)
+        self.lr = args.lr
+        self.alpha = args.alpha
+        self.seq_len = args.sequence_length
+        self.num_particle = args.num_particles
+        self.batch_size = args.batchsize
+        self.labeledRatio = args.labeledRatio
+        self.spring_force = 0.1
+        self.drag_force = 0.0075
+        self.pos_noise = args.pos_noise
+        self.vel_noise = args.vel_noise
+        self.NF_lr = args.NF_lr
+        self.n_sequence = 2
+        self.build_model()
+        self.eps = args.epsilon
+        self.scaling = args.scaling
+        self.threshold = args.threshold
+        self.max_iter = args.max_iter
+        self.resampler = resampler(self.param)
+
+    # ------------------------------------------------------------------------------------
+    def build_model(self):
+        """Same sub-modules (and state_dict keys) as DPFs.py:56-94."""
+        H, D = self.hidden_size, self.state_dim
+        if self.measurement == "CGLOW":
+            self.encoder, self.decoder = build_encoder_cglow(H), build_decoder_cglow(H)
+            self.build_particle_encoder = build_particle_encoder_cglow
+        else:
+            self.encoder, self.decoder = build_encoder(H), build_decoder(H)
+            self.build_particle_encoder = build_particle_encoder
+        self.particle_encoder = self.build_particle_encoder(H, D)
+        self.transition_model = build_transition_model(D)
+        self.motion_update = motion_update
+        if getattr(self.param, "NF_dyn_flow", "RealNVP") == "MAF":
+            self.nf_dyn = build_maf_dyn(self.n_sequence, D)
+        else:
+            self.nf_dyn = build_conditional_nf(self.n_sequence, 2 * D, D, init_var=0.01)
+        self.cond_model = build_conditional_nf(self.n_sequence, 2 * D + H, D, init_var=0.01)
+        m = self.measurement
+        if m == "CRNVP":
+            self.cnf_measurement = build_conditional_nf(self.n_sequence, H, H, init_var=0.01, prior_std=2.5)
+            self.measurement_model = measurement_model_cnf(self.particle_encoder, self.cnf_measurement)
+        elif m == "cos":
+            self.measurement_model = measurement_model_cosine_distance(self.particle_encoder)
+        elif m == "NN":
+            self.likelihood_est = build_likelihood(H, D)
+            self.measurement_model = measurement_model_NN(self.particle_encoder, self.likelihood_est)
+        elif m == "gaussian":
+            self.gaussian_distribution = torch.distributions.MultivariateNormal(
+                torch.ones(H).to(device), 100 * torch.eye(H).to(device))
+            self.measurement_model = measurement_model_Gaussian(self.particle_encoder, self.gaussian_distribution)
+        elif m == "CGLOW":
+            self.cglow_measurement = build_conditional_glow(self.param).to(device)
+            self.measurement_model = measurement_model_cglow(self.particle_encoder, self.cglow_measurement)
+        self.prototype_density = compute_normal_density(pos_noise=self.pos_noise, vel_noise=self.vel_noise)
+        self.optim = torch.optim.Adam(self.parameters(), lr=self.lr)
+        self.optim_scheduler = torch.optim.lr_scheduler.MultiStepLR(
+            self.optim, milestones=[30 * (1 + x) for x in range(10)], gamma=1.0)
+
+    # ------------------------------------------------------------------------------------
+    def forward(self, inputs, train=True):
+        """Filter a batch and compute the losses (DPFs.py:96-142) -> 13-tuple."""
+        (start_image, start_state, image, state, q, visible) = inputs
+        state = state.to(device)
+        start_state = start_state.to(device)
+        image = image.permute(0, 1, 4, 2, 3).to(device)
+        vel = state[:, :, 2:] + torch.normal(0.0, 4.0, (state[:, :, 2:]).shape).to(device)
+        (particle_list, particle_weight_list, noise_list, likelihood_list, init_weights_log, index_list, jac_list,
+         prior_list, obs_likelihood) = self.filtering_pos(image, start_state, vel)
+        mask = self.get_mask() if train else 1.0
+        loss_sup, predictions = supervised_loss(particle_list, particle_weight_list, state, mask, train)
+        loss_ae = autoencoder_loss(image, train, self.encoder, self.decoder)
+        if self.param.trainType == "DPF":
+            loss_pseud_lik = None
+            total_loss = 1.0 * loss_sup + 2.0 * loss_ae
+        elif self.param.trainType == "SDPF":
+            if self.NF:
+                loss_pseud_lik = pseudolikelihood_loss_nf(particle_weight_list, noise_list, likelihood_list,
+                                                          index_list, jac_list, prior_list, self.param.block_length)
+            else:
+                loss_pseud_lik = pseudolikelihood_loss(particle_weight_list, noise_list, likelihood_list, index_list,
+                                                       self.param.block_length, self.param.pos_noise,
+                                                       self.param.vel_noise)
+            total_loss = 1.0 * loss_sup + 0.01 * loss_pseud_lik + 2.0 * loss_ae
+        else:
+            raise ValueError('Please select the training type in DPF (supervised learning) and SDPF '
+                             '(semi-supervised learning)')
+        return (total_loss, loss_sup, loss_pseud_lik, loss_ae, predictions, particle_list, particle_weight_list,
+                state, start_state, image, likelihood_list, noise_list, obs_likelihood)
+
+    # ------------------------------------------------------------------------------------
+    def _autograd_active(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
+    def _frame_encodings(self, obs, T):
+        if isinstance(self.encoder, nn.Identity):
+            return obs[:, :T].float()
+        return torch.stack([self.encoder(obs[:, t].float()) for t in range(T)], dim=1)
+
+    def filter_config(self) -> FilterConfig:
+        a = self.param
+        return FilterConfig(
+            N=self.num_particle, NF_dyn=bool(self.NF), NF_cond=bool(self.NFcond), measurement=self.measurement,
+            resampler=a.resampler_type, alpha=a.alpha, eps=a.epsilon, scaling=a.scaling, threshold=a.threshold,
+            max_iter=a.max_iter, pos_noise=self.pos_noise, vel_noise=self.vel_noise, width=a.width,
+            init_with_true_state=a.init_with_true_state, n_flows=self.n_sequence,
+            rng_mode=getattr(a, "rng_mode", "device"), seed=a.seed,
+            force_resample=getattr(a, "force_resample", False))
+
+    def _fused_supported(self):
+        return (self.measurement in ("cos", "CRNVP", "NN", "gaussian") and self.hidden_size == 32
+                and getattr(self.param, "NF_dyn_flow", "RealNVP") == "RealNVP")
+
+    def filtering_pos(self, obs, start_state_vs, vel_input):
+        """The T-step particle filter (DPFs.py:144-216) -> the reference's 9-tuple."""
+        if self._autograd_active() or not self._fused_supported():
+            return self._filtering_modules(obs, start_state_vs, vel_input)
+        with torch.no_grad():
+            enc = self._frame_encodings(obs, self.seq_len)
+            eng = FilterEngine(self.filter_config(), self)
+            shard = ShardInfo.from_env(enc.shape[0])
+            res = eng.run(enc, start_state_vs, vel_input[:, :self.seq_len], shard=shard)
+        self.last_filter_result = res
+        return res.as_tuple()
+
+    def _filtering_modules(self, obs, start_state_vs, vel_input):
+        """The reference loop over this package's HIP-backed modules (autograd path)."""
+        start_state, vel = start_state_vs[:, :2], start_state_vs[:, 2:]
+        B, N = start_state.shape[0], self.num_particle
+        particles, init_weights_log = particle_initialization(start_state, self.param.width, N, self.state_dim,
+                                                              init_with_true_state=self.param.init_with_true_state)
+        probs = normalize_log_probs(init_weights_log)
+        obs_likelihood = 0.0
+        force = getattr(self.param, "force_resample", False)
+        hist = {k: [] for k in ("x", "p", "n", "l", "i", "j", "r")}
+        for step in range(self.seq_len):
+            index_p = (torch.arange(N) + N * torch.arange(B)[:, None].repeat((1, N))).long().to(particles.device)
+            ess = torch.mean(1 / torch.sum(probs ** 2, dim=-1))
+            if force or ess < 0.5 * N:
+                xr, pr, index_p = self.resampler(particles, probs)
+                lr = pr.log()
+            else:
+                xr, lr = particles, probs.log()
+            x_phys, noise = self.motion_update(xr, vel, pos_noise=self.pos_noise)
+            vel = vel_input[:, step, :]
+            x_dyn, jac = nf_dynamic_model(self.nf_dyn, x_phys, probs.shape, NF=self.NF)
+            enc = self.encoder(obs[:, step].float())
+            prop, lik, prior, propose = proposal_likelihood(self.cond_model, self.nf_dyn, self.measurement_model,
+                                                            x_dyn, x_phys, enc, noise, jac, self.NF, self.NFcond,
+                                                            prototype_density=self.prototype_density)
+            lw = lr + lik + prior - propose
+            particles = prop
+            obs_likelihood += lw.mean()
+            probs = normalize_log_probs(lw) + 1e-12
+            for k, v in (("x", particles), ("p", probs), ("n", noise), ("l", lik), ("i", index_p), ("j", jac),
+                         ("r", prior)):
+                hist[k].append(v)
+        st = lambda k: torch.stack(hist[k], dim=1)
+        return (st("x"), st("p"), st("n"), st("l"), init_weights_log, st("i"), st("j") if self.NF else None,
+                st("r") if self.NF else None, obs_likelihood)
+
+    # ------------------------------------------------------------------------------------
+    def get_mask(self):
+        """Random labelled mask with labeledRatio ones (DPFs.py:218-229)."""
+        n1 = int(self.batch_size * self.seq_len * self.labeledRatio)
+        arr = np.array([0] * (self.batch_size * self.seq_len - n1) + [1] * n1)
+        np.random.shuffle(arr)
+        return torch.tensor(arr.reshape(self.batch_size, self.seq_len)).to(device)
+
+    def pretrain_ae(self, train_loader, valid_loader, start_epoch=-1, epoch_num=100, logger=None):
+        """Auto-encoder pretraining (DPFs.py:231-302)."""
+        logger = logger or _NullLogger()
+        best, ckpt = 1e10, None
+        for epoch in range(start_epoch + 1, epoch_num):
+            self.train()
+            losses = []
+            for it, (_, _, image, _, _, _) in enumerate(train_loader):
+                img = image.permute(0, 1, 4, 2, 3).reshape(-1, 3, 128, 128).to(device)
+                loss = F.mse_loss(self.decoder(self.encoder(img)), img)
+                self.zero_grad()
+                loss.backward()
+                self.optim.step()
+                losses.append(loss.detach().cpu().numpy())
+            print(f"Train AE: Epoch: {epoch}, loss: {np.mean(losses)}")
+            self.eval()
+            with torch.no_grad():
+                vl = [F.mse_loss(self.decoder(self.encoder(im)), im).cpu().numpy()
+                      for im in (image.permute(0, 1, 4, 2, 3).reshape(-1, 3, 128, 128).to(device)
+                                 for (_, _, image, _, _, _) in valid_loader)]
+            ev = float(np.mean(vl))
+            logger.add_scalar("PretrainAE_loss_eval/loss", ev, epoch)
+            if ev < best:
+                best = ev
+                ckpt = {"model": self.state_dict(), "optim": self.optim.state_dict()}
+                os.makedirs("./model", exist_ok=True)
+                torch.save(ckpt, "./model/ae_pretrain.pth")
+        if ckpt is not None:
+            self.load_state_dict(ckpt["model"])
+            self.optim.load_state_dict(ckpt["optim"])
+
+    def e2e_train(self, train_loader, valid_loader, start_epoch=-1, epoch_num=100, logger=None, run_id=None):
+        """End-to-end training with validation and best-model checkpoints (DPFs.py:304-383)."""
+        logger = logger or _NullLogger()
+        best = 1e10
+        if self.param.load_pretrainModel:
+            self.load_state_dict(torch.load("./model/ae_pretrain.pth", weights_only=True)["model"])
+        eval_hist = []
+        for epoch in range(start_epoch + 1, epoch_num):
+            self.train()
+            sup, ae = [], []
+            for inputs in train_loader:
+                out = self.forward(inputs, train=True)
+                self.zero_grad()
+                out[0].backward()
+                self.optim.step()
+                sup.append(out[1].detach().cpu().numpy())
+                ae.append(out[3].detach().cpu().numpy())
+            self.optim_scheduler.step()
+            logger.add_scalar("Sup_loss/loss", float(np.mean(sup)), epoch)
+            print(f"End-to-end loss: epoch: {epoch}, loss: {np.mean(sup)}, loss_ae: {np.mean(ae)}")
+            self.eval()
+            ev = []
+            with torch.no_grad():
+                for inputs in valid_loader:
+                    out = self.forward(inputs, train=False)
+                    ev.append(out[1].detach().cpu().numpy())
+            ev_mean = float(np.mean(ev))
+            logger.add_scalar("Sup_loss_eval/loss", ev_mean, epoch)
+            print(f"End-to-end loss evaluation: epoch: {epoch}, loss: {ev_mean}", self.NF)
+            eval_hist.append(ev_mean)
+            data_dir = os.path.join("logs", run_id or "run", "data")
+            os.makedirs(data_dir, exist_ok=True)
+            np.save(os.path.join(data_dir, "eval_loss_epoch.npy"), eval_hist)
+            if ev_mean < best:
+                best = ev_mean
+                (_, _, _, _, pred, pl, pwl, state, _, _, ll, _, _) = out
+                np.savez(os.path.join(data_dir, "eval_result_best.npz"), particle_list=pl.cpu().numpy(),
+                         particle_weight_list=pwl.cpu().numpy(), likelihood_list=ll.cpu().numpy(),
+                         pred=pred.cpu().numpy(), state=state.cpu().numpy(), loss=ev)
+                mdir = os.path.join("logs", run_id or "run", "models")
+                os.makedirs(mdir, exist_ok=True)
+                torch.save(checkpoint_state(self, epoch), os.path.join(mdir, "e2e_model_bestval_e2e.pth"))
+
+    def load_model(self, file_name):
+        ckpt = torch.load(file_name, weights_only=True)
+        load_model(self, ckpt)
+        print(f"Load epcoh: {ckpt['epoch']}")
+
+    def train_val(self, train_loader, valid_loader, run_id):
+        for d in ("result", "model", "checkpoint", "logger"):
+            os.makedirs(d, exist_ok=True)
+        logger = _summary_writer("./logger")
+        if self.param.resume:
+            self.load_model("./model/e2e_model_bestval_e2e.pth")
+        if self.param.pretrain_ae:
+            self.pretrain_ae(train_loader, valid_loader, start_epoch=-1, epoch_num=300, logger=logger)
+        if self.param.e2e_train:
+            self.e2e_train(train_loader, valid_loader, start_epoch=-1, epoch_num=self.param.num_epochs,
+                           logger=logger, run_id=run_id)
+
+    def testing(self, test_loader, run_id, model_path="./model/e2e_model_bestval_e2e.pth"):
+        """Test-set RMSE and result dump (DPFs.py:419-451)."""
+        if self.param.testing:
+            self.load_model(os.path.join(model_path, "e2e_model_bestval_e2e.pth"))
+        self.eval()
+        losses = []
+        with torch.no_grad():
+            for inputs in test_loader:
+                out = self.forward(inputs, train=False)
+                losses.append(out[1].detach().cpu().numpy())
+        data_dir = os.path.join("logs", run_id, "data")
+        os.makedirs(data_dir, exist_ok=True)
+        np.save(os.path.join(data_dir, "test_loss_epoch.npy"), losses)
+        print(f"End-to-end loss testing: loss: {np.mean(losses)}")
+        (_, _, _, _, pred, pl, pwl, state, _, image, ll, nl, _) = out
+        np.savez(os.path.join(data_dir, "test_result.npz"), particle_list=pl.cpu().numpy(),
+                 particle_weight_list=pwl.cpu().numpy(), likelihood_list=ll.cpu().numpy(),
+                 state=state.cpu().numpy(), pred=pred.cpu().numpy(), images=image.cpu().numpy(),
+                 noise=nl.cpu().numpy())

@@ -1,0 +1,240 @@
+// common.hpp -- device utilities shared by the libnfdpf kernels (gfx950 / CDNA4).
+//
+// * error plumbing for the C ABI (include/nfdpf.h)
+// * Philox4x32-10 counter RNG + Box-Muller (shard-invariant device RNG mode)
+// * tanh with Cephes-style small-argument polynomial (FCNN activations, nf/flows.py:105-111)
+// * wave64 / workgroup reductions with a fixed, thread-count-independent combine order
+// * the ATen-CPU cascade row sum (oracle/cascade.py) for bit-exact soft resampling
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <string>
+
+#include "../../include/nfdpf.h"
+
+namespace nfdpf {
+
+// ----------------------------------------------------------------------------------------
+// host-side error plumbing
+// ----------------------------------------------------------------------------------------
+void set_error(const char *fmt, ...);
+int launch_status(const char *what);
+
+#define NFDPF_REQUIRE(cond, ...)            \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::nfdpf::set_error(__VA_ARGS__);      \
+      return NFDPF_EINVAL;                  \
+    }                                       \
+  } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+
+// ----------------------------------------------------------------------------------------
+// RNG: Philox4x32-10 (Salmon et al., SC'11).  Counter = (particle, global row, step, tag),
+// key = seed.  Streams (tag): see RngTag.
+// ----------------------------------------------------------------------------------------
+enum RngTag : uint32_t { kTagMotion = 0, kTagOffset = 1, kTagInitPos = 2, kTagInitNormal = 3 };
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+    const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ U4 rng_draw(uint64_t seed, uint32_t tag, uint32_t step, int64_t row,
+                                       uint32_t idx) {
+  U4 c{idx, (uint32_t)row, (uint32_t)(row >> 32) ^ (step << 8), tag};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// [0,1) with 24 random bits
+__device__ __forceinline__ float u01(uint32_t u) { return (float)(u >> 8) * 0x1.0p-24f; }
+// (0,1]
+__device__ __forceinline__ float u01_open0(uint32_t u) { return ((float)(u >> 8) + 1.0f) * 0x1.0p-24f; }
+
+// two standard normals from two uniforms (Box-Muller)
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float &z0, float &z1) {
+  const float r = sqrtf(-2.0f * logf(u01_open0(a)));
+  float s, c;
+  sincospif(2.0f * u01(b), &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// ----------------------------------------------------------------------------------------
+// activations
+// ----------------------------------------------------------------------------------------
+// tanh: |x| < 0.625 -> odd minimax polynomial (Cephes tanhf coefficients, rel. err ~1e-7),
+// otherwise 1 - 2/(exp(2x)+1).  Both are evaluated and selected (no divergence).
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float z = x * x;
+  float p = fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f);
+  p = fmaf(p, z, -5.37397155531e-2f);
+  p = fmaf(p, z, 1.33314422036e-1f);
+  p = fmaf(p, z, -3.33332819422e-1f);
+  const float small = fmaf(p * z, x, x);
+  const float e = __expf(2.0f * x);
+  const float big = 1.0f - __fdividef(2.0f, e + 1.0f);
+  return fabsf(x) < 0.625f ? small : big;
+}
+
+__device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.0f); }
+
+// ----------------------------------------------------------------------------------------
+// reductions (fixed combine order: lanes by xor-butterfly, then waves in index order)
+// ----------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Workgroup reductions.  `sh` is LDS scratch of >= 16 elements of T, reused across calls
+// (the leading barrier protects the previous use).  Every thread gets the result.
+template <typename T>
+__device__ T block_sum(T v, T *sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+  T r = sh[0];
+  for (int i = 1; i < nw; ++i) r += sh[i];
+  return r;
+}
+template <typename T>
+__device__ T block_max(T v, T *sh) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+  T r = sh[0];
+  for (int i = 1; i < nw; ++i) r = fmax(r, sh[i]);
+  return r;
+}
+
+// Exclusive prefix over the workgroup of one value per thread (thread order).
+template <typename T>
+__device__ T block_exclusive_scan(T v, T *sh, T *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  __syncthreads();
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+  T base = 0, all = 0;
+  for (int i = 0; i < nw; ++i) {
+    if (i < w) base += sh[i];
+    all += sh[i];
+  }
+  if (total) *total = all;
+  return base + inc - v;
+}
+
+__device__ __forceinline__ int ceil_log2_i(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
+
+// ----------------------------------------------------------------------------------------
+// ATen CPU cascade sum of a contiguous float row (torch.sum(x, -1) on CPU), bit-exact.
+// Order (oracle/cascade.py): 8-wide vectors, 4 ILP slots, 4-level cascade with level step
+// 2^max(4, ceil_log2(nvec/4)/4); leftover vectors into slot 0; fold slots 0+1+2+3; scalar
+// tail first, then the 8 lanes in order.  Rows shorter than 8 use width-1 vectors.
+// Must be called by all 64 lanes of ONE wave; returns the sum in every lane.
+// ----------------------------------------------------------------------------------------
+template <class Get>
+__device__ float cascade_row_sum(const Get &v, int n) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int W = (n < 8) ? 1 : 8;
+  const int nv = n / W;
+  const int n4 = nv / 4;
+  const int k = lane / W, j = lane - (lane / W) * W;
+  const bool act = lane < 4 * W;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (act) {
+    const int power = max(4, ceil_log2_i(n4) / 4);
+    const int step = 1 << power, mask = step - 1;
+    int i = 0;
+    while (i + step <= n4) {
+      for (int jj = 0; jj < step; ++jj) a0 += v(((i + jj) * 4 + k) * W + j);
+      i += step;
+      a1 += a0;
+      a0 = 0.f;
+      if ((i & (mask << power)) == 0) {
+        a2 += a1;
+        a1 = 0.f;
+        if ((i & (mask << (2 * power))) == 0) {
+          a3 += a2;
+          a2 = 0.f;
+        }
+      }
+    }
+    for (; i < n4; ++i) a0 += v((i * 4 + k) * W + j);
+    a0 += a1;
+    a0 += a2;
+    a0 += a3;
+    if (k == 0)
+      for (int r = n4 * 4; r < nv; ++r) a0 += v(r * W + j);
+  }
+  const float s1 = __shfl(a0, j + W), s2 = __shfl(a0, j + 2 * W), s3 = __shfl(a0, j + 3 * W);
+  float ps = a0;
+  ps += s1;
+  ps += s2;
+  ps += s3;
+  if (W == 1) return __shfl(ps, 0);
+  float tot = 0.f;
+  for (int r = nv * 8; r < n; ++r) tot += v(r);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) tot += __shfl(ps, q);
+  return tot;
+}
+
+// ----------------------------------------------------------------------------------------
+// misc
+// ----------------------------------------------------------------------------------------
+// Hide a wave-uniform pointer from loop-invariant code motion, so weight loads stay inside
+// the particle loop (re-read from the scalar cache) instead of being hoisted into hundreds
+// of SGPRs that then spill into VGPR lanes.
+template <class T>
+__device__ __forceinline__ const T *opaque(const T *p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// threads per workgroup for a one-row-per-workgroup kernel over n particles
+inline int row_threads(int n) {
+  int t = round_up(n < 64 ? 64 : n, 64);
+  return t > 1024 ? 1024 : t;
+}
+
+}  // namespace nfdpf

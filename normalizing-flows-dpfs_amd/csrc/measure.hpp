@@ -1,0 +1,143 @@
+// measure.hpp -- per-particle measurement models (model/models.py:206-278) and the per-row
+// shared state of the fused filter step.
+#pragma once
+
+#include "flows.hpp"
+
+namespace nfdpf {
+
+constexpr int kH = 8;           // FCNN hidden width (nf/flows.py:183, fixed by the reference)
+constexpr int kMaxFlows = 4;    // n_sequence (DPFs.py:46) is 2
+constexpr int kE = 32;          // frame-encoding width of the fused measurements (--hiddensize)
+constexpr int kNnH = 64;        // likelihood_est width (model/models.py:119-128)
+constexpr int kStepMaxN = 12288;  // soft resampler C[] in LDS
+constexpr int kMaxCtx = 260;      // proposal context [enc (E <= 256), mean, std]
+
+struct StepShared {
+  float cb_dyn[kMaxFlows * 4 * kH];
+  float cb_cond[kMaxFlows * 4 * kH];
+  float ctx[kMaxCtx];
+  float encv[kE];       // this row's frame encoding (normalised for cos)
+  float nnrow[kNnH];    // NN: folded first layer of the obs half
+  float f[16];
+  double d[16];
+  float bc[4];
+};
+
+__device__ __forceinline__ float density(float e0, float e1, float K, float two_var) {
+#pragma clang fp contract(off)
+  // compute_normal_density (utils.py:22-37) with D = 2: K - (e0^2/(2s^2) + e1^2/(2s^2))
+  return K - (e0 * e0 / two_var + e1 * e1 / two_var);
+}
+
+struct MeasArgs {
+  const float *pe_params, *meas_params;
+  int n_flows;
+  float meas_prior_std;
+};
+
+template <int MEAS>
+__device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L, float x0,
+                                         float x1) {
+  if constexpr (MEAS == NFDPF_MEAS_COS) {
+    // measurement_model_cosine_distance + et_distance (model/models.py:206-219, utils.py:8-15)
+    // <e/|e|, v> computed as <e, v>/|e| (same value to ~1 ulp, no E-wide register array)
+    float ss, dot;
+    encode_dot<kE>(opaque(d.pe_params), x0, x1, L.encv, ss, dot);
+    const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
+    return logf(1.0f / (1e-7f + cosd));
+  } else if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
+    // measurement_model_cnf (model/models.py:256-278): flow input = frame encoding,
+    // condition = particle encoding; N(0, prior_std^2 I) prior + log-det
+    float e[kE];
+    particle_encode<kE>(opaque(d.pe_params), x0, x1, e);
+    constexpr int HALF = kE / 2;
+    constexpr int in = HALF + kE;
+    const int ns = fcnn_size<kH>(in, HALF);
+    float lo[HALF], up[HALF];
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) {
+      lo[k] = L.encv[k];
+      up[k] = L.encv[HALF + k];
+    }
+    float ld = 0.f;
+    for (int f = 0; f < d.n_flows; ++f) {
+      const float *fw = opaque(d.meas_params) + (int64_t)f * 4 * ns;
+      float cb[4 * kH];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_bias_c<kH, kE>(fw + n * ns, in, HALF, j, e);
+      ld += coupling_forward<HALF, kH>(fw, in, lo, up, cb);
+    }
+    const float is = 1.0f / d.meas_prior_std;
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) {
+      m = fmaf(lo[k] * is, lo[k] * is, m);
+      m = fmaf(up[k] * is, up[k] * is, m);
+    }
+    const float lp = -0.5f * (kE * 1.8378770664093453f + m) - kE * logf(d.meas_prior_std);
+    return lp + ld;
+  } else if constexpr (MEAS == NFDPF_MEAS_GAUSSIAN) {
+    // measurement_model_Gaussian with N(1, 100 I) (DPFs.py:84-86, model/models.py:237-254)
+    float e[kE];
+    particle_encode<kE>(opaque(d.pe_params), x0, x1, e);
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
+      const float v = (L.encv[j] - e[j] - 1.0f) * 0.1f;
+      m = fmaf(v, v, m);
+    }
+    return -0.5f * (kE * 1.8378770664093453f + m) - kE * 2.302585092994046f;
+  } else if constexpr (MEAS == NFDPF_MEAS_NN) {
+    // measurement_model_NN (model/models.py:221-235): sigmoid(MLP([enc_obs, enc_particle])).log()
+    float e[kE];
+    particle_encode<kE>(opaque(d.pe_params), x0, x1, e);
+    const float *W1 = opaque(d.meas_params);  // [64, 2E], b1 [64]
+    float h[kNnH];
+#pragma unroll
+    for (int j = 0; j < kNnH; ++j) {
+      float a = L.nnrow[j];
+#pragma unroll
+      for (int k = 0; k < kE; ++k) a = fmaf(W1[j * 2 * kE + kE + k], e[k], a);
+      h[j] = relu(a);
+    }
+    const float *W2 = W1 + kNnH * 2 * kE + kNnH, *b2 = W2 + kNnH * kNnH;
+    const float *W3 = b2 + kNnH, *b3 = W3 + kNnH;
+    float o = b3[0];
+    for (int j = 0; j < kNnH; ++j) {
+      float a = b2[j];
+#pragma unroll
+      for (int k = 0; k < kNnH; ++k) a = fmaf(W2[j * kNnH + k], h[k], a);
+      o = fmaf(W3[j], relu(a), o);
+    }
+    return logf(1.0f / (1.0f + expf(-o)));
+  } else {
+    return 0.f;  // EXTERNAL: supplied by lik_ext in phase 2
+  }
+}
+
+
+// per-row constants of the measurement (frame encoding, NN obs-half fold); all threads call
+template <int MEAS>
+__device__ __forceinline__ void measure_row_setup(const float *enc, const float *meas_params,
+                                                  StepShared &L) {
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const float v = tid < kE ? enc[tid] : 0.f;
+    if (MEAS == NFDPF_MEAS_COS) {
+      const float nrm = sqrtf(wave_sum(v * v));
+      if (tid < kE) L.encv[tid] = v / fmaxf(nrm, 1e-12f);
+    } else if (tid < kE) {
+      L.encv[tid] = v;
+    }
+  }
+  if (MEAS == NFDPF_MEAS_NN && tid < kNnH) {
+    float a = meas_params[kNnH * 2 * kE + tid];
+    for (int k = 0; k < kE; ++k) a = fmaf(meas_params[tid * 2 * kE + k], enc[k], a);
+    L.nnrow[tid] = a;
+  }
+}
+
+}  // namespace nfdpf

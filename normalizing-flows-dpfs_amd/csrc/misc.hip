@@ -1,0 +1,45 @@
+// misc.hip -- particle_initialization (utils.py:46-62) in DEVICE rng mode.
+#include "common.hpp"
+
+namespace nfdpf {
+
+__global__ void particle_init_kernel(const float *__restrict__ start_xy, int B, int N, float width,
+                                     int true_state, uint64_t seed, int64_t row_base,
+                                     float *__restrict__ x, float *__restrict__ logw) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (int64_t)B * N) return;
+  const int b = (int)(o / N), i = (int)(o - (int64_t)b * N);
+  const int64_t grow = row_base + b;
+  float a0, a1;
+  if (true_state) {
+    const U4 r = rng_draw(seed, kTagInitNormal, 0u, grow, (uint32_t)i);
+    box_muller(r.x, r.y, a0, a1);
+    a0 += start_xy[2 * b];
+    a1 += start_xy[2 * b + 1];
+  } else {
+    // (hi - lo) * U[0,1) + lo, hi = width/2, lo = -width/2 (utils.py:53-56)
+    const U4 r = rng_draw(seed, kTagInitPos, 0u, grow, (uint32_t)i);
+    const float hi = width / 2.0f, lo = -width / 2.0f;
+    a0 = (hi - lo) * u01(r.x) + lo;
+    a1 = (hi - lo) * u01(r.y) + lo;
+  }
+  x[2 * o] = a0;
+  x[2 * o + 1] = a1;
+  logw[o] = logf(1.0f / (float)N);  // torch.log(ones / N) (:60)
+}
+
+}  // namespace nfdpf
+
+using namespace nfdpf;
+
+extern "C" int nfdpf_particle_init(const float *start_xy, int B, int N, float width, int true_state,
+                                   uint64_t seed, int64_t row_base, float *x, float *logw,
+                                   void *stream) {
+  NFDPF_REQUIRE(x && logw && (!true_state || start_xy), "nfdpf_particle_init: null pointer");
+  NFDPF_REQUIRE(B >= 0 && N >= 1, "nfdpf_particle_init: bad sizes");
+  const int64_t M = (int64_t)B * N;
+  if (M == 0) return NFDPF_OK;
+  particle_init_kernel<<<(unsigned)((M + 255) / 256), 256, 0, as_stream(stream)>>>(
+      start_xy, B, N, width, true_state, seed, row_base, x, logw);
+  return launch_status("nfdpf_particle_init");
+}

@@ -1,0 +1,314 @@
+"""Model assembly (model/models.py of the reference): builders, dynamics, proposal and
+measurement models with the reference's names, signatures and state_dict keys.
+
+Hot-path pieces run on libnfdpf: the flow stacks (via nf.models), the measurement models
+(``nfdpf_measurement``) and -- inside ``DPF.filtering_pos`` -- everything fused into one
+kernel per step (nfdpf.engine).  The frame encoder / decoder CNNs are per-image work
+(B x T frames, not B x N x T particles) and stay on PyTorch/MIOpen.
+"""
+import math
+
+import torch
+from torch import nn
+
+from nf.flows import FCNN, RealNVP, RealNVP_cond, MAF  # noqa: F401  (reference re-exports nf.flows)
+from nf.models import NormalizingFlowModel, NormalizingFlowModel_cond
+from nfdpf import autograd as _ag
+from nfdpf import ops as _ops
+from nfdpf.pack import blob, flows_tensors, mlp_tensors
+from utils import et_distance
+
+device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+_CHANNELS = (3, 16, 32, 64, 128, 256)
+
+
+def _conv_stack(out_features):
+    """5 x [Conv(4, s2, p1, no bias) ReLU BN] + Linear(256*4*4, out) (model/models.py:10-60)."""
+    layers = []
+    for cin, cout in zip(_CHANNELS[:-1], _CHANNELS[1:]):
+        layers += [nn.Conv2d(cin, cout, kernel_size=4, stride=2, padding=1, bias=False), nn.ReLU(True),
+                   nn.BatchNorm2d(cout)]
+    layers += [nn.Flatten(), nn.Linear(256 * 4 * 4, out_features)]
+    return nn.Sequential(*layers)
+
+
+def _deconv_stack(in_features):
+    """Linear + Unflatten + 5 x ConvTranspose (model/models.py:62-117), sigmoid output."""
+    layers = [nn.Linear(in_features, 256 * 4 * 4), nn.Unflatten(-1, (256, 4, 4))]
+    rev = _CHANNELS[::-1]
+    for k, (cin, cout) in enumerate(zip(rev[:-1], rev[1:])):
+        layers.append(nn.ConvTranspose2d(cin, cout, kernel_size=4, padding=1, stride=2, bias=False))
+        if cout != 3:
+            layers.append(nn.ReLU(True))
+        layers.append(nn.BatchNorm2d(cout))
+    layers.append(nn.Sigmoid())
+    return nn.Sequential(*layers)
+
+
+def build_encoder(hidden_size):
+    return _conv_stack(hidden_size)
+
+
+def build_encoder_cglow(hidden_size):
+    return _conv_stack(192)
+
+
+def build_decoder(hidden_size):
+    return _deconv_stack(hidden_size)
+
+
+def build_decoder_cglow(hidden_size):
+    return _deconv_stack(192)
+
+
+def _mlp(sizes, act, last_act=None):
+    layers = []
+    for i, (a, b) in enumerate(zip(sizes[:-1], sizes[1:])):
+        layers.append(nn.Linear(a, b))
+        if i < len(sizes) - 2:
+            layers.append(act())
+    if last_act is not None:
+        layers.append(last_act())
+    return nn.Sequential(*layers)
+
+
+def build_likelihood(hidden_size, state_dim):
+    """likelihood_est: Linear(2H,64) ReLU Linear(64,64) ReLU Linear(64,1) Sigmoid (:119-128)."""
+    return _mlp([2 * hidden_size, 64, 64, 1], lambda: nn.ReLU(True), nn.Sigmoid)
+
+
+def build_particle_encoder(hidden_size, state_dim):
+    """Linear(D,16) ReLU Linear(16,32) ReLU Linear(32,H) (:130-139)."""
+    return _mlp([state_dim, 16, 32, hidden_size], nn.ReLU)
+
+
+def build_particle_encoder_cglow(hidden_size, state_dim):
+    return _mlp([state_dim, 16, 32, 192], nn.ReLU)
+
+
+def build_transition_model(state_dim):
+    return _mlp([state_dim, 64, 64, state_dim], nn.ReLU)
+
+
+def build_conditional_nf(n_sequence, hidden_size, state_dim, init_var=0.01, prior_mean=0.0, prior_std=1.0):
+    """Stack of RealNVP_cond(dim=state_dim, obser_dim=hidden_size) with N(0, init_var^2)
+    weights and an isotropic MVN prior (model/models.py:161-172)."""
+    flows = [RealNVP_cond(dim=state_dim, obser_dim=hidden_size) for _ in range(n_sequence)]
+    for f in flows:
+        f.zero_initialization(var=init_var)
+    prior = torch.distributions.MultivariateNormal(torch.zeros(state_dim).to(device) + prior_mean,
+                                                   torch.eye(state_dim).to(device) * prior_std ** 2)
+    return NormalizingFlowModel_cond(prior, flows, device=device)
+
+
+def build_maf_dyn(n_sequence, state_dim, hidden_dim=8):
+    """MAF dynamic flow stack for --NF-dyn-flow MAF (BASELINE config 4; not wired in the
+    reference)."""
+    flows = [MAF(dim=state_dim, hidden_dim=hidden_dim) for _ in range(n_sequence)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(state_dim).to(device), torch.eye(state_dim).to(device))
+    return NormalizingFlowModel(prior, flows, device=device)
+
+
+def build_conditional_glow(args):
+    from nf.cglow.CGlowModel import CondGlowModel
+    return CondGlowModel(args)
+
+
+def build_dyn_nf(n_sequence, hidden_size, state_dim, init_var=0.01):
+    flows = [RealNVP(dim=state_dim) for _ in range(n_sequence)]
+    for f in flows:
+        f.zero_initialization(var=init_var)
+    prior = torch.distributions.MultivariateNormal(torch.zeros(state_dim).to(device), torch.eye(state_dim).to(device))
+    return NormalizingFlowModel(prior, flows, device=device)
+
+
+def motion_update(particles, vel, pos_noise=20.0):
+    """x + vel + N(0, pos_noise^2) noise drawn on the CPU generator (model/models.py:191-204)."""
+    B, N, _ = particles.shape
+    noise = torch.normal(mean=0., std=pos_noise, size=(B, N, 2)).to(particles.device)
+    return particles + vel[:, None, :].repeat((1, N, 1)) + noise, noise
+
+
+# ------------------------------------------------------------------------------------------
+# measurement models: forward(encodings (B,H), particles (B,N,2)) -> log-likelihood (B,N)
+# ------------------------------------------------------------------------------------------
+class _MeasRunner:
+    def __init__(self, model, kind):
+        self.model, self.kind = model, kind
+
+    def hip(self, enc, x):
+        m = self.model
+        pe = blob(m, "pe", mlp_tensors(m.particle_encoder), x.device)
+        meas, nfl, pstd = None, 0, 2.5
+        if self.kind == "CRNVP":
+            meas = blob(m, "meas", flows_tensors(m.CNF.flows), x.device)
+            nfl = len(m.CNF.flows)
+            pstd = math.sqrt(float(m.CNF.prior.covariance_matrix[0, 0]))
+        elif self.kind == "NN":
+            meas = blob(m, "meas", mlp_tensors(m.likelihood_estimator), x.device)
+        return (_ops.measurement(self.kind, pe, meas, nfl, enc, x, pstd),)
+
+    def torch(self, enc, x):
+        return (self.model.torch_forward(enc, x),)
+
+
+def _meas_apply(model, kind, enc, x):
+    return _ag.apply(_MeasRunner(model, kind), (enc, x), list(model.parameters()))[0]
+
+
+def _obs_rep(encodings, n):
+    return encodings[:, None, :].repeat(1, n, 1)
+
+
+class measurement_model_cosine_distance(nn.Module):
+    """log(1/(1e-7 + cos-distance(enc_obs, enc_particle))) (model/models.py:206-219)."""
+
+    def __init__(self, particle_encoder):
+        super().__init__()
+        self.particle_encoder = particle_encoder
+
+    def forward(self, encodings, update_particles):
+        return _meas_apply(self, "cos", encodings, update_particles)
+
+    def torch_forward(self, encodings, particles):
+        es = self.particle_encoder(particles.float())
+        return (1 / (1e-7 + et_distance(_obs_rep(encodings, particles.shape[1]), es))).log()
+
+
+class measurement_model_NN(nn.Module):
+    """sigmoid-MLP on [enc_obs, enc_particle] (model/models.py:221-235)."""
+
+    def __init__(self, particle_encoder, likelihood_estimator):
+        super().__init__()
+        self.particle_encoder = particle_encoder
+        self.likelihood_estimator = likelihood_estimator
+
+    def forward(self, encodings, update_particles):
+        return _meas_apply(self, "NN", encodings, update_particles)
+
+    def torch_forward(self, encodings, particles):
+        es = self.particle_encoder(particles.float())
+        h = torch.cat([_obs_rep(encodings, particles.shape[1]), es], dim=-1)
+        return self.likelihood_estimator(h)[..., 0].log()
+
+
+class measurement_model_Gaussian(nn.Module):
+    """N(1, 100 I) log-density of enc_obs - enc_particle, minus the row max (:237-254)."""
+
+    def __init__(self, particle_encoder, gaussian_distribution):
+        super().__init__()
+        self.particle_encoder = particle_encoder
+        self.gaussian_distribution = gaussian_distribution
+
+    def forward(self, encodings, update_particles):
+        return _meas_apply(self, "gaussian", encodings, update_particles)
+
+    def torch_forward(self, encodings, particles):
+        es = self.particle_encoder(particles.float())
+        lik = self.gaussian_distribution.log_prob(_obs_rep(encodings, particles.shape[1]) - es)
+        return lik - lik.max(dim=-1, keepdim=True)[0]
+
+
+class measurement_model_cnf(nn.Module):
+    """Conditional-RealNVP likelihood of the frame encoding given the particle encoding,
+    minus the row max (model/models.py:256-278)."""
+
+    def __init__(self, particle_encoder, CNF):
+        super().__init__()
+        self.particle_encoder = particle_encoder
+        self.CNF = CNF
+
+    def forward(self, encodings, update_particles):
+        return _meas_apply(self, "CRNVP", encodings, update_particles)
+
+    def torch_forward(self, encodings, particles):
+        from nf.flows import CouplingStack
+        from nf.models import _isotropic
+        B, N = particles.shape[:2]
+        H = encodings.shape[-1]
+        es = self.particle_encoder(particles.float()).reshape(-1, H)
+        eo = _obs_rep(encodings, N).reshape(-1, H)
+        fl = list(self.CNF.flows)
+        _, ld, lp = CouplingStack(self.CNF, fl, H, H, fl[0].hidden_dim, False,
+                                  prior=_isotropic(self.CNF.prior)).torch(eo, es)
+        lik = (lp + ld).reshape(B, N)
+        return lik - lik.max(dim=-1, keepdim=True)[0]
+
+
+class measurement_model_cglow(nn.Module):
+    """Conditional-GLOW likelihood (model/models.py:280-303)."""
+
+    def __init__(self, particle_encoder, CGLOW):
+        super().__init__()
+        self.particle_encoder = particle_encoder
+        self.CGLOW = CGLOW
+
+    def forward(self, encodings, update_particles):
+        B, N, D = update_particles.shape
+        es = self.particle_encoder(update_particles.reshape(-1, D).float()).reshape(B * N, 3, 8, 8)
+        eo = encodings[:, None, ...].repeat(1, N, 1).reshape(B * N, 3, 8, 8)
+        _, nll = self.CGLOW(es, eo)
+        lik = -nll.reshape(B, N)
+        return lik - lik.max(dim=-1, keepdim=True)[0]
+
+
+# ------------------------------------------------------------------------------------------
+# dynamics / proposal (model/models.py:305-379)
+# ------------------------------------------------------------------------------------------
+def _row_context(x, mean=None, std=None):
+    n = x.shape[1]
+    m = x.mean(dim=1, keepdim=True) if mean is None else mean
+    s = x.std(dim=1, keepdim=True) if std is None else std
+    return torch.cat([m.detach().clone().repeat([1, n, 1]).reshape(-1, x.shape[-1]),
+                      s.detach().clone().repeat([1, n, 1]).reshape(-1, x.shape[-1])], dim=-1)
+
+
+def nf_dynamic_model(dynamical_nf, dynamic_particles, jac_shape, NF=False, forward=False, mean=None, std=None):
+    """Dynamic flow with per-row [mean, std] context; returns (x', jac = -log_det) (:305-332)."""
+    if not NF:
+        return dynamic_particles, torch.zeros(jac_shape).to(dynamic_particles.device)
+    B, N, D = dynamic_particles.shape
+    ctx = _row_context(dynamic_particles, mean, std)
+    flat = dynamic_particles.reshape(-1, D)
+    if isinstance(dynamical_nf, NormalizingFlowModel):  # MAF dynamic flow: no context
+        if forward:
+            out, _, ld = dynamical_nf.forward(flat)
+        else:
+            out, ld = dynamical_nf.inverse(flat)
+    elif forward:
+        out, _, ld = dynamical_nf.forward(flat, ctx)
+    else:
+        out, ld = dynamical_nf.inverse(flat, ctx)
+    return out.reshape(B, N, D), (-ld).reshape(B, N)
+
+
+def normalising_flow_propose(cond_model, particles_pred, obs, flow=RealNVP_cond, n_sequence=2, hidden_dimension=8,
+                             obser_dim=None):
+    """Proposal flow conditioned on [frame encoding, mean, std] (:334-356)."""
+    B, N, D = particles_pred.shape
+    ctx = _row_context(particles_pred)
+    cond = torch.cat([obs[:, None, :].repeat([1, N, 1]).reshape(B * N, -1), ctx], dim=-1)
+    out, ld = cond_model.inverse(particles_pred.reshape(-1, D), cond)
+    return out.reshape(B, N, D), (-ld).reshape(B, N)
+
+
+def proposal_likelihood(cond_model, dynamical_nf, measurement_model, particles_dynamic, particles_physical,
+                        encodings, noise, jac_dynamic, NF, NF_cond, prototype_density):
+    """(proposal particles, lik, prior, proposal log-density) (:358-379)."""
+    enc = encodings.detach().clone()
+    if NF_cond:
+        prop, jac_prop = normalising_flow_propose(cond_model, particles_dynamic, enc)
+        if NF:
+            back, jac_back = nf_dynamic_model(dynamical_nf, prop, jac_dynamic.shape, NF=NF, forward=True,
+                                              mean=particles_physical.mean(dim=1, keepdim=True),
+                                              std=particles_physical.std(dim=1, keepdim=True))
+            prior = prototype_density(back - (particles_physical - noise)) - jac_back
+        else:
+            prior = prototype_density(prop - (particles_physical - noise))
+        propose = prototype_density(noise) + jac_dynamic + jac_prop
+    else:
+        prop = particles_dynamic
+        prior = prototype_density(noise) + jac_dynamic
+        propose = prototype_density(noise) + jac_dynamic
+    return prop, measurement_model(encodings, prop), prior, propose

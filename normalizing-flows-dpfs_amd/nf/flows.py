@@ -1,0 +1,210 @@
+"""Flows of the hot path -- same classes, constructor arguments and state_dict keys as the
+reference's nf/flows.py, forward/inverse run by libnfdpf (HIP, gfx950).
+
+* ``RealNVP_cond`` (nf/flows.py:181-239): conditional affine coupling, the only flow the
+  DPF instantiates (model/models.py:162);
+* ``RealNVP`` (:117-179): unconditional coupling (the HIP kernel with obser_dim = 0);
+* ``MAF`` (:241-284): masked autoregressive flow (BASELINE config 4 dynamic flow);
+* ``FCNN`` (:101-114): the coupling nets' MLP.
+
+Each ``forward``/``inverse`` call runs the whole flow in one kernel launch; a stack of
+flows is run by ``nf.models`` in ONE launch over all flows.  Parameters are packed into a
+cached fp32 blob (nfdpf.pack).  Tensors must live on the HIP device.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.init as init
+
+from nfdpf import autograd as _ag
+from nfdpf import ops as _ops
+from nfdpf.pack import blob, flows_tensors
+
+device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+class FCNN(nn.Module):
+    """Linear(in,H) Tanh Linear(H,H) Tanh Linear(H,out) on ``x.float()`` (nf/flows.py:101-114)."""
+
+    def __init__(self, in_dim, out_dim, hidden_dim):
+        super().__init__()
+        layers = [nn.Linear(in_dim, hidden_dim), nn.Tanh(), nn.Linear(hidden_dim, hidden_dim), nn.Tanh(),
+                  nn.Linear(hidden_dim, out_dim)]
+        self.network = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return self.network(x.float())
+
+
+def _coupling_nets(flow, in_dim, half, hidden_dim, base_network):
+    for name in ("t1", "s1", "t2", "s2"):
+        setattr(flow, name, base_network(in_dim, half, hidden_dim))
+
+
+def _normal_init(flow, var):
+    """zero_initialization (nf/flows.py:131-151 / 191-211): N(0, var^2) weights, zero biases."""
+    for net in (flow.t1, flow.s1, flow.t2, flow.s2):
+        for layer in net.network:
+            if isinstance(layer, nn.Linear):
+                nn.init.normal_(layer.weight, std=var)
+                layer.bias.data.fill_(0)
+
+
+# ------------------------------------------------------------------------------------------
+# PyTorch restatement of the coupling math, used ONLY to differentiate in backward
+# (nfdpf.autograd); the forward values come from the HIP kernel.
+# ------------------------------------------------------------------------------------------
+def torch_coupling(flow, x, obser, inverse):
+    half = x.shape[1] // 2
+    lo, up = x[:, :half], x[:, half:]
+    cat = (lambda a: torch.cat([a, obser], dim=-1)) if obser is not None else (lambda a: a)
+    if not inverse:
+        s1_in = cat(lo)
+        t1, s1 = flow.t1(s1_in), flow.s1(s1_in)
+        up = t1 + up * torch.exp(s1)
+        s2_in = cat(up)
+        t2, s2 = flow.t2(s2_in), flow.s2(s2_in)
+        lo = t2 + lo * torch.exp(s2)
+        return torch.cat([lo, up], dim=1), s1.sum(1) + s2.sum(1)
+    s2_in = cat(up)
+    t2, s2 = flow.t2(s2_in), flow.s2(s2_in)
+    lo = (lo - t2) * torch.exp(-s2)
+    s1_in = cat(lo)
+    t1, s1 = flow.t1(s1_in), flow.s1(s1_in)
+    up = (up - t1) * torch.exp(-s1)
+    return torch.cat([lo, up], dim=1), (-s1).sum(1) + (-s2).sum(1)
+
+
+def torch_maf(flow, x, inverse):
+    dim = x.shape[1]
+    cols, ld = [], torch.zeros(x.shape[0], device=x.device)
+    src = x.flip(dims=(1,)) if inverse else x
+    for i in range(dim):
+        if i == 0:
+            mu, alpha = flow.initial_param[0], flow.initial_param[1]
+        else:
+            prev = torch.stack(cols, 1) if inverse else x[:, :i]
+            out = flow.layers[i - 1](prev)
+            mu, alpha = out[:, 0], out[:, 1]
+        if inverse:
+            cols.append(mu + torch.exp(alpha) * src[:, i])
+            ld = ld + alpha
+        else:
+            cols.append((src[:, i] - mu) / torch.exp(alpha))
+            ld = ld - alpha
+    z = torch.stack(cols, 1)
+    return (z, ld) if inverse else (z.flip(dims=(1,)), ld)
+
+
+class CouplingStack:
+    """Runner for a list of RealNVP(_cond) flows: one HIP launch for the whole stack."""
+
+    def __init__(self, owner, flows, dim, obser_dim, hidden, inverse, prior=None):
+        self.owner, self.flows, self.dim, self.obser_dim = owner, list(flows), dim, obser_dim
+        self.hidden, self.inverse, self.prior = hidden, inverse, prior
+
+    def hip(self, x, obser):
+        b = blob(self.owner, "stack", flows_tensors(self.flows), x.device)
+        pm, ps = self.prior if self.prior is not None else (0.0, 1.0)
+        out, ld, lp = _ops.cond_stack(b, len(self.flows), self.dim, self.obser_dim, self.hidden, x,
+                                      obser, 1, self.inverse, pm, ps, want_prior=self.prior is not None)
+        return (out, ld) if lp is None else (out, ld, lp)
+
+    def torch(self, x, obser):
+        ld = torch.zeros(x.shape[0], device=x.device)
+        seq = self.flows[::-1] if self.inverse else self.flows
+        for f in seq:
+            x, l = torch_coupling(f, x, obser if self.obser_dim else None, self.inverse)
+            ld = ld + l
+        if self.prior is None:
+            return x, ld
+        pm, ps = self.prior
+        d = x.shape[-1]
+        z = (x - pm) / ps
+        lp = -0.5 * (z * z).sum(-1) - d * math.log(ps) - 0.5 * d * math.log(2 * math.pi)
+        return x, ld, lp
+
+
+class MafStack:
+    def __init__(self, owner, flows, dim, hidden, inverse):
+        self.owner, self.flows, self.dim, self.hidden, self.inverse = owner, list(flows), dim, hidden, inverse
+
+    def hip(self, x):
+        b = blob(self.owner, "maf", flows_tensors(self.flows), x.device)
+        return _ops.maf_stack(b, len(self.flows), self.dim, self.hidden, x, self.inverse)
+
+    def torch(self, x):
+        ld = torch.zeros(x.shape[0], device=x.device)
+        for f in (self.flows[::-1] if self.inverse else self.flows):
+            x, l = torch_maf(f, x, self.inverse)
+            ld = ld + l
+        return x, ld
+
+
+def _params(mods):
+    return [p for m in mods for p in m.parameters()]
+
+
+class RealNVP(nn.Module):
+    """Non-volume preserving flow (nf/flows.py:117-179) [Dinh et al. 2017]."""
+
+    def __init__(self, dim, hidden_dim=8, base_network=FCNN):
+        super().__init__()
+        self.dim = dim
+        self.hidden_dim = hidden_dim
+        _coupling_nets(self, dim // 2, dim // 2, hidden_dim, base_network)
+
+    def zero_initialization(self, var=0.1):
+        _normal_init(self, var)
+
+    def forward(self, x):
+        r = CouplingStack(self, [self], self.dim, 0, self.hidden_dim, False)
+        return _ag.apply(r, (x, None), _params([self]))
+
+    def inverse(self, z):
+        r = CouplingStack(self, [self], self.dim, 0, self.hidden_dim, True)
+        return _ag.apply(r, (z, None), _params([self]))
+
+
+class RealNVP_cond(nn.Module):
+    """Conditional affine coupling (nf/flows.py:181-239): nets see [half, obser]."""
+
+    def __init__(self, dim, hidden_dim=8, base_network=FCNN, obser_dim=None):
+        super().__init__()
+        self.dim = dim
+        self.obser_dim = obser_dim
+        self.hidden_dim = hidden_dim
+        _coupling_nets(self, dim // 2 + obser_dim, dim // 2, hidden_dim, base_network)
+
+    def zero_initialization(self, var=0.1):
+        _normal_init(self, var)
+
+    def forward(self, x, obser):
+        r = CouplingStack(self, [self], self.dim, self.obser_dim, self.hidden_dim, False)
+        return _ag.apply(r, (x, obser), _params([self]))
+
+    def inverse(self, z, obser):
+        r = CouplingStack(self, [self], self.dim, self.obser_dim, self.hidden_dim, True)
+        return _ag.apply(r, (z, obser), _params([self]))
+
+
+class MAF(nn.Module):
+    """Masked autoregressive flow (nf/flows.py:241-284) [Papamakarios et al. 2018]."""
+
+    def __init__(self, dim, hidden_dim=8, base_network=FCNN):
+        super().__init__()
+        self.dim = dim
+        self.hidden_dim = hidden_dim
+        self.layers = nn.ModuleList([base_network(i, 2, hidden_dim) for i in range(1, dim)])
+        self.initial_param = nn.Parameter(torch.Tensor(2))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        init.uniform_(self.initial_param, -math.sqrt(0.5), math.sqrt(0.5))
+
+    def forward(self, x):
+        return _ag.apply(MafStack(self, [self], self.dim, self.hidden_dim, False), (x,), _params([self]))
+
+    def inverse(self, z):
+        return _ag.apply(MafStack(self, [self], self.dim, self.hidden_dim, True), (z,), _params([self]))

@@ -1,0 +1,113 @@
+"""ctypes binding of libnfdpf.so (C ABI: include/nfdpf.h).
+
+The library is built in-tree (``normalizing-flows-dpfs_amd/libnfdpf.so``) by
+``__graft_entry__.build()`` / ``make -C normalizing-flows-dpfs_amd/csrc``.  There is no
+fallback: if the library is missing, or no HIP device is present, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_int32, c_int64, c_uint64, c_void_p
+
+import torch  # noqa: F401  (load torch's HIP runtime first; libnfdpf binds to the same one)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("NFDPF_LIB", os.path.join(PKG_DIR, "libnfdpf.so"))
+
+NFDPF_OK, NFDPF_EINVAL, NFDPF_ELAUNCH = 0, 1, 2
+MEAS = {"cos": 0, "CRNVP": 1, "NN": 2, "gaussian": 3, "external": 4}
+MEAS_EXTERNAL = 4
+RESAMPLE = {"soft": 0, "ot": 1}
+RNG_DEVICE, RNG_HOST = 0, 1
+
+
+class FilterDesc(Structure):
+    """Mirror of ``nfdpf_filter_desc`` (include/nfdpf.h); field order must match."""
+
+    _fields_ = [
+        ("B", c_int32), ("N", c_int32), ("T", c_int32), ("E", c_int32),
+        ("B_global", c_int32), ("t", c_int32), ("phase", c_int32),
+        ("row_base", c_int64),
+        ("nf_dyn", c_int32), ("nf_cond", c_int32), ("measurement", c_int32), ("resampler", c_int32),
+        ("rng_mode", c_int32), ("force_resample", c_int32), ("n_flows", c_int32), ("hidden", c_int32),
+        ("alpha", c_float), ("pos_noise", c_float), ("dens_const", c_float), ("meas_prior_std", c_float),
+        ("seed", c_uint64),
+        ("dyn_params", c_void_p), ("cond_params", c_void_p), ("pe_params", c_void_p), ("meas_params", c_void_p),
+        ("enc", c_void_p), ("vel", c_void_p), ("lin", c_void_p), ("host_noise", c_void_p),
+        ("host_offsets", c_void_p), ("x_prev", c_void_p), ("p_prev", c_void_p),
+        ("x_prev_rs", c_int64), ("p_prev_rs", c_int64),
+        ("ess_all", c_void_p), ("gate", c_void_p), ("ot_x", c_void_p), ("lik_ext", c_void_p),
+        ("hist_x", c_void_p), ("hist_p", c_void_p), ("hist_noise", c_void_p), ("hist_lik", c_void_p),
+        ("hist_jac", c_void_p), ("hist_prior", c_void_p), ("hist_idx", c_void_p),
+        ("ess_out", c_void_p), ("lw_sum", c_void_p), ("pred", c_void_p), ("scratch", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "nfdpf_version": (c_int, []),
+    "nfdpf_last_error": (c_char_p, []),
+    "nfdpf_cond_stack": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int64,
+                                 c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_maf_stack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                                c_void_p]),
+    "nfdpf_soft_resample": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int64,
+                                    c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_ot_workspace_bytes": (c_int64, [c_int, c_int]),
+    "nfdpf_ot_resample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_int64,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_ess_gate": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_normalize_log_probs": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_measurement": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                  c_float, c_void_p, c_void_p]),
+    "nfdpf_particle_init": (c_int, [c_void_p, c_int, c_int, c_float, c_int, c_uint64, c_int64, c_void_p, c_void_p,
+                                    c_void_p]),
+    "nfdpf_filter_step": (c_int, [POINTER(FilterDesc), c_void_p]),
+}
+
+_lib = None
+
+
+class NfdpfError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libnfdpf.so and declare every C-ABI signature (no device needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NfdpfError(f"libnfdpf.so not found at {path}: build it with "
+                         f"`python -c 'import __graft_entry__ as g; g.build()'` or `make -C {PKG_DIR}/csrc`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(rc: int, what: str):
+    if rc != NFDPF_OK:
+        msg = lib().nfdpf_last_error().decode(errors="replace")
+        raise NfdpfError(f"{what} failed (rc={rc}): {msg}")
+
+
+def require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise NfdpfError(f"{what}: the nfdpf hot path runs on the HIP device only (got a {t.device} tensor)")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,304 @@
+"""Filtering driver: DPF.filtering_pos (DPFs.py:144-216) on the HIP path.
+
+Per step one ``nfdpf_filter_step`` launch (soft / no resampling), preceded by the OT
+resampler kernels when ``resampler == 'ot'``.  Histories are preallocated (B, T, N, .)
+tensors written in place (the reference grows them with torch.cat, O(T^2) copies).  The
+ESS gate never syncs the host in device-RNG mode: each step reads the previous step's
+per-row 1/sum(p^2) from device memory.  With a process group of world size > 1 the batch
+is sharded by rows; the per-row terms are all-gathered each step so every rank takes the
+same batch-global gate decision (DPFs.py:163-165), and nothing else is exchanged.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from . import ops
+from .pack import blob, flows_tensors, mlp_tensors
+
+
+@dataclass
+class FilterConfig:
+    N: int
+    NF_dyn: bool = False
+    NF_cond: bool = False
+    measurement: str = "cos"
+    resampler: str = "ot"
+    alpha: float = 0.5
+    eps: float = 0.1
+    scaling: float = 0.75
+    threshold: float = 1e-3
+    max_iter: int = 100
+    pos_noise: float = 20.0
+    vel_noise: float = 20.0
+    width: float = 128.0
+    init_with_true_state: bool = False
+    n_flows: int = 2
+    hidden: int = 8
+    meas_prior_std: float = 2.5
+    rng_mode: str = "device"     # "device" (Philox on the GPU) | "host" (reference CPU generator)
+    seed: int = 2
+    force_resample: bool = False
+
+
+@dataclass
+class ShardInfo:
+    """Batch sharding over a torch.distributed group (rows [row_base, row_base + B))."""
+    world: int = 1
+    rank: int = 0
+    B_global: int = 0
+    row_base: int = 0
+    group: Optional[object] = None
+
+    @staticmethod
+    def from_env(B_local: int, group=None) -> "ShardInfo":
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            w, r = dist.get_world_size(group), dist.get_rank(group)
+            return ShardInfo(w, r, B_local * w, B_local * r, group)
+        return ShardInfo(1, 0, B_local, 0, None)
+
+
+def density_const(pos_noise: float, d: int = 2) -> float:
+    """d*log_c - 2*log(std_pos) in float32, the op order of utils.py:30-33."""
+    log_c = -0.5 * torch.log(torch.tensor(2 * np.pi))
+    return float(d * log_c - 2 * torch.log(torch.tensor(pos_noise)))
+
+
+class HostDraws:
+    """The reference's CPU-generator draws (parity mode), optionally a recorded tape."""
+
+    def __init__(self, gen: Optional[torch.Generator] = None):
+        self.gen = gen
+
+    def init(self, start_xy, N, width, true_state):
+        B = start_xy.shape[0]
+        if true_state:
+            return start_xy[:, None, :].cpu().repeat(1, N, 1) + torch.randn(B, N, 2, generator=self.gen)
+        x = torch.tensor(width / 2.0 + width / 2.0) * torch.rand(B, N, 2, generator=self.gen) \
+            + torch.tensor(-width / 2.0)
+        torch.randn(B, N, 2, generator=self.gen)  # drawn and discarded (utils.py:58)
+        return x
+
+    def offsets(self, B, N):
+        return torch.empty(B).uniform_(0.0, 1.0 / N, generator=self.gen)
+
+    def noise(self, B, N, std):
+        return torch.normal(mean=0.0, std=std, size=(B, N, 2), generator=self.gen)
+
+
+@dataclass
+class FilterResult:
+    particles: torch.Tensor
+    probs: torch.Tensor
+    noise: torch.Tensor
+    lik: torch.Tensor
+    init_logw: torch.Tensor
+    index: torch.Tensor
+    jac: Optional[torch.Tensor]
+    prior: Optional[torch.Tensor]
+    obs_likelihood: torch.Tensor
+    pred: torch.Tensor = None          # (B,T,2) sum_n p x, the losses.py:21 prediction
+    fired: Optional[list] = None        # per-step gate (host RNG mode only)
+
+    def as_tuple(self):
+        return (self.particles, self.probs, self.noise, self.lik, self.init_logw, self.index, self.jac,
+                self.prior, self.obs_likelihood)
+
+
+class FilterEngine:
+    """Runs the T-step particle update with the fused HIP step kernel.
+
+    ``models`` provides ``nf_dyn``, ``cond_model``, ``particle_encoder`` and, per measurement,
+    ``cnf_measurement`` (CRNVP) or ``likelihood_est`` (NN) -- the DPF module's attributes.
+    """
+
+    def __init__(self, cfg: FilterConfig, models):
+        self.cfg = cfg
+        self.m = models
+        self.step_events = None  # list -> (start, end) HIP events around every step launch
+
+    # -- parameters -------------------------------------------------------------------------
+    def _blobs(self, dev):
+        c, m = self.cfg, self.m
+        dyn = blob(m, "dyn", flows_tensors(m.nf_dyn.flows), dev) if c.NF_dyn else None
+        cond = blob(m, "cond", flows_tensors(m.cond_model.flows), dev) if c.NF_cond else None
+        pe = blob(m, "pe", mlp_tensors(m.particle_encoder), dev)
+        meas = None
+        if c.measurement == "CRNVP":
+            meas = blob(m, "meas", flows_tensors(m.cnf_measurement.flows), dev)
+        elif c.measurement == "NN":
+            meas = blob(m, "meas", mlp_tensors(m.likelihood_est), dev)
+        return dyn, cond, pe, meas
+
+    # -- main loop --------------------------------------------------------------------------
+    @torch.no_grad()
+    def run(self, enc: torch.Tensor, start_state: torch.Tensor, vel_input: torch.Tensor,
+            shard: Optional[ShardInfo] = None, host: Optional[HostDraws] = None, init=None,
+            teacher=None) -> FilterResult:
+        """``teacher`` (tests only): dict with the reference's own history ``x`` (B,T,N,2) and
+        ``p`` (B,T,N); step t then starts from the reference's step t-1 state and its gate
+        is the reference's own torch expression (one-step parity)."""
+        c = self.cfg
+        dev = enc.device
+        L.require_device(enc, "FilterEngine.run")
+        if c.measurement not in ("cos", "CRNVP", "NN", "gaussian"):
+            raise L.NfdpfError(f"measurement '{c.measurement}' has no HIP kernel in this build")
+        enc = enc.float().contiguous()
+        B, T, E = enc.shape
+        N = c.N
+        shard = shard or ShardInfo(1, 0, B, 0, None)
+        host_mode = c.rng_mode == "host"
+        if host_mode and host is None:
+            host = HostDraws()
+        start_state = start_state.float()
+        vel_input = vel_input.float()
+
+        # initial particles / weights (utils.py:46-62) and p0 = normalize_log_probs (DPFs.py:153)
+        if init is not None:
+            x0, logw0 = (t.to(dev).float().contiguous() for t in init)
+        elif host_mode:
+            xg = host.init(self._global(start_state[:, :2], shard), N, c.width, c.init_with_true_state)
+            x0 = xg[shard.row_base:shard.row_base + B].to(dev).contiguous()
+            logw0 = torch.log(torch.ones([B, N], device=dev) / N)
+        else:
+            x0, logw0 = ops.particle_init(start_state[:, :2].to(dev), B, N, c.width, c.init_with_true_state,
+                                          c.seed, shard.row_base, dev)
+        p0, ie0 = ops.normalize_log_probs(logw0)
+
+        f32 = dict(device=dev, dtype=torch.float32)
+        hx = torch.empty((B, T, N, 2), **f32)
+        hp = torch.empty((B, T, N), **f32)
+        hn = torch.empty((B, T, N, 2), **f32)
+        hl = torch.empty((B, T, N), **f32)
+        hi = torch.empty((B, T, N), device=dev, dtype=torch.int64)
+        hj = torch.empty((B, T, N), **f32) if c.NF_dyn else None
+        hr = torch.empty((B, T, N), **f32) if c.NF_dyn else None
+        scratch = torch.empty((B, N, 4), **f32)
+        lw_sum = torch.empty((B, T), **f32)
+        pred = torch.empty((B, T, 2), **f32)
+        ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
+        ess_all = self._gather(ie0, shard)
+        gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
+        gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
+        # velocity used by each step's motion: start velocity, then vel_input[:, t-1] (DPFs.py:158,173)
+        vel_steps = torch.cat([start_state[:, None, 2:4].to(dev), vel_input[:, :T - 1].to(dev)], 1)
+        vel_steps = vel_steps.transpose(0, 1).contiguous()  # (T, B, 2)
+        dyn, cond, pe, meas = self._blobs(dev)
+        lin = ops.linspace_markers(N, dev) if c.resampler == "soft" else None
+
+        d = L.FilterDesc()
+        d.B, d.N, d.T, d.E = B, N, T, E
+        d.B_global, d.phase, d.row_base = shard.B_global, 0, shard.row_base
+        d.nf_dyn, d.nf_cond = int(c.NF_dyn), int(c.NF_cond)
+        d.measurement, d.resampler = L.MEAS[c.measurement], L.RESAMPLE[c.resampler]
+        d.rng_mode = L.RNG_HOST if host_mode else L.RNG_DEVICE
+        d.force_resample, d.n_flows, d.hidden = int(c.force_resample), c.n_flows, c.hidden
+        d.alpha, d.pos_noise = c.alpha, c.pos_noise
+        d.dens_const, d.meas_prior_std = density_const(c.pos_noise), c.meas_prior_std
+        d.seed = int(c.seed) & (2 ** 64 - 1)
+        d.dyn_params, d.cond_params = L.ptr(dyn), L.ptr(cond)
+        d.pe_params, d.meas_params = L.ptr(pe), L.ptr(meas)
+        d.enc, d.lin = enc.data_ptr(), L.ptr(lin)
+        d.hist_x, d.hist_p, d.hist_noise, d.hist_lik = hx.data_ptr(), hp.data_ptr(), hn.data_ptr(), hl.data_ptr()
+        d.hist_jac, d.hist_prior, d.hist_idx = L.ptr(hj), L.ptr(hr), hi.data_ptr()
+        d.lw_sum, d.pred, d.scratch = lw_sum.data_ptr(), pred.data_ptr(), scratch.data_ptr()
+
+        fired = [] if host_mode else None
+        keep = []  # host uploads must outlive their kernels
+        for t in range(T):
+            if t == 0:
+                xp, pp, xrs, prs = x0, p0, N * 2, N
+            elif teacher is not None:
+                xp = teacher["x"][:, t - 1].to(dev).float().contiguous()
+                pp = teacher["p"][:, t - 1].to(dev).float().contiguous()
+                keep += [xp, pp]
+                xrs, prs = N * 2, N
+            else:
+                xp, pp, xrs, prs = hx[:, t - 1], hp[:, t - 1], T * N * 2, T * N
+            d.t = t
+            d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = xp.data_ptr(), pp.data_ptr(), xrs, prs
+            d.vel = vel_steps[t].data_ptr()
+            d.ess_all = ess_all.data_ptr()
+            d.ess_out = ess_bufs[t & 1].data_ptr()
+            d.gate = None
+            d.host_noise = d.host_offsets = None
+            if host_mode:
+                if teacher is not None and t > 0:
+                    pc = teacher["p"][:, t - 1].cpu().float()
+                    fire = bool(c.force_resample or torch.mean(1 / torch.sum(pc ** 2, dim=-1)) < 0.5 * N)
+                else:
+                    fire = self._host_gate(ess_all, N, c.force_resample)
+                fired.append(fire)
+                gate_buf.fill_(int(fire))
+                d.gate = gate_buf.data_ptr()
+                if fire and c.resampler == "soft":
+                    off = host.offsets(shard.B_global, N)[shard.row_base:shard.row_base + B].to(dev)
+                    keep.append(off)
+                    d.host_offsets = off.data_ptr()
+                nz = host.noise(shard.B_global, N, c.pos_noise)[shard.row_base:shard.row_base + B]
+                nz = nz.to(dev).contiguous()
+                keep.append(nz)
+                d.host_noise = nz.data_ptr()
+            elif c.resampler == "ot":
+                ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
+                d.gate = gate_buf.data_ptr()
+            if c.resampler == "ot":
+                contiguous = t == 0 or teacher is not None
+                xo, _, _, _ = ops.ot_resample(xp if contiguous else hx[:, t - 1].contiguous(),
+                                              pp if contiguous else hp[:, t - 1].contiguous(),
+                                              c.eps, c.scaling, c.threshold, c.max_iter, shard.row_base,
+                                              gate=gate_buf)
+                keep.append(xo)
+                d.ot_x = xo.data_ptr()
+            if self.step_events is not None:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                ops.filter_step(d, dev)
+                ev1.record()
+                self.step_events.append((ev0, ev1))
+            else:
+                ops.filter_step(d, dev)
+            ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
+        # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
+        tot = lw_sum.double().sum(0)
+        if shard.world > 1:
+            dist.all_reduce(tot, group=shard.group)
+        obs = (tot / (shard.B_global * N)).sum().float()
+        return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, obs, pred, fired)
+
+    # -- helpers ----------------------------------------------------------------------------
+    @staticmethod
+    def _global(t: torch.Tensor, shard: ShardInfo) -> torch.Tensor:
+        """Host copy of a per-row tensor over the whole (sharded) batch."""
+        t = t.detach()
+        if shard.world == 1:
+            return t.cpu()
+        out = torch.empty((shard.B_global,) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=shard.group)
+        return out.cpu()
+
+    @staticmethod
+    def _gather(ie: torch.Tensor, shard: ShardInfo, buf=None) -> torch.Tensor:
+        if shard.world == 1:
+            return ie
+        out = buf if buf is not None else torch.empty(shard.B_global, device=ie.device, dtype=ie.dtype)
+        dist.all_gather_into_tensor(out, ie, group=shard.group)
+        return out
+
+    @staticmethod
+    def _host_gate(ess_all: torch.Tensor, N: int, force: bool) -> bool:
+        """The kernel's gate rule evaluated on the host (parity mode syncs here, as the
+        reference does at DPFs.py:165): sequential float32 mean of 1/sum(p^2) < 0.5 N."""
+        if force:
+            return True
+        v = ess_all.float().cpu().numpy()
+        s = np.float32(0.0)
+        for a in v:
+            s = np.float32(s + a)
+        return bool(np.float32(s / np.float32(len(v))) < np.float32(0.5 * N))

@@ -1,0 +1,164 @@
+"""torch-facing wrappers of the C ABI (one function per nfdpf_* entry point).
+
+Every wrapper takes device tensors, allocates its outputs with torch (the library never
+allocates), launches on torch's current HIP stream and raises on error.  No host copies,
+no synchronisation.
+"""
+from __future__ import annotations
+
+import functools
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import check, lib, ptr, require_device, stream_ptr
+
+f32 = torch.float32
+
+
+def _c(t: torch.Tensor, dtype=f32) -> torch.Tensor:
+    return t.to(dtype=dtype).contiguous()
+
+
+def cond_stack(blob, n_flows, dim, obser_dim, hidden, x, cond, cond_group=1, inverse=False,
+               prior_mean=0.0, prior_std=1.0, want_prior=False):
+    """NormalizingFlowModel_cond.forward/.inverse (nf/models.py:45-61) -> (out, logdet, prior_lp)."""
+    require_device(x, "cond_stack")
+    x = _c(x)
+    rows = x.shape[0]
+    cond = _c(cond) if cond is not None and obser_dim > 0 else None
+    out = torch.empty_like(x)
+    ld = torch.empty(rows, device=x.device, dtype=f32)
+    lp = torch.empty(rows, device=x.device, dtype=f32) if (want_prior and not inverse) else None
+    check(lib().nfdpf_cond_stack(ptr(blob), n_flows, dim, obser_dim, hidden, ptr(x), ptr(cond), rows,
+                                 max(1, int(cond_group)), int(bool(inverse)), float(prior_mean), float(prior_std),
+                                 ptr(out), ptr(ld), ptr(lp), stream_ptr(x.device)), "nfdpf_cond_stack")
+    return out, ld, lp
+
+
+def maf_stack(blob, n_flows, dim, hidden, x, inverse=False):
+    """NormalizingFlowModel over MAF flows (nf/models.py:13-30, nf/flows.py:259-284)."""
+    require_device(x, "maf_stack")
+    x = _c(x)
+    out = torch.empty_like(x)
+    ld = torch.empty(x.shape[0], device=x.device, dtype=f32)
+    check(lib().nfdpf_maf_stack(ptr(blob), n_flows, dim, hidden, ptr(x), x.shape[0], int(bool(inverse)),
+                                ptr(out), ptr(ld), stream_ptr(x.device)), "nfdpf_maf_stack")
+    return out, ld
+
+
+@functools.lru_cache(maxsize=64)
+def _lin_cpu(N: int) -> torch.Tensor:
+    # the reference's marker base, torch.linspace on CPU (resamplers.py:42); a per-N constant
+    return torch.linspace(0.0, (N - 1.0) / N, N)
+
+
+_lin_dev = {}
+
+
+def linspace_markers(N: int, device) -> torch.Tensor:
+    key = (N, str(device))
+    t = _lin_dev.get(key)
+    if t is None:
+        t = _lin_dev[key] = _lin_cpu(N).to(device)
+    return t
+
+
+def soft_resample(x, p, alpha, offsets, row_base=0):
+    """soft_resampler (resamplers.py:20-60) -> (x', w', flat idx int64)."""
+    require_device(x, "soft_resample")
+    B, N = p.shape
+    x, p = _c(x), _c(p)
+    D = x.shape[-1]
+    xo = torch.empty_like(x)
+    wo = torch.empty_like(p)
+    idx = torch.empty((B, N), device=x.device, dtype=torch.int64)
+    off = _c(offsets.to(x.device))
+    check(lib().nfdpf_soft_resample(ptr(x), ptr(p), ptr(linspace_markers(N, x.device)), ptr(off), B, N, D,
+                                    float(alpha), int(row_base), ptr(xo), ptr(wo), ptr(idx),
+                                    stream_ptr(x.device)), "nfdpf_soft_resample")
+    return xo, wo, idx
+
+
+_ws = {}
+
+
+def workspace(nbytes: int, device, tag="ot") -> torch.Tensor:
+    key = (tag, str(device))
+    t = _ws.get(key)
+    if t is None or t.numel() < nbytes:
+        t = _ws[key] = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)
+    return t
+
+
+def _aligned_ptr(t: torch.Tensor) -> int:
+    p = t.data_ptr()
+    return (p + 255) // 256 * 256
+
+
+def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_base=0, gate=None):
+    """resampler_ot (resamplers.py:62-70) -> (x', w', flat idx, iterations int32[1])."""
+    require_device(x, "ot_resample")
+    B, N, D = x.shape
+    if D != 2:
+        raise L.NfdpfError("ot_resample: the HIP Sinkhorn is built for 2-D particles (state_dim = 2)")
+    x, w = _c(x), _c(w)
+    xo = torch.empty_like(x)
+    wo = torch.empty_like(w)
+    idx = torch.empty((B, N), device=x.device, dtype=torch.int64)
+    it = torch.zeros(1, device=x.device, dtype=torch.int32)
+    nb = int(lib().nfdpf_ot_workspace_bytes(B, N))
+    ws = workspace(nb, x.device)
+    check(lib().nfdpf_ot_resample(ptr(x), ptr(w), B, N, float(eps), float(scaling), float(threshold),
+                                  int(max_iter), int(row_base), ptr(xo), ptr(wo), ptr(idx), ptr(it),
+                                  _aligned_ptr(ws), ptr(gate), stream_ptr(x.device)), "nfdpf_ot_resample")
+    return xo, wo, idx, it
+
+
+def ess_gate(inv_ess, N, force=False, out=None):
+    """DPFs.py:163-165 gate as a device int32[1] (no host sync)."""
+    B = inv_ess.shape[0]
+    g = out if out is not None else torch.empty(1, device=inv_ess.device, dtype=torch.int32)
+    check(lib().nfdpf_ess_gate(ptr(inv_ess), B, N, int(bool(force)), ptr(g), stream_ptr(inv_ess.device)),
+          "nfdpf_ess_gate")
+    return g
+
+
+def normalize_log_probs(logw, add=0.0):
+    """normalize_log_probs (utils.py:39-44) + add -> (p, 1/sum p^2)."""
+    require_device(logw, "normalize_log_probs")
+    lw = _c(logw)
+    B, N = lw.shape
+    p = torch.empty_like(lw)
+    ie = torch.empty(B, device=lw.device, dtype=f32)
+    check(lib().nfdpf_normalize_log_probs(ptr(lw), B, N, float(add), ptr(p), ptr(ie), stream_ptr(lw.device)),
+          "nfdpf_normalize_log_probs")
+    return p, ie
+
+
+def measurement(kind: str, pe_blob, meas_blob, n_flows, enc, x, prior_std=2.5):
+    """measurement models (model/models.py:206-278) -> lik [B,N]."""
+    require_device(x, "measurement")
+    enc, x = _c(enc), _c(x)
+    B, N, _ = x.shape
+    lik = torch.empty((B, N), device=x.device, dtype=f32)
+    check(lib().nfdpf_measurement(L.MEAS[kind], ptr(pe_blob), ptr(meas_blob), int(n_flows), ptr(enc), ptr(x),
+                                  B, N, enc.shape[-1], float(prior_std), ptr(lik), stream_ptr(x.device)),
+          "nfdpf_measurement")
+    return lik
+
+
+def particle_init(start_xy, B, N, width, true_state, seed, row_base=0, device=None):
+    """particle_initialization (utils.py:46-62), device RNG -> (x [B,N,2], logw [B,N])."""
+    device = device if device is not None else start_xy.device
+    x = torch.empty((B, N, 2), device=device, dtype=f32)
+    lw = torch.empty((B, N), device=device, dtype=f32)
+    s = _c(start_xy) if start_xy is not None else None
+    check(lib().nfdpf_particle_init(ptr(s), B, N, float(width), int(bool(true_state)), int(seed) & (2**64 - 1),
+                                    int(row_base), ptr(x), ptr(lw), stream_ptr(device)), "nfdpf_particle_init")
+    return x, lw
+
+
+def filter_step(desc: L.FilterDesc, device):
+    check(lib().nfdpf_filter_step(desc, stream_ptr(device)), "nfdpf_filter_step")

@@ -1,0 +1,70 @@
+"""Differentiable resamplers (resamplers/resamplers.py of the reference) on libnfdpf.
+
+* ``soft_resampler`` (resamplers.py:20-60): the HIP kernel reproduces the reference's
+  indices bit for bit (same reduction orders, exact f64 prefix, lower-bound search) without
+  the B x N x N comparison tensor; gradients (training) flow through the gathered weights
+  p/q as in the reference.
+* ``resampler_ot`` (resamplers.py:62-277): streamed Sinkhorn with the reference's
+  batch-coupled stop rule; the transport matrix is never materialised.  As in the
+  reference, the particles' gradient is T^T g with T treated as a constant (its own
+  autograd.grad result is discarded, :241-245).
+"""
+import torch
+import torch.nn as nn
+
+from nfdpf import ops as _ops
+
+device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+class resampler(nn.Module):
+    """Dispatch on ``param.resampler_type`` ('ot' | 'soft') (resamplers.py:6-17)."""
+
+    def __init__(self, param):
+        super().__init__()
+        if param.resampler_type == "ot":
+            self.kargs = {"eps": param.epsilon, "scaling": param.scaling, "threshold": param.threshold,
+                          "max_iter": param.max_iter, "device": device}
+            self.resampling = resampler_ot
+        elif param.resampler_type == "soft":
+            self.kargs = {"num_resampled": param.num_particles, "index": True, "alpha": param.alpha,
+                          "device": device}
+            self.resampling = soft_resampler
+
+    def forward(self, particles, particle_probs):
+        return self.resampling(particles, particle_probs, **self.kargs)
+
+
+def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, device="cuda", offsets=None):
+    """Soft resampling with q = alpha p + (1 - alpha)/N; the CPU-generator offset draw of
+    the reference (:43) is kept (pass ``offsets`` to supply it)."""
+    assert 0.0 < alpha <= 1.0
+    B, N = particle_probs.shape
+    if offsets is None:
+        offsets = torch.FloatTensor(B).uniform_(0.0, 1.0 / num_resampled)
+    xo, wo, idx = _ops.soft_resample(particles.detach(), particle_probs.detach(), alpha, offsets)
+    if torch.is_grad_enabled() and (particles.requires_grad or particle_probs.requires_grad):
+        # differentiable gather with the kernel's indices (resamplers.py:52-56)
+        if alpha < 1.0:
+            uni = torch.ones((B, N), device=particle_probs.device) / N
+            q = torch.stack((particle_probs * alpha, uni * (1.0 - alpha)), dim=-1).sum(dim=-1)
+            q = q / q.sum(dim=-1, keepdim=True)
+            w = particle_probs / q
+        else:
+            w = torch.ones_like(particle_probs) / N
+        xo = particles.reshape(B * N, -1)[idx, :]
+        wo = w.reshape(B * N)[idx]
+        wo = wo / wo.sum(dim=-1, keepdim=True)
+    return (xo, wo, idx) if index else (xo, wo)
+
+
+def resampler_ot(particles, weights, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, device="cuda",
+                 flag=None):
+    """OT resampling -> (x', uniform weights, identity flat index) (resamplers.py:62-70)."""
+    xo, wo, idx, _ = _ops.ot_resample(particles.detach(), weights.detach(), eps, scaling, threshold, max_iter)
+    return xo, wo, idx
+
+
+def ot_resample_with_info(particles, weights, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100):
+    """As resampler_ot, also returning the reference's Sinkhorn iteration count (:179)."""
+    return _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter)

@@ -1,0 +1,295 @@
+"""Parity of the HIP path (through the C ABI) against the reference's golden vectors and
+the CPU oracle.  GPU box only.
+
+Tolerances: indices bit-exact; log-dets / weights |d| <= 1e-5 |ref| + atol
+with atol 1e-6 (D = 2) and 5e-6 (D = 32 with std-0.3 weights) -- pure relative error is
+meaningless on near-zero log-dets (the reference's own fp32-vs-fp64 gap is ~1e-2 relative
+there).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _util import assert_close, e2e_cfg, group, load, t, TapeRNG, weights
+from oracle import dpf_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _flow_blob(w, n_flows):
+    from nfdpf.pack import fcnn_tensors  # noqa
+    parts = []
+    for i in range(n_flows):
+        pre = "" if n_flows == 1 else f"flows.{i}."
+        for net in ("t1", "s1", "t2", "s2"):
+            for layer in (0, 2, 4):
+                parts += [w[f"{pre}{net}.network.{layer}.weight"], w[f"{pre}{net}.network.{layer}.bias"]]
+    return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
+
+
+def _maf_blob(w, n_flows, D):
+    parts = []
+    for i in range(n_flows):
+        parts.append(w[f"flows.{i}.initial_param"])
+        for j in range(D - 1):
+            for layer in (0, 2, 4):
+                parts += [w[f"flows.{i}.layers.{j}.network.{layer}.weight"],
+                          w[f"flows.{i}.layers.{j}.network.{layer}.bias"]]
+    return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
+
+
+def _mlp_blob(w, prefix):
+    parts = []
+    for layer in (0, 2, 4):
+        parts += [w[f"{prefix}.{layer}.weight"], w[f"{prefix}.{layer}.bias"]]
+    return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from nfdpf import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+
+
+@pytest.mark.parametrize("D,O_", [(2, 4), (2, 36), (2, 196), (32, 32)])
+@pytest.mark.parametrize("tag", ["init", "wide"])
+def test_realnvp_cond_golden(D, O_, tag):
+    from nfdpf import ops
+    fx = group(load("flows.npz"), f"D{D}_O{O_}_{tag}")
+    w = weights(fx)
+    b = _flow_blob(w, 1)
+    atol = 5e-6 if D == 32 else 1e-6
+    x, c = t(fx["x"]).to(DEV), t(fx["c"]).to(DEV)
+    z, ld, _ = ops.cond_stack(b, 1, D, O_, 8, x, c, 1, False)
+    assert_close(ld.cpu(), fx["ld_fwd"], 1e-5, atol, "logdet fwd")
+    assert_close(z.cpu(), fx["z"], 1e-5, 1e-5, "z")
+    xi, ldi, _ = ops.cond_stack(b, 1, D, O_, 8, x, c, 1, True)
+    assert_close(ldi.cpu(), fx["ld_inv"], 1e-5, atol, "logdet inv")
+    assert_close(xi.cpu(), fx["xinv"], 1e-5, 1e-5, "x inv")
+
+
+@pytest.mark.parametrize("case,D,O_", [("cond_D2_O4", 2, 4), ("cond_D2_O36", 2, 36), ("cond_D32_O32", 32, 32)])
+def test_cond_stack_golden(case, D, O_):
+    from nfdpf import ops
+    fx = group(load("stacks.npz"), case)
+    w = weights(fx)
+    b = _flow_blob(w, 2)
+    x, c = t(fx["x"]).to(DEV), t(fx["c"]).to(DEV)
+    atol = 5e-6 if D == 32 else 1e-6
+    z, ld, lp = ops.cond_stack(b, 2, D, O_, 8, x, c, 1, False, 0.0, float(fx["prior_std"]), want_prior=True)
+    assert_close(ld.cpu(), fx["ld_fwd"], 1e-5, atol, "logdet")
+    assert_close(z.cpu(), fx["z"], 1e-5, 1e-5, "z")
+    assert_close(lp.cpu(), fx["lp"], 1e-5, 1e-5, "prior log-prob")
+    xi, ldi, _ = ops.cond_stack(b, 2, D, O_, 8, x, c, 1, True)
+    assert_close(ldi.cpu(), fx["ld_inv"], 1e-5, atol, "logdet inv")
+    assert_close(xi.cpu(), fx["xinv"], 1e-5, 1e-5, "x inv")
+
+
+def test_cond_stack_broadcast_context_matches_per_row():
+    """cond_group = N (per-batch context, never materialised) == the per-row expansion."""
+    from nfdpf import ops
+    fx = group(load("stacks.npz"), "cond_D2_O36")
+    b = _flow_blob(weights(fx), 2)
+    B, N = 6, 333
+    x = torch.randn(B * N, 2, device=DEV) * 10
+    c = torch.randn(B, 36, device=DEV)
+    z1, l1, _ = ops.cond_stack(b, 2, 2, 36, 8, x, c, N, True)
+    z2, l2, _ = ops.cond_stack(b, 2, 2, 36, 8, x, c.repeat_interleave(N, 0), 1, True)
+    assert torch.equal(z1, z2) and torch.equal(l1, l2)
+
+
+@pytest.mark.parametrize("D", [2, 4])
+def test_maf_golden(D):
+    from nfdpf import ops
+    fx = group(load("stacks.npz"), f"maf_D{D}")
+    b = _maf_blob(weights(fx), 2, D)
+    x = t(fx["x"]).to(DEV)
+    z, ld = ops.maf_stack(b, 2, D, 8, x, False)
+    assert_close(z.cpu(), fx["z"], 1e-5, 1e-5, "z")
+    assert_close(ld.cpu(), fx["ld_fwd"], 1e-5, 1e-6, "logdet")
+    xi, ldi = ops.maf_stack(b, 2, D, 8, x, True)
+    assert_close(xi.cpu(), fx["xinv"], 1e-5, 1e-5, "x inv")
+    assert_close(ldi.cpu(), fx["ld_inv"], 1e-5, 1e-6, "logdet inv")
+
+
+def test_soft_resampler_bit_exact_golden():
+    from nfdpf import ops
+    fx = load("soft.npz")
+    for i in range(int(fx["n_cases"])):
+        c = group(fx, f"c{i}")
+        x, p = t(c["x"]), t(c["p"])
+        xo, wo, idx = ops.soft_resample(x.to(DEV), p.to(DEV), float(c["alpha"]), t(c["offsets"]).to(DEV))
+        np.testing.assert_array_equal(idx.cpu().numpy(), c["idx"].astype(np.int64), err_msg=f"case {i}")
+        np.testing.assert_array_equal(wo.cpu().numpy(), c["w"], err_msg=f"case {i} weights")
+        B, N = p.shape
+        np.testing.assert_array_equal(xo.cpu().numpy(), x.reshape(B * N, 2)[idx.cpu()].numpy())
+
+
+def test_soft_resampler_bit_exact_random_vs_oracle():
+    """Larger random sweep (incl. N = 10000) against the oracle's dense O(N^2) matching."""
+    from nfdpf import ops
+    g = torch.Generator().manual_seed(5)
+    for B, N, scale in ((64, 1000, 3.0), (4, 10000, 5.0), (16, 100, 30.0), (8, 4000, 1.0)):
+        p = torch.softmax(torch.randn(B, N, generator=g) * scale, -1) + 1e-12
+        x = torch.randn(B, N, 2, generator=g)
+        off = torch.empty(B).uniform_(0, 1.0 / N, generator=g)
+        _, wo, idx = ops.soft_resample(x.to(DEV), p.to(DEV), 0.5, off.to(DEV))
+        _, wr, idr = O.soft_resample(x, p, 0.5, off)
+        assert torch.equal(idx.cpu(), idr.long()), (B, N)
+        assert torch.equal(wo.cpu(), wr), (B, N)
+
+
+def test_ot_resampler_golden():
+    from nfdpf import ops
+    fx = load("ot.npz")
+    for i in range(int(fx["n_cases"])):
+        c = group(fx, f"c{i}")
+        xo, wo, idx, it = ops.ot_resample(t(c["x"]).to(DEV), t(c["p"]).to(DEV))
+        assert int(it.item()) == int(c["iters"]), f"case {i}: iterations {int(it.item())} vs {int(c['iters'])}"
+        # fp32 Sinkhorn vs the reference's fp64: positions ~1e2, agree to ~1e-3 absolute
+        assert_close(xo.cpu(), c["xr"], 1e-4, 2e-3, f"OT x' case {i}")
+        np.testing.assert_array_equal(wo.cpu().numpy(), c["wr"])
+        B, N = c["p"].shape
+        np.testing.assert_array_equal(idx.cpu().numpy(), np.arange(B * N).reshape(B, N))
+
+
+@pytest.mark.parametrize("meas", ["cos", "CRNVP", "NN", "gaussian"])
+def test_measurement_golden(meas):
+    from nfdpf import ops
+    fx = group(load("meas.npz"), meas)
+    w = weights(fx)
+    pe = _mlp_blob(w, "particle_encoder")
+    mb = None
+    if meas == "CRNVP":
+        mb = _flow_blob({k[len("cnf_measurement."):]: v for k, v in w.items() if k.startswith("cnf_measurement.")}, 2)
+    elif meas == "NN":
+        mb = _mlp_blob(w, "likelihood_est")
+    lik = ops.measurement(meas, pe, mb, 2, t(fx["enc"]).to(DEV), t(fx["x"]).to(DEV), 2.5)
+    assert_close(lik.cpu(), fx["lik"], 1e-5, 2e-5, meas)
+
+
+class _Models(torch.nn.Module):
+    """Minimal holder with the DPF attribute names the engine reads."""
+
+    def __init__(self, w, cfg):
+        super().__init__()
+        from model.models import build_conditional_nf, build_likelihood, build_particle_encoder
+        self.nf_dyn = build_conditional_nf(2, 4, 2)
+        self.cond_model = build_conditional_nf(2, 36, 2)
+        self.particle_encoder = build_particle_encoder(32, 2)
+        if cfg["measurement"] == "CRNVP":
+            self.cnf_measurement = build_conditional_nf(2, 32, 32, prior_std=2.5)
+        if cfg["measurement"] == "NN":
+            self.likelihood_est = build_likelihood(32, 2)
+        sd = self.state_dict()
+        sd.update({k: v for k, v in w.items() if k in sd})
+        self.load_state_dict(sd)
+        self.to(DEV)
+
+
+def _engine(fx):
+    from nfdpf.engine import FilterConfig, FilterEngine
+    c = e2e_cfg(fx)
+    cfg = FilterConfig(N=c["N"], NF_dyn=c["NF_dyn"], NF_cond=c["NF_cond"], measurement=c["measurement"],
+                       resampler=c["resampler"], rng_mode="host")
+    return FilterEngine(cfg, _Models(weights(fx), c)), c
+
+
+class _TapeDraws:
+    def __init__(self, fx):
+        self.tape = TapeRNG(fx)
+
+    def offsets(self, B, N):
+        return self.tape.offsets(B, N)
+
+    def noise(self, B, N, std):
+        return self.tape.noise(B, N, std)
+
+
+E2E_FUSED = ["c1", "c2", "c2w", "c3", "c3n"]
+
+
+@pytest.mark.parametrize("name", E2E_FUSED)
+def test_filter_step_one_step_parity(name):
+    """Each fused step started from the reference's own previous state (teacher forcing)."""
+    fx = load(f"e2e_{name}.npz")
+    eng, c = _engine(fx)
+    res = eng.run(t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV),
+                  host=_TapeDraws(fx), init=(t(fx["init_x"]), t(fx["logw0"])),
+                  teacher={"x": t(fx["x"]), "p": t(fx["p"])})
+    assert res.fired == [bool(f) for f in fx["fired"]]
+    np.testing.assert_array_equal(res.index.cpu().numpy(), fx["idx"].astype(np.int64))
+    np.testing.assert_array_equal(res.noise.cpu().numpy(), fx["noise"])
+    assert_close(res.particles.cpu(), fx["x"], 1e-5, 1e-4, "particles")
+    assert_close(res.probs.cpu(), fx["p"], 1e-5, 1e-9, "weights")
+    assert_close(res.lik.cpu(), fx["lik"], 1e-5, 2e-5, "likelihood")
+    if c["NF_dyn"]:
+        assert_close(res.jac.cpu(), fx["jac"], 1e-5, 1e-6, "jac")
+        assert_close(res.prior.cpu(), fx["prior"], 1e-5, 1e-5, "prior")
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+def test_filtering_free_running(name):
+    """Whole sequences from the reference's initial state and draws."""
+    fx = load(f"e2e_{name}.npz")
+    eng, c = _engine(fx)
+    res = eng.run(t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV),
+                  host=_TapeDraws(fx), init=(t(fx["init_x"]), t(fx["logw0"])))
+    assert res.fired == [bool(f) for f in fx["fired"]]
+    np.testing.assert_array_equal(res.index.cpu().numpy(), fx["idx"].astype(np.int64))
+    assert_close(res.particles.cpu(), fx["x"], 1e-4, 1e-3, "particles")
+    assert_close(res.probs.cpu(), fx["p"], 1e-4, 1e-7, "weights")
+    assert abs(float(res.obs_likelihood) - float(fx["obs_lik"])) <= 1e-4 * abs(float(fx["obs_lik"])) + 1e-3
+    rm, _ = O.rmse(res.particles.cpu(), res.probs.cpu(), t(fx["state"]))
+    assert abs(float(rm) - float(fx["rmse"])) <= 1e-4 * float(fx["rmse"])
+    pred = res.pred.cpu()
+    _, pr = O.rmse(res.particles.cpu(), res.probs.cpu(), t(fx["state"]))
+    assert_close(pred, pr, 1e-5, 1e-3, "fused prediction")
+
+
+def test_device_rng_shard_invariance():
+    """Device RNG is keyed on the GLOBAL row: rows [4,8) of a B=8 run equal a B=4 run with
+    row_base = 4 (what each rank computes under batch sharding) when the gate is global."""
+    from nfdpf.engine import FilterConfig, FilterEngine, ShardInfo
+    fx = load("e2e_c2.npz")
+    c = e2e_cfg(fx)
+    models = _Models(weights(fx), c)
+    N, T = 256, 6
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", force_resample=True,
+                       seed=1234)
+    g = torch.Generator().manual_seed(3)
+    enc = torch.randn(8, T, 32, generator=g).to(DEV)
+    start = (torch.randn(8, 4, generator=g) * 10).to(DEV)
+    vel = (torch.randn(8, T, 2, generator=g) * 3).to(DEV)
+    full = FilterEngine(cfg, models).run(enc, start, vel)
+    half = FilterEngine(cfg, models).run(enc[4:], start[4:], vel[4:], shard=ShardInfo(1, 0, 4, 4, None))
+    assert torch.equal(full.particles[4:], half.particles)
+    assert torch.equal(full.probs[4:], half.probs)
+    assert torch.equal(full.index[4:], half.index)
+
+
+@pytest.mark.parametrize("meas,res,nfd,nfc", [("cos", "soft", True, True), ("CRNVP", "ot", False, False),
+                                              ("NN", "soft", True, False), ("gaussian", "soft", False, True)])
+def test_device_rng_sanity(meas, res, nfd, nfc):
+    """Device-RNG runs of each fused variant: finite, normalised, valid indices, repeatable."""
+    from nfdpf.engine import FilterConfig, FilterEngine
+    from model.models import build_likelihood
+    fx = load("e2e_c3.npz" if meas == "CRNVP" else "e2e_c2.npz")
+    c = dict(e2e_cfg(fx), measurement=meas)
+    models = _Models(weights(fx), c)
+    B, N, T = 8, 300, 5
+    cfg = FilterConfig(N=N, NF_dyn=nfd, NF_cond=nfc, measurement=meas, resampler=res, force_resample=True, seed=9)
+    g = torch.Generator().manual_seed(4)
+    enc = torch.randn(B, T, 32, generator=g).to(DEV)
+    start = (torch.randn(B, 4, generator=g) * 10).to(DEV)
+    vel = (torch.randn(B, T, 2, generator=g) * 3).to(DEV)
+    a = FilterEngine(cfg, models).run(enc, start, vel)
+    b = FilterEngine(cfg, models).run(enc, start, vel)
+    assert torch.equal(a.particles, b.particles) and torch.equal(a.probs, b.probs)
+    assert torch.isfinite(a.particles).all() and torch.isfinite(a.probs).all()
+    s = a.probs.sum(-1)
+    assert torch.allclose(s, torch.ones_like(s) + N * 1e-12, atol=1e-5)
+    rows = torch.arange(B, device=DEV)[:, None, None] * N
+    assert ((a.index >= rows) & (a.index < rows + N)).all()
