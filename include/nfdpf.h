@@ -150,7 +150,8 @@ typedef struct nfdpf_filter_desc {
   const float *vel;         /* [B,2] velocity used by this step's motion */
   const float *lin;         /* [N] soft-resampler markers base (host torch.linspace) */
   const float *host_noise;  /* [B,N,2] parity-mode noise of this step (rng_mode HOST) */
-  const float *host_offsets;/* [B] parity-mode offsets (rng_mode HOST, soft) */
+  const float *host_offsets;/* [B] parity-mode offsets (rng_mode HOST, soft; read only when the
+                               host-decided gate fires -- NULL there falls back to Philox) */
   const float *x_prev;      /* particles after the previous step, rows of x_prev_rs */
   const float *p_prev;      /* probabilities after the previous step, rows of p_prev_rs */
   int64_t x_prev_rs, p_prev_rs;

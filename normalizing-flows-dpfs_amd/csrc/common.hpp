@@ -80,18 +80,12 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float &z0, fl
 // ----------------------------------------------------------------------------------------
 // activations
 // ----------------------------------------------------------------------------------------
-// tanh: |x| < 0.625 -> odd minimax polynomial (Cephes tanhf coefficients, rel. err ~1e-7),
-// otherwise 1 - 2/(exp(2x)+1).  Both are evaluated and selected (no divergence).
+// tanh(x) = 1 - 2 / (1 + e^{2x}): one v_exp_f32 + one v_rcp_f32 + 2 VALU.  Absolute error
+// ~1e-7 over the whole range (relative accuracy near 0 is not needed: every tanh feeds a
+// Linear layer, so absolute error is what propagates into t, s and the log-det).
 __device__ __forceinline__ float tanh_fast(float x) {
-  const float z = x * x;
-  float p = fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f);
-  p = fmaf(p, z, -5.37397155531e-2f);
-  p = fmaf(p, z, 1.33314422036e-1f);
-  p = fmaf(p, z, -3.33332819422e-1f);
-  const float small = fmaf(p * z, x, x);
-  const float e = __expf(2.0f * x);
-  const float big = 1.0f - __fdividef(2.0f, e + 1.0f);
-  return fabsf(x) < 0.625f ? small : big;
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // 2^(2x log2 e)
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
 
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.0f); }

@@ -20,6 +20,10 @@
 
 namespace nfdpf {
 
+struct Ctx4 {
+  float m0, m1, s0, s1;  // per-row [mean, std] context (model/models.py:309-315)
+};
+
 template <int BLK, bool NFD, bool NFC, int MEAS>
 __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_desc d) {
   extern __shared__ float Cbuf[];
@@ -63,7 +67,7 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
     float S2 = 1.f;
     if (soft) {
       float off;
-      if (d.rng_mode == NFDPF_RNG_HOST)
+      if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
         off = d.host_offsets[b];
       else
         off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, grow, 0u).x) * (1.0f / (float)N);
@@ -139,19 +143,18 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
       q1 += (double)p1 * p1;
     }
     // context [mean, std(unbiased)] (model/models.py:309-315); reductions in f64
-    auto row_ctx = [&](double a0, double a1, double b0, double b1, float *c) {
+    auto row_ctx = [&](double a0, double a1, double b0, double b1) {
       a0 = block_sum(a0, L.d);
       a1 = block_sum(a1, L.d);
       b0 = block_sum(b0, L.d);
       b1 = block_sum(b1, L.d);
       const double m0 = a0 / N, m1 = a1 / N;
-      c[0] = (float)m0;
-      c[1] = (float)m1;
-      c[2] = (float)sqrt((b0 - a0 * m0) / (N - 1));
-      c[3] = (float)sqrt((b1 - a1 * m1) / (N - 1));
+      return Ctx4{(float)m0, (float)m1, (float)sqrt((b0 - a0 * m0) / (N - 1)),
+                  (float)sqrt((b1 - a1 * m1) / (N - 1))};
     };
-    float cdyn[4] = {0.f, 0.f, 0.f, 0.f};
-    if (NFD || NFC) row_ctx(s0, s1, q0, q1, cdyn);
+    Ctx4 c4{0.f, 0.f, 0.f, 0.f};
+    if (NFD || NFC) c4 = row_ctx(s0, s1, q0, q1);
+    const float cdyn[4] = {c4.m0, c4.m1, c4.s0, c4.s1};
 
     // ---------------- nf_dyn inverse (model/models.py:305-332)
     constexpr int inD = 1 + 4;
@@ -183,11 +186,8 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
     const int inC = 1 + d.E + 4;
     const int nsC = fcnn_size<kH>(inC, 1);
     if (NFC) {
-      float cprop[4];
-      if (NFD)
-        row_ctx(s0, s1, q0, q1, cprop);
-      else
-        for (int k = 0; k < 4; ++k) cprop[k] = cdyn[k];
+      const Ctx4 cp = NFD ? row_ctx(s0, s1, q0, q1) : c4;
+      const float cprop[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
       if (tid < d.E) L.ctx[tid] = enc[tid];
       if (tid == 0) {
         L.ctx[d.E] = cprop[0];
@@ -360,8 +360,10 @@ extern "C" int nfdpf_filter_step(const nfdpf_filter_desc *dp, void *stream) {
   if (d.resampler == NFDPF_RESAMPLE_SOFT) {
     NFDPF_REQUIRE(d.N <= kStepMaxN, "nfdpf_filter_step: soft resampling supports N <= %d",
                   kStepMaxN);
-    NFDPF_REQUIRE(d.lin && (d.rng_mode == NFDPF_RNG_DEVICE || d.host_offsets || d.phase == 2),
-                  "nfdpf_filter_step: soft resampling needs lin (and host_offsets in HOST mode)");
+    NFDPF_REQUIRE(d.lin || d.phase == 2, "nfdpf_filter_step: soft resampling needs lin");
+    NFDPF_REQUIRE(d.rng_mode == NFDPF_RNG_DEVICE || d.gate || d.phase == 2,
+                  "nfdpf_filter_step: HOST rng mode needs the host-decided gate (host_offsets are "
+                  "read only when it fires)");
   } else {
     NFDPF_REQUIRE(d.ot_x || d.phase == 2, "nfdpf_filter_step: OT path needs ot_x");
   }

@@ -35,6 +35,38 @@ import torch.nn.functional as F
 Params = Dict[str, torch.Tensor]
 NETS = ("t1", "s1", "t2", "s2")
 
+# Working precision.  float32 = the reference's own arithmetic.  float64 (via ``precision``)
+# evaluates the same algorithm in double: the GPU tests use |ref64 - ref32| as the
+# reference's own rounding envelope where the computation is ill-conditioned (e.g. the
+# cosine likelihood -log(1 - <a,b>) near alignment).
+_DT = torch.float32
+
+
+def _f(x: torch.Tensor) -> torch.Tensor:
+    return x.to(_DT)
+
+
+class precision:
+    """``with precision(torch.float64): ...`` -- run the oracle in double."""
+
+    def __init__(self, dt):
+        self.dt = dt
+
+    def __enter__(self):
+        global _DT
+        self.prev, self.prev_default = _DT, torch.get_default_dtype()
+        _DT = self.dt
+        torch.set_default_dtype(self.dt)
+
+    def __exit__(self, *exc):
+        global _DT
+        _DT = self.prev
+        torch.set_default_dtype(self.prev_default)
+
+
+def cast_params(params: Params, dt) -> Params:
+    return {k: (v.to(dt) if v.is_floating_point() else v) for k, v in params.items()}
+
 
 def sub(params: Params, prefix: str) -> Params:
     """Slice a state-dict-like mapping down to ``prefix.*`` (prefix stripped)."""
@@ -47,7 +79,7 @@ def sub(params: Params, prefix: str) -> Params:
 # ----------------------------------------------------------------------------
 def fcnn(params: Params, x: torch.Tensor) -> torch.Tensor:
     """FCNN: Linear-Tanh-Linear-Tanh-Linear on ``x.float()`` (nf/flows.py:101-114)."""
-    h = torch.tanh(F.linear(x.float(), params["network.0.weight"], params["network.0.bias"]))
+    h = torch.tanh(F.linear(_f(x), params["network.0.weight"], params["network.0.bias"]))
     h = torch.tanh(F.linear(h, params["network.2.weight"], params["network.2.bias"]))
     return F.linear(h, params["network.4.weight"], params["network.4.bias"])
 
@@ -141,7 +173,7 @@ def mvn_isotropic_logprob(z: torch.Tensor, mean: float, std: float) -> torch.Ten
     torch ``MultivariateNormal(mean*1, std^2 I)`` evaluated on ``z.float()`` (nf/models.py:51)."""
     d = z.shape[-1]
     mvn = torch.distributions.MultivariateNormal(torch.zeros(d) + mean, torch.eye(d) * std ** 2)
-    return mvn.log_prob(z.float())
+    return mvn.log_prob(_f(z))
 
 
 def cond_stack_forward(params: Params, n_flows: int, x, obser, prior_mean=0.0, prior_std=1.0):
@@ -261,7 +293,7 @@ def nf_propose(params: Params, n_flows, x, enc):
 
 def particle_encode(params: Params, x):
     """build_particle_encoder MLP: Linear-ReLU-Linear-ReLU-Linear (model/models.py:130-150)."""
-    h = F.relu(F.linear(x.float(), params["0.weight"], params["0.bias"]))
+    h = F.relu(F.linear(_f(x), params["0.weight"], params["0.bias"]))
     h = F.relu(F.linear(h, params["2.weight"], params["2.bias"]))
     return F.linear(h, params["4.weight"], params["4.bias"])
 
@@ -497,8 +529,8 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, retur
     tmp = (f[:, :, None] + g[:, None, :] - C) / eps_t
     tmp = tmp - torch.logsumexp(tmp, dim=1, keepdim=True) + log_n
     T = torch.exp(tmp + logw[:, None, :])
-    xr = torch.matmul(T.float(), x.float())                           # apply_transport_matrix (:254-264)
-    wr = torch.ones_like(w) / torch.tensor(N).float()
+    xr = torch.matmul(_f(T), _f(x))                           # apply_transport_matrix (:254-264)
+    wr = torch.ones_like(w) / _f(torch.tensor(N))
     idx = (torch.arange(N) + N * torch.arange(B)[:, None].repeat((1, N))).long()
     if return_info:
         return xr, wr, idx, {"iters": it + 2, "a_y": f, "b_x": g}
@@ -549,7 +581,7 @@ def filter_step(cfg: dict, params: Params, meas: Callable, x, p, vel, enc_t, rng
         xr, lr = x, p.log()
     x_phys, noise = motion(xr, vel, cfg["pos_noise"], rng.noise(B, N, cfg["pos_noise"]))
     x_dyn, jac = dyn_flow(dyn_p, nfl, x_phys, cfg["NF_dyn"])
-    xp, lik, prior, prop = proposal_likelihood(dyn_p, cond_p, nfl, meas, x_dyn, x_phys, enc_t.float(),
+    xp, lik, prior, prop = proposal_likelihood(dyn_p, cond_p, nfl, meas, x_dyn, x_phys, _f(enc_t),
                                                noise, jac, cfg["NF_dyn"], cfg["NF_cond"],
                                                cfg["pos_noise"], cfg["vel_noise"])
     lw = lr + lik + prior - prop

