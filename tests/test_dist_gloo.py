@@ -1,0 +1,83 @@
+"""world_size-2 rehearsal (gloo, CPU) of the batch-sharded exchange logic of nfdpf.engine:
+shard geometry, the per-step all-gather of per-row ESS terms feeding an identical gate on
+every rank, host-draw slicing in parity mode and the end-of-sequence obs-likelihood reduce.
+The RCCL/GPU path uses the same code with device tensors."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf.engine import FilterEngine, HostDraws, ShardInfo
+        B, N = 3, 50
+        sh = ShardInfo.from_env(B)
+        g = torch.Generator().manual_seed(7)
+        inv_all = torch.rand(world * B, generator=g) * N
+        mine = inv_all[sh.row_base:sh.row_base + B].contiguous()
+        gathered = FilterEngine._gather(mine, sh)
+        gate = FilterEngine._host_gate(gathered, N, False)
+        # parity-mode draws: every rank draws the GLOBAL tensor and keeps its rows
+        h = HostDraws(torch.Generator().manual_seed(11))
+        nz = h.noise(sh.B_global, N, 20.0)[sh.row_base:sh.row_base + B]
+        lw = torch.full((B, 4), float(rank + 1))
+        tot = lw.double().sum(0)
+        dist.all_reduce(tot)
+        q.put((rank, sh.world, sh.B_global, sh.row_base, gathered.numpy(), gate, nz.numpy(), tot.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_exchange_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    from nfdpf.engine import FilterEngine, HostDraws
+    B, N = 3, 50
+    inv_all = torch.rand(world * B, generator=torch.Generator().manual_seed(7)) * N
+    ref_gate = FilterEngine._host_gate(inv_all, N, False)
+    ref_noise = HostDraws(torch.Generator().manual_seed(11)).noise(world * B, N, 20.0)
+    for rank, w, bg, base, gathered, gate, nz, tot in res:
+        assert (w, bg, base) == (world, world * B, rank * B)
+        np.testing.assert_array_equal(gathered, inv_all.numpy())
+        assert gate == ref_gate
+        np.testing.assert_array_equal(nz, ref_noise[rank * B:(rank + 1) * B].numpy())
+        np.testing.assert_array_equal(tot, np.full(4, 3.0 * (1 + 2)))
+
+
+def test_single_process_shard_is_identity():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    from nfdpf.engine import ShardInfo
+    sh = ShardInfo.from_env(5)
+    assert (sh.world, sh.B_global, sh.row_base) == (1, 5, 0)

@@ -245,11 +245,13 @@ def _oracle64_one_step(fx, monkeypatch):
     return {k: torch.stack(v, 1).numpy() for k, v in out.items()}
 
 
-def _check_envelope(ours, ref32, ref64, rtol, atol, what, k=4.0):
-    """|ours - ref32| <= k |ref64 - ref32| + rtol |ref32| + atol; also report how many
-    elements already meet the plain rtol/atol bound."""
+def _check_envelope(ours, ref32, ref64, rtol, atol, what, k=2.0):
+    """|ours - ref32| <= k * E + rtol |ref32| + atol, where E is the reference's own float32
+    rounding noise on the same (batch row, step): max_n |ref64 - ref32| over the N particles
+    (all particles of a row share the row's normalisation and context)."""
     ours, ref32, ref64 = (np.asarray(a, dtype=np.float64) for a in (ours, ref32, ref64))
     env = np.abs(ref64 - ref32)
+    env = env.max(axis=2, keepdims=True) if env.ndim >= 3 else env
     err = np.abs(ours - ref32)
     bound = k * env + rtol * np.abs(ref32) + atol
     assert np.all(err <= bound), f"{what}: worst excess {(err - bound).max():.3e} (env {env.max():.3e})"
