@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--force-resample", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", default="tiled", choices=["tiled", "fused"],
+                    help="tiled: multi-CU pipeline per step; fused: one workgroup per batch row")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,7 +135,9 @@ def main():
     sl = slice(rank * B, (rank + 1) * B)
     start, state, vel_in, enc = (t[sl].to(dev) for t in (start, state, vel_in, enc))
     shard = ShardInfo.from_env(B)
-    eng = FilterEngine(dpf.filter_config(), dpf)
+    fcfg = dpf.filter_config()
+    fcfg.kernel = args.kernel
+    eng = FilterEngine(fcfg, dpf)
 
     def step():
         return eng.run(enc, start, vel_in, shard=shard)

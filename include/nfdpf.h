@@ -170,6 +170,23 @@ typedef struct nfdpf_filter_desc {
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
 
+/* The same step as a pipeline of launches over (particle tile of 256, batch row) workgroups
+ * (soft-resample -> motion -> dyn inverse -> proposal+measurement -> normalise), so a small
+ * batch fills every CU.  In this mode ess_all / ess_out hold per-(row, tile) sums of p^2
+ * as doubles ([B_global][tiles] / [B][tiles]; nfdpf_filter_tiled_tiles(N) tiles per row),
+ * and pred / lw_sum are written after the last step (t == T-1) for all steps at once.
+ * workspace: nfdpf_filter_tiled_workspace_bytes(B, N, T) bytes, 256-B aligned, shared by
+ * the T steps of one sequence.                                                        */
+NFDPF_API int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T);
+NFDPF_API int nfdpf_filter_tiled_tiles(int N);
+/* per-tile sums of p0^2 -> ess_parts [B][tiles] (the t = 0 gate input) */
+NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
+                            void *stream);
+NFDPF_API int nfdpf_filter_step_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);
+/* the ESS gate (DPFs.py:163-165) from per-(row, tile) sums of p^2 -> int32 [1] (OT path) */
+NFDPF_API int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int force, int32_t *gate,
+                         void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,14 +15,59 @@
 // Between stages a particle's intermediates are parked in its own history slot (written
 // and re-read by the same lane, L1/L2-resident) and in `scratch`; the stage order and all
 // reductions are fixed, so results do not depend on timing or placement.
-#include "measure.hpp"
 #include "soft.hpp"
+#include "stages.hpp"
 
 namespace nfdpf {
 
-struct Ctx4 {
-  float m0, m1, s0, s1;  // per-row [mean, std] context (model/models.py:309-315)
-};
+// ESS gate (DPFs.py:163-165): every workgroup evaluates the same expression
+__device__ __forceinline__ bool step_gate(const nfdpf_filter_desc &d) {
+  if (d.gate) return d.gate[0] != 0;
+  if (d.force_resample) return true;
+  float s = 0.f;
+  for (int i = 0; i < d.B_global; ++i) s += d.ess_all[i];
+  return (s / (float)d.B_global) < 0.5f * (float)d.N;
+}
+
+// Soft resampling of row b (resamplers.py:20-60) into slot t: hx = x_res, hp = w' (not yet
+// renormalised), hidx.  Returns S2 = the cascade sum of w' (the renormaliser).  `Cbuf` is
+// LDS of N floats.  All threads of the workgroup call it.
+__device__ float soft_row(const nfdpf_filter_desc &d, const RowSlot &S, int b, int64_t grow,
+                          const float *xprev, const float *pprev, float *Cbuf, StepShared &L) {
+  const int N = d.N;
+  float off;
+  if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
+    off = d.host_offsets[b];
+  else
+    off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, grow, 0u).x) * (1.0f / (float)N);
+  SoftRow row{pprev, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
+  const int64_t flat0 = (int64_t)N * grow;
+  soft_row_search(row, d.lin, off, Cbuf, L.d, L.f, [&](int i, int src) {
+    const float *xs;
+    float w;
+    if (src < N) {
+      xs = xprev + 2 * src;
+      w = row.w(src);
+    } else if (b + 1 < d.B) {  // reference edge: flat index N*(b+1) is the next row
+      xs = xprev + d.x_prev_rs;
+      w = 0.f;
+    } else {
+      xs = xprev + 2 * (N - 1);
+      w = 0.f;
+    }
+    S.hx[2 * i] = xs[0];
+    S.hx[2 * i + 1] = xs[1];
+    S.hp[i] = w;
+    S.hidx[i] = flat0 + src;
+  });
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const float s = cascade_row_sum([&](int j) { return S.hp[j]; }, N);
+    if (threadIdx.x == 0) L.bc[0] = s;
+  }
+  __syncthreads();
+  return L.bc[0];
+}
 
 template <int BLK, bool NFD, bool NFC, int MEAS>
 __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_desc d) {
@@ -30,230 +75,78 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
   __shared__ StepShared L;
   const int b = blockIdx.x, tid = threadIdx.x, N = d.N;
   const int64_t grow = d.row_base + b;
-  const int64_t flat0 = (int64_t)N * grow;
-  const int64_t hrow = ((int64_t)b * d.T + d.t) * N;
-  float *hx = d.hist_x + hrow * 2;
-  float *hp = d.hist_p + hrow;
-  float *hlik = d.hist_lik + hrow;
-  float *hnoise = d.hist_noise + hrow * 2;
-  int64_t *hidx = d.hist_idx + hrow;
-  float *hjac = d.hist_jac ? d.hist_jac + hrow : nullptr;
-  float *hprior = d.hist_prior ? d.hist_prior + hrow : nullptr;
-  float *scr = d.scratch + (int64_t)b * N * 4;  // per particle: x_dyn0, x_dyn1, propose, prior
-  const float K = d.dens_const;
-  const float two_var = 2.0f * (d.pos_noise * d.pos_noise);
+  const RowSlot S = row_slot(d, b);
   const int nfl = d.n_flows;
-  const float *enc = d.enc + ((int64_t)b * d.T + d.t) * d.E;
 
   if (d.phase != 2) {
-    // ---------------- frame encoding of this row (+ per-row measurement constants)
-    if (MEAS != NFDPF_MEAS_EXTERNAL) measure_row_setup<MEAS>(enc, d.meas_params, L);
-    // ---------------- ESS gate (DPFs.py:163-165), identical in every workgroup
-    bool fire;
-    if (d.gate) {
-      fire = d.gate[0] != 0;
-    } else if (d.force_resample) {
-      fire = true;
-    } else {
-      float s = 0.f;
-      for (int i = 0; i < d.B_global; ++i) s += d.ess_all[i];
-      fire = (s / (float)d.B_global) < 0.5f * (float)N;
-    }
-    const bool soft = fire && d.resampler == NFDPF_RESAMPLE_SOFT;
-    const bool ot = fire && d.resampler == NFDPF_RESAMPLE_OT;
+    if (MEAS != NFDPF_MEAS_EXTERNAL) measure_row_setup<MEAS>(S.enc, d.meas_params, L);
+    const bool fire = step_gate(d);
+    const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
     const float *xprev = d.x_prev + b * d.x_prev_rs;
     const float *pprev = d.p_prev + b * d.p_prev_rs;
+    const float S2 = mode == kSrcSoft ? soft_row(d, S, b, grow, xprev, pprev, Cbuf, L) : 1.f;
 
-    float S2 = 1.f;
-    if (soft) {
-      float off;
-      if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
-        off = d.host_offsets[b];
-      else
-        off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, grow, 0u).x) * (1.0f / (float)N);
-      SoftRow row{pprev, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
-      soft_row_search(row, d.lin, off, Cbuf, L.d, L.f, [&](int i, int src) {
-        const float *xs;
-        float w;
-        if (src < N) {
-          xs = xprev + 2 * src;
-          w = row.w(src);
-        } else if (b + 1 < d.B) {  // reference edge: flat index N*(b+1) is the next row
-          xs = xprev + d.x_prev_rs;
-          w = 0.f;
-        } else {
-          xs = xprev + 2 * (N - 1);
-          w = 0.f;
-        }
-        hx[2 * i] = xs[0];
-        hx[2 * i + 1] = xs[1];
-        hp[i] = w;
-        hidx[i] = flat0 + src;
-      });
-      __syncthreads();
-      if (tid < 64) {
-        const float s = cascade_row_sum([&](int j) { return hp[j]; }, N);
-        if (tid == 0) L.bc[0] = s;
-      }
-      __syncthreads();
-      S2 = L.bc[0];
-    }
-
-    // ---------------- motion (model/models.py:191-204) + mean/std of x_phys
+    // ---------------- motion + mean/std of x_phys
     const float v0 = d.vel[2 * b], v1 = d.vel[2 * b + 1];
     const float lr_ot = logf(1.0f / (float)N);
     double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
     for (int i = tid; i < N; i += BLK) {
-      float x0, x1, lr;
-      if (soft) {
-        x0 = hx[2 * i];
-        x1 = hx[2 * i + 1];
-        lr = logf(hp[i] / S2);
-      } else {
-        if (ot) {
-          x0 = d.ot_x[((int64_t)b * N + i) * 2];
-          x1 = d.ot_x[((int64_t)b * N + i) * 2 + 1];
-          lr = lr_ot;
-        } else {
-          x0 = xprev[2 * i];
-          x1 = xprev[2 * i + 1];
-          lr = logf(pprev[i]);
-        }
-        hidx[i] = flat0 + i;
-      }
-      float e0, e1;
-      if (d.rng_mode == NFDPF_RNG_HOST) {
-        e0 = d.host_noise[((int64_t)b * N + i) * 2];
-        e1 = d.host_noise[((int64_t)b * N + i) * 2 + 1];
-      } else {
-        const U4 r = rng_draw(d.seed, kTagMotion, (uint32_t)d.t, grow, (uint32_t)i);
-        box_muller(r.x, r.y, e0, e1);
-        e0 *= d.pos_noise;
-        e1 *= d.pos_noise;
-      }
-      const float p0 = (x0 + v0) + e0, p1 = (x1 + v1) + e1;
-      hnoise[2 * i] = e0;
-      hnoise[2 * i + 1] = e1;
-      hx[2 * i] = p0;
-      hx[2 * i + 1] = p1;
-      hp[i] = lr;
+      float p0, p1;
+      stage_motion(d, S, b, grow, i, mode, xprev, pprev, S2, lr_ot, v0, v1, p0, p1);
       s0 += p0;
       s1 += p1;
       q0 += (double)p0 * p0;
       q1 += (double)p1 * p1;
     }
-    // context [mean, std(unbiased)] (model/models.py:309-315); reductions in f64
     auto row_ctx = [&](double a0, double a1, double b0, double b1) {
       a0 = block_sum(a0, L.d);
       a1 = block_sum(a1, L.d);
       b0 = block_sum(b0, L.d);
       b1 = block_sum(b1, L.d);
-      const double m0 = a0 / N, m1 = a1 / N;
-      return Ctx4{(float)m0, (float)m1, (float)sqrt((b0 - a0 * m0) / (N - 1)),
-                  (float)sqrt((b1 - a1 * m1) / (N - 1))};
+      return ctx_from_sums(a0, a1, b0, b1, N);
     };
-    Ctx4 c4{0.f, 0.f, 0.f, 0.f};
-    if (NFD || NFC) c4 = row_ctx(s0, s1, q0, q1);
-    const float cdyn[4] = {c4.m0, c4.m1, c4.s0, c4.s1};
+    Ctx4 cphys{0.f, 0.f, 0.f, 0.f};
+    if (NFD || NFC) cphys = row_ctx(s0, s1, q0, q1);
 
     // ---------------- nf_dyn inverse (model/models.py:305-332)
-    constexpr int inD = 1 + 4;
-    const int nsD = fcnn_size<kH>(inD, 1);
     if (NFD) {
-      if (tid < nfl * 4 * kH) {
-        const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
-        L.cb_dyn[tid] = fold_bias_c<kH, 4>(d.dyn_params + (int64_t)(f * 4 + n) * nsD, inD, 1, j, cdyn);
-      }
+      fold_dyn(d.dyn_params, nfl, cphys, L.cb_dyn);
       __syncthreads();
       s0 = s1 = q0 = q1 = 0;
       for (int i = tid; i < N; i += BLK) {
-        float lo[1] = {hx[2 * i]}, up[1] = {hx[2 * i + 1]};
-        float ld = 0.f;
-        for (int f = nfl - 1; f >= 0; --f)
-          ld += coupling_inverse<1, kH>(opaque(d.dyn_params) + (int64_t)f * 4 * nsD, inD, lo, up,
-                                        L.cb_dyn + f * 4 * kH);
-        scr[4 * i] = lo[0];
-        scr[4 * i + 1] = up[0];
-        if (hjac) hjac[i] = -ld;
-        s0 += lo[0];
-        s1 += up[0];
-        q0 += (double)lo[0] * lo[0];
-        q1 += (double)up[0] * up[0];
+        float x0, x1;
+        stage_dyn_inverse(d, S, i, L.cb_dyn, x0, x1);
+        s0 += x0;
+        s1 += x1;
+        q0 += (double)x0 * x0;
+        q1 += (double)x1 * x1;
       }
     }
-
-    // ---------------- proposal + densities + measurement (model/models.py:334-379)
-    const int inC = 1 + d.E + 4;
-    const int nsC = fcnn_size<kH>(inC, 1);
+    // ---------------- proposal context [enc, mean, std] (model/models.py:334-346)
     if (NFC) {
-      const Ctx4 cp = NFD ? row_ctx(s0, s1, q0, q1) : c4;
-      const float cprop[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
-      if (tid < d.E) L.ctx[tid] = enc[tid];
+      const Ctx4 cp = NFD ? row_ctx(s0, s1, q0, q1) : cphys;
+      if (tid < d.E) L.ctx[tid] = S.enc[tid];
       if (tid == 0) {
-        L.ctx[d.E] = cprop[0];
-        L.ctx[d.E + 1] = cprop[1];
-        L.ctx[d.E + 2] = cprop[2];
-        L.ctx[d.E + 3] = cprop[3];
+        L.ctx[d.E] = cp.m0;
+        L.ctx[d.E + 1] = cp.m1;
+        L.ctx[d.E + 2] = cp.s0;
+        L.ctx[d.E + 3] = cp.s1;
       }
       __syncthreads();
-      if (tid < nfl * 4 * kH) {
-        const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
-        L.cb_cond[tid] =
-            fold_bias<kH>(d.cond_params + (int64_t)(f * 4 + n) * nsC, inC, 1, j, L.ctx, d.E + 4);
-      }
+      fold_cond(d.cond_params, nfl, d.E, L.ctx, L.cb_cond);
     }
     __syncthreads();
     float lmax = -INFINITY;
     for (int i = tid; i < N; i += BLK) {
-      const float p0 = hx[2 * i], p1 = hx[2 * i + 1];
-      const float e0 = hnoise[2 * i], e1 = hnoise[2 * i + 1];
-      float xd0 = p0, xd1 = p1, jac = 0.f;
-      if (NFD) {
-        xd0 = scr[4 * i];
-        xd1 = scr[4 * i + 1];
-        jac = hjac ? hjac[i] : 0.f;
-      }
-      const float de = density(e0, e1, K, two_var);
-      float q0x = xd0, q1x = xd1, prior, propose;
-      if (NFC) {
-        float lo[1] = {xd0}, up[1] = {xd1};
-        float ld = 0.f;
-        for (int f = nfl - 1; f >= 0; --f)
-          ld += coupling_inverse<1, kH>(opaque(d.cond_params) + (int64_t)f * 4 * nsC, inC, lo, up,
-                                        L.cb_cond + f * 4 * kH);
-        q0x = lo[0];
-        q1x = up[0];
-        const float jac_prop = -ld;
-        const float r0 = p0 - e0, r1 = p1 - e1;
-        if (NFD) {
-          float ld2 = 0.f;
-          for (int f = 0; f < nfl; ++f)
-            ld2 += coupling_forward<1, kH>(opaque(d.dyn_params) + (int64_t)f * 4 * nsD, inD, lo, up,
-                                           L.cb_dyn + f * 4 * kH);
-          prior = density(lo[0] - r0, up[0] - r1, K, two_var) - (-ld2);
-        } else {
-          prior = density(q0x - r0, q1x - r1, K, two_var);
-        }
-        propose = (de + jac) + jac_prop;
-      } else {
-        prior = de + jac;
-        propose = de + jac;
-      }
-      hx[2 * i] = q0x;
-      hx[2 * i + 1] = q1x;
-      scr[4 * i + 2] = propose;
-      scr[4 * i + 3] = prior;
-      if (hprior) hprior[i] = prior;
+      float q0x, q1x;
+      const float lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, L.cb_dyn, L.cb_cond, q0x, q1x);
       if (MEAS != NFDPF_MEAS_EXTERNAL) {
-        const float lk = measure<MEAS>(MeasArgs{d.pe_params, d.meas_params, d.n_flows, d.meas_prior_std}, L, q0x, q1x);
-        hlik[i] = lk;
+        S.hlik[i] = lk;
         lmax = fmaxf(lmax, lk);
       }
     }
     if (d.phase == 1) return;
-    // row max of the raw likelihood for the models that subtract it (model/models.py:276,301)
-    if (MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_GAUSSIAN)
-      L.bc[1] = block_max(lmax, L.f);
+    if (MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_GAUSSIAN) L.bc[1] = block_max(lmax, L.f);
   }
 
   // ---------------- likelihood -> log-weights (DPFs.py:187-191)
@@ -269,13 +162,13 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
   float wmax = -INFINITY;
   double wsum = 0.0;
   for (int i = tid; i < N; i += BLK) {
-    float lk = MEAS == NFDPF_MEAS_EXTERNAL ? d.lik_ext[(int64_t)b * N + i] : hlik[i];
-    if (MEAS == NFDPF_MEAS_EXTERNAL || MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_GAUSSIAN) {
+    float lk = MEAS == NFDPF_MEAS_EXTERNAL ? d.lik_ext[(int64_t)b * N + i] : S.hlik[i];
+    if (meas_shifted<MEAS>()) {
       lk = lk - lshift;
-      hlik[i] = lk;
+      S.hlik[i] = lk;
     }
-    const float lw = ((hp[i] + lk) + scr[4 * i + 3]) - scr[4 * i + 2];
-    hp[i] = lw;
+    const float lw = stage_logw(S, i, lk);
+    S.hp[i] = lw;
     wmax = fmaxf(wmax, lw);
     wsum += lw;
   }
@@ -284,18 +177,18 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
   // ---------------- normalize_log_probs(...) + 1e-12 (utils.py:39-44, DPFs.py:192)
   double es = 0.0;
   for (int i = tid; i < N; i += BLK) {
-    const float e = expf(hp[i] - wmax);
-    hp[i] = e;
+    const float e = expf(S.hp[i] - wmax);
+    S.hp[i] = e;
     es += e;
   }
-  const float S = (float)block_sum(es, L.d);
+  const float Ssum = (float)block_sum(es, L.d);
   double sp2 = 0.0, px = 0.0, py = 0.0;
   for (int i = tid; i < N; i += BLK) {
-    const float p = hp[i] / S + 1e-12f;
-    hp[i] = p;
+    const float p = S.hp[i] / Ssum + 1e-12f;
+    S.hp[i] = p;
     sp2 += (double)p * p;
-    px += (double)p * hx[2 * i];
-    py += (double)p * hx[2 * i + 1];
+    px += (double)p * S.hx[2 * i];
+    py += (double)p * S.hx[2 * i + 1];
   }
   sp2 = block_sum(sp2, L.d);
   px = block_sum(px, L.d);

@@ -1,0 +1,460 @@
+// filter_tiled.hip -- one filtering step (DPFs.py:160-192) as a short pipeline of launches
+// over (particle tile, batch row) workgroups, so a batch of 64 rows fills all 256 CUs.
+//
+// The stages are coupled only through per-row reductions (mean/std before each flow, the
+// weight normalisation, the ESS gate), so each stage ends at a launch boundary and leaves
+// per-(row, tile) partial sums in the workspace; the next stage's workgroups combine the
+// partials of their row in a fixed order (deterministic, no atomics, no inter-workgroup
+// hand-off inside a launch):
+//
+//   K0 soft   (row)        : ESS gate; soft resampling of fired rows (resamplers.py:20-60)
+//   K1 motion (tile, row)  : motion (model/models.py:191-204)         -> sum x, x^2 partials
+//   K2 dyn    (tile, row)  : nf_dyn inverse (model/models.py:305-332)  -> sum x, x^2 partials
+//   K3 prop   (tile, row)  : NF proposal, nf_dyn forward, densities, measurement
+//                            (model/models.py:334-379)                 -> max / sum-exp partials
+//   K4 norm   (tile, row)  : log-weights, normalize_log_probs + 1e-12 (DPFs.py:187-192)
+//                            -> sum p^2 (next gate), sum p x, sum logw partials
+//
+// ess_all / ess_out of the descriptor hold per-(row, tile) sums of p^2 as doubles
+// ([B_global][tiles] / [B][tiles]); everything else has the fused kernel's meaning.
+#include "soft.hpp"
+#include "stages.hpp"
+
+namespace nfdpf {
+
+constexpr int kTile = 256;  // particles per workgroup, one per lane
+
+struct TiledWs {
+  double *st_phys;  // [B][tiles][4] sum x0, x1, x0^2, x1^2 of x_phys
+  double *st_dyn;   // [B][tiles][4] same for x_dyn
+  float *lmax;      // [B][tiles] max raw likelihood
+  float *umax;      // [B][tiles] max of the unshifted log-weight u
+  double *usum;     // [B][tiles] sum exp(u - umax)
+  float *S2;        // [B] soft-resampling renormaliser
+  double *fin;      // [B][T][tiles][4] sum p^2, sum p x0, sum p x1, sum logw
+};
+
+static inline int64_t al256(int64_t v) { return (v + 255) / 256 * 256; }
+__host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / kTile; }
+
+static int64_t tiled_bytes(int B, int N, int T) {
+  const int64_t bt = (int64_t)B * n_tiles(N);
+  return al256(bt * 32) * 2 + al256(bt * 4) * 2 + al256(bt * 8) + al256((int64_t)B * 4) +
+         al256(bt * T * 32);
+}
+
+static TiledWs tiled_carve(void *ws, int B, int N, int T) {
+  char *p = (char *)ws;
+  const int64_t bt = (int64_t)B * n_tiles(N);
+  TiledWs w;
+  w.st_phys = (double *)p;
+  p += al256(bt * 32);
+  w.st_dyn = (double *)p;
+  p += al256(bt * 32);
+  w.lmax = (float *)p;
+  p += al256(bt * 4);
+  w.umax = (float *)p;
+  p += al256(bt * 4);
+  w.usum = (double *)p;
+  p += al256(bt * 8);
+  w.S2 = (float *)p;
+  p += al256((int64_t)B * 4);
+  w.fin = (double *)p;
+  return w;
+}
+
+// ESS gate from per-(row, tile) sums of p^2 (DPFs.py:163-165); same value in every workgroup
+__device__ __forceinline__ bool tiled_gate(const nfdpf_filter_desc &d, int tiles) {
+  if (d.gate) return d.gate[0] != 0;
+  if (d.force_resample) return true;
+  const double *parts = reinterpret_cast<const double *>(d.ess_all);
+  float s = 0.f;
+  for (int r = 0; r < d.B_global; ++r) {
+    double s2 = 0.0;
+    for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
+    s += 1.0f / (float)s2;
+  }
+  return (s / (float)d.B_global) < 0.5f * (float)d.N;
+}
+
+// combine the 4-sum partials of row b -> context
+__device__ __forceinline__ Ctx4 tiled_ctx(const double *st, int b, int tiles, int N) {
+  double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  const double *p = st + (int64_t)b * tiles * 4;
+  for (int k = 0; k < tiles; ++k) {
+    a0 += p[4 * k];
+    a1 += p[4 * k + 1];
+    b0 += p[4 * k + 2];
+    b1 += p[4 * k + 3];
+  }
+  return ctx_from_sums(a0, a1, b0, b1, N);
+}
+
+__device__ __forceinline__ void store_sums4(double *dst, double a, double b, double c, double e,
+                                            double *sh) {
+  a = block_sum(a, sh);
+  b = block_sum(b, sh);
+  c = block_sum(c, sh);
+  e = block_sum(e, sh);
+  if (threadIdx.x == 0) {
+    dst[0] = a;
+    dst[1] = b;
+    dst[2] = c;
+    dst[3] = e;
+  }
+}
+
+// ---- K0: soft resampling of the rows where the gate fires (one workgroup per row)
+__global__ __launch_bounds__(512) void tiled_soft_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  extern __shared__ float Cbuf[];
+  __shared__ StepShared L;
+  const int tiles = n_tiles(d.N);
+  if (d.resampler != NFDPF_RESAMPLE_SOFT || !tiled_gate(d, tiles)) return;
+  const int b = blockIdx.x;
+  const RowSlot S = row_slot(d, b);
+  const float *xprev = d.x_prev + b * d.x_prev_rs;
+  const float *pprev = d.p_prev + b * d.p_prev_rs;
+  SoftRow row{pprev, d.N, d.alpha, 1.0f / (float)d.N, (float)(1.0 - (double)d.alpha), 1.0f};
+  float off;
+  if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
+    off = d.host_offsets[b];
+  else
+    off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, d.row_base + b, 0u).x) * (1.0f / (float)d.N);
+  const int64_t flat0 = (int64_t)d.N * (d.row_base + b);
+  const int N = d.N;
+  soft_row_search(row, d.lin, off, Cbuf, L.d, L.f, [&](int i, int src) {
+    const float *xs;
+    float w;
+    if (src < N) {
+      xs = xprev + 2 * src;
+      w = row.w(src);
+    } else if (b + 1 < d.B) {
+      xs = xprev + d.x_prev_rs;
+      w = 0.f;
+    } else {
+      xs = xprev + 2 * (N - 1);
+      w = 0.f;
+    }
+    S.hx[2 * i] = xs[0];
+    S.hx[2 * i + 1] = xs[1];
+    S.hp[i] = w;
+    S.hidx[i] = flat0 + src;
+  });
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const float s = cascade_row_sum([&](int j) { return S.hp[j]; }, N);
+    if (threadIdx.x == 0) ws.S2[b] = s;
+  }
+}
+
+// ---- K1: motion
+__global__ __launch_bounds__(kTile) void tiled_motion_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ double shd[16];
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int i = tile * kTile + threadIdx.x;
+  const int64_t grow = d.row_base + b;
+  const bool fire = tiled_gate(d, tiles);
+  const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
+  const RowSlot S = row_slot(d, b);
+  double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
+  if (i < d.N) {
+    float p0, p1;
+    stage_motion(d, S, b, grow, i, mode, d.x_prev + b * d.x_prev_rs, d.p_prev + b * d.p_prev_rs,
+                 mode == kSrcSoft ? ws.S2[b] : 1.f, logf(1.0f / (float)d.N), d.vel[2 * b],
+                 d.vel[2 * b + 1], p0, p1);
+    s0 = p0;
+    s1 = p1;
+    q0 = (double)p0 * p0;
+    q1 = (double)p1 * p1;
+  }
+  store_sums4(ws.st_phys + ((int64_t)b * tiles + tile) * 4, s0, s1, q0, q1, shd);
+}
+
+// ---- K2: nf_dyn inverse
+__global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ double shd[16];
+  __shared__ float cb[kMaxFlows * 4 * kH];
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int i = tile * kTile + threadIdx.x;
+  fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb);
+  __syncthreads();
+  const RowSlot S = row_slot(d, b);
+  double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
+  if (i < d.N) {
+    float x0, x1;
+    stage_dyn_inverse(d, S, i, cb, x0, x1);
+    s0 = x0;
+    s1 = x1;
+    q0 = (double)x0 * x0;
+    q1 = (double)x1 * x1;
+  }
+  store_sums4(ws.st_dyn + ((int64_t)b * tiles + tile) * 4, s0, s1, q0, q1, shd);
+}
+
+// softmax partials of the unshifted log-weight u over this tile
+__device__ __forceinline__ void store_softmax(float u, bool valid, float *umax, double *usum, float *shf,
+                                              double *shd) {
+  const float m = block_max(valid ? u : -INFINITY, shf);
+  const double e = valid ? (double)expf(u - m) : 0.0;
+  const double s = block_sum(e, shd);
+  if (threadIdx.x == 0) {
+    *umax = m;
+    *usum = s;
+  }
+}
+
+// ---- K3: proposal + measurement
+template <bool NFD, bool NFC, int MEAS>
+__global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ StepShared L;
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int i = tile * kTile + threadIdx.x;
+  const RowSlot S = row_slot(d, b);
+  if (MEAS != NFDPF_MEAS_EXTERNAL) measure_row_setup<MEAS>(S.enc, d.meas_params, L);
+  if (NFD) fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), L.cb_dyn);
+  if (NFC) {
+    const Ctx4 cp = tiled_ctx(NFD ? ws.st_dyn : ws.st_phys, b, tiles, d.N);
+    if (threadIdx.x < d.E) L.ctx[threadIdx.x] = S.enc[threadIdx.x];
+    if (threadIdx.x == 0) {
+      L.ctx[d.E] = cp.m0;
+      L.ctx[d.E + 1] = cp.m1;
+      L.ctx[d.E + 2] = cp.s0;
+      L.ctx[d.E + 3] = cp.s1;
+    }
+    __syncthreads();
+    fold_cond(d.cond_params, d.n_flows, d.E, L.ctx, L.cb_cond);
+  }
+  __syncthreads();
+  const bool valid = i < d.N;
+  float lk = -INFINITY, u = 0.f;
+  if (valid) {
+    float q0x, q1x;
+    lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, L.cb_dyn, L.cb_cond, q0x, q1x);
+    if (MEAS != NFDPF_MEAS_EXTERNAL) {
+      S.hlik[i] = lk;
+      u = stage_logw(S, i, lk);
+    }
+  }
+  if (MEAS == NFDPF_MEAS_EXTERNAL) return;  // phase 1: the external likelihood comes next
+  const int64_t bt = (int64_t)b * tiles + tile;
+  if (meas_shifted<MEAS>()) {
+    const float m = block_max(lk, L.f);
+    if (threadIdx.x == 0) ws.lmax[bt] = m;
+  }
+  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, L.f, L.d);
+}
+
+// ---- K3b (phase 2 of an EXTERNAL measurement): raw likelihood from lik_ext
+__global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ float shf[16];
+  __shared__ double shd[16];
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int i = tile * kTile + threadIdx.x;
+  const RowSlot S = row_slot(d, b);
+  const bool valid = i < d.N;
+  float lk = -INFINITY, u = 0.f;
+  if (valid) {
+    lk = d.lik_ext[(int64_t)b * d.N + i];
+    S.hlik[i] = lk;
+    u = stage_logw(S, i, lk);
+  }
+  const int64_t bt = (int64_t)b * tiles + tile;
+  const float m = block_max(lk, shf);
+  if (threadIdx.x == 0) ws.lmax[bt] = m;
+  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, shf, shd);
+}
+
+// ---- K4: log-weights, normalisation, per-tile sums for the gate / prediction / obs-likelihood
+template <bool SHIFT>
+__global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ double shd[16];
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int i = tile * kTile + threadIdx.x;
+  const int64_t rb = (int64_t)b * tiles;
+  float M = -INFINITY, Lmax = -INFINITY;
+  for (int k = 0; k < tiles; ++k) {
+    M = fmaxf(M, ws.umax[rb + k]);
+    if (SHIFT) Lmax = fmaxf(Lmax, ws.lmax[rb + k]);
+  }
+  double Sd = 0.0;
+  for (int k = 0; k < tiles; ++k) Sd += ws.usum[rb + k] * (double)expf(ws.umax[rb + k] - M);
+  const float Ssum = (float)Sd;
+  // u = logw + Lmax for the shifted models: normalise with the same shift
+  const float shift = SHIFT ? M - Lmax : M;
+  const RowSlot S = row_slot(d, b);
+  double sp2 = 0, px = 0, py = 0, sw = 0;
+  if (i < d.N) {
+    float lk = S.hlik[i];
+    if (SHIFT) {
+      lk = lk - Lmax;
+      S.hlik[i] = lk;
+    }
+    const float lw = stage_logw(S, i, lk);
+    const float p = expf(lw - shift) / Ssum + 1e-12f;
+    S.hp[i] = p;
+    sp2 = (double)p * p;
+    px = (double)p * S.hx[2 * i];
+    py = (double)p * S.hx[2 * i + 1];
+    sw = lw;
+  }
+  double *fin = ws.fin + (((int64_t)b * d.T + d.t) * tiles + tile) * 4;
+  store_sums4(fin, sp2, px, py, sw, shd);
+  if (threadIdx.x == 0) reinterpret_cast<double *>(d.ess_out)[rb + tile] = fin[0];
+}
+
+// per-row prediction / obs-likelihood sums of every step (after the last step)
+__global__ void tiled_finalize_kernel(const double *__restrict__ fin, int BT, int tiles,
+                                      float *__restrict__ pred, float *__restrict__ lw_sum) {
+  const int bt = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bt >= BT) return;
+  double px = 0, py = 0, sw = 0;
+  for (int k = 0; k < tiles; ++k) {
+    const double *f = fin + ((int64_t)bt * tiles + k) * 4;
+    px += f[1];
+    py += f[2];
+    sw += f[3];
+  }
+  pred[2 * bt] = (float)px;
+  pred[2 * bt + 1] = (float)py;
+  lw_sum[bt] = (float)sw;
+}
+
+// initial per-tile sums of p^2 (t = 0 gate) from p0 [B,N]
+__global__ __launch_bounds__(kTile) void tiled_ess_init_kernel(const float *__restrict__ p, int N,
+                                                               double *__restrict__ parts) {
+  __shared__ double shd[16];
+  const int tiles = n_tiles(N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int i = tile * kTile + threadIdx.x;
+  double v = 0.0;
+  if (i < N) {
+    const float x = p[(int64_t)b * N + i];
+    v = (double)x * x;
+  }
+  v = block_sum(v, shd);
+  if (threadIdx.x == 0) parts[(int64_t)b * tiles + tile] = v;
+}
+
+__global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int tiles, int N, int force,
+                                  int32_t *gate) {
+  float s = 0.f;
+  for (int r = 0; r < B; ++r) {
+    double s2 = 0.0;
+    for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
+    s += 1.0f / (float)s2;
+  }
+  gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
+}
+
+template <bool NFD, bool NFC, int MEAS>
+static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStream_t st) {
+  tiled_prop_kernel<NFD, NFC, MEAS><<<g, kTile, 0, st>>>(d, ws);
+}
+
+template <int MEAS>
+static void dispatch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStream_t st) {
+  if (d.nf_dyn && d.nf_cond)
+    launch_prop<true, true, MEAS>(d, ws, g, st);
+  else if (d.nf_dyn)
+    launch_prop<true, false, MEAS>(d, ws, g, st);
+  else if (d.nf_cond)
+    launch_prop<false, true, MEAS>(d, ws, g, st);
+  else
+    launch_prop<false, false, MEAS>(d, ws, g, st);
+}
+
+}  // namespace nfdpf
+
+using namespace nfdpf;
+
+extern "C" int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T) {
+  return (B <= 0 || N <= 0 || T <= 0) ? 256 : tiled_bytes(B, N, T);
+}
+
+extern "C" int nfdpf_filter_tiled_tiles(int N) { return N <= 0 ? 0 : n_tiles(N); }
+
+extern "C" int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int force, int32_t *gate,
+                                    void *stream) {
+  NFDPF_REQUIRE(gate && (force || parts) && B >= 1 && N >= 1, "nfdpf_ess_gate_tiled: bad arguments");
+  tiled_gate_kernel<<<1, 1, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, force, gate);
+  return launch_status("nfdpf_ess_gate_tiled");
+}
+
+extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
+                                       void *stream) {
+  NFDPF_REQUIRE(p0 && ess_parts && B >= 0 && N >= 1, "nfdpf_filter_tiled_init: bad arguments");
+  if (B == 0) return NFDPF_OK;
+  tiled_ess_init_kernel<<<dim3(n_tiles(N), B), kTile, 0, as_stream(stream)>>>(p0, N, ess_parts);
+  return launch_status("nfdpf_filter_tiled_init");
+}
+
+extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *workspace, void *stream) {
+  NFDPF_REQUIRE(dp && workspace, "nfdpf_filter_step_tiled: null argument");
+  const nfdpf_filter_desc &d = *dp;
+  NFDPF_REQUIRE(d.B >= 0 && d.N >= 2 && d.T >= 1 && d.t >= 0 && d.t < d.T,
+                "nfdpf_filter_step_tiled: bad sizes (B=%d N=%d T=%d t=%d)", d.B, d.N, d.T, d.t);
+  NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_filter_step_tiled: workspace not 256-B aligned");
+  NFDPF_REQUIRE(d.n_flows >= 0 && d.n_flows <= kMaxFlows && d.hidden == kH,
+                "nfdpf_filter_step_tiled: n_flows <= %d and hidden == %d", kMaxFlows, kH);
+  NFDPF_REQUIRE(d.hist_x && d.hist_p && d.hist_noise && d.hist_lik && d.hist_idx && d.scratch &&
+                    d.ess_out && d.enc && d.vel,
+                "nfdpf_filter_step_tiled: null output/input pointer");
+  NFDPF_REQUIRE(d.phase == 2 || (d.x_prev && d.p_prev && (d.gate || d.force_resample || d.ess_all)),
+                "nfdpf_filter_step_tiled: previous-step state missing");
+  NFDPF_REQUIRE(!d.nf_dyn || (d.dyn_params && d.hist_jac && d.hist_prior),
+                "nfdpf_filter_step_tiled: nf_dyn needs dyn_params, hist_jac, hist_prior");
+  NFDPF_REQUIRE(!d.nf_cond || d.cond_params, "nfdpf_filter_step_tiled: nf_cond needs cond_params");
+  NFDPF_REQUIRE(d.measurement == NFDPF_MEAS_EXTERNAL || (d.E == kE && d.pe_params),
+                "nfdpf_filter_step_tiled: fused measurements need E == %d", kE);
+  NFDPF_REQUIRE(!(d.measurement == NFDPF_MEAS_CRNVP || d.measurement == NFDPF_MEAS_NN) || d.meas_params,
+                "nfdpf_filter_step_tiled: measurement parameters missing");
+  NFDPF_REQUIRE(d.E + 4 <= kMaxCtx, "nfdpf_filter_step_tiled: E too large");
+  NFDPF_REQUIRE(d.measurement != NFDPF_MEAS_EXTERNAL || d.phase != 0,
+                "nfdpf_filter_step_tiled: EXTERNAL measurement runs as phase 1 + phase 2");
+  NFDPF_REQUIRE(d.measurement != NFDPF_MEAS_EXTERNAL || d.phase != 2 || d.lik_ext,
+                "nfdpf_filter_step_tiled: phase 2 needs lik_ext");
+  if (d.resampler == NFDPF_RESAMPLE_SOFT) {
+    NFDPF_REQUIRE(d.N <= kStepMaxN, "nfdpf_filter_step_tiled: soft resampling supports N <= %d", kStepMaxN);
+    NFDPF_REQUIRE(d.lin || d.phase == 2, "nfdpf_filter_step_tiled: soft resampling needs lin");
+  } else {
+    NFDPF_REQUIRE(d.ot_x || d.phase == 2, "nfdpf_filter_step_tiled: OT path needs ot_x");
+  }
+  NFDPF_REQUIRE(d.rng_mode == NFDPF_RNG_DEVICE || (d.gate && d.host_noise) || d.phase == 2,
+                "nfdpf_filter_step_tiled: HOST rng mode needs gate and host_noise");
+  if (d.B == 0) return NFDPF_OK;
+  hipStream_t st = as_stream(stream);
+  TiledWs ws = tiled_carve(workspace, d.B, d.N, d.T);
+  const dim3 g(n_tiles(d.N), d.B);
+  if (d.phase != 2) {
+    if (d.resampler == NFDPF_RESAMPLE_SOFT)
+      tiled_soft_kernel<<<d.B, 512, d.N * sizeof(float), st>>>(d, ws);
+    tiled_motion_kernel<<<g, kTile, 0, st>>>(d, ws);
+    if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
+    switch (d.measurement) {
+      case NFDPF_MEAS_COS: dispatch_prop<NFDPF_MEAS_COS>(d, ws, g, st); break;
+      case NFDPF_MEAS_CRNVP: dispatch_prop<NFDPF_MEAS_CRNVP>(d, ws, g, st); break;
+      case NFDPF_MEAS_NN: dispatch_prop<NFDPF_MEAS_NN>(d, ws, g, st); break;
+      case NFDPF_MEAS_GAUSSIAN: dispatch_prop<NFDPF_MEAS_GAUSSIAN>(d, ws, g, st); break;
+      case NFDPF_MEAS_EXTERNAL: dispatch_prop<NFDPF_MEAS_EXTERNAL>(d, ws, g, st); break;
+      default: set_error("nfdpf_filter_step_tiled: unknown measurement %d", d.measurement); return NFDPF_EINVAL;
+    }
+    if (d.phase == 1) return launch_status("nfdpf_filter_step_tiled");
+  }
+  if (d.measurement == NFDPF_MEAS_EXTERNAL) tiled_extlik_kernel<<<g, kTile, 0, st>>>(d, ws);
+  const bool shift = d.measurement == NFDPF_MEAS_CRNVP || d.measurement == NFDPF_MEAS_GAUSSIAN ||
+                     d.measurement == NFDPF_MEAS_EXTERNAL;
+  if (shift)
+    tiled_norm_kernel<true><<<g, kTile, 0, st>>>(d, ws);
+  else
+    tiled_norm_kernel<false><<<g, kTile, 0, st>>>(d, ws);
+  if (d.t == d.T - 1 && d.pred && d.lw_sum) {
+    const int BT = d.B * d.T;
+    tiled_finalize_kernel<<<(BT + 255) / 256, 256, 0, st>>>(ws.fin, BT, n_tiles(d.N), d.pred, d.lw_sum);
+  }
+  return launch_status("nfdpf_filter_step_tiled");
+}

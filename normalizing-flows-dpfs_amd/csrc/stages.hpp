@@ -1,0 +1,202 @@
+// stages.hpp -- per-particle stages of one filtering step (DPFs.py:160-192), shared by the
+// row-per-workgroup fused kernel (filter_step.hip) and the tiled multi-CU kernels
+// (filter_tiled.hip).  Each stage reads / writes the particle's own history slot t, so a
+// stage may run in a different launch than the one before it.
+#pragma once
+
+#include "measure.hpp"
+
+namespace nfdpf {
+
+struct Ctx4 {
+  float m0, m1, s0, s1;  // per-row [mean, std (unbiased)] context (model/models.py:309-315)
+};
+
+// Row-local pointers into history slot t and the scratch row.
+struct RowSlot {
+  float *hx, *hp, *hlik, *hnoise, *hjac, *hprior, *scr;  // scr: x_dyn0, x_dyn1, propose, prior
+  int64_t *hidx;
+  const float *enc;
+};
+
+__device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) {
+  const int64_t hrow = ((int64_t)b * d.T + d.t) * d.N;
+  RowSlot s;
+  s.hx = d.hist_x + hrow * 2;
+  s.hp = d.hist_p + hrow;
+  s.hlik = d.hist_lik + hrow;
+  s.hnoise = d.hist_noise + hrow * 2;
+  s.hidx = d.hist_idx + hrow;
+  s.hjac = d.hist_jac ? d.hist_jac + hrow : nullptr;
+  s.hprior = d.hist_prior ? d.hist_prior + hrow : nullptr;
+  s.scr = d.scratch + (int64_t)b * d.N * 4;
+  s.enc = d.enc + ((int64_t)b * d.T + d.t) * d.E;
+  return s;
+}
+
+// context from (sum x, sum y, sum x^2, sum y^2) over N particles
+__device__ __forceinline__ Ctx4 ctx_from_sums(double a0, double a1, double b0, double b1, int N) {
+  const double m0 = a0 / N, m1 = a1 / N;
+  return Ctx4{(float)m0, (float)m1, (float)sqrt((b0 - a0 * m0) / (N - 1)),
+              (float)sqrt((b1 - a1 * m1) / (N - 1))};
+}
+
+// source of the particle before motion
+enum SrcMode { kSrcPrev = 0, kSrcSoft = 1, kSrcOt = 2 };
+
+// motion (model/models.py:191-204): x_phys = (x_res + vel) + eps, eps ~ N(0, pos_noise^2).
+// Writes hx = x_phys, hnoise = eps, hp = log p_res, hidx (pass-through / OT).
+__device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const RowSlot &S, int b,
+                                             int64_t grow, int i, int mode, const float *xprev,
+                                             const float *pprev, float S2, float lr_ot, float v0,
+                                             float v1, float &p0, float &p1) {
+  const int N = d.N;
+  float x0, x1, lr;
+  if (mode == kSrcSoft) {
+    x0 = S.hx[2 * i];
+    x1 = S.hx[2 * i + 1];
+    lr = logf(S.hp[i] / S2);
+  } else {
+    if (mode == kSrcOt) {
+      x0 = d.ot_x[((int64_t)b * N + i) * 2];
+      x1 = d.ot_x[((int64_t)b * N + i) * 2 + 1];
+      lr = lr_ot;
+    } else {
+      x0 = xprev[2 * i];
+      x1 = xprev[2 * i + 1];
+      lr = logf(pprev[i]);
+    }
+    S.hidx[i] = (int64_t)N * grow + i;
+  }
+  float e0, e1;
+  if (d.rng_mode == NFDPF_RNG_HOST) {
+    e0 = d.host_noise[((int64_t)b * N + i) * 2];
+    e1 = d.host_noise[((int64_t)b * N + i) * 2 + 1];
+  } else {
+    const U4 r = rng_draw(d.seed, kTagMotion, (uint32_t)d.t, grow, (uint32_t)i);
+    box_muller(r.x, r.y, e0, e1);
+    e0 *= d.pos_noise;
+    e1 *= d.pos_noise;
+  }
+  p0 = (x0 + v0) + e0;
+  p1 = (x1 + v1) + e1;
+  S.hnoise[2 * i] = e0;
+  S.hnoise[2 * i + 1] = e1;
+  S.hx[2 * i] = p0;
+  S.hx[2 * i + 1] = p1;
+  S.hp[i] = lr;
+}
+
+constexpr int kInDyn = 1 + 4;  // nf_dyn coupling-net input: [half, mean(2), std(2)]
+
+// per-row fold of the nf_dyn context into the first-layer biases: cb[f][net][j]
+__device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &c, float *cb) {
+  const int tid = threadIdx.x;
+  const int ns = fcnn_size<kH>(kInDyn, 1);
+  if (tid < nfl * 4 * kH) {
+    const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
+    const float cc[4] = {c.m0, c.m1, c.s0, c.s1};
+    cb[tid] = fold_bias_c<kH, 4>(dyn + (int64_t)(f * 4 + n) * ns, kInDyn, 1, j, cc);
+  }
+}
+
+// per-row fold of the proposal context [enc, mean, std] (model/models.py:338-346); ctx in LDS
+__device__ __forceinline__ void fold_cond(const float *cond, int nfl, int E, const float *ctx,
+                                          float *cb) {
+  const int tid = threadIdx.x;
+  const int in = 1 + E + 4;
+  const int ns = fcnn_size<kH>(in, 1);
+  if (tid < nfl * 4 * kH) {
+    const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
+    cb[tid] = fold_bias<kH>(cond + (int64_t)(f * 4 + n) * ns, in, 1, j, ctx, E + 4);
+  }
+}
+
+// nf_dyn inverse (model/models.py:305-332): reads hx (x_phys), writes scr x_dyn and hjac
+__device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, const RowSlot &S, int i,
+                                                  const float *cb, float &xd0, float &xd1) {
+  const int ns = fcnn_size<kH>(kInDyn, 1);
+  float lo[1] = {S.hx[2 * i]}, up[1] = {S.hx[2 * i + 1]};
+  float ld = 0.f;
+  for (int f = d.n_flows - 1; f >= 0; --f)
+    ld += coupling_inverse<1, kH>(opaque(d.dyn_params) + (int64_t)f * 4 * ns, kInDyn, lo, up,
+                                  cb + f * 4 * kH);
+  S.scr[4 * i] = lo[0];
+  S.scr[4 * i + 1] = up[0];
+  if (S.hjac) S.hjac[i] = -ld;
+  xd0 = lo[0];
+  xd1 = up[0];
+}
+
+// NF proposal + nf_dyn forward + densities (model/models.py:358-377) and the measurement.
+// Reads hx (x_phys), hnoise, scr/hjac; writes hx = proposal, scr propose/prior, hprior.
+// Returns the raw likelihood (0 for an EXTERNAL measurement).
+template <bool NFD, bool NFC, int MEAS>
+__device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, const RowSlot &S,
+                                                const StepShared &L, int i, const float *cb_dyn,
+                                                const float *cb_cond, float &q0x, float &q1x) {
+  const float K = d.dens_const;
+  const float two_var = 2.0f * (d.pos_noise * d.pos_noise);
+  const int nfl = d.n_flows;
+  const float p0 = S.hx[2 * i], p1 = S.hx[2 * i + 1];
+  const float e0 = S.hnoise[2 * i], e1 = S.hnoise[2 * i + 1];
+  float xd0 = p0, xd1 = p1, jac = 0.f;
+  if (NFD) {
+    xd0 = S.scr[4 * i];
+    xd1 = S.scr[4 * i + 1];
+    jac = S.hjac ? S.hjac[i] : 0.f;
+  }
+  const float de = density(e0, e1, K, two_var);
+  float prior, propose;
+  q0x = xd0;
+  q1x = xd1;
+  if (NFC) {
+    const int inC = 1 + d.E + 4;
+    const int nsC = fcnn_size<kH>(inC, 1);
+    const int nsD = fcnn_size<kH>(kInDyn, 1);
+    float lo[1] = {xd0}, up[1] = {xd1};
+    float ld = 0.f;
+    for (int f = nfl - 1; f >= 0; --f)
+      ld += coupling_inverse<1, kH>(opaque(d.cond_params) + (int64_t)f * 4 * nsC, inC, lo, up,
+                                    cb_cond + f * 4 * kH);
+    q0x = lo[0];
+    q1x = up[0];
+    const float jac_prop = -ld;
+    const float r0 = p0 - e0, r1 = p1 - e1;
+    if (NFD) {
+      float ld2 = 0.f;
+      for (int f = 0; f < nfl; ++f)
+        ld2 += coupling_forward<1, kH>(opaque(d.dyn_params) + (int64_t)f * 4 * nsD, kInDyn, lo, up,
+                                       cb_dyn + f * 4 * kH);
+      prior = density(lo[0] - r0, up[0] - r1, K, two_var) - (-ld2);
+    } else {
+      prior = density(q0x - r0, q1x - r1, K, two_var);
+    }
+    propose = (de + jac) + jac_prop;
+  } else {
+    prior = de + jac;
+    propose = de + jac;
+  }
+  S.hx[2 * i] = q0x;
+  S.hx[2 * i + 1] = q1x;
+  S.scr[4 * i + 2] = propose;
+  S.scr[4 * i + 3] = prior;
+  if (S.hprior) S.hprior[i] = prior;
+  if (MEAS != NFDPF_MEAS_EXTERNAL)
+    return measure<MEAS>(MeasArgs{d.pe_params, d.meas_params, d.n_flows, d.meas_prior_std}, L, q0x,
+                         q1x);
+  return 0.f;
+}
+
+// log-weight update (DPFs.py:187): ((log p_res + lik) + prior) - propose
+__device__ __forceinline__ float stage_logw(const RowSlot &S, int i, float lik) {
+  return ((S.hp[i] + lik) + S.scr[4 * i + 3]) - S.scr[4 * i + 2];
+}
+
+template <int MEAS>
+__host__ __device__ constexpr bool meas_shifted() {
+  // measurement models that subtract the row max of the raw likelihood (model/models.py:276,301)
+  return MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_GAUSSIAN || MEAS == NFDPF_MEAS_EXTERNAL;
+}
+
+}  // namespace nfdpf

@@ -45,6 +45,7 @@ class FilterConfig:
     rng_mode: str = "device"     # "device" (Philox on the GPU) | "host" (reference CPU generator)
     seed: int = 2
     force_resample: bool = False
+    kernel: str = "tiled"        # "tiled" (multi-CU pipeline per step) | "fused" (one launch per step)
 
 
 @dataclass
@@ -170,6 +171,7 @@ class FilterEngine:
             x0, logw0 = ops.particle_init(start_state[:, :2].to(dev), B, N, c.width, c.init_with_true_state,
                                           c.seed, shard.row_base, dev)
         p0, ie0 = ops.normalize_log_probs(logw0)
+        tiled = c.kernel == "tiled"
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)
@@ -182,9 +184,19 @@ class FilterEngine:
         scratch = torch.empty((B, N, 4), **f32)
         lw_sum = torch.empty((B, T), **f32)
         pred = torch.empty((B, T, 2), **f32)
-        ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
-        ess_all = self._gather(ie0, shard)
-        gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
+        if tiled:
+            # per-(row, tile) sums of p^2 (double) feed the next step's gate
+            tiles = ops.tiled_tiles(N)
+            ess_bufs = [torch.empty((B, tiles), device=dev, dtype=torch.float64) for _ in range(2)]
+            ess0 = ops.tiled_init(p0, torch.empty((B, tiles), device=dev, dtype=torch.float64))
+            ws = ops.tiled_workspace(B, N, T, dev)
+            gather_buf = torch.empty((shard.B_global, tiles), device=dev, dtype=torch.float64) \
+                if shard.world > 1 else None
+        else:
+            ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
+            ess0 = ie0
+            gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
+        ess_all = self._gather(ess0, shard)
         gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
         # velocity used by each step's motion: start velocity, then vel_input[:, t-1] (DPFs.py:158,173)
         vel_steps = torch.cat([start_state[:, None, 2:4].to(dev), vel_input[:, :T - 1].to(dev)], 1)
@@ -232,6 +244,8 @@ class FilterEngine:
                 if teacher is not None and t > 0:
                     pc = teacher["p"][:, t - 1].cpu().float()
                     fire = bool(c.force_resample or torch.mean(1 / torch.sum(pc ** 2, dim=-1)) < 0.5 * N)
+                elif tiled:
+                    fire = self._host_gate_parts(ess_all, N, c.force_resample)
                 else:
                     fire = self._host_gate(ess_all, N, c.force_resample)
                 fired.append(fire)
@@ -246,7 +260,10 @@ class FilterEngine:
                 keep.append(nz)
                 d.host_noise = nz.data_ptr()
             elif c.resampler == "ot":
-                ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
+                if tiled:
+                    ops.ess_gate_tiled(ess_all, N, c.force_resample, out=gate_buf)
+                else:
+                    ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
                 d.gate = gate_buf.data_ptr()
             if c.resampler == "ot":
                 contiguous = t == 0 or teacher is not None
@@ -256,14 +273,15 @@ class FilterEngine:
                                               gate=gate_buf)
                 keep.append(xo)
                 d.ot_x = xo.data_ptr()
+            launch = (lambda: ops.filter_step_tiled(d, ws, dev)) if tiled else (lambda: ops.filter_step(d, dev))
             if self.step_events is not None:
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ev0.record()
-                ops.filter_step(d, dev)
+                launch()
                 ev1.record()
                 self.step_events.append((ev0, ev1))
             else:
-                ops.filter_step(d, dev)
+                launch()
             ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)
@@ -290,6 +308,21 @@ class FilterEngine:
         out = buf if buf is not None else torch.empty(shard.B_global, device=ie.device, dtype=ie.dtype)
         dist.all_gather_into_tensor(out, ie, group=shard.group)
         return out
+
+    @staticmethod
+    def _host_gate_parts(parts: torch.Tensor, N: int, force: bool) -> bool:
+        """Tiled-mode gate on the host: per row sum the per-tile p^2 sums (double, in order),
+        1/sum in float32, then the sequential float32 mean (csrc/filter_tiled.hip)."""
+        if force:
+            return True
+        s = np.float32(0.0)
+        rows = parts.double().cpu().numpy()
+        for row in rows:
+            s2 = 0.0
+            for v in row:
+                s2 += float(v)
+            s = np.float32(s + np.float32(np.float32(1.0) / np.float32(s2)))
+        return bool(np.float32(s / np.float32(len(rows))) < np.float32(0.5 * N))
 
     @staticmethod
     def _host_gate(ess_all: torch.Tensor, N: int, force: bool) -> bool:

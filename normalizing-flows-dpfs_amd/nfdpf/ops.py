@@ -162,3 +162,29 @@ def particle_init(start_xy, B, N, width, true_state, seed, row_base=0, device=No
 
 def filter_step(desc: L.FilterDesc, device):
     check(lib().nfdpf_filter_step(desc, stream_ptr(device)), "nfdpf_filter_step")
+
+
+def tiled_tiles(N: int) -> int:
+    return int(lib().nfdpf_filter_tiled_tiles(N))
+
+
+def tiled_workspace(B: int, N: int, T: int, device) -> torch.Tensor:
+    return workspace(int(lib().nfdpf_filter_tiled_workspace_bytes(B, N, T)), device, tag="tiled")
+
+
+def tiled_init(p0: torch.Tensor, out: torch.Tensor):
+    B, N = p0.shape
+    check(lib().nfdpf_filter_tiled_init(ptr(p0), B, N, ptr(out), stream_ptr(p0.device)), "nfdpf_filter_tiled_init")
+    return out
+
+
+def ess_gate_tiled(parts, N, force=False, out=None):
+    B = parts.shape[0]
+    g = out if out is not None else torch.empty(1, device=parts.device, dtype=torch.int32)
+    check(lib().nfdpf_ess_gate_tiled(ptr(parts), B, N, int(bool(force)), ptr(g), stream_ptr(parts.device)),
+          "nfdpf_ess_gate_tiled")
+    return g
+
+
+def filter_step_tiled(desc: L.FilterDesc, ws: torch.Tensor, device):
+    check(lib().nfdpf_filter_step_tiled(desc, _aligned_ptr(ws), stream_ptr(device)), "nfdpf_filter_step_tiled")

@@ -189,11 +189,14 @@ class _Models(torch.nn.Module):
         self.to(DEV)
 
 
-def _engine(fx):
+KERNELS = ["fused", "tiled"]
+
+
+def _engine(fx, kernel="tiled"):
     from nfdpf.engine import FilterConfig, FilterEngine
     c = e2e_cfg(fx)
     cfg = FilterConfig(N=c["N"], NF_dyn=c["NF_dyn"], NF_cond=c["NF_cond"], measurement=c["measurement"],
-                       resampler=c["resampler"], rng_mode="host")
+                       resampler=c["resampler"], rng_mode="host", kernel=kernel)
     return FilterEngine(cfg, _Models(weights(fx), c)), c
 
 
@@ -258,15 +261,16 @@ def _check_envelope(ours, ref32, ref64, rtol, atol, what, k=2.0):
     return float(np.mean(err <= rtol * np.abs(ref32) + atol))
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", E2E_FUSED)
-def test_filter_step_one_step_parity(name, monkeypatch):
+def test_filter_step_one_step_parity(name, kernel, monkeypatch):
     """Each fused step started from the reference's own previous state (teacher forcing).
 
     Exact: gate decisions, resampling indices, noise.  Floating point: within the
     reference's own float32 rounding envelope (|ref64 - ref32|, e.g. the cosine likelihood
     is -log(1 - <a,b>) and loses digits as particles align) plus 1e-5 relative."""
     fx = load(f"e2e_{name}.npz")
-    eng, c = _engine(fx)
+    eng, c = _engine(fx, kernel)
     res = eng.run(t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV),
                   host=_TapeDraws(fx), init=(t(fx["init_x"]), t(fx["logw0"])),
                   teacher={"x": t(fx["x"]), "p": t(fx["p"])})
@@ -282,11 +286,12 @@ def test_filter_step_one_step_parity(name, monkeypatch):
         _check_envelope(res.prior.cpu(), fx["prior"], r64["prior"], 1e-5, 1e-5, "prior")
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
-def test_filtering_free_running(name):
+def test_filtering_free_running(name, kernel):
     """Whole sequences from the reference's initial state and draws."""
     fx = load(f"e2e_{name}.npz")
-    eng, c = _engine(fx)
+    eng, c = _engine(fx, kernel)
     res = eng.run(t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV),
                   host=_TapeDraws(fx), init=(t(fx["init_x"]), t(fx["logw0"])))
     assert res.fired == [bool(f) for f in fx["fired"]]
@@ -301,7 +306,8 @@ def test_filtering_free_running(name):
     assert_close(pred, pr, 1e-5, 1e-3, "fused prediction")
 
 
-def test_device_rng_shard_invariance():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_device_rng_shard_invariance(kernel):
     """Device RNG is keyed on the GLOBAL row: rows [4,8) of a B=8 run equal a B=4 run with
     row_base = 4 (what each rank computes under batch sharding) when the gate is global."""
     from nfdpf.engine import FilterConfig, FilterEngine, ShardInfo
@@ -310,7 +316,7 @@ def test_device_rng_shard_invariance():
     models = _Models(weights(fx), c)
     N, T = 256, 6
     cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", force_resample=True,
-                       seed=1234)
+                       seed=1234, kernel=kernel)
     g = torch.Generator().manual_seed(3)
     enc = torch.randn(8, T, 32, generator=g).to(DEV)
     start = (torch.randn(8, 4, generator=g) * 10).to(DEV)
@@ -322,9 +328,10 @@ def test_device_rng_shard_invariance():
     assert torch.equal(full.index[4:], half.index)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("meas,res,nfd,nfc", [("cos", "soft", True, True), ("CRNVP", "ot", False, False),
                                               ("NN", "soft", True, False), ("gaussian", "soft", False, True)])
-def test_device_rng_sanity(meas, res, nfd, nfc):
+def test_device_rng_sanity(meas, res, nfd, nfc, kernel):
     """Device-RNG runs of each fused variant: finite, normalised, valid indices, repeatable."""
     from nfdpf.engine import FilterConfig, FilterEngine
     from model.models import build_likelihood
@@ -332,7 +339,8 @@ def test_device_rng_sanity(meas, res, nfd, nfc):
     c = dict(e2e_cfg(fx), measurement=meas)
     models = _Models(weights(fx), c)
     B, N, T = 8, 300, 5
-    cfg = FilterConfig(N=N, NF_dyn=nfd, NF_cond=nfc, measurement=meas, resampler=res, force_resample=True, seed=9)
+    cfg = FilterConfig(N=N, NF_dyn=nfd, NF_cond=nfc, measurement=meas, resampler=res, force_resample=True, seed=9,
+                       kernel=kernel)
     g = torch.Generator().manual_seed(4)
     enc = torch.randn(B, T, 32, generator=g).to(DEV)
     start = (torch.randn(B, 4, generator=g) * 10).to(DEV)
@@ -345,3 +353,28 @@ def test_device_rng_sanity(meas, res, nfd, nfc):
     assert torch.allclose(s, torch.ones_like(s) + N * 1e-12, atol=1e-5)
     rows = torch.arange(B, device=DEV)[:, None, None] * N
     assert ((a.index >= rows) & (a.index < rows + N)).all()
+
+
+@pytest.mark.parametrize("gated", [True, False])
+def test_tiled_matches_fused(gated):
+    """The tiled pipeline and the row-per-workgroup kernel compute the same step (same device
+    RNG draws); only reduction orders differ.  N = 1000 spans 4 tiles per row."""
+    from nfdpf.engine import FilterConfig, FilterEngine
+    fx = load("e2e_c2.npz")
+    models = _Models(weights(fx), e2e_cfg(fx))
+    B, N, T = 6, 1000, 8
+    g = torch.Generator().manual_seed(8)
+    enc = torch.randn(B, T, 32, generator=g).to(DEV)
+    start = (torch.randn(B, 4, generator=g) * 10).to(DEV)
+    vel = (torch.randn(B, T, 2, generator=g) * 3).to(DEV)
+    out = {}
+    for k in KERNELS:
+        cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft",
+                           force_resample=not gated, seed=21, kernel=k)
+        out[k] = FilterEngine(cfg, models).run(enc, start, vel)
+    a, b = out["fused"], out["tiled"]
+    assert torch.equal(a.noise, b.noise)
+    agree = (a.index == b.index).float().mean().item()
+    assert agree > 0.999, agree
+    assert torch.allclose(a.particles[:, :2], b.particles[:, :2], rtol=1e-4, atol=1e-2)
+    assert torch.allclose(a.pred[:, :2], b.pred[:, :2], rtol=1e-4, atol=1e-2)
