@@ -29,10 +29,15 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 CONFIGS = {
-    # name: (flags, B, N, T, algorithmic FLOP per particle-step)
-    "c1": (dict(NF_dyn=False, NF_cond=False, measurement="cos", resampler_type="soft"), 16, 100, 24, 3.3e3),
-    "c2": (dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="soft"), 64, 1000, 50, 13.1e3),
-    "c3": (dict(NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler_type="ot"), 64, 1000, 50, 12.7e3),
+    # name: (flags, B, N, T, algorithmic FLOP per particle-step,
+    #        of which in the proposal+measurement launch of the tiled pipeline)
+    # C2 matmul FLOP per particle: nf_dyn inverse 1,792 + proposal 5,888 +
+    # nf_dyn forward 1,792 + cos measurement 3,136 = 12,608, x 13.1/12.608 elementwise.
+    "c1": (dict(NF_dyn=False, NF_cond=False, measurement="cos", resampler_type="soft"), 16, 100, 24, 3.3e3, 3.3e3),
+    "c2": (dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="soft"), 64, 1000, 50, 13.1e3,
+           13.1e3 * (5888 + 1792 + 3136) / 12608),
+    "c3": (dict(NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler_type="ot"), 64, 1000, 50, 12.7e3,
+           12.7e3),
 }
 B_ALG = 52.0            # algorithmic HBM bytes per particle-step
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
@@ -73,7 +78,7 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
     """The oracle (PyTorch-CPU restatement, timing-faithful: O(N^2) marker matching, FP64
     Sinkhorn, torch.cat history) on the host cores, on a bounded sample of the workload."""
     from oracle import dpf_oracle as O
-    flags, B, N, T, _ = CONFIGS[cfg_name]
+    flags, B, N, T, _, _ = CONFIGS[cfg_name]
     cores = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(cores)
     torch.manual_seed(2)
@@ -127,7 +132,8 @@ def main():
 
     from DPFs import DPF
     from nfdpf.engine import FilterEngine, ShardInfo
-    flags, B, N, T, F_ALG = CONFIGS[args.config]
+    flags, B, N, T, F_STEP, F_PROP = CONFIGS[args.config]
+    F_ALG = F_PROP if args.kernel == "tiled" else F_STEP
     torch.manual_seed(2)
     a = make_args(flags, B, N, T, {"force_resample": args.force_resample})
     dpf = DPF(a).to(dev).eval()
@@ -163,7 +169,10 @@ def main():
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    kernel_ms = float(np.mean([e.ms() for e in evs]))
+    for e in evs:
+        e.close()
+    kname = "tiled_prop_kernel" if args.kernel == "tiled" else "filter_step_kernel"
     # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
     se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
     cnt = torch.tensor(float(res.pred.numel()), device=dev, dtype=torch.float64)
@@ -191,7 +200,7 @@ def main():
             "rmse": rmse,
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
-                         "kernel": "filter_step_kernel", "kernel_avg_ms": kernel_ms,
+                         "kernel": kname, "kernel_avg_ms": kernel_ms,
                          "flop_per_unit": F_ALG, "units_per_launch": per_launch_units,
                          "hbm_achieved_GBs": hbm_gbs, "hbm_frac": hbm_gbs / PEAK_HBM_GBS},
         }

@@ -165,7 +165,10 @@ typedef struct nfdpf_filter_desc {
   float *ess_out;           /* [B] 1/sum(p^2) of this step */
   float *lw_sum;            /* [B,T] row sums of the unnormalised log-weights (obs likelihood) */
   float *pred;              /* [B,T,2] sum_n p*x (losses.py:18-31 prediction) */
-  float *scratch;           /* [B,N,2] phase 1 -> 2 hand-off (log p_resampled, log proposal) */
+  float *scratch;           /* [B,N,4] per-particle hand-off between stages (x_dyn, propose, prior) */
+  void *prof_events;        /* optional hipEvent_t[2]: recorded around the dominant launch
+                               (the whole step for nfdpf_filter_step, the proposal+measurement
+                               launch for nfdpf_filter_step_tiled) -- live kernel timing */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);

@@ -205,7 +205,10 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
 template <int BLK, bool NFD, bool NFC, int MEAS>
 static int launch_step(const nfdpf_filter_desc &d, hipStream_t st) {
   const size_t lds = (d.resampler == NFDPF_RESAMPLE_SOFT && d.phase != 2) ? d.N * sizeof(float) : 0;
+  hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+  if (ev) hipEventRecord(ev[0], st);
   filter_step_kernel<BLK, NFD, NFC, MEAS><<<d.B, BLK, lds, st>>>(d);
+  if (ev) hipEventRecord(ev[1], st);
   return launch_status("nfdpf_filter_step");
 }
 

@@ -435,6 +435,8 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
       tiled_soft_kernel<<<d.B, 512, d.N * sizeof(float), st>>>(d, ws);
     tiled_motion_kernel<<<g, kTile, 0, st>>>(d, ws);
     if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
+    hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+    if (ev) hipEventRecord(ev[0], st);
     switch (d.measurement) {
       case NFDPF_MEAS_COS: dispatch_prop<NFDPF_MEAS_COS>(d, ws, g, st); break;
       case NFDPF_MEAS_CRNVP: dispatch_prop<NFDPF_MEAS_CRNVP>(d, ws, g, st); break;
@@ -443,6 +445,7 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
       case NFDPF_MEAS_EXTERNAL: dispatch_prop<NFDPF_MEAS_EXTERNAL>(d, ws, g, st); break;
       default: set_error("nfdpf_filter_step_tiled: unknown measurement %d", d.measurement); return NFDPF_EINVAL;
     }
+    if (ev) hipEventRecord(ev[1], st);
     if (d.phase == 1) return launch_status("nfdpf_filter_step_tiled");
   }
   if (d.measurement == NFDPF_MEAS_EXTERNAL) tiled_extlik_kernel<<<g, kTile, 0, st>>>(d, ws);

@@ -41,6 +41,7 @@ class FilterDesc(Structure):
         ("hist_x", c_void_p), ("hist_p", c_void_p), ("hist_noise", c_void_p), ("hist_lik", c_void_p),
         ("hist_jac", c_void_p), ("hist_prior", c_void_p), ("hist_idx", c_void_p),
         ("ess_out", c_void_p), ("lw_sum", c_void_p), ("pred", c_void_p), ("scratch", c_void_p),
+        ("prof_events", c_void_p),
     ]
 
 

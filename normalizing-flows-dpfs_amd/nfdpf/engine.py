@@ -122,7 +122,7 @@ class FilterEngine:
     def __init__(self, cfg: FilterConfig, models):
         self.cfg = cfg
         self.m = models
-        self.step_events = None  # list -> (start, end) HIP events around every step launch
+        self.step_events = None  # list -> nfdpf.prof.EventPair around every step's dominant launch
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -273,15 +273,16 @@ class FilterEngine:
                                               gate=gate_buf)
                 keep.append(xo)
                 d.ot_x = xo.data_ptr()
-            launch = (lambda: ops.filter_step_tiled(d, ws, dev)) if tiled else (lambda: ops.filter_step(d, dev))
+            d.prof_events = None
             if self.step_events is not None:
-                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ev0.record()
-                launch()
-                ev1.record()
-                self.step_events.append((ev0, ev1))
+                from .prof import EventPair
+                ev = EventPair()
+                self.step_events.append(ev)
+                d.prof_events = ev.ptr
+            if tiled:
+                ops.filter_step_tiled(d, ws, dev)
             else:
-                launch()
+                ops.filter_step(d, dev)
             ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)

@@ -1,0 +1,53 @@
+"""Live kernel timing with raw hipEvents (recorded by libnfdpf around the dominant launch
+of a step, on the launch's own stream; see nfdpf_filter_desc.prof_events)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_hip = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        _hip = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")
+        _hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        _hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        _hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        _hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+    return _hip
+
+
+class EventPair:
+    """Two hipEvents in a C array (the ABI's prof_events)."""
+
+    def __init__(self):
+        self.arr = (ctypes.c_void_p * 2)()
+        for k in range(2):
+            e = ctypes.c_void_p()
+            rc = hip().hipEventCreate(ctypes.byref(e))
+            if rc != 0:
+                raise RuntimeError(f"hipEventCreate failed ({rc})")
+            self.arr[k] = e.value
+
+    @property
+    def ptr(self) -> int:
+        return ctypes.addressof(self.arr)
+
+    def ms(self) -> float:
+        hip().hipEventSynchronize(self.arr[1])
+        out = ctypes.c_float()
+        rc = hip().hipEventElapsedTime(ctypes.byref(out), self.arr[0], self.arr[1])
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
+        return float(out.value)
+
+    def close(self):
+        for k in range(2):
+            if self.arr[k]:
+                hip().hipEventDestroy(self.arr[k])
+                self.arr[k] = None
