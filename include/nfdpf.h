@@ -19,7 +19,10 @@
  * Packed parameter blobs (fp32, concatenated in this order, each tensor row-major as
  * nn.Linear stores it):
  *   FCNN(in,out,H)          : W1[H,in] b1[H] W2[H,H] b2[H] W3[out,H] b3[out]   (nf/flows.py:101-114)
- *   RealNVP(_cond) flow     : FCNN t1, s1, t2, s2 with in = dim/2 + obser_dim   (nf/flows.py:181-190)
+ *   coupling net            : FCNN(h + O, h, H) of a RealNVP(_cond) flow, h = dim/2, O = obser_dim,
+ *                             stored core-first: W1[:, :h] W2 b2 W3 b3, then W1[:, h:] b1
+ *                             (the context columns are folded into a bias once per row)
+ *   RealNVP(_cond) flow     : coupling nets t1, s1, t2, s2                      (nf/flows.py:181-190)
  *   stack of n flows        : flow 0, flow 1, ... (model order, i.e. nf_dyn.flows[i])
  *   MAF flow (dim d)        : initial_param[2], then FCNN(i, 2, H) for i = 1..d-1 (nf/flows.py:247-254)
  *   particle encoder        : Linear(2,16) Linear(16,32) Linear(32,E): W,b each  (model/models.py:130-150)

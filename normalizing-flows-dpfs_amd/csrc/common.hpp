@@ -214,13 +214,17 @@ __device__ float cascade_row_sum(const Get &v, int n) {
 // ----------------------------------------------------------------------------------------
 // misc
 // ----------------------------------------------------------------------------------------
-// Hide a wave-uniform pointer from loop-invariant code motion, so weight loads stay inside
-// the particle loop (re-read from the scalar cache) instead of being hoisted into hundreds
-// of SGPRs that then spill into VGPR lanes.
-template <class T>
-__device__ __forceinline__ const T *opaque(const T *p) {
+// Weights are read through the CONSTANT address space: wave-uniform addresses with
+// compile-time offsets become s_load_dwordx16 into SGPRs (operands of v_fma_f32 directly),
+// instead of one flat/global vector load per weight.
+typedef const float __attribute__((address_space(4))) cfloat;
+
+// Hide a wave-uniform pointer from loop-invariant code motion (so a particle loop re-reads
+// weights from the scalar cache instead of hoisting hundreds into SGPRs that then spill),
+// and re-type it as a constant-address-space pointer.
+__device__ __forceinline__ cfloat *wptr(const float *p) {
   asm volatile("" : "+s"(p));
-  return p;
+  return (cfloat *)p;
 }
 
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }

@@ -24,8 +24,9 @@ namespace nfdpf {
 __device__ __forceinline__ bool step_gate(const nfdpf_filter_desc &d) {
   if (d.gate) return d.gate[0] != 0;
   if (d.force_resample) return true;
-  float s = 0.f;
-  for (int i = 0; i < d.B_global; ++i) s += d.ess_all[i];
+  // torch.mean over the batch (ATen cascade order); every wave evaluates it
+  const float *ess = d.ess_all;
+  const float s = cascade_row_sum([&](int i) { return ess[i]; }, d.B_global);
   return (s / (float)d.B_global) < 0.5f * (float)d.N;
 }
 
@@ -206,9 +207,9 @@ template <int BLK, bool NFD, bool NFC, int MEAS>
 static int launch_step(const nfdpf_filter_desc &d, hipStream_t st) {
   const size_t lds = (d.resampler == NFDPF_RESAMPLE_SOFT && d.phase != 2) ? d.N * sizeof(float) : 0;
   hipEvent_t *ev = (hipEvent_t *)d.prof_events;
-  if (ev) hipEventRecord(ev[0], st);
+  if (ev) (void)hipEventRecord(ev[0], st);
   filter_step_kernel<BLK, NFD, NFC, MEAS><<<d.B, BLK, lds, st>>>(d);
-  if (ev) hipEventRecord(ev[1], st);
+  if (ev) (void)hipEventRecord(ev[1], st);
   return launch_status("nfdpf_filter_step");
 }
 

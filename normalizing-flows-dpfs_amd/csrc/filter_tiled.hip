@@ -63,17 +63,20 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   return w;
 }
 
-// ESS gate from per-(row, tile) sums of p^2 (DPFs.py:163-165); same value in every workgroup
+// ESS gate from per-(row, tile) sums of p^2 (DPFs.py:163-165): torch.mean over the batch of
+// 1 / sum p^2, in ATen's cascade order.  Every wave evaluates it (lanes in parallel over
+// rows), so all workgroups take the same decision without a hand-off.
 __device__ __forceinline__ bool tiled_gate(const nfdpf_filter_desc &d, int tiles) {
   if (d.gate) return d.gate[0] != 0;
   if (d.force_resample) return true;
   const double *parts = reinterpret_cast<const double *>(d.ess_all);
-  float s = 0.f;
-  for (int r = 0; r < d.B_global; ++r) {
-    double s2 = 0.0;
-    for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
-    s += 1.0f / (float)s2;
-  }
+  const float s = cascade_row_sum(
+      [&](int r) {
+        double s2 = 0.0;
+        for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
+        return 1.0f / (float)s2;
+      },
+      d.B_global);
   return (s / (float)d.B_global) < 0.5f * (float)d.N;
 }
 
@@ -342,13 +345,14 @@ __global__ __launch_bounds__(kTile) void tiled_ess_init_kernel(const float *__re
 
 __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int tiles, int N, int force,
                                   int32_t *gate) {
-  float s = 0.f;
-  for (int r = 0; r < B; ++r) {
-    double s2 = 0.0;
-    for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
-    s += 1.0f / (float)s2;
-  }
-  gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
+  const float s = cascade_row_sum(
+      [&](int r) {
+        double s2 = 0.0;
+        for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
+        return 1.0f / (float)s2;
+      },
+      force ? 0 : B);
+  if (threadIdx.x == 0) gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 
 template <bool NFD, bool NFC, int MEAS>
@@ -381,7 +385,7 @@ extern "C" int nfdpf_filter_tiled_tiles(int N) { return N <= 0 ? 0 : n_tiles(N);
 extern "C" int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int force, int32_t *gate,
                                     void *stream) {
   NFDPF_REQUIRE(gate && (force || parts) && B >= 1 && N >= 1, "nfdpf_ess_gate_tiled: bad arguments");
-  tiled_gate_kernel<<<1, 1, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, force, gate);
+  tiled_gate_kernel<<<1, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, force, gate);
   return launch_status("nfdpf_ess_gate_tiled");
 }
 
@@ -436,7 +440,7 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
     tiled_motion_kernel<<<g, kTile, 0, st>>>(d, ws);
     if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
     hipEvent_t *ev = (hipEvent_t *)d.prof_events;
-    if (ev) hipEventRecord(ev[0], st);
+    if (ev) (void)hipEventRecord(ev[0], st);
     switch (d.measurement) {
       case NFDPF_MEAS_COS: dispatch_prop<NFDPF_MEAS_COS>(d, ws, g, st); break;
       case NFDPF_MEAS_CRNVP: dispatch_prop<NFDPF_MEAS_CRNVP>(d, ws, g, st); break;
@@ -445,7 +449,7 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
       case NFDPF_MEAS_EXTERNAL: dispatch_prop<NFDPF_MEAS_EXTERNAL>(d, ws, g, st); break;
       default: set_error("nfdpf_filter_step_tiled: unknown measurement %d", d.measurement); return NFDPF_EINVAL;
     }
-    if (ev) hipEventRecord(ev[1], st);
+    if (ev) (void)hipEventRecord(ev[1], st);
     if (d.phase == 1) return launch_status("nfdpf_filter_step_tiled");
   }
   if (d.measurement == NFDPF_MEAS_EXTERNAL) tiled_extlik_kernel<<<g, kTile, 0, st>>>(d, ws);

@@ -21,8 +21,7 @@ __global__ __launch_bounds__(kStackBlock) void cond_stack_kernel(
   const int64_t r = (int64_t)blockIdx.x * kStackBlock + threadIdx.x;
   if (r >= rows) return;
   constexpr int D = 2 * HALF;
-  const int in = HALF + O;
-  const int ns = fcnn_size<H>(in, HALF);
+  const int ns = net_size<HALF, H>(O);
   float lo[HALF], up[HALF];
 #pragma unroll
   for (int k = 0; k < HALF; ++k) {
@@ -34,13 +33,13 @@ __global__ __launch_bounds__(kStackBlock) void cond_stack_kernel(
   float cb[4 * H];
   for (int f = 0; f < n_flows; ++f) {
     const int fi = INV ? n_flows - 1 - f : f;
-    const float *fw = params + (int64_t)fi * 4 * ns;
+    cfloat *fw = wptr(params) + fi * 4 * ns;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int j = 0; j < H; ++j) cb[n * H + j] = fold_bias<H>(fw + n * ns, in, HALF, j, c, O);
-    const float l = INV ? coupling_inverse<HALF, H>(fw, in, lo, up, cb)
-                        : coupling_forward<HALF, H>(fw, in, lo, up, cb);
+      for (int j = 0; j < H; ++j) cb[n * H + j] = fold_bias<HALF, H>(fw + n * ns, O, j, c);
+    const float l = INV ? coupling_inverse<HALF, H>(fw, O, lo, up, cb)
+                        : coupling_forward<HALF, H>(fw, O, lo, up, cb);
     ld += l;
   }
 #pragma unroll
@@ -91,8 +90,8 @@ __global__ __launch_bounds__(kStackBlock) void maf_stack_kernel(const float *__r
   float ld = 0.f;
   for (int f = 0; f < n_flows; ++f) {
     const int fi = INV ? n_flows - 1 - f : f;
-    const float l = INV ? maf_inverse<D, H>(params + (int64_t)fi * fs, v)
-                        : maf_forward<D, H>(params + (int64_t)fi * fs, v);
+    const float l = INV ? maf_inverse<D, H>(wptr(params) + fi * fs, v)
+                        : maf_forward<D, H>(wptr(params) + fi * fs, v);
     ld += l;
   }
 #pragma unroll

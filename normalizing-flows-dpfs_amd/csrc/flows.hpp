@@ -1,63 +1,66 @@
 // flows.hpp -- per-particle device functions for the flows and MLPs of the hot path.
 //
-// All weights are read through wave-uniform pointers, so hipcc keeps them in the scalar
-// data cache (s_load_dwordx*) and feeds v_fma_f32 straight from SGPRs: no LDS traffic and
-// no VGPR per weight.  One particle per lane; the hidden width (8) is far too narrow for
-// a 16x16 MFMA tile, see DESIGN.md "Why VALU for the coupling nets".
+// Weights come through `cfloat*` (constant address space, common.hpp): every offset inside
+// a net is a compile-time constant, so hipcc emits s_load_dwordx16 and feeds v_fma_f32
+// from SGPRs -- no LDS traffic, no VGPR per weight.  One particle per lane; the hidden
+// width (8) is far too narrow for a 16x16 MFMA tile.
+//
+// Coupling-net layout (nfdpf.pack.realnvp_tensors, include/nfdpf.h):
+//   [ W1[:, :HALF] (H x HALF) | W2 (H x H) | b2 (H) | W3 (HALF x H) | b3 (HALF)   <- "core",
+//     W1[:, HALF:] (H x O) | b1 (H) ]                                              <- context
+// The per-particle path touches only the core; the context columns are folded into a bias
+// once per batch row (or per particle when the condition is per particle).
 #pragma once
 
 #include "common.hpp"
 
 namespace nfdpf {
 
-// Packed FCNN(in, out, H): W1[H,in] b1[H] W2[H,H] b2[H] W3[out,H] b3[out]  (nf/flows.py:101-114)
-template <int H>
-__host__ __device__ constexpr int fcnn_size(int in, int out) {
-  return H * in + H + H * H + H + out * H + out;
-}
-
-// Folded first-layer bias for the conditioning part of the input:
-//   cb[j] = b1[j] + sum_c W1[j, lead + c] * ctx[c]   (ctx has `octx` entries)
-// For nf_dyn / the proposal flow the context is per batch row (model/models.py:309-315,
-// 338-346), so the fused step computes cb once per row and each particle pays only the
-// `lead` leading columns.
-template <int H>
-__device__ __forceinline__ float fold_bias(const float *__restrict__ w, int in, int lead, int j,
-                                           const float *ctx, int octx) {
-  float a = w[H * in + j];
-  for (int c = 0; c < octx; ++c) a = fmaf(w[j * in + lead + c], ctx[c], a);
-  return a;
-}
-
-// Same with a compile-time context length (context held in registers, fully unrolled).
-template <int H, int OCTX>
-__device__ __forceinline__ float fold_bias_c(const float *__restrict__ w, int in, int lead, int j,
-                                             const float (&ctx)[OCTX]) {
-  float a = w[H * in + j];
-#pragma unroll
-  for (int c = 0; c < OCTX; ++c) a = fmaf(w[j * in + lead + c], ctx[c], a);
-  return a;
-}
-
-// Nets t and s of one coupling half (same input), first layer restricted to the leading
-// `HALF` columns with the rest folded into cbt/cbs.  Outputs t[HALF], s[HALF].
 template <int HALF, int H>
-__device__ __forceinline__ void ts_pair(const float *__restrict__ wt, const float *__restrict__ ws,
-                                        int in, const float (&u)[HALF], const float *cbt,
-                                        const float *cbs, float (&t)[HALF], float (&s)[HALF]) {
+__host__ __device__ constexpr int net_core() {
+  return H * HALF + H * H + H + HALF * H + HALF;
+}
+template <int HALF, int H>
+__host__ __device__ constexpr int net_size(int O) {
+  return net_core<HALF, H>() + H * O + H;
+}
+
+// cb[j] = b1[j] + sum_c W1[j, HALF + c] * ctx[c]  (context folded into the first layer)
+template <int HALF, int H>
+__device__ __forceinline__ float fold_bias(cfloat *w, int O, int j, const float *ctx) {
+  cfloat *w1c = w + net_core<HALF, H>();
+  float a = w1c[H * O + j];
+  for (int c = 0; c < O; ++c) a = fmaf(w1c[j * O + c], ctx[c], a);
+  return a;
+}
+template <int HALF, int H, int O>
+__device__ __forceinline__ float fold_bias_c(cfloat *w, int j, const float (&ctx)[O]) {
+  cfloat *w1c = w + net_core<HALF, H>();
+  float a = w1c[H * O + j];
+#pragma unroll
+  for (int c = 0; c < O; ++c) a = fmaf(w1c[j * O + c], ctx[c], a);
+  return a;
+}
+
+// Nets t and s of one coupling half (same input u), first layer on the HALF leading columns
+// plus the folded biases cbt/cbs.  Outputs t[HALF], s[HALF].
+template <int HALF, int H>
+__device__ __forceinline__ void ts_pair(cfloat *wt, cfloat *ws, const float (&u)[HALF],
+                                        const float *cbt, const float *cbs, float (&t)[HALF],
+                                        float (&s)[HALF]) {
   float ht[H], hs[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
     float at = cbt[j], as = cbs[j];
 #pragma unroll
     for (int k = 0; k < HALF; ++k) {
-      at = fmaf(wt[j * in + k], u[k], at);
-      as = fmaf(ws[j * in + k], u[k], as);
+      at = fmaf(wt[j * HALF + k], u[k], at);
+      as = fmaf(ws[j * HALF + k], u[k], as);
     }
     ht[j] = tanh_fast(at);
     hs[j] = tanh_fast(as);
   }
-  const float *w2t = wt + H * in + H, *w2s = ws + H * in + H;
+  cfloat *w2t = wt + H * HALF, *w2s = ws + H * HALF;
   float gt[H], gs[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
@@ -70,7 +73,7 @@ __device__ __forceinline__ void ts_pair(const float *__restrict__ wt, const floa
     gt[j] = tanh_fast(at);
     gs[j] = tanh_fast(as);
   }
-  const float *w3t = w2t + H * H + H, *w3s = w2s + H * H + H;
+  cfloat *w3t = w2t + H * H + H, *w3s = w2s + H * H + H;
 #pragma unroll
   for (int o = 0; o < HALF; ++o) {
     float at = w3t[HALF * H + o], as = w3s[HALF * H + o];
@@ -106,38 +109,36 @@ __device__ __forceinline__ float half_sum(const float (&s)[HALF]) {
   }
 }
 
-// One RealNVP_cond flow.  `fw` = packed flow (t1,s1,t2,s2); `in` = HALF + O; cb = folded
-// biases [4][H] (net order t1,s1,t2,s2).  Forward: nf/flows.py:215-226; inverse: :228-239.
+// One RealNVP_cond flow (nets t1,s1,t2,s2 of net_size(O) floats each); cb = folded biases
+// [4][H].  Forward: nf/flows.py:215-226; inverse: :228-239.  Returns the flow's log-det.
 template <int HALF, int H>
-__device__ __forceinline__ float coupling_forward(const float *__restrict__ fw, int in,
-                                                  float (&lo)[HALF], float (&up)[HALF],
-                                                  const float *cb) {
-  const int ns = fcnn_size<H>(in, HALF);
+__device__ __forceinline__ float coupling_forward(cfloat *fw, int O, float (&lo)[HALF],
+                                                  float (&up)[HALF], const float *cb) {
+  const int ns = net_size<HALF, H>(O);
   float t[HALF], s[HALF];
-  ts_pair<HALF, H>(fw, fw + ns, in, lo, cb, cb + H, t, s);
+  ts_pair<HALF, H>(fw, fw + ns, lo, cb, cb + H, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) up[k] = t[k] + up[k] * expf(s[k]);
   const float l1 = half_sum<HALF>(s);
-  ts_pair<HALF, H>(fw + 2 * ns, fw + 3 * ns, in, up, cb + 2 * H, cb + 3 * H, t, s);
+  ts_pair<HALF, H>(fw + 2 * ns, fw + 3 * ns, up, cb + 2 * H, cb + 3 * H, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) lo[k] = t[k] + lo[k] * expf(s[k]);
   return l1 + half_sum<HALF>(s);
 }
 
 template <int HALF, int H>
-__device__ __forceinline__ float coupling_inverse(const float *__restrict__ fw, int in,
-                                                  float (&lo)[HALF], float (&up)[HALF],
-                                                  const float *cb) {
-  const int ns = fcnn_size<H>(in, HALF);
+__device__ __forceinline__ float coupling_inverse(cfloat *fw, int O, float (&lo)[HALF],
+                                                  float (&up)[HALF], const float *cb) {
+  const int ns = net_size<HALF, H>(O);
   float t[HALF], s[HALF];
-  ts_pair<HALF, H>(fw + 2 * ns, fw + 3 * ns, in, up, cb + 2 * H, cb + 3 * H, t, s);
+  ts_pair<HALF, H>(fw + 2 * ns, fw + 3 * ns, up, cb + 2 * H, cb + 3 * H, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) {
     lo[k] = (lo[k] - t[k]) * expf(-s[k]);
     s[k] = -s[k];
   }
   const float l2 = half_sum<HALF>(s);
-  ts_pair<HALF, H>(fw, fw + ns, in, lo, cb, cb + H, t, s);
+  ts_pair<HALF, H>(fw, fw + ns, lo, cb, cb + H, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) {
     up[k] = (up[k] - t[k]) * expf(-s[k]);
@@ -146,10 +147,14 @@ __device__ __forceinline__ float coupling_inverse(const float *__restrict__ fw, 
   return half_sum<HALF>(s) + l2;
 }
 
-// Generic small FCNN (runtime `in`, out = OUT) used by MAF (nf/flows.py:253).
+// Plain FCNN(in, OUT, H): W1[H,in] b1 W2 b2 W3[OUT,H] b3 (nf/flows.py:101-114), used by MAF.
+template <int H>
+__host__ __device__ constexpr int fcnn_size(int in, int out) {
+  return H * in + H + H * H + H + out * H + out;
+}
+
 template <int H, int OUT>
-__device__ __forceinline__ void fcnn_small(const float *__restrict__ w, int in, const float *x,
-                                           float (&o)[OUT]) {
+__device__ __forceinline__ void fcnn_small(cfloat *w, int in, const float *x, float (&o)[OUT]) {
   float h[H], g[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
@@ -157,7 +162,7 @@ __device__ __forceinline__ void fcnn_small(const float *__restrict__ w, int in, 
     for (int k = 0; k < in; ++k) a = fmaf(w[j * in + k], x[k], a);
     h[j] = tanh_fast(a);
   }
-  const float *w2 = w + H * in + H;
+  cfloat *w2 = w + H * in + H;
 #pragma unroll
   for (int j = 0; j < H; ++j) {
     float a = w2[H * H + j];
@@ -165,7 +170,7 @@ __device__ __forceinline__ void fcnn_small(const float *__restrict__ w, int in, 
     for (int k = 0; k < H; ++k) a = fmaf(w2[j * H + k], h[k], a);
     g[j] = tanh_fast(a);
   }
-  const float *w3 = w2 + H * H + H;
+  cfloat *w3 = w2 + H * H + H;
 #pragma unroll
   for (int q = 0; q < OUT; ++q) {
     float a = w3[OUT * H + q];
@@ -185,10 +190,10 @@ __host__ __device__ constexpr int maf_size(int D) {
 
 // MAF forward (nf/flows.py:259-270): z_i = (x_i - mu_i) / exp(alpha_i), output flipped.
 template <int D, int H>
-__device__ __forceinline__ float maf_forward(const float *__restrict__ fw, float (&x)[D]) {
+__device__ __forceinline__ float maf_forward(cfloat *fw, float (&x)[D]) {
   float z[D];
   float ld = 0.f;
-  const float *w = fw + 2;
+  cfloat *w = fw + 2;
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     float mu, al;
@@ -212,7 +217,7 @@ __device__ __forceinline__ float maf_forward(const float *__restrict__ fw, float
 
 // MAF inverse (nf/flows.py:272-284): z flipped, then x_i = mu_i + exp(alpha_i) z_i.
 template <int D, int H>
-__device__ __forceinline__ float maf_inverse(const float *__restrict__ fw, float (&v)[D]) {
+__device__ __forceinline__ float maf_inverse(cfloat *fw, float (&v)[D]) {
   float z[D], x[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
@@ -220,7 +225,7 @@ __device__ __forceinline__ float maf_inverse(const float *__restrict__ fw, float
     x[i] = 0.f;
   }
   float ld = 0.f;
-  const float *w = fw + 2;
+  cfloat *w = fw + 2;
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     float mu, al;
@@ -250,14 +255,12 @@ __host__ __device__ constexpr int pe_size(int E) {
   return kPeH1 * 2 + kPeH1 + kPeH2 * kPeH1 + kPeH2 + E * kPeH2 + E;
 }
 
-template <int E>
-__device__ __forceinline__ void particle_encode(const float *__restrict__ pe, float x0, float x1,
-                                                float (&e)[E]) {
-  float h1[kPeH1], h2[kPeH2];
-  const float *b1 = pe + kPeH1 * 2;
+__device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, float (&h2)[kPeH2]) {
+  float h1[kPeH1];
+  cfloat *b1 = pe + kPeH1 * 2;
 #pragma unroll
   for (int j = 0; j < kPeH1; ++j) h1[j] = relu(fmaf(pe[2 * j + 1], x1, fmaf(pe[2 * j], x0, b1[j])));
-  const float *w2 = b1 + kPeH1, *b2 = w2 + kPeH2 * kPeH1;
+  cfloat *w2 = b1 + kPeH1, *b2 = w2 + kPeH2 * kPeH1;
 #pragma unroll
   for (int j = 0; j < kPeH2; ++j) {
     float a = b2[j];
@@ -265,7 +268,13 @@ __device__ __forceinline__ void particle_encode(const float *__restrict__ pe, fl
     for (int k = 0; k < kPeH1; ++k) a = fmaf(w2[j * kPeH1 + k], h1[k], a);
     h2[j] = relu(a);
   }
-  const float *w3 = b2 + kPeH2, *b3 = w3 + E * kPeH2;
+}
+
+template <int E>
+__device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, float (&e)[E]) {
+  float h2[kPeH2];
+  pe_hidden(pe, x0, x1, h2);
+  cfloat *w3 = pe + kPeH1 * 2 + kPeH1 + kPeH2 * kPeH1 + kPeH2, *b3 = w3 + E * kPeH2;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     float a = b3[j];
@@ -275,54 +284,14 @@ __device__ __forceinline__ void particle_encode(const float *__restrict__ pe, fl
   }
 }
 
-// torch.sum(a * b, -1) over E (multiple of 8, E <= 480) in ATen's CPU order
-// (oracle/cascade.py): products first, 8-wide vectors dealt to 4 ILP slots, leftover
-// vectors into slot 0, slots folded, lanes added in order.  No contraction: the reference
-// rounds each product before summing.
+// Cosine-distance pieces for the particle encoder output, streamed: (|e|^2, <e, v>) without
+// materialising e (model/models.py:130-139 then utils.py:8-15).
 template <int E>
-__device__ __forceinline__ float dot_cpu_order(const float (&a)[E], const float *b) {
-#pragma clang fp contract(off)
-  static_assert(E % 8 == 0 && E / 8 / 4 < 16, "E must be a multiple of 8 below 512");
-  constexpr int NV = E / 8, N4 = NV / 4;
-  float tot = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float slot[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      slot[k] = 0.f;
-#pragma unroll
-      for (int i = 0; i < N4; ++i) slot[k] += a[(i * 4 + k) * 8 + j] * b[(i * 4 + k) * 8 + j];
-    }
-#pragma unroll
-    for (int r = N4 * 4; r < NV; ++r) slot[0] += a[r * 8 + j] * b[r * 8 + j];
-    float l = slot[0];
-    l += slot[1];
-    l += slot[2];
-    l += slot[3];
-    tot += l;
-  }
-  return tot;
-}
-
-// Cosine-distance pieces for the particle encoder output, streamed: returns (|e|^2, <e, v>)
-// without materialising e (model/models.py:130-139 then utils.py:8-15).
-template <int E>
-__device__ __forceinline__ void encode_dot(const float *__restrict__ pe, float x0, float x1,
-                                           const float *v, float &ss, float &dot) {
-  float h1[kPeH1], h2[kPeH2];
-  const float *b1 = pe + kPeH1 * 2;
-#pragma unroll
-  for (int j = 0; j < kPeH1; ++j) h1[j] = relu(fmaf(pe[2 * j + 1], x1, fmaf(pe[2 * j], x0, b1[j])));
-  const float *w2 = b1 + kPeH1, *b2 = w2 + kPeH2 * kPeH1;
-#pragma unroll
-  for (int j = 0; j < kPeH2; ++j) {
-    float a = b2[j];
-#pragma unroll
-    for (int k = 0; k < kPeH1; ++k) a = fmaf(w2[j * kPeH1 + k], h1[k], a);
-    h2[j] = relu(a);
-  }
-  const float *w3 = b2 + kPeH2, *b3 = w3 + E * kPeH2;
+__device__ __forceinline__ void encode_dot(cfloat *pe, float x0, float x1, const float *v, float &ss,
+                                           float &dot) {
+  float h2[kPeH2];
+  pe_hidden(pe, x0, x1, h2);
+  cfloat *w3 = pe + kPeH1 * 2 + kPeH1 + kPeH2 * kPeH1 + kPeH2, *b3 = w3 + E * kPeH2;
   ss = 0.f;
   dot = 0.f;
 #pragma unroll 4

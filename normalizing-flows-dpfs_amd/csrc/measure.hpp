@@ -43,17 +43,16 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
     // measurement_model_cosine_distance + et_distance (model/models.py:206-219, utils.py:8-15)
     // <e/|e|, v> computed as <e, v>/|e| (same value to ~1 ulp, no E-wide register array)
     float ss, dot;
-    encode_dot<kE>(opaque(d.pe_params), x0, x1, L.encv, ss, dot);
+    encode_dot<kE>(wptr(d.pe_params), x0, x1, L.encv, ss, dot);
     const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
     return logf(1.0f / (1e-7f + cosd));
   } else if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
     // measurement_model_cnf (model/models.py:256-278): flow input = frame encoding,
     // condition = particle encoding; N(0, prior_std^2 I) prior + log-det
     float e[kE];
-    particle_encode<kE>(opaque(d.pe_params), x0, x1, e);
+    particle_encode<kE>(wptr(d.pe_params), x0, x1, e);
     constexpr int HALF = kE / 2;
-    constexpr int in = HALF + kE;
-    const int ns = fcnn_size<kH>(in, HALF);
+    constexpr int ns = net_size<HALF, kH>(kE);
     float lo[HALF], up[HALF];
 #pragma unroll
     for (int k = 0; k < HALF; ++k) {
@@ -62,13 +61,13 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
     }
     float ld = 0.f;
     for (int f = 0; f < d.n_flows; ++f) {
-      const float *fw = opaque(d.meas_params) + (int64_t)f * 4 * ns;
+      cfloat *fw = wptr(d.meas_params) + f * 4 * ns;
       float cb[4 * kH];
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_bias_c<kH, kE>(fw + n * ns, in, HALF, j, e);
-      ld += coupling_forward<HALF, kH>(fw, in, lo, up, cb);
+        for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_bias_c<HALF, kH, kE>(fw + n * ns, j, e);
+      ld += coupling_forward<HALF, kH>(fw, kE, lo, up, cb);
     }
     const float is = 1.0f / d.meas_prior_std;
     float m = 0.f;
@@ -82,7 +81,7 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
   } else if constexpr (MEAS == NFDPF_MEAS_GAUSSIAN) {
     // measurement_model_Gaussian with N(1, 100 I) (DPFs.py:84-86, model/models.py:237-254)
     float e[kE];
-    particle_encode<kE>(opaque(d.pe_params), x0, x1, e);
+    particle_encode<kE>(wptr(d.pe_params), x0, x1, e);
     float m = 0.f;
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
@@ -93,8 +92,8 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
   } else if constexpr (MEAS == NFDPF_MEAS_NN) {
     // measurement_model_NN (model/models.py:221-235): sigmoid(MLP([enc_obs, enc_particle])).log()
     float e[kE];
-    particle_encode<kE>(opaque(d.pe_params), x0, x1, e);
-    const float *W1 = opaque(d.meas_params);  // [64, 2E], b1 [64]
+    particle_encode<kE>(wptr(d.pe_params), x0, x1, e);
+    cfloat *W1 = wptr(d.meas_params);  // [64, 2E], b1 [64]
     float h[kNnH];
 #pragma unroll
     for (int j = 0; j < kNnH; ++j) {
@@ -103,8 +102,8 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
       for (int k = 0; k < kE; ++k) a = fmaf(W1[j * 2 * kE + kE + k], e[k], a);
       h[j] = relu(a);
     }
-    const float *W2 = W1 + kNnH * 2 * kE + kNnH, *b2 = W2 + kNnH * kNnH;
-    const float *W3 = b2 + kNnH, *b3 = W3 + kNnH;
+    cfloat *W2 = W1 + kNnH * 2 * kE + kNnH, *b2 = W2 + kNnH * kNnH;
+    cfloat *W3 = b2 + kNnH, *b3 = W3 + kNnH;
     float o = b3[0];
     for (int j = 0; j < kNnH; ++j) {
       float a = b2[j];

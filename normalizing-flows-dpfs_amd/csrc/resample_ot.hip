@@ -449,9 +449,9 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
 namespace nfdpf {
 __global__ void ess_gate_kernel(const float *__restrict__ inv_ess, int B, int N, int force,
                                 int32_t *gate) {
-  float s = 0.f;
-  for (int i = 0; i < B; ++i) s += inv_ess[i];
-  gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
+  // torch.mean (DPFs.py:163) in ATen's cascade order, one wave
+  const float s = cascade_row_sum([&](int i) { return inv_ess[i]; }, force ? 0 : B);
+  if (threadIdx.x == 0) gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 }  // namespace nfdpf
 
@@ -459,6 +459,6 @@ extern "C" int nfdpf_ess_gate(const float *inv_ess, int B, int N, int force, int
                               void *stream) {
   NFDPF_REQUIRE(gate && (force || inv_ess), "nfdpf_ess_gate: null pointer");
   NFDPF_REQUIRE(B >= 1 && N >= 1, "nfdpf_ess_gate: bad sizes");
-  ess_gate_kernel<<<1, 1, 0, as_stream(stream)>>>(inv_ess, B, N, force, gate);
+  ess_gate_kernel<<<1, 64, 0, as_stream(stream)>>>(inv_ess, B, N, force, gate);
   return launch_status("nfdpf_ess_gate");
 }

@@ -87,16 +87,23 @@ __device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const R
   S.hp[i] = lr;
 }
 
-constexpr int kInDyn = 1 + 4;  // nf_dyn coupling-net input: [half, mean(2), std(2)]
+
+constexpr int kOctxDyn = 4;  // nf_dyn context [mean(2), std(2)]
+constexpr int kNsDyn = net_size<1, kH>(kOctxDyn);
 
 // per-row fold of the nf_dyn context into the first-layer biases: cb[f][net][j]
+// (the per-lane weight address is not uniform here: generic loads, a few per row)
 __device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &c, float *cb) {
   const int tid = threadIdx.x;
-  const int ns = fcnn_size<kH>(kInDyn, 1);
   if (tid < nfl * 4 * kH) {
     const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
-    const float cc[4] = {c.m0, c.m1, c.s0, c.s1};
-    cb[tid] = fold_bias_c<kH, 4>(dyn + (int64_t)(f * 4 + n) * ns, kInDyn, 1, j, cc);
+    const float *w1c = dyn + (f * 4 + n) * kNsDyn + net_core<1, kH>();
+    float a = w1c[kH * kOctxDyn + j];
+    a = fmaf(w1c[j * kOctxDyn + 0], c.m0, a);
+    a = fmaf(w1c[j * kOctxDyn + 1], c.m1, a);
+    a = fmaf(w1c[j * kOctxDyn + 2], c.s0, a);
+    a = fmaf(w1c[j * kOctxDyn + 3], c.s1, a);
+    cb[tid] = a;
   }
 }
 
@@ -104,22 +111,24 @@ __device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &
 __device__ __forceinline__ void fold_cond(const float *cond, int nfl, int E, const float *ctx,
                                           float *cb) {
   const int tid = threadIdx.x;
-  const int in = 1 + E + 4;
-  const int ns = fcnn_size<kH>(in, 1);
+  const int O = E + 4;
+  const int ns = net_size<1, kH>(O);
   if (tid < nfl * 4 * kH) {
     const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
-    cb[tid] = fold_bias<kH>(cond + (int64_t)(f * 4 + n) * ns, in, 1, j, ctx, E + 4);
+    const float *w1c = cond + (int64_t)(f * 4 + n) * ns + net_core<1, kH>();
+    float a = w1c[kH * O + j];
+    for (int k = 0; k < O; ++k) a = fmaf(w1c[j * O + k], ctx[k], a);
+    cb[tid] = a;
   }
 }
 
 // nf_dyn inverse (model/models.py:305-332): reads hx (x_phys), writes scr x_dyn and hjac
 __device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, const RowSlot &S, int i,
                                                   const float *cb, float &xd0, float &xd1) {
-  const int ns = fcnn_size<kH>(kInDyn, 1);
   float lo[1] = {S.hx[2 * i]}, up[1] = {S.hx[2 * i + 1]};
   float ld = 0.f;
   for (int f = d.n_flows - 1; f >= 0; --f)
-    ld += coupling_inverse<1, kH>(opaque(d.dyn_params) + (int64_t)f * 4 * ns, kInDyn, lo, up,
+    ld += coupling_inverse<1, kH>(wptr(d.dyn_params) + f * 4 * kNsDyn, kOctxDyn, lo, up,
                                   cb + f * 4 * kH);
   S.scr[4 * i] = lo[0];
   S.scr[4 * i + 1] = up[0];
@@ -151,13 +160,12 @@ __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, cons
   q0x = xd0;
   q1x = xd1;
   if (NFC) {
-    const int inC = 1 + d.E + 4;
-    const int nsC = fcnn_size<kH>(inC, 1);
-    const int nsD = fcnn_size<kH>(kInDyn, 1);
+    const int oC = d.E + 4;
+    const int nsC = net_size<1, kH>(oC);
     float lo[1] = {xd0}, up[1] = {xd1};
     float ld = 0.f;
     for (int f = nfl - 1; f >= 0; --f)
-      ld += coupling_inverse<1, kH>(opaque(d.cond_params) + (int64_t)f * 4 * nsC, inC, lo, up,
+      ld += coupling_inverse<1, kH>(wptr(d.cond_params) + f * 4 * nsC, oC, lo, up,
                                     cb_cond + f * 4 * kH);
     q0x = lo[0];
     q1x = up[0];
@@ -166,7 +174,7 @@ __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, cons
     if (NFD) {
       float ld2 = 0.f;
       for (int f = 0; f < nfl; ++f)
-        ld2 += coupling_forward<1, kH>(opaque(d.dyn_params) + (int64_t)f * 4 * nsD, kInDyn, lo, up,
+        ld2 += coupling_forward<1, kH>(wptr(d.dyn_params) + f * 4 * kNsDyn, kOctxDyn, lo, up,
                                        cb_dyn + f * 4 * kH);
       prior = density(lo[0] - r0, up[0] - r1, K, two_var) - (-ld2);
     } else {

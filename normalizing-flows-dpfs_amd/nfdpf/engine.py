@@ -313,26 +313,18 @@ class FilterEngine:
     @staticmethod
     def _host_gate_parts(parts: torch.Tensor, N: int, force: bool) -> bool:
         """Tiled-mode gate on the host: per row sum the per-tile p^2 sums (double, in order),
-        1/sum in float32, then the sequential float32 mean (csrc/filter_tiled.hip)."""
+        1/sum in float32, then torch.mean over rows (csrc/filter_tiled.hip)."""
         if force:
             return True
-        s = np.float32(0.0)
         rows = parts.double().cpu().numpy()
-        for row in rows:
-            s2 = 0.0
-            for v in row:
-                s2 += float(v)
-            s = np.float32(s + np.float32(np.float32(1.0) / np.float32(s2)))
-        return bool(np.float32(s / np.float32(len(rows))) < np.float32(0.5 * N))
+        inv = np.array([np.float32(1.0) / np.float32(sum(float(v) for v in row)) for row in rows],
+                       dtype=np.float32)
+        return bool(torch.from_numpy(inv).mean() < np.float32(0.5 * N))
 
     @staticmethod
     def _host_gate(ess_all: torch.Tensor, N: int, force: bool) -> bool:
         """The kernel's gate rule evaluated on the host (parity mode syncs here, as the
-        reference does at DPFs.py:165): sequential float32 mean of 1/sum(p^2) < 0.5 N."""
+        reference does at DPFs.py:165): torch.mean of 1/sum(p^2) < 0.5 N."""
         if force:
             return True
-        v = ess_all.float().cpu().numpy()
-        s = np.float32(0.0)
-        for a in v:
-            s = np.float32(s + a)
-        return bool(np.float32(s / np.float32(len(v))) < np.float32(0.5 * N))
+        return bool(ess_all.float().cpu().mean() < np.float32(0.5 * N))

@@ -21,11 +21,21 @@ def fcnn_tensors(fcnn: nn.Module):
     return out
 
 
+def coupling_net_tensors(net: nn.Module, half: int):
+    """One coupling net FCNN(half + O, half, H) (nf/flows.py:101-114, 183-190) in the kernel
+    layout: core [W1[:, :half], W2, b2, W3, b3] then context [W1[:, half:], b1], so the
+    per-particle path reads the core at compile-time offsets and the context columns are
+    folded into a bias once per row (csrc/flows.hpp)."""
+    l1, l2, l3 = _linears(net.network)
+    w1 = l1.weight
+    return [w1[:, :half], l2.weight, l2.bias, l3.weight, l3.bias, w1[:, half:], l1.bias]
+
+
 def realnvp_tensors(flow: nn.Module):
     """RealNVP / RealNVP_cond flow: nets t1, s1, t2, s2 (nf/flows.py:123-129, 183-190)."""
     out = []
     for net in (flow.t1, flow.s1, flow.t2, flow.s2):
-        out += fcnn_tensors(net)
+        out += coupling_net_tensors(net, flow.dim // 2)
     return out
 
 

@@ -18,13 +18,17 @@ DEV = torch.device("cuda:0")
 
 
 def _flow_blob(w, n_flows):
-    from nfdpf.pack import fcnn_tensors  # noqa
+    """Coupling nets in the kernel layout (include/nfdpf.h): per net
+    [W1[:, :half], W2, b2, W3, b3, W1[:, half:], b1]."""
     parts = []
     for i in range(n_flows):
         pre = "" if n_flows == 1 else f"flows.{i}."
         for net in ("t1", "s1", "t2", "s2"):
-            for layer in (0, 2, 4):
-                parts += [w[f"{pre}{net}.network.{layer}.weight"], w[f"{pre}{net}.network.{layer}.bias"]]
+            g = lambda layer, k: w[f"{pre}{net}.network.{layer}.{k}"]  # noqa: E731
+            half = g(4, "weight").shape[0]
+            w1 = g(0, "weight")
+            parts += [w1[:, :half], g(2, "weight"), g(2, "bias"), g(4, "weight"), g(4, "bias"),
+                      w1[:, half:], g(0, "bias")]
     return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
 
 
@@ -248,17 +252,29 @@ def _oracle64_one_step(fx, monkeypatch):
     return {k: torch.stack(v, 1).numpy() for k, v in out.items()}
 
 
-def _check_envelope(ours, ref32, ref64, rtol, atol, what, k=2.0):
-    """|ours - ref32| <= k * E + rtol |ref32| + atol, where E is the reference's own float32
-    rounding noise on the same (batch row, step): max_n |ref64 - ref32| over the N particles
-    (all particles of a row share the row's normalisation and context)."""
+def _check_envelope(ours, ref32, ref64, rtol, atol, what, k_stat=3.0, k_row=16.0):
+    """Ours must be as accurate as the reference's own float32 run, both measured against the
+    float64 evaluation of the same step (ref64):
+
+      max  |ours - ref64| <= k_stat * max  |ref32 - ref64| + atol      (whole case)
+      mean |ours - ref64| <= k_stat * mean |ref32 - ref64| + atol
+      |ours - ref64| <= k_row * E_row + rtol |ref64| + atol             (every element)
+
+    E_row = max over the N particles of |ref32 - ref64| on that (batch row, step): the
+    particles of a row share its context and normalisation, so the row's rounding noise is
+    one quantity; k_row covers rows where the reference's own error happens to be small
+    (measured on MI355X: worst row ratio 12.6, case max ratio 2.2, mean ratio 3.2)."""
     ours, ref32, ref64 = (np.asarray(a, dtype=np.float64) for a in (ours, ref32, ref64))
-    env = np.abs(ref64 - ref32)
-    env = env.max(axis=2, keepdims=True) if env.ndim >= 3 else env
-    err = np.abs(ours - ref32)
-    bound = k * env + rtol * np.abs(ref32) + atol
-    assert np.all(err <= bound), f"{what}: worst excess {(err - bound).max():.3e} (env {env.max():.3e})"
-    return float(np.mean(err <= rtol * np.abs(ref32) + atol))
+    e_ref = np.abs(ref32 - ref64)
+    e_ours = np.abs(ours - ref64)
+    assert e_ours.max() <= k_stat * e_ref.max() + atol, \
+        f"{what}: max err {e_ours.max():.3e} vs reference float32 {e_ref.max():.3e}"
+    assert e_ours.mean() <= k_stat * e_ref.mean() + atol, \
+        f"{what}: mean err {e_ours.mean():.3e} vs reference float32 {e_ref.mean():.3e}"
+    env = e_ref.max(axis=2, keepdims=True) if e_ref.ndim >= 3 else e_ref
+    bound = k_row * env + rtol * np.abs(ref64) + atol
+    assert np.all(e_ours <= bound), f"{what}: worst excess {(e_ours - bound).max():.3e} (env {env.max():.3e})"
+    return float(np.mean(e_ours <= rtol * np.abs(ref64) + atol))
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
