@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--force-resample", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--batch", type=int, default=None, help="override B per GPU (exploration only)")
     ap.add_argument("--kernel", default="tiled", choices=["tiled", "fused"],
                     help="tiled: multi-CU pipeline per step; fused: one workgroup per batch row")
     args = ap.parse_args()
@@ -133,6 +134,7 @@ def main():
     from DPFs import DPF
     from nfdpf.engine import FilterEngine, ShardInfo
     flags, B, N, T, F_STEP, F_PROP = CONFIGS[args.config]
+    B = args.batch or B
     F_ALG = F_PROP if args.kernel == "tiled" else F_STEP
     torch.manual_seed(2)
     a = make_args(flags, B, N, T, {"force_resample": args.force_resample})

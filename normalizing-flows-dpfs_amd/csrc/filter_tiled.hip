@@ -31,6 +31,7 @@ struct TiledWs {
   float *umax;      // [B][tiles] max of the unshifted log-weight u
   double *usum;     // [B][tiles] sum exp(u - umax)
   float *S2;        // [B] soft-resampling renormaliser
+  int *fire;        // [B] gate decision taken by K0 (soft resampler)
   double *fin;      // [B][T][tiles][4] sum p^2, sum p x0, sum p x1, sum logw
 };
 
@@ -39,7 +40,7 @@ __host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / 
 
 static int64_t tiled_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(bt * 32) * 2 + al256(bt * 4) * 2 + al256(bt * 8) + al256((int64_t)B * 4) +
+  return al256(bt * 32) * 2 + al256(bt * 4) * 2 + al256(bt * 8) + al256((int64_t)B * 4) * 2 +
          al256(bt * T * 32);
 }
 
@@ -58,6 +59,8 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   w.usum = (double *)p;
   p += al256(bt * 8);
   w.S2 = (float *)p;
+  p += al256((int64_t)B * 4);
+  w.fire = (int *)p;
   p += al256((int64_t)B * 4);
   w.fin = (double *)p;
   return w;
@@ -78,6 +81,26 @@ __device__ __forceinline__ bool tiled_gate(const nfdpf_filter_desc &d, int tiles
       },
       d.B_global);
   return (s / (float)d.B_global) < 0.5f * (float)d.N;
+}
+
+// The same gate, block-parallel (all threads call): thread r stages row r's 1 / sum p^2 in
+// `buf` (one round trip for the whole batch), wave 0 folds them in cascade order.
+__device__ bool tiled_gate_block(const nfdpf_filter_desc &d, int tiles, float *buf, int *flag) {
+  if (d.gate) return d.gate[0] != 0;
+  if (d.force_resample) return true;
+  const double *parts = reinterpret_cast<const double *>(d.ess_all);
+  for (int r = threadIdx.x; r < d.B_global; r += blockDim.x) {
+    double s2 = 0.0;
+    for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
+    buf[r] = 1.0f / (float)s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const float s = cascade_row_sum([&](int r) { return buf[r]; }, d.B_global);
+    if (threadIdx.x == 0) *flag = (s / (float)d.B_global) < 0.5f * (float)d.N;
+  }
+  __syncthreads();
+  return *flag != 0;
 }
 
 // combine the 4-sum partials of row b -> context
@@ -111,9 +134,12 @@ __device__ __forceinline__ void store_sums4(double *dst, double a, double b, dou
 __global__ __launch_bounds__(512) void tiled_soft_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   extern __shared__ float Cbuf[];
   __shared__ StepShared L;
+  __shared__ int fire_sh;
   const int tiles = n_tiles(d.N);
-  if (d.resampler != NFDPF_RESAMPLE_SOFT || !tiled_gate(d, tiles)) return;
   const int b = blockIdx.x;
+  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh);
+  if (threadIdx.x == 0) ws.fire[b] = fire;  // the motion kernel's decision for this row
+  if (!fire) return;
   const RowSlot S = row_slot(d, b);
   const float *xprev = d.x_prev + b * d.x_prev_rs;
   const float *pprev = d.p_prev + b * d.p_prev_rs;
@@ -157,7 +183,8 @@ __global__ __launch_bounds__(kTile) void tiled_motion_kernel(const nfdpf_filter_
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
   const int64_t grow = d.row_base + b;
-  const bool fire = tiled_gate(d, tiles);
+  // soft: the decision K0 took for this row; OT: the gate launched before the resampler
+  const bool fire = d.resampler == NFDPF_RESAMPLE_SOFT ? ws.fire[b] != 0 : tiled_gate(d, tiles);
   const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
   const RowSlot S = row_slot(d, b);
   double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
@@ -177,7 +204,7 @@ __global__ __launch_bounds__(kTile) void tiled_motion_kernel(const nfdpf_filter_
 // ---- K2: nf_dyn inverse
 __global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ double shd[16];
-  __shared__ float cb[kMaxFlows * 4 * kH];
+  __shared__ f2 cb[kMaxFlows * 2 * kH];
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
@@ -425,6 +452,8 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
   if (d.resampler == NFDPF_RESAMPLE_SOFT) {
     NFDPF_REQUIRE(d.N <= kStepMaxN, "nfdpf_filter_step_tiled: soft resampling supports N <= %d", kStepMaxN);
     NFDPF_REQUIRE(d.lin || d.phase == 2, "nfdpf_filter_step_tiled: soft resampling needs lin");
+    NFDPF_REQUIRE(d.B_global <= kStepMaxN, "nfdpf_filter_step_tiled: soft resampling supports B_global <= %d",
+                  kStepMaxN);
   } else {
     NFDPF_REQUIRE(d.ot_x || d.phase == 2, "nfdpf_filter_step_tiled: OT path needs ot_x");
   }
@@ -436,7 +465,7 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
   const dim3 g(n_tiles(d.N), d.B);
   if (d.phase != 2) {
     if (d.resampler == NFDPF_RESAMPLE_SOFT)
-      tiled_soft_kernel<<<d.B, 512, d.N * sizeof(float), st>>>(d, ws);
+      tiled_soft_kernel<<<d.B, 512, std::max(d.N, d.B_global) * sizeof(float), st>>>(d, ws);
     tiled_motion_kernel<<<g, kTile, 0, st>>>(d, ws);
     if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
     hipEvent_t *ev = (hipEvent_t *)d.prof_events;

@@ -30,14 +30,14 @@ __global__ __launch_bounds__(kStackBlock) void cond_stack_kernel(
   }
   const float *c = cond ? cond + (r / cond_group) * O : nullptr;
   float ld = 0.f;
-  float cb[4 * H];
+  f2 cb[2 * H];
   for (int f = 0; f < n_flows; ++f) {
     const int fi = INV ? n_flows - 1 - f : f;
-    cfloat *fw = wptr(params) + fi * 4 * ns;
+    cf2 *fw = wptr2(params) + fi * 2 * ns;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int j = 0; j < H; ++j) cb[n * H + j] = fold_bias<HALF, H>(fw + n * ns, O, j, c);
+      for (int j = 0; j < H; ++j) cb[n * H + j] = fold_pair<HALF, H>(fw + n * ns, O, j, c);
     const float l = INV ? coupling_inverse<HALF, H>(fw, O, lo, up, cb)
                         : coupling_forward<HALF, H>(fw, O, lo, up, cb);
     ld += l;

@@ -5,17 +5,36 @@
 // from SGPRs -- no LDS traffic, no VGPR per weight.  One particle per lane; the hidden
 // width (8) is far too narrow for a 16x16 MFMA tile.
 //
-// Coupling-net layout (nfdpf.pack.realnvp_tensors, include/nfdpf.h):
-//   [ W1[:, :HALF] (H x HALF) | W2 (H x H) | b2 (H) | W3 (HALF x H) | b3 (HALF)   <- "core",
+// Coupling layout (nfdpf.pack.coupling_pair_tensors, include/nfdpf.h): the nets t and s of
+// one coupling half share their input, so they are stored interleaved elementwise (float2
+// {t, s}) and advance together, one v_pk_fma_f32 per weight pair:
+//   [ W1[:, :HALF] (H x HALF) | W2 (H x H) | b2 (H) | W3 (HALF x H) | b3 (HALF)   <- core,
 //     W1[:, HALF:] (H x O) | b1 (H) ]                                              <- context
-// The per-particle path touches only the core; the context columns are folded into a bias
-// once per batch row (or per particle when the condition is per particle).
+// (every entry a {t, s} pair).  A flow is pair (t1, s1) then pair (t2, s2).  The per-particle
+// path touches only the core; the context columns are folded into a bias pair once per batch
+// row (or per particle when the condition is per particle).  Each component sees exactly the
+// fma sequence of an unpacked net.
 #pragma once
 
 #include "common.hpp"
 
 namespace nfdpf {
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef const f2 __attribute__((address_space(4))) cf2;
+
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// tanh_fast (common.hpp) on both components, the non-transcendental steps packed
+__device__ __forceinline__ f2 tanh2(f2 x) {
+  const f2 y = x * splat(2.8853900817779268f);
+  const f2 d = f2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + splat(1.0f);
+  return pfma(splat(-2.0f), f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, splat(1.0f));
+}
+__device__ __forceinline__ cf2 *wptr2(const float *p) { return (cf2 *)wptr(p); }
+__device__ __forceinline__ f2 relu2(f2 x) { return f2{relu(x.x), relu(x.y)}; }
+
+// pairs in a (t, s) core / a whole (t, s) coupling half
 template <int HALF, int H>
 __host__ __device__ constexpr int net_core() {
   return H * HALF + H * H + H + HALF * H + HALF;
@@ -25,65 +44,53 @@ __host__ __device__ constexpr int net_size(int O) {
   return net_core<HALF, H>() + H * O + H;
 }
 
-// cb[j] = b1[j] + sum_c W1[j, HALF + c] * ctx[c]  (context folded into the first layer)
+// cb[j] = b1[j] + sum_c W1[j, HALF + c] * ctx[c], for t and s at once
 template <int HALF, int H>
-__device__ __forceinline__ float fold_bias(cfloat *w, int O, int j, const float *ctx) {
-  cfloat *w1c = w + net_core<HALF, H>();
-  float a = w1c[H * O + j];
-  for (int c = 0; c < O; ++c) a = fmaf(w1c[j * O + c], ctx[c], a);
+__device__ __forceinline__ f2 fold_pair(cf2 *w, int O, int j, const float *ctx) {
+  cf2 *w1c = w + net_core<HALF, H>();
+  f2 a = w1c[H * O + j];
+  for (int c = 0; c < O; ++c) a = pfma(w1c[j * O + c], splat(ctx[c]), a);
   return a;
 }
 template <int HALF, int H, int O>
-__device__ __forceinline__ float fold_bias_c(cfloat *w, int j, const float (&ctx)[O]) {
-  cfloat *w1c = w + net_core<HALF, H>();
-  float a = w1c[H * O + j];
+__device__ __forceinline__ f2 fold_pair_c(cf2 *w, int j, const float (&ctx)[O]) {
+  cf2 *w1c = w + net_core<HALF, H>();
+  f2 a = w1c[H * O + j];
 #pragma unroll
-  for (int c = 0; c < O; ++c) a = fmaf(w1c[j * O + c], ctx[c], a);
+  for (int c = 0; c < O; ++c) a = pfma(w1c[j * O + c], splat(ctx[c]), a);
   return a;
 }
 
-// Nets t and s of one coupling half (same input u), first layer on the HALF leading columns
-// plus the folded biases cbt/cbs.  Outputs t[HALF], s[HALF].
+// Nets t and s of one coupling half on input u, first layer on the HALF leading columns plus
+// the folded bias pairs cb[H].  Outputs t[HALF], s[HALF].
 template <int HALF, int H>
-__device__ __forceinline__ void ts_pair(cfloat *wt, cfloat *ws, const float (&u)[HALF],
-                                        const float *cbt, const float *cbs, float (&t)[HALF],
-                                        float (&s)[HALF]) {
-  float ht[H], hs[H];
+__device__ __forceinline__ void ts_pair(cf2 *w, const float (&u)[HALF], const f2 *cb,
+                                        float (&t)[HALF], float (&s)[HALF]) {
+  f2 h[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
-    float at = cbt[j], as = cbs[j];
+    f2 a = cb[j];
 #pragma unroll
-    for (int k = 0; k < HALF; ++k) {
-      at = fmaf(wt[j * HALF + k], u[k], at);
-      as = fmaf(ws[j * HALF + k], u[k], as);
-    }
-    ht[j] = tanh_fast(at);
-    hs[j] = tanh_fast(as);
+    for (int k = 0; k < HALF; ++k) a = pfma(w[j * HALF + k], splat(u[k]), a);
+    h[j] = tanh2(a);
   }
-  cfloat *w2t = wt + H * HALF, *w2s = ws + H * HALF;
-  float gt[H], gs[H];
+  cf2 *w2 = w + H * HALF;
+  f2 g[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
-    float at = w2t[H * H + j], as = w2s[H * H + j];
+    f2 a = w2[H * H + j];
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      at = fmaf(w2t[j * H + k], ht[k], at);
-      as = fmaf(w2s[j * H + k], hs[k], as);
-    }
-    gt[j] = tanh_fast(at);
-    gs[j] = tanh_fast(as);
+    for (int k = 0; k < H; ++k) a = pfma(w2[j * H + k], h[k], a);
+    g[j] = tanh2(a);
   }
-  cfloat *w3t = w2t + H * H + H, *w3s = w2s + H * H + H;
+  cf2 *w3 = w2 + H * H + H;
 #pragma unroll
   for (int o = 0; o < HALF; ++o) {
-    float at = w3t[HALF * H + o], as = w3s[HALF * H + o];
+    f2 a = w3[HALF * H + o];
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      at = fmaf(w3t[o * H + k], gt[k], at);
-      as = fmaf(w3s[o * H + k], gs[k], as);
-    }
-    t[o] = at;
-    s[o] = as;
+    for (int k = 0; k < H; ++k) a = pfma(w3[o * H + k], g[k], a);
+    t[o] = a.x;
+    s[o] = a.y;
   }
 }
 
@@ -109,36 +116,37 @@ __device__ __forceinline__ float half_sum(const float (&s)[HALF]) {
   }
 }
 
-// One RealNVP_cond flow (nets t1,s1,t2,s2 of net_size(O) floats each); cb = folded biases
-// [4][H].  Forward: nf/flows.py:215-226; inverse: :228-239.  Returns the flow's log-det.
+// One RealNVP_cond flow: pair (t1, s1) then pair (t2, s2), net_size(O) pairs each; cb = the
+// folded bias pairs [2][H].  Forward: nf/flows.py:215-226; inverse: :228-239.  Returns the
+// flow's log-det.
 template <int HALF, int H>
-__device__ __forceinline__ float coupling_forward(cfloat *fw, int O, float (&lo)[HALF],
-                                                  float (&up)[HALF], const float *cb) {
+__device__ __forceinline__ float coupling_forward(cf2 *fw, int O, float (&lo)[HALF],
+                                                  float (&up)[HALF], const f2 *cb) {
   const int ns = net_size<HALF, H>(O);
   float t[HALF], s[HALF];
-  ts_pair<HALF, H>(fw, fw + ns, lo, cb, cb + H, t, s);
+  ts_pair<HALF, H>(fw, lo, cb, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) up[k] = t[k] + up[k] * expf(s[k]);
   const float l1 = half_sum<HALF>(s);
-  ts_pair<HALF, H>(fw + 2 * ns, fw + 3 * ns, up, cb + 2 * H, cb + 3 * H, t, s);
+  ts_pair<HALF, H>(fw + ns, up, cb + H, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) lo[k] = t[k] + lo[k] * expf(s[k]);
   return l1 + half_sum<HALF>(s);
 }
 
 template <int HALF, int H>
-__device__ __forceinline__ float coupling_inverse(cfloat *fw, int O, float (&lo)[HALF],
-                                                  float (&up)[HALF], const float *cb) {
+__device__ __forceinline__ float coupling_inverse(cf2 *fw, int O, float (&lo)[HALF],
+                                                  float (&up)[HALF], const f2 *cb) {
   const int ns = net_size<HALF, H>(O);
   float t[HALF], s[HALF];
-  ts_pair<HALF, H>(fw + 2 * ns, fw + 3 * ns, up, cb + 2 * H, cb + 3 * H, t, s);
+  ts_pair<HALF, H>(fw + ns, up, cb + H, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) {
     lo[k] = (lo[k] - t[k]) * expf(-s[k]);
     s[k] = -s[k];
   }
   const float l2 = half_sum<HALF>(s);
-  ts_pair<HALF, H>(fw, fw + ns, lo, cb, cb + H, t, s);
+  ts_pair<HALF, H>(fw, lo, cb, t, s);
 #pragma unroll
   for (int k = 0; k < HALF; ++k) {
     up[k] = (up[k] - t[k]) * expf(-s[k]);
@@ -249,38 +257,50 @@ __device__ __forceinline__ float maf_inverse(cfloat *fw, float (&v)[D]) {
 
 // ----------------------------------------------------------------------------------------
 // particle encoder (model/models.py:130-150): Linear(2,16) ReLU Linear(16,32) ReLU Linear(32,E)
+// Weights in row_pairs layout (nfdpf.pack.paired_mlp_tensors): outputs 2m, 2m+1 advance
+// together, W[m][k] = {W[2m, k], W[2m+1, k]}; biases as stored by nn.Linear.
 // ----------------------------------------------------------------------------------------
 constexpr int kPeH1 = 16, kPeH2 = 32;
 __host__ __device__ constexpr int pe_size(int E) {
   return kPeH1 * 2 + kPeH1 + kPeH2 * kPeH1 + kPeH2 + E * kPeH2 + E;
 }
+constexpr int kPeB1 = kPeH1 * 2, kPeW2 = kPeB1 + kPeH1, kPeB2 = kPeW2 + kPeH2 * kPeH1,
+              kPeW3 = kPeB2 + kPeH2;
 
-__device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, float (&h2)[kPeH2]) {
-  float h1[kPeH1];
-  cfloat *b1 = pe + kPeH1 * 2;
+__device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, f2 (&h2)[kPeH2 / 2]) {
+  cf2 *w1 = (cf2 *)pe, *b1 = (cf2 *)(pe + kPeB1);
+  f2 h1[kPeH1 / 2];
 #pragma unroll
-  for (int j = 0; j < kPeH1; ++j) h1[j] = relu(fmaf(pe[2 * j + 1], x1, fmaf(pe[2 * j], x0, b1[j])));
-  cfloat *w2 = b1 + kPeH1, *b2 = w2 + kPeH2 * kPeH1;
+  for (int m = 0; m < kPeH1 / 2; ++m)
+    h1[m] = relu2(pfma(w1[2 * m + 1], splat(x1), pfma(w1[2 * m], splat(x0), b1[m])));
+  cf2 *w2 = (cf2 *)(pe + kPeW2), *b2 = (cf2 *)(pe + kPeB2);
 #pragma unroll
-  for (int j = 0; j < kPeH2; ++j) {
-    float a = b2[j];
+  for (int m = 0; m < kPeH2 / 2; ++m) {
+    f2 a = b2[m];
 #pragma unroll
-    for (int k = 0; k < kPeH1; ++k) a = fmaf(w2[j * kPeH1 + k], h1[k], a);
-    h2[j] = relu(a);
+    for (int k = 0; k < kPeH1; ++k) a = pfma(w2[m * kPeH1 + k], splat(k & 1 ? h1[k >> 1].y : h1[k >> 1].x), a);
+    h2[m] = relu2(a);
   }
 }
 
 template <int E>
+__device__ __forceinline__ f2 pe_out(cfloat *pe, const f2 (&h2)[kPeH2 / 2], int m) {
+  cf2 *w3 = (cf2 *)(pe + kPeW3), *b3 = (cf2 *)(pe + kPeW3 + E * kPeH2);
+  f2 a = b3[m];
+#pragma unroll
+  for (int k = 0; k < kPeH2; ++k) a = pfma(w3[m * kPeH2 + k], splat(k & 1 ? h2[k >> 1].y : h2[k >> 1].x), a);
+  return a;
+}
+
+template <int E>
 __device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, float (&e)[E]) {
-  float h2[kPeH2];
+  f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
-  cfloat *w3 = pe + kPeH1 * 2 + kPeH1 + kPeH2 * kPeH1 + kPeH2, *b3 = w3 + E * kPeH2;
 #pragma unroll
-  for (int j = 0; j < E; ++j) {
-    float a = b3[j];
-#pragma unroll
-    for (int k = 0; k < kPeH2; ++k) a = fmaf(w3[j * kPeH2 + k], h2[k], a);
-    e[j] = a;
+  for (int m = 0; m < E / 2; ++m) {
+    const f2 a = pe_out<E>(pe, h2, m);
+    e[2 * m] = a.x;
+    e[2 * m + 1] = a.y;
   }
 }
 
@@ -289,18 +309,17 @@ __device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, 
 template <int E>
 __device__ __forceinline__ void encode_dot(cfloat *pe, float x0, float x1, const float *v, float &ss,
                                            float &dot) {
-  float h2[kPeH2];
+  f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
-  cfloat *w3 = pe + kPeH1 * 2 + kPeH1 + kPeH2 * kPeH1 + kPeH2, *b3 = w3 + E * kPeH2;
   ss = 0.f;
   dot = 0.f;
-#pragma unroll 4
-  for (int j = 0; j < E; ++j) {
-    float a = b3[j];
-#pragma unroll
-    for (int k = 0; k < kPeH2; ++k) a = fmaf(w3[j * kPeH2 + k], h2[k], a);
-    ss = fmaf(a, a, ss);
-    dot = fmaf(a, v[j], dot);
+#pragma unroll 2
+  for (int m = 0; m < E / 2; ++m) {
+    const f2 a = pe_out<E>(pe, h2, m);
+    ss = fmaf(a.x, a.x, ss);
+    dot = fmaf(a.x, v[2 * m], dot);
+    ss = fmaf(a.y, a.y, ss);
+    dot = fmaf(a.y, v[2 * m + 1], dot);
   }
 }
 

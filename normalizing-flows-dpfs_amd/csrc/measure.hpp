@@ -14,8 +14,8 @@ constexpr int kStepMaxN = 12288;  // soft resampler C[] in LDS
 constexpr int kMaxCtx = 260;      // proposal context [enc (E <= 256), mean, std]
 
 struct StepShared {
-  float cb_dyn[kMaxFlows * 4 * kH];
-  float cb_cond[kMaxFlows * 4 * kH];
+  f2 cb_dyn[kMaxFlows * 2 * kH];   // folded bias pairs [flow][coupling half][j] of nf_dyn
+  f2 cb_cond[kMaxFlows * 2 * kH];  // ... of the proposal flow
   float ctx[kMaxCtx];
   float encv[kE];       // this row's frame encoding (normalised for cos)
   float nnrow[kNnH];    // NN: folded first layer of the obs half
@@ -61,12 +61,12 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
     }
     float ld = 0.f;
     for (int f = 0; f < d.n_flows; ++f) {
-      cfloat *fw = wptr(d.meas_params) + f * 4 * ns;
-      float cb[4 * kH];
+      cf2 *fw = wptr2(d.meas_params) + f * 2 * ns;
+      f2 cb[2 * kH];
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_bias_c<HALF, kH, kE>(fw + n * ns, j, e);
+        for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_pair_c<HALF, kH, kE>(fw + n * ns, j, e);
       ld += coupling_forward<HALF, kH>(fw, kE, lo, up, cb);
     }
     const float is = 1.0f / d.meas_prior_std;
@@ -93,23 +93,26 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
     // measurement_model_NN (model/models.py:221-235): sigmoid(MLP([enc_obs, enc_particle])).log()
     float e[kE];
     particle_encode<kE>(wptr(d.pe_params), x0, x1, e);
-    cfloat *W1 = wptr(d.meas_params);  // [64, 2E], b1 [64]
-    float h[kNnH];
+    // W1 [64, 2E] and W2 [64, 64] in row_pairs layout, W3 [1, 64] and biases plain
+    cfloat *P = wptr(d.meas_params);
+    cf2 *W1 = (cf2 *)P;
+    f2 h[kNnH / 2];
 #pragma unroll
-    for (int j = 0; j < kNnH; ++j) {
-      float a = L.nnrow[j];
+    for (int m = 0; m < kNnH / 2; ++m) {
+      f2 a = f2{L.nnrow[2 * m], L.nnrow[2 * m + 1]};
 #pragma unroll
-      for (int k = 0; k < kE; ++k) a = fmaf(W1[j * 2 * kE + kE + k], e[k], a);
-      h[j] = relu(a);
+      for (int k = 0; k < kE; ++k) a = pfma(W1[m * 2 * kE + kE + k], splat(e[k]), a);
+      h[m] = relu2(a);
     }
-    cfloat *W2 = W1 + kNnH * 2 * kE + kNnH, *b2 = W2 + kNnH * kNnH;
-    cfloat *W3 = b2 + kNnH, *b3 = W3 + kNnH;
+    cf2 *W2 = (cf2 *)(P + kNnH * 2 * kE + kNnH), *b2 = (cf2 *)(P + kNnH * 2 * kE + kNnH + kNnH * kNnH);
+    cfloat *W3 = P + kNnH * 2 * kE + kNnH + kNnH * kNnH + kNnH, *b3 = W3 + kNnH;
     float o = b3[0];
-    for (int j = 0; j < kNnH; ++j) {
-      float a = b2[j];
+    for (int m = 0; m < kNnH / 2; ++m) {
+      f2 a = b2[m];
 #pragma unroll
-      for (int k = 0; k < kNnH; ++k) a = fmaf(W2[j * kNnH + k], h[k], a);
-      o = fmaf(W3[j], relu(a), o);
+      for (int k = 0; k < kNnH; ++k) a = pfma(W2[m * kNnH + k], splat(k & 1 ? h[k >> 1].y : h[k >> 1].x), a);
+      o = fmaf(W3[2 * m], relu(a.x), o);
+      o = fmaf(W3[2 * m + 1], relu(a.y), o);
     }
     return logf(1.0f / (1.0f + expf(-o)));
   } else {
@@ -133,8 +136,10 @@ __device__ __forceinline__ void measure_row_setup(const float *enc, const float 
     }
   }
   if (MEAS == NFDPF_MEAS_NN && tid < kNnH) {
+    // obs half of likelihood_est's first layer (row_pairs layout: [m][k][2], m = tid / 2)
     float a = meas_params[kNnH * 2 * kE + tid];
-    for (int k = 0; k < kE; ++k) a = fmaf(meas_params[tid * 2 * kE + k], enc[k], a);
+    const float *w = meas_params + (tid >> 1) * 2 * kE * 2 + (tid & 1);
+    for (int k = 0; k < kE; ++k) a = fmaf(w[2 * k], enc[k], a);
     L.nnrow[tid] = a;
   }
 }

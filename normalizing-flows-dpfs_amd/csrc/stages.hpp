@@ -89,47 +89,43 @@ __device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const R
 
 
 constexpr int kOctxDyn = 4;  // nf_dyn context [mean(2), std(2)]
-constexpr int kNsDyn = net_size<1, kH>(kOctxDyn);
+constexpr int kNsDyn = net_size<1, kH>(kOctxDyn);  // pairs per coupling half
 
-// per-row fold of the nf_dyn context into the first-layer biases: cb[f][net][j]
+// Folded first-layer bias of one float of the [flow][half][j][t|s] table, thread tid
 // (the per-lane weight address is not uniform here: generic loads, a few per row)
-__device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &c, float *cb) {
+__device__ __forceinline__ float fold_one(const float *flows, int ns, int O, int tid, const float *ctx) {
+  const int f = tid / (4 * kH), r = tid % (4 * kH);
+  const int n = r / (2 * kH), j = (r >> 1) % kH, w = r & 1;
+  const float *w1c = flows + 2 * ((f * 2 + n) * ns + net_core<1, kH>());
+  float a = w1c[2 * (kH * O + j) + w];
+  for (int c = 0; c < O; ++c) a = fmaf(w1c[2 * (j * O + c) + w], ctx[c], a);
+  return a;
+}
+
+// per-row fold of the nf_dyn context into the first-layer biases (model/models.py:309-315)
+__device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &c, f2 *cb) {
   const int tid = threadIdx.x;
   if (tid < nfl * 4 * kH) {
-    const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
-    const float *w1c = dyn + (f * 4 + n) * kNsDyn + net_core<1, kH>();
-    float a = w1c[kH * kOctxDyn + j];
-    a = fmaf(w1c[j * kOctxDyn + 0], c.m0, a);
-    a = fmaf(w1c[j * kOctxDyn + 1], c.m1, a);
-    a = fmaf(w1c[j * kOctxDyn + 2], c.s0, a);
-    a = fmaf(w1c[j * kOctxDyn + 3], c.s1, a);
-    cb[tid] = a;
+    const float cc[4] = {c.m0, c.m1, c.s0, c.s1};
+    reinterpret_cast<float *>(cb)[tid] = fold_one(dyn, kNsDyn, kOctxDyn, tid, cc);
   }
 }
 
 // per-row fold of the proposal context [enc, mean, std] (model/models.py:338-346); ctx in LDS
-__device__ __forceinline__ void fold_cond(const float *cond, int nfl, int E, const float *ctx,
-                                          float *cb) {
+__device__ __forceinline__ void fold_cond(const float *cond, int nfl, int E, const float *ctx, f2 *cb) {
   const int tid = threadIdx.x;
-  const int O = E + 4;
-  const int ns = net_size<1, kH>(O);
-  if (tid < nfl * 4 * kH) {
-    const int f = tid / (4 * kH), n = (tid / kH) & 3, j = tid % kH;
-    const float *w1c = cond + (int64_t)(f * 4 + n) * ns + net_core<1, kH>();
-    float a = w1c[kH * O + j];
-    for (int k = 0; k < O; ++k) a = fmaf(w1c[j * O + k], ctx[k], a);
-    cb[tid] = a;
-  }
+  if (tid < nfl * 4 * kH)
+    reinterpret_cast<float *>(cb)[tid] = fold_one(cond, net_size<1, kH>(E + 4), E + 4, tid, ctx);
 }
 
 // nf_dyn inverse (model/models.py:305-332): reads hx (x_phys), writes scr x_dyn and hjac
 __device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, const RowSlot &S, int i,
-                                                  const float *cb, float &xd0, float &xd1) {
+                                                  const f2 *cb, float &xd0, float &xd1) {
   float lo[1] = {S.hx[2 * i]}, up[1] = {S.hx[2 * i + 1]};
   float ld = 0.f;
   for (int f = d.n_flows - 1; f >= 0; --f)
-    ld += coupling_inverse<1, kH>(wptr(d.dyn_params) + f * 4 * kNsDyn, kOctxDyn, lo, up,
-                                  cb + f * 4 * kH);
+    ld += coupling_inverse<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
+                                  cb + f * 2 * kH);
   S.scr[4 * i] = lo[0];
   S.scr[4 * i + 1] = up[0];
   if (S.hjac) S.hjac[i] = -ld;
@@ -142,8 +138,8 @@ __device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, co
 // Returns the raw likelihood (0 for an EXTERNAL measurement).
 template <bool NFD, bool NFC, int MEAS>
 __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, const RowSlot &S,
-                                                const StepShared &L, int i, const float *cb_dyn,
-                                                const float *cb_cond, float &q0x, float &q1x) {
+                                                const StepShared &L, int i, const f2 *cb_dyn,
+                                                const f2 *cb_cond, float &q0x, float &q1x) {
   const float K = d.dens_const;
   const float two_var = 2.0f * (d.pos_noise * d.pos_noise);
   const int nfl = d.n_flows;
@@ -165,8 +161,8 @@ __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, cons
     float lo[1] = {xd0}, up[1] = {xd1};
     float ld = 0.f;
     for (int f = nfl - 1; f >= 0; --f)
-      ld += coupling_inverse<1, kH>(wptr(d.cond_params) + f * 4 * nsC, oC, lo, up,
-                                    cb_cond + f * 4 * kH);
+      ld += coupling_inverse<1, kH>(wptr2(d.cond_params) + f * 2 * nsC, oC, lo, up,
+                                    cb_cond + f * 2 * kH);
     q0x = lo[0];
     q1x = up[0];
     const float jac_prop = -ld;
@@ -174,8 +170,8 @@ __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, cons
     if (NFD) {
       float ld2 = 0.f;
       for (int f = 0; f < nfl; ++f)
-        ld2 += coupling_forward<1, kH>(wptr(d.dyn_params) + f * 4 * kNsDyn, kOctxDyn, lo, up,
-                                       cb_dyn + f * 4 * kH);
+        ld2 += coupling_forward<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
+                                       cb_dyn + f * 2 * kH);
       prior = density(lo[0] - r0, up[0] - r1, K, two_var) - (-ld2);
     } else {
       prior = density(q0x - r0, q1x - r1, K, two_var);

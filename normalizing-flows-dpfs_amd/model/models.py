@@ -15,7 +15,7 @@ from nf.flows import FCNN, RealNVP, RealNVP_cond, MAF  # noqa: F401  (reference 
 from nf.models import NormalizingFlowModel, NormalizingFlowModel_cond
 from nfdpf import autograd as _ag
 from nfdpf import ops as _ops
-from nfdpf.pack import blob, flows_tensors, mlp_tensors
+from nfdpf.pack import blob, flows_tensors, paired_mlp_tensors
 from utils import et_distance
 
 device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
@@ -139,14 +139,14 @@ class _MeasRunner:
 
     def hip(self, enc, x):
         m = self.model
-        pe = blob(m, "pe", mlp_tensors(m.particle_encoder), x.device)
+        pe = blob(m, "pe", m.particle_encoder, lambda: paired_mlp_tensors(m.particle_encoder), x.device)
         meas, nfl, pstd = None, 0, 2.5
         if self.kind == "CRNVP":
-            meas = blob(m, "meas", flows_tensors(m.CNF.flows), x.device)
+            meas = blob(m, "meas", m.CNF.flows, lambda: flows_tensors(m.CNF.flows), x.device)
             nfl = len(m.CNF.flows)
             pstd = math.sqrt(float(m.CNF.prior.covariance_matrix[0, 0]))
         elif self.kind == "NN":
-            meas = blob(m, "meas", mlp_tensors(m.likelihood_estimator), x.device)
+            meas = blob(m, "meas", m.likelihood_estimator, lambda: paired_mlp_tensors(m.likelihood_estimator), x.device)
         return (_ops.measurement(self.kind, pe, meas, nfl, enc, x, pstd),)
 
     def torch(self, enc, x):

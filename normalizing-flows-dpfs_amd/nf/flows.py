@@ -105,7 +105,7 @@ class CouplingStack:
         self.hidden, self.inverse, self.prior = hidden, inverse, prior
 
     def hip(self, x, obser):
-        b = blob(self.owner, "stack", flows_tensors(self.flows), x.device)
+        b = blob(self.owner, "stack", self.flows, lambda: flows_tensors(self.flows), x.device)
         pm, ps = self.prior if self.prior is not None else (0.0, 1.0)
         out, ld, lp = _ops.cond_stack(b, len(self.flows), self.dim, self.obser_dim, self.hidden, x,
                                       obser, 1, self.inverse, pm, ps, want_prior=self.prior is not None)
@@ -131,7 +131,7 @@ class MafStack:
         self.owner, self.flows, self.dim, self.hidden, self.inverse = owner, list(flows), dim, hidden, inverse
 
     def hip(self, x):
-        b = blob(self.owner, "maf", flows_tensors(self.flows), x.device)
+        b = blob(self.owner, "maf", self.flows, lambda: flows_tensors(self.flows), x.device)
         return _ops.maf_stack(b, len(self.flows), self.dim, self.hidden, x, self.inverse)
 
     def torch(self, x):

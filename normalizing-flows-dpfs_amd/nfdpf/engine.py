@@ -20,7 +20,7 @@ import torch.distributed as dist
 
 from . import _lib as L
 from . import ops
-from .pack import blob, flows_tensors, mlp_tensors
+from .pack import blob, flows_tensors, paired_mlp_tensors
 
 
 @dataclass
@@ -122,19 +122,19 @@ class FilterEngine:
     def __init__(self, cfg: FilterConfig, models):
         self.cfg = cfg
         self.m = models
-        self.step_events = None  # list -> nfdpf.prof.EventPair around every step's dominant launch
+        self.step_events = None  # list -> nfdpf.prof.EventPair around the dominant launch of step T//2 of every pass
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
         c, m = self.cfg, self.m
-        dyn = blob(m, "dyn", flows_tensors(m.nf_dyn.flows), dev) if c.NF_dyn else None
-        cond = blob(m, "cond", flows_tensors(m.cond_model.flows), dev) if c.NF_cond else None
-        pe = blob(m, "pe", mlp_tensors(m.particle_encoder), dev)
+        dyn = blob(m, "dyn", m.nf_dyn.flows, lambda: flows_tensors(m.nf_dyn.flows), dev) if c.NF_dyn else None
+        cond = blob(m, "cond", m.cond_model.flows, lambda: flows_tensors(m.cond_model.flows), dev) if c.NF_cond else None
+        pe = blob(m, "pe", m.particle_encoder, lambda: paired_mlp_tensors(m.particle_encoder), dev)
         meas = None
         if c.measurement == "CRNVP":
-            meas = blob(m, "meas", flows_tensors(m.cnf_measurement.flows), dev)
+            meas = blob(m, "meas", m.cnf_measurement.flows, lambda: flows_tensors(m.cnf_measurement.flows), dev)
         elif c.measurement == "NN":
-            meas = blob(m, "meas", mlp_tensors(m.likelihood_est), dev)
+            meas = blob(m, "meas", m.likelihood_est, lambda: paired_mlp_tensors(m.likelihood_est), dev)
         return dyn, cond, pe, meas
 
     # -- main loop --------------------------------------------------------------------------
@@ -274,7 +274,8 @@ class FilterEngine:
                 keep.append(xo)
                 d.ot_x = xo.data_ptr()
             d.prof_events = None
-            if self.step_events is not None:
+            if self.step_events is not None and t == T // 2:
+                # one sampled step per pass: an event pair costs ~6 us of stream time
                 from .prof import EventPair
                 ev = EventPair()
                 self.step_events.append(ev)

