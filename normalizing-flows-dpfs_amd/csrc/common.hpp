@@ -106,6 +106,71 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// Row-local wave reductions on DPP (no LDS traffic): butterflies inside quads, then the
+// half-row and row mirrors give every lane its 16-lane row's total; the four row totals are
+// read with v_readlane and added in a fixed order ((r0 + r1) + (r2 + r3)).  The result is
+// wave-uniform.  Fixed order, so deterministic; values are combined commutatively.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(x >> 32), (int)(x >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, l), hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_d<kDppXor1>(v);
+  v += dpp_d<kDppXor2>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  v += dpp_d<kDppMirror>(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f<kDppXor1>(v));
+  v = fmaxf(v, dpp_f<kDppXor2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f<kDppMirror>(v));
+  return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
+
+// Four workgroup sums with ONE barrier; thread q < 4 stores sum q to dst[q].  `sh` holds
+// 4 doubles per wave and must not be in use by a concurrent reduction.
+__device__ __forceinline__ void block_sum4_store(double a, double b, double c, double e, double *sh,
+                                                 double *dst) {
+  a = wave_sum_dpp(a);
+  b = wave_sum_dpp(b);
+  c = wave_sum_dpp(c);
+  e = wave_sum_dpp(e);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[4 * w] = a;
+    sh[4 * w + 1] = b;
+    sh[4 * w + 2] = c;
+    sh[4 * w + 3] = e;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int nw = (blockDim.x + 63) >> 6;
+    double r = sh[threadIdx.x];
+    for (int i = 1; i < nw; ++i) r += sh[4 * i + threadIdx.x];
+    dst[threadIdx.x] = r;
+  }
+}
+
 // Workgroup reductions.  `sh` is LDS scratch of >= 16 elements of T, reused across calls
 // (the leading barrier protects the previous use).  Every thread gets the result.
 template <typename T>

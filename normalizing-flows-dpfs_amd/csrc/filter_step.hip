@@ -116,7 +116,7 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
       s0 = s1 = q0 = q1 = 0;
       for (int i = tid; i < N; i += BLK) {
         float x0, x1;
-        stage_dyn_inverse(d, S, i, L.cb_dyn, x0, x1);
+        stage_dyn_inverse(d, S, i, S.hx[2 * i], S.hx[2 * i + 1], L.cb_dyn, x0, x1);
         s0 += x0;
         s1 += x1;
         q0 += (double)x0 * x0;
@@ -139,8 +139,9 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
     __syncthreads();
     float lmax = -INFINITY;
     for (int i = tid; i < N; i += BLK) {
-      float q0x, q1x;
-      const float lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, L.cb_dyn, L.cb_cond, q0x, q1x);
+      float q0x, q1x, propose, prior;
+      const float lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, load_prop_in<NFD>(S, i), L.cb_dyn,
+                                                      L.cb_cond, q0x, q1x, propose, prior);
       if (MEAS != NFDPF_MEAS_EXTERNAL) {
         S.hlik[i] = lk;
         lmax = fmaxf(lmax, lk);

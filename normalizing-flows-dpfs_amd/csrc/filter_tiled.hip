@@ -24,6 +24,16 @@ namespace nfdpf {
 
 constexpr int kTile = 256;  // particles per workgroup, one per lane
 
+#ifdef NFDPF_EXP_TRACE
+// experiment-only: per-workgroup phase timestamps (s_memrealtime, 100 MHz) of one launch
+__device__ unsigned long long g_trace[4][2048][8];
+#define TRACE(K, P)                                                                        \
+  if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < 2048)                     \
+    g_trace[K][blockIdx.y * gridDim.x + blockIdx.x][P] = __builtin_amdgcn_s_memrealtime();
+#else
+#define TRACE(K, P)
+#endif
+
 struct TiledWs {
   double *st_phys;  // [B][tiles][4] sum x0, x1, x0^2, x1^2 of x_phys
   double *st_dyn;   // [B][tiles][4] same for x_dyn
@@ -32,8 +42,12 @@ struct TiledWs {
   double *usum;     // [B][tiles] sum exp(u - umax)
   float *S2;        // [B] soft-resampling renormaliser
   int *fire;        // [B] gate decision taken by K0 (soft resampler)
+  float *cb_dyn;    // [B][kCb] folded nf_dyn biases of the row (K2, tile 0)
+  float *cb_cond;   // [B][kCb] proposal fold over the encoding columns (K1, tile 0)
   double *fin;      // [B][T][tiles][4] sum p^2, sum p x0, sum p x1, sum logw
 };
+
+constexpr int kCb = kMaxFlows * 4 * kH;  // floats of one row's folded-bias table
 
 static inline int64_t al256(int64_t v) { return (v + 255) / 256 * 256; }
 __host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / kTile; }
@@ -41,7 +55,7 @@ __host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / 
 static int64_t tiled_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
   return al256(bt * 32) * 2 + al256(bt * 4) * 2 + al256(bt * 8) + al256((int64_t)B * 4) * 2 +
-         al256(bt * T * 32);
+         al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32);
 }
 
 static TiledWs tiled_carve(void *ws, int B, int N, int T) {
@@ -62,6 +76,10 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   p += al256((int64_t)B * 4);
   w.fire = (int *)p;
   p += al256((int64_t)B * 4);
+  w.cb_dyn = (float *)p;
+  p += al256((int64_t)B * kCb * 4);
+  w.cb_cond = (float *)p;
+  p += al256((int64_t)B * kCb * 4);
   w.fin = (double *)p;
   return w;
 }
@@ -107,6 +125,7 @@ __device__ bool tiled_gate_block(const nfdpf_filter_desc &d, int tiles, float *b
 __device__ __forceinline__ Ctx4 tiled_ctx(const double *st, int b, int tiles, int N) {
   double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
   const double *p = st + (int64_t)b * tiles * 4;
+#pragma unroll 4
   for (int k = 0; k < tiles; ++k) {
     a0 += p[4 * k];
     a1 += p[4 * k + 1];
@@ -118,16 +137,7 @@ __device__ __forceinline__ Ctx4 tiled_ctx(const double *st, int b, int tiles, in
 
 __device__ __forceinline__ void store_sums4(double *dst, double a, double b, double c, double e,
                                             double *sh) {
-  a = block_sum(a, sh);
-  b = block_sum(b, sh);
-  c = block_sum(c, sh);
-  e = block_sum(e, sh);
-  if (threadIdx.x == 0) {
-    dst[0] = a;
-    dst[1] = b;
-    dst[2] = c;
-    dst[3] = e;
-  }
+  block_sum4_store(a, b, c, e, sh, dst);
 }
 
 // ---- K0: soft resampling of the rows where the gate fires (one workgroup per row)
@@ -179,6 +189,7 @@ __global__ __launch_bounds__(512) void tiled_soft_kernel(const nfdpf_filter_desc
 // ---- K1: motion
 __global__ __launch_bounds__(kTile) void tiled_motion_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ double shd[16];
+  TRACE(0, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
@@ -198,40 +209,70 @@ __global__ __launch_bounds__(kTile) void tiled_motion_kernel(const nfdpf_filter_
     q0 = (double)p0 * p0;
     q1 = (double)p1 * p1;
   }
+  if (d.nf_cond && tile == 0 && threadIdx.x < d.n_flows * 4 * kH) {
+    // proposal fold over the encoding columns (model/models.py:338-346); K3 adds mean/std
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), threadIdx.x);
+    ws.cb_cond[b * kCb + threadIdx.x] = fold_acc(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
+  }
+  TRACE(0, 2)
   store_sums4(ws.st_phys + ((int64_t)b * tiles + tile) * 4, s0, s1, q0, q1, shd);
+  TRACE(0, 3)
 }
 
 // ---- K2: nf_dyn inverse
 __global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ double shd[16];
   __shared__ f2 cb[kMaxFlows * 2 * kH];
+  TRACE(1, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
+  const RowSlot S = row_slot(d, b);
+  float p0 = 0.f, p1 = 0.f;
+  if (i < d.N) {  // before the fold, so the loads overlap it
+    p0 = S.hx[2 * i];
+    p1 = S.hx[2 * i + 1];
+  }
   fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb);
   __syncthreads();
-  const RowSlot S = row_slot(d, b);
+  if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
+    ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
+  TRACE(1, 1)
   double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
   if (i < d.N) {
     float x0, x1;
-    stage_dyn_inverse(d, S, i, cb, x0, x1);
+    stage_dyn_inverse(d, S, i, p0, p1, cb, x0, x1);
     s0 = x0;
     s1 = x1;
     q0 = (double)x0 * x0;
     q1 = (double)x1 * x1;
   }
+  TRACE(1, 2)
   store_sums4(ws.st_dyn + ((int64_t)b * tiles + tile) * 4, s0, s1, q0, q1, shd);
+  TRACE(1, 3)
 }
 
 // softmax partials of the unshifted log-weight u over this tile
 __device__ __forceinline__ void store_softmax(float u, bool valid, float *umax, double *usum, float *shf,
                                               double *shd) {
-  const float m = block_max(valid ? u : -INFINITY, shf);
-  const double e = valid ? (double)expf(u - m) : 0.0;
-  const double s = block_sum(e, shd);
+  // per wave (max, sum exp(u - max)), merged over the waves with one barrier
+  const float mw = wave_max_dpp(valid ? u : -INFINITY);
+  const double ew = wave_sum_dpp(valid ? (double)expf(u - mw) : 0.0);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    shf[w] = mw;
+    shd[w] = ew;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    float m = shf[0];
+    for (int k = 1; k < nw; ++k) m = fmaxf(m, shf[k]);
+    double sum = 0.0;
+    for (int k = 0; k < nw; ++k)
+      if (shf[k] > -INFINITY) sum += shd[k] * (double)expf(shf[k] - m);
     *umax = m;
-    *usum = s;
+    *usum = sum;
   }
 }
 
@@ -239,42 +280,50 @@ __device__ __forceinline__ void store_softmax(float u, bool valid, float *umax, 
 template <bool NFD, bool NFC, int MEAS>
 __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;
+  TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
   const RowSlot S = row_slot(d, b);
+  const bool valid = i < d.N;
+  PropIn in{};
+  float lr = 0.f;
+  if (valid) {  // issued before the row prologue so they overlap it
+    in = load_prop_in<NFD>(S, i);
+    lr = S.hp[i];
+  }
   if (MEAS != NFDPF_MEAS_EXTERNAL) measure_row_setup<MEAS>(S.enc, d.meas_params, L);
-  if (NFD) fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), L.cb_dyn);
-  if (NFC) {
+  const int ncb = d.n_flows * 4 * kH;
+  if (NFD && threadIdx.x < ncb)
+    reinterpret_cast<float *>(L.cb_dyn)[threadIdx.x] = ws.cb_dyn[b * kCb + threadIdx.x];
+  if (NFC && threadIdx.x < ncb) {
+    // finish the proposal fold: the encoding columns came from K1, add [mean, std] of x_dyn
     const Ctx4 cp = tiled_ctx(NFD ? ws.st_dyn : ws.st_phys, b, tiles, d.N);
-    if (threadIdx.x < d.E) L.ctx[threadIdx.x] = S.enc[threadIdx.x];
-    if (threadIdx.x == 0) {
-      L.ctx[d.E] = cp.m0;
-      L.ctx[d.E + 1] = cp.m1;
-      L.ctx[d.E + 2] = cp.s0;
-      L.ctx[d.E + 3] = cp.s1;
-    }
-    __syncthreads();
-    fold_cond(d.cond_params, d.n_flows, d.E, L.ctx, L.cb_cond);
+    const float c4[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), threadIdx.x);
+    reinterpret_cast<float *>(L.cb_cond)[threadIdx.x] =
+        fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + threadIdx.x], c4, d.E, d.E + 4);
   }
   __syncthreads();
-  const bool valid = i < d.N;
+  TRACE(2, 1)
   float lk = -INFINITY, u = 0.f;
   if (valid) {
-    float q0x, q1x;
-    lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, L.cb_dyn, L.cb_cond, q0x, q1x);
+    float q0x, q1x, propose, prior;
+    lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, in, L.cb_dyn, L.cb_cond, q0x, q1x, propose, prior);
     if (MEAS != NFDPF_MEAS_EXTERNAL) {
       S.hlik[i] = lk;
-      u = stage_logw(S, i, lk);
+      u = logw(lr, lk, prior, propose);
     }
   }
+  TRACE(2, 2)
   if (MEAS == NFDPF_MEAS_EXTERNAL) return;  // phase 1: the external likelihood comes next
   const int64_t bt = (int64_t)b * tiles + tile;
   if (meas_shifted<MEAS>()) {
     const float m = block_max(lk, L.f);
     if (threadIdx.x == 0) ws.lmax[bt] = m;
   }
-  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, L.f, L.d);
+  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, L.f + 8, L.d);  // L.f[0:8] held block_max
+  TRACE(2, 3)
 }
 
 // ---- K3b (phase 2 of an EXTERNAL measurement): raw likelihood from lik_ext
@@ -295,12 +344,13 @@ __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_
   const int64_t bt = (int64_t)b * tiles + tile;
   const float m = block_max(lk, shf);
   if (threadIdx.x == 0) ws.lmax[bt] = m;
-  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, shf, shd);
+  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, shf + 8, shd);  // shf[0:8] held block_max
 }
 
 // ---- K4: log-weights, normalisation, per-tile sums for the gate / prediction / obs-likelihood
 template <bool SHIFT>
 __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  TRACE(3, 0)
   __shared__ double shd[16];
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -333,8 +383,10 @@ __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_de
     sw = lw;
   }
   double *fin = ws.fin + (((int64_t)b * d.T + d.t) * tiles + tile) * 4;
+  TRACE(3, 2)
   store_sums4(fin, sp2, px, py, sw, shd);
   if (threadIdx.x == 0) reinterpret_cast<double *>(d.ess_out)[rb + tile] = fin[0];
+  TRACE(3, 3)
 }
 
 // per-row prediction / obs-likelihood sums of every step (after the last step)
@@ -423,6 +475,12 @@ extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *es
   tiled_ess_init_kernel<<<dim3(n_tiles(N), B), kTile, 0, as_stream(stream)>>>(p0, N, ess_parts);
   return launch_status("nfdpf_filter_tiled_init");
 }
+
+#ifdef NFDPF_EXP_TRACE
+extern "C" NFDPF_API int nfdpf_exp_trace_read(void *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), sizeof(g_trace)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *workspace, void *stream) {
   NFDPF_REQUIRE(dp && workspace, "nfdpf_filter_step_tiled: null argument");

@@ -91,15 +91,40 @@ __device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const R
 constexpr int kOctxDyn = 4;  // nf_dyn context [mean(2), std(2)]
 constexpr int kNsDyn = net_size<1, kH>(kOctxDyn);  // pairs per coupling half
 
-// Folded first-layer bias of one float of the [flow][half][j][t|s] table, thread tid
-// (the per-lane weight address is not uniform here: generic loads, a few per row)
-__device__ __forceinline__ float fold_one(const float *flows, int ns, int O, int tid, const float *ctx) {
+// Folded first-layer bias of one float of the [flow][half][j][t|s] table, thread tid:
+// b1 + sum_c W1[j, 1 + c] ctx[c], accumulated in column order.  fold_acc adds the columns
+// [c0, c1) to a running value, so a fold can be split across launches (the encoding columns
+// of the proposal context are known before the row statistics) without changing the
+// fma sequence.  The per-lane weight address is not uniform: generic loads, a few per row.
+struct FoldRef {
+  const float *w1c;
+  int j, w;
+};
+
+__device__ __forceinline__ FoldRef fold_ref(const float *flows, int ns, int tid) {
   const int f = tid / (4 * kH), r = tid % (4 * kH);
-  const int n = r / (2 * kH), j = (r >> 1) % kH, w = r & 1;
-  const float *w1c = flows + 2 * ((f * 2 + n) * ns + net_core<1, kH>());
-  float a = w1c[2 * (kH * O + j) + w];
-  for (int c = 0; c < O; ++c) a = fmaf(w1c[2 * (j * O + c) + w], ctx[c], a);
+  const int n = r / (2 * kH);
+  return FoldRef{flows + 2 * ((f * 2 + n) * ns + net_core<1, kH>()), (r >> 1) % kH, r & 1};
+}
+__device__ __forceinline__ float fold_bias0(const FoldRef &r, int O) { return r.w1c[2 * (kH * O + r.j) + r.w]; }
+
+__device__ __forceinline__ float fold_acc(const FoldRef &r, int O, float a, const float *ctx, int c0, int c1) {
+  const float *wr = r.w1c + 2 * r.j * O + r.w;
+  int c = c0;
+  for (; c + 12 <= c1; c += 12) {  // 12 weight loads in flight, then the fmas in order
+    float wv[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) wv[q] = wr[2 * (c + q)];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) a = fmaf(wv[q], ctx[c + q - c0], a);
+  }
+  for (; c < c1; ++c) a = fmaf(wr[2 * c], ctx[c - c0], a);
   return a;
+}
+
+__device__ __forceinline__ float fold_one(const float *flows, int ns, int O, int tid, const float *ctx) {
+  const FoldRef r = fold_ref(flows, ns, tid);
+  return fold_acc(r, O, fold_bias0(r, O), ctx, 0, O);
 }
 
 // per-row fold of the nf_dyn context into the first-layer biases (model/models.py:309-315)
@@ -118,10 +143,11 @@ __device__ __forceinline__ void fold_cond(const float *cond, int nfl, int E, con
     reinterpret_cast<float *>(cb)[tid] = fold_one(cond, net_size<1, kH>(E + 4), E + 4, tid, ctx);
 }
 
-// nf_dyn inverse (model/models.py:305-332): reads hx (x_phys), writes scr x_dyn and hjac
+// nf_dyn inverse (model/models.py:305-332) of x_phys = (x0, x1): writes scr x_dyn and hjac
 __device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, const RowSlot &S, int i,
-                                                  const f2 *cb, float &xd0, float &xd1) {
-  float lo[1] = {S.hx[2 * i]}, up[1] = {S.hx[2 * i + 1]};
+                                                  float x0, float x1, const f2 *cb, float &xd0,
+                                                  float &xd1) {
+  float lo[1] = {x0}, up[1] = {x1};
   float ld = 0.f;
   for (int f = d.n_flows - 1; f >= 0; --f)
     ld += coupling_inverse<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
@@ -133,63 +159,91 @@ __device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, co
   xd1 = up[0];
 }
 
+// Per-particle inputs of the proposal stage, loaded up front so the loads overlap the
+// per-row prologue (context folds) instead of following it.
+struct PropIn {
+  float p0, p1, e0, e1, xd0, xd1, jac;
+};
+
+template <bool NFD>
+__device__ __forceinline__ PropIn load_prop_in(const RowSlot &S, int i) {
+  PropIn a;
+  a.p0 = S.hx[2 * i];
+  a.p1 = S.hx[2 * i + 1];
+  a.e0 = S.hnoise[2 * i];
+  a.e1 = S.hnoise[2 * i + 1];
+  a.xd0 = a.p0;
+  a.xd1 = a.p1;
+  a.jac = 0.f;
+  if (NFD) {
+    a.xd0 = S.scr[4 * i];
+    a.xd1 = S.scr[4 * i + 1];
+    a.jac = S.hjac ? S.hjac[i] : 0.f;
+  }
+  return a;
+}
+
 // NF proposal + nf_dyn forward + densities (model/models.py:358-377) and the measurement.
-// Reads hx (x_phys), hnoise, scr/hjac; writes hx = proposal, scr propose/prior, hprior.
-// Returns the raw likelihood (0 for an EXTERNAL measurement).
+// Writes hx = proposal, scr propose/prior, hprior; returns the raw likelihood (0 for an
+// EXTERNAL measurement) and the (propose, prior) pair for the log-weight.
 template <bool NFD, bool NFC, int MEAS>
 __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, const RowSlot &S,
-                                                const StepShared &L, int i, const f2 *cb_dyn,
-                                                const f2 *cb_cond, float &q0x, float &q1x) {
+                                                const StepShared &L, int i, const PropIn &in,
+                                                const f2 *cb_dyn, const f2 *cb_cond, float &q0x,
+                                                float &q1x, float &propose, float &prior) {
   const float K = d.dens_const;
   const float two_var = 2.0f * (d.pos_noise * d.pos_noise);
   const int nfl = d.n_flows;
-  const float p0 = S.hx[2 * i], p1 = S.hx[2 * i + 1];
-  const float e0 = S.hnoise[2 * i], e1 = S.hnoise[2 * i + 1];
-  float xd0 = p0, xd1 = p1, jac = 0.f;
-  if (NFD) {
-    xd0 = S.scr[4 * i];
-    xd1 = S.scr[4 * i + 1];
-    jac = S.hjac ? S.hjac[i] : 0.f;
-  }
-  const float de = density(e0, e1, K, two_var);
-  float prior, propose;
-  q0x = xd0;
-  q1x = xd1;
+  const float de = density(in.e0, in.e1, K, two_var);
+  q0x = in.xd0;
+  q1x = in.xd1;
   if (NFC) {
     const int oC = d.E + 4;
     const int nsC = net_size<1, kH>(oC);
-    float lo[1] = {xd0}, up[1] = {xd1};
+    float lo[1] = {in.xd0}, up[1] = {in.xd1};
     float ld = 0.f;
+#ifndef NFDPF_EXP_NOCOND
     for (int f = nfl - 1; f >= 0; --f)
       ld += coupling_inverse<1, kH>(wptr2(d.cond_params) + f * 2 * nsC, oC, lo, up,
                                     cb_cond + f * 2 * kH);
+#endif
     q0x = lo[0];
     q1x = up[0];
     const float jac_prop = -ld;
-    const float r0 = p0 - e0, r1 = p1 - e1;
+    const float r0 = in.p0 - in.e0, r1 = in.p1 - in.e1;
     if (NFD) {
       float ld2 = 0.f;
+#ifndef NFDPF_EXP_NODYNF
       for (int f = 0; f < nfl; ++f)
         ld2 += coupling_forward<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
                                        cb_dyn + f * 2 * kH);
+#endif
       prior = density(lo[0] - r0, up[0] - r1, K, two_var) - (-ld2);
     } else {
       prior = density(q0x - r0, q1x - r1, K, two_var);
     }
-    propose = (de + jac) + jac_prop;
+    propose = (de + in.jac) + jac_prop;
   } else {
-    prior = de + jac;
-    propose = de + jac;
+    prior = de + in.jac;
+    propose = de + in.jac;
   }
   S.hx[2 * i] = q0x;
   S.hx[2 * i + 1] = q1x;
   S.scr[4 * i + 2] = propose;
   S.scr[4 * i + 3] = prior;
   if (S.hprior) S.hprior[i] = prior;
+#ifdef NFDPF_EXP_NOMEAS
+  return q0x * 1e-3f;
+#endif
   if (MEAS != NFDPF_MEAS_EXTERNAL)
     return measure<MEAS>(MeasArgs{d.pe_params, d.meas_params, d.n_flows, d.meas_prior_std}, L, q0x,
                          q1x);
   return 0.f;
+}
+
+// log-weight from registers: ((log p_res + lik) + prior) - propose
+__device__ __forceinline__ float logw(float lr, float lik, float prior, float propose) {
+  return ((lr + lik) + prior) - propose;
 }
 
 // log-weight update (DPFs.py:187): ((log p_res + lik) + prior) - propose
