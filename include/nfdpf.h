@@ -58,6 +58,11 @@ extern "C" {
 #define NFDPF_RESAMPLE_SOFT 0
 #define NFDPF_RESAMPLE_OT 1
 
+/* nf_dyn values of nfdpf_filter_desc: the dynamic flow (--NF-dyn / --NF-dyn-flow) */
+#define NFDPF_DYN_NONE 0
+#define NFDPF_DYN_REALNVP 1 /* NormalizingFlowModel_cond over RealNVP_cond, [mean,std] context */
+#define NFDPF_DYN_MAF 2     /* NormalizingFlowModel over MAF (context-free) */
+
 /* RNG modes: DEVICE = counter-based Philox4x32-10 keyed by (seed, step, global row,
  * particle), shard invariant; HOST = caller uploads the draws of the reference's CPU
  * generator (parity mode) */

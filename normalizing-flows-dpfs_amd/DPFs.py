@@ -161,11 +161,11 @@ class DPF(nn.Module):
             max_iter=a.max_iter, pos_noise=self.pos_noise, vel_noise=self.vel_noise, width=a.width,
             init_with_true_state=a.init_with_true_state, n_flows=self.n_sequence,
             rng_mode=getattr(a, "rng_mode", "device"), seed=a.seed,
-            force_resample=getattr(a, "force_resample", False))
+            force_resample=getattr(a, "force_resample", False),
+            dyn_flow=getattr(a, "NF_dyn_flow", "RealNVP"))
 
     def _fused_supported(self):
-        return (self.measurement in ("cos", "CRNVP", "NN", "gaussian") and self.hidden_size == 32
-                and getattr(self.param, "NF_dyn_flow", "RealNVP") == "RealNVP")
+        return self.measurement in ("cos", "CRNVP", "NN", "gaussian") and self.hidden_size == 32
 
     def filtering_pos(self, obs, start_state_vs, vel_input):
         """The T-step particle filter (DPFs.py:144-216) -> the reference's 9-tuple."""

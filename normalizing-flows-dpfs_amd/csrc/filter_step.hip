@@ -111,7 +111,7 @@ __global__ __launch_bounds__(BLK) void filter_step_kernel(const nfdpf_filter_des
 
     // ---------------- nf_dyn inverse (model/models.py:305-332)
     if (NFD) {
-      fold_dyn(d.dyn_params, nfl, cphys, L.cb_dyn);
+      fold_dyn(d.dyn_params, nfl, cphys, L.cb_dyn, d.nf_dyn);
       __syncthreads();
       s0 = s1 = q0 = q1 = 0;
       for (int i = tid; i < N; i += BLK) {
@@ -243,6 +243,8 @@ extern "C" int nfdpf_filter_step(const nfdpf_filter_desc *dp, void *stream) {
                 "nfdpf_filter_step: previous-step state missing");
   NFDPF_REQUIRE(!d.nf_dyn || (d.dyn_params && d.hist_jac && d.hist_prior),
                 "nfdpf_filter_step: nf_dyn needs dyn_params, hist_jac, hist_prior");
+  NFDPF_REQUIRE(d.nf_dyn >= NFDPF_DYN_NONE && d.nf_dyn <= NFDPF_DYN_MAF, "nfdpf_filter_step: bad nf_dyn %d",
+                d.nf_dyn);
   NFDPF_REQUIRE(!d.nf_cond || d.cond_params, "nfdpf_filter_step: nf_cond needs cond_params");
   NFDPF_REQUIRE(d.measurement == NFDPF_MEAS_EXTERNAL || (d.E == kE && d.pe_params),
                 "nfdpf_filter_step: fused measurements need E == %d and pe_params (got E=%d)", kE,

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_des
     p0 = S.hx[2 * i];
     p1 = S.hx[2 * i + 1];
   }
-  fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb);
+  fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb, d.nf_dyn);
   __syncthreads();
   if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
     ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
@@ -497,6 +497,8 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_step_tiled: previous-step state missing");
   NFDPF_REQUIRE(!d.nf_dyn || (d.dyn_params && d.hist_jac && d.hist_prior),
                 "nfdpf_filter_step_tiled: nf_dyn needs dyn_params, hist_jac, hist_prior");
+  NFDPF_REQUIRE(d.nf_dyn >= NFDPF_DYN_NONE && d.nf_dyn <= NFDPF_DYN_MAF,
+                "nfdpf_filter_step_tiled: bad nf_dyn %d", d.nf_dyn);
   NFDPF_REQUIRE(!d.nf_cond || d.cond_params, "nfdpf_filter_step_tiled: nf_cond needs cond_params");
   NFDPF_REQUIRE(d.measurement == NFDPF_MEAS_EXTERNAL || (d.E == kE && d.pe_params),
                 "nfdpf_filter_step_tiled: fused measurements need E == %d", kE);

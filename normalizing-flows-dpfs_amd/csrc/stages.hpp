@@ -90,6 +90,7 @@ __device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const R
 
 constexpr int kOctxDyn = 4;  // nf_dyn context [mean(2), std(2)]
 constexpr int kNsDyn = net_size<1, kH>(kOctxDyn);  // pairs per coupling half
+constexpr int kMafDyn = maf_size<kH>(2);           // floats per MAF flow of the dynamic stack
 
 // Folded first-layer bias of one float of the [flow][half][j][t|s] table, thread tid:
 // b1 + sum_c W1[j, 1 + c] ctx[c], accumulated in column order.  fold_acc adds the columns
@@ -128,9 +129,9 @@ __device__ __forceinline__ float fold_one(const float *flows, int ns, int O, int
 }
 
 // per-row fold of the nf_dyn context into the first-layer biases (model/models.py:309-315)
-__device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &c, f2 *cb) {
+__device__ __forceinline__ void fold_dyn(const float *dyn, int nfl, const Ctx4 &c, f2 *cb, int kind) {
   const int tid = threadIdx.x;
-  if (tid < nfl * 4 * kH) {
+  if (kind == NFDPF_DYN_REALNVP && tid < nfl * 4 * kH) {  // MAF takes no context
     const float cc[4] = {c.m0, c.m1, c.s0, c.s1};
     reinterpret_cast<float *>(cb)[tid] = fold_one(dyn, kNsDyn, kOctxDyn, tid, cc);
   }
@@ -149,9 +150,17 @@ __device__ __forceinline__ void stage_dyn_inverse(const nfdpf_filter_desc &d, co
                                                   float &xd1) {
   float lo[1] = {x0}, up[1] = {x1};
   float ld = 0.f;
-  for (int f = d.n_flows - 1; f >= 0; --f)
-    ld += coupling_inverse<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
-                                  cb + f * 2 * kH);
+  if (d.nf_dyn == NFDPF_DYN_MAF) {
+    // NormalizingFlowModel.inverse over MAF flows, last flow first (nf/models.py:23-30)
+    float v[2] = {x0, x1};
+    for (int f = d.n_flows - 1; f >= 0; --f) ld += maf_inverse<2, kH>(wptr(d.dyn_params) + f * kMafDyn, v);
+    lo[0] = v[0];
+    up[0] = v[1];
+  } else {
+    for (int f = d.n_flows - 1; f >= 0; --f)
+      ld += coupling_inverse<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
+                                    cb + f * 2 * kH);
+  }
   S.scr[4 * i] = lo[0];
   S.scr[4 * i + 1] = up[0];
   if (S.hjac) S.hjac[i] = -ld;
@@ -214,9 +223,17 @@ __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, cons
     if (NFD) {
       float ld2 = 0.f;
 #ifndef NFDPF_EXP_NODYNF
-      for (int f = 0; f < nfl; ++f)
-        ld2 += coupling_forward<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
-                                       cb_dyn + f * 2 * kH);
+      if (d.nf_dyn == NFDPF_DYN_MAF) {
+        // NormalizingFlowModel.forward over MAF flows (nf/models.py:13-21)
+        float v[2] = {lo[0], up[0]};
+        for (int f = 0; f < nfl; ++f) ld2 += maf_forward<2, kH>(wptr(d.dyn_params) + f * kMafDyn, v);
+        lo[0] = v[0];
+        up[0] = v[1];
+      } else {
+        for (int f = 0; f < nfl; ++f)
+          ld2 += coupling_forward<1, kH>(wptr2(d.dyn_params) + f * 2 * kNsDyn, kOctxDyn, lo, up,
+                                         cb_dyn + f * 2 * kH);
+      }
 #endif
       prior = density(lo[0] - r0, up[0] - r1, K, two_var) - (-ld2);
     } else {

@@ -20,6 +20,7 @@ MEAS = {"cos": 0, "CRNVP": 1, "NN": 2, "gaussian": 3, "external": 4}
 MEAS_EXTERNAL = 4
 RESAMPLE = {"soft": 0, "ot": 1}
 RNG_DEVICE, RNG_HOST = 0, 1
+DYN_NONE, DYN_REALNVP, DYN_MAF = 0, 1, 2
 
 
 class FilterDesc(Structure):

@@ -27,6 +27,7 @@ from .pack import blob, flows_tensors, paired_mlp_tensors
 class FilterConfig:
     N: int
     NF_dyn: bool = False
+    dyn_flow: str = "RealNVP"  # "RealNVP" (RealNVP_cond, [mean, std] context) or "MAF" (--NF-dyn-flow)
     NF_cond: bool = False
     measurement: str = "cos"
     resampler: str = "ot"
@@ -207,7 +208,8 @@ class FilterEngine:
         d = L.FilterDesc()
         d.B, d.N, d.T, d.E = B, N, T, E
         d.B_global, d.phase, d.row_base = shard.B_global, 0, shard.row_base
-        d.nf_dyn, d.nf_cond = int(c.NF_dyn), int(c.NF_cond)
+        d.nf_dyn = (L.DYN_MAF if c.dyn_flow == "MAF" else L.DYN_REALNVP) if c.NF_dyn else L.DYN_NONE
+        d.nf_cond = int(c.NF_cond)
         d.measurement, d.resampler = L.MEAS[c.measurement], L.RESAMPLE[c.resampler]
         d.rng_mode = L.RNG_HOST if host_mode else L.RNG_DEVICE
         d.force_resample, d.n_flows, d.hidden = int(c.force_resample), c.n_flows, c.hidden

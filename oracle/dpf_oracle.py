@@ -268,11 +268,20 @@ def row_context(x: torch.Tensor) -> torch.Tensor:
     return torch.cat([x.mean(dim=1), x.std(dim=1)], dim=-1)
 
 
-def dyn_flow(params: Params, n_flows, x, NF, forward=False, ctx=None):
-    """nf_dynamic_model (model/models.py:305-332) -> (x', jac = -log_det)."""
+def dyn_flow(params: Params, n_flows, x, NF, forward=False, ctx=None, kind="RealNVP"):
+    """nf_dynamic_model (model/models.py:305-332) -> (x', jac = -log_det).  kind "MAF": the
+    context-free MAF stack (NormalizingFlowModel, nf/models.py:5-30) of --NF-dyn-flow MAF,
+    which the reference builds (nf/flows.py:241-284) but does not wire into DPF."""
     B, N, D = x.shape
     if not NF:
         return x, torch.zeros(B, N)
+    if kind == "MAF":
+        flat = x.reshape(-1, D)
+        if forward:
+            y, _, ld = stack_forward(params, n_flows, flat, kind="maf")
+        else:
+            y, ld = stack_inverse(params, n_flows, flat, kind="maf")
+        return y.reshape(B, N, D), (-ld).reshape(B, N)
     c = row_context(x) if ctx is None else ctx
     c = c[:, None, :].repeat(1, N, 1).reshape(B * N, -1)
     flat = x.reshape(-1, D)
@@ -338,14 +347,14 @@ def meas_crnvp(pe_params: Params, cnf_params: Params, n_flows, enc, x, prior_std
 
 
 def proposal_likelihood(dyn_p, cond_p, n_flows, meas: Callable, x_dyn, x_phys, enc, noise, jac,
-                        NF, NF_cond, pos_noise, vel_noise):
+                        NF, NF_cond, pos_noise, vel_noise, dyn_kind="RealNVP"):
     """proposal_likelihood (model/models.py:358-379) -> (x_prop, lik, prior, propose)."""
     dens = lambda e: normal_density(e, pos_noise, vel_noise)
     if NF_cond:
         x_prop, jac_prop = nf_propose(cond_p, n_flows, x_dyn, enc.detach())
         if NF:
             ctx = row_context(x_phys)
-            back, jac_back = dyn_flow(dyn_p, n_flows, x_prop, True, forward=True, ctx=ctx)
+            back, jac_back = dyn_flow(dyn_p, n_flows, x_prop, True, forward=True, ctx=ctx, kind=dyn_kind)
             prior = dens(back - (x_phys - noise)) - jac_back
         else:
             prior = dens(x_prop - (x_phys - noise))
@@ -580,10 +589,11 @@ def filter_step(cfg: dict, params: Params, meas: Callable, x, p, vel, enc_t, rng
     else:
         xr, lr = x, p.log()
     x_phys, noise = motion(xr, vel, cfg["pos_noise"], rng.noise(B, N, cfg["pos_noise"]))
-    x_dyn, jac = dyn_flow(dyn_p, nfl, x_phys, cfg["NF_dyn"])
+    dk = cfg.get("dyn_flow", "RealNVP")
+    x_dyn, jac = dyn_flow(dyn_p, nfl, x_phys, cfg["NF_dyn"], kind=dk)
     xp, lik, prior, prop = proposal_likelihood(dyn_p, cond_p, nfl, meas, x_dyn, x_phys, _f(enc_t),
                                                noise, jac, cfg["NF_dyn"], cfg["NF_cond"],
-                                               cfg["pos_noise"], cfg["vel_noise"])
+                                               cfg["pos_noise"], cfg["vel_noise"], dyn_kind=dk)
     lw = lr + lik + prior - prop
     return dict(x=xp, p=normalize_log_probs(lw) + 1e-12, noise=noise, lik=lik, idx=idx, jac=jac,
                 prior=prior, lw_mean=lw.mean(), fired=fired, logw=lw)

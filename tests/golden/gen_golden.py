@@ -245,7 +245,34 @@ E2E = {
     "c3": (dict(NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler_type="ot"), 3, 48, 4, 32, 0.5, 0.05, "random"),
     "c3n": (dict(NF_dyn=True, NF_cond=True, measurement="CRNVP", resampler_type="ot"), 3, 48, 4, 32, 0.5, 0.3, "random"),
     "c5": (dict(NF_dyn=True, NF_cond=True, measurement="CGLOW", resampler_type="soft", hiddensize=192), 3, 40, 4, 192, 1.0, 0.05, "random"),
+    # C4: MAF dynamic flow (nf/flows.py:241-284) behind a context-dropping adapter -- the
+    # reference builds MAF but never wires it into DPF -- with OT resampling
+    "c4": (dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="ot", NF_dyn_flow="MAF"), 3, 48, 4, 32, 0.5, 0.3, "aligned"),
 }
+
+
+def maf_adapter(n_flows=2, dim=2, hidden=8):
+    """The reference's MAF stack (nf/flows.py MAF in nf/models.py NormalizingFlowModel) with
+    nf_dynamic_model's (x, context) call signature; the context is ignored."""
+    import torch
+    from nf.flows import MAF
+    from nf.models import NormalizingFlowModel
+
+    class Adapter(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            prior = torch.distributions.MultivariateNormal(torch.zeros(dim), torch.eye(dim))
+            self.m = NormalizingFlowModel(prior, [MAF(dim=dim, hidden_dim=hidden) for _ in range(n_flows)],
+                                          device="cpu")
+            self.flows = self.m.flows
+
+        def forward(self, x, context=None):
+            return self.m.forward(x)
+
+        def inverse(self, z, context=None):
+            return self.m.inverse(z)
+
+    return Adapter()
 
 
 def gen_e2e(mods, name):
@@ -255,8 +282,13 @@ def gen_e2e(mods, name):
     flags, B, N, T, H, pe_std, fl_std, enc_mode = E2E[name]
     g = torch.Generator().manual_seed(16)
     torch.manual_seed(500)
+    dyn_kind = flags.get("NF_dyn_flow", "RealNVP")
+    flags = {k: v for k, v in flags.items() if k != "NF_dyn_flow"}
     a = make_args(num_particles=N, batchsize=B, sequence_length=T, **flags)
     dpf = DPF(a)
+    if dyn_kind == "MAF":
+        dpf.nf_dyn = maf_adapter()
+        dpf.nf_dyn.eval()
     dpf.eval()
     # sharpen the likelihood so ESS-gated resampling fires within a few steps
     perturb(dpf.particle_encoder, pe_std, g)
@@ -303,7 +335,10 @@ def gen_e2e(mods, name):
     out = {"B": np.int32(B), "N": np.int32(N), "T": np.int32(T), "H": np.int32(Henc)}
     for k, v in flags.items():
         out[f"flag/{k}"] = np.array(v)
+    if dyn_kind != "RealNVP":
+        out["flag/NF_dyn_flow"] = np.array(dyn_kind)
     for k, v in sd_np(dpf).items():
+        k = k.replace("nf_dyn.m.", "nf_dyn.")  # the adapter's stack -> DPF's nf_dyn key names
         if k.split(".")[0] in ("nf_dyn", "cond_model", "particle_encoder", "cnf_measurement", "cglow_measurement"):
             out[f"w/{k}"] = v
     out.update(enc=enc.numpy(), start=start.numpy(), vel=vel.numpy(), state=state.numpy(),

@@ -186,8 +186,8 @@ class _Models(torch.nn.Module):
 
     def __init__(self, w, cfg):
         super().__init__()
-        from model.models import build_conditional_nf, build_likelihood, build_particle_encoder
-        self.nf_dyn = build_conditional_nf(2, 4, 2)
+        from model.models import build_conditional_nf, build_likelihood, build_maf_dyn, build_particle_encoder
+        self.nf_dyn = build_maf_dyn(2, 2) if cfg.get("dyn_flow") == "MAF" else build_conditional_nf(2, 4, 2)
         self.cond_model = build_conditional_nf(2, 36, 2)
         self.particle_encoder = build_particle_encoder(32, 2)
         if cfg["measurement"] == "CRNVP":
@@ -207,7 +207,7 @@ def _engine(fx, kernel="tiled"):
     from nfdpf.engine import FilterConfig, FilterEngine
     c = e2e_cfg(fx)
     cfg = FilterConfig(N=c["N"], NF_dyn=c["NF_dyn"], NF_cond=c["NF_cond"], measurement=c["measurement"],
-                       resampler=c["resampler"], rng_mode="host", kernel=kernel)
+                       resampler=c["resampler"], rng_mode="host", kernel=kernel, dyn_flow=c["dyn_flow"])
     return FilterEngine(cfg, _Models(weights(fx), c)), c
 
 
@@ -222,7 +222,7 @@ class _TapeDraws:
         return self.tape.noise(B, N, std)
 
 
-E2E_FUSED = ["c1", "c2", "c2w", "c3", "c3n"]
+E2E_FUSED = ["c1", "c2", "c2w", "c3", "c3n", "c4"]
 
 
 def _oracle64_one_step(fx, monkeypatch):
@@ -311,7 +311,7 @@ def test_filter_step_one_step_parity(name, kernel, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
 def test_filtering_free_running(name, kernel):
     """Whole sequences from the reference's initial state and draws."""
     fx = load(f"e2e_{name}.npz")

@@ -88,7 +88,7 @@ def test_measurements(meas):
     assert_close(lik, fx["lik"], 1e-5, 1e-5, meas)
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c2w", "c3", "c3n", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c2w", "c3", "c3n", "c4", "c5"])
 def test_filtering_e2e(name):
     fx = load(f"e2e_{name}.npz")
     cfg = e2e_cfg(fx)
@@ -108,7 +108,7 @@ def test_filtering_e2e(name):
     assert abs(float(rm) - float(fx["rmse"])) <= 1e-5 * float(fx["rmse"])
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c2w", "c3", "c3n", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c2w", "c3", "c3n", "c4", "c5"])
 def test_filter_step_teacher_forced(name):
     """Each step from the reference's own previous-step state: tight tolerances."""
     fx = load(f"e2e_{name}.npz")
