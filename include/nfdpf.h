@@ -108,9 +108,15 @@ NFDPF_API int64_t nfdpf_ot_workspace_bytes(int B, int N);
 NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps, float scaling,
                       float threshold, int max_iter, int64_t row_base, float *x_out,
                       float *w_out, int64_t *idx_out, int32_t *iters_out, void *workspace,
-                      const int32_t *gate, void *stream);
+                      const int32_t *gate, const int32_t *stop_at, void *stream);
 /*   gate: optional device flag; when non-NULL and *gate == 0 every kernel is a no-op (the
- *         ESS gate of DPFs.py:165 decided not to resample this step, without a host sync) */
+ *         ESS gate of DPFs.py:165 decided not to resample this step, without a host sync)
+ *   stop_at: optional device int32, in the iters_out encoding (total_iter + 2).  NULL: the
+ *         reference's rule -- stop after the first iteration at which ANY of these B rows
+ *         has converged (resamplers.py:126-129).  Non-NULL: run exactly that many
+ *         iterations.  A batch sharded over ranks reproduces the unsharded loop by running
+ *         once with NULL, taking the MIN of iters_out over ranks (the first row to converge
+ *         anywhere), and running again with stop_at = that minimum.                      */
 
 /* ESS gate of DPFs.py:163-165: gate = mean_b(inv_ess[b]) < 0.5 N (or force) -> int32 [1] */
 NFDPF_API int nfdpf_ess_gate(const float *inv_ess, int B, int N, int force, int32_t *gate,

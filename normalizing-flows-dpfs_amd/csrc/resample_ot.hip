@@ -208,7 +208,8 @@ __device__ void softmin_pair(const float *xs, int N, int i, bool active, float i
 struct OtParams {
   int B, N, splits, max_iter;
   double eps, sf, thr;
-  const int32_t *gate;  // optional: skip everything when *gate == 0
+  const int32_t *gate;     // optional: skip everything when *gate == 0
+  const int32_t *stop_at;  // optional: total_iter + 2 to run (sharded batches), else the rule
 };
 
 __device__ __forceinline__ bool ot_off(const OtParams &P) { return P.gate && *P.gate == 0; }
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(kOtThreads) void ot_init_kernel(OtParams P, OtWs ws
 // evaluates the same residuals of iteration k-1 in the same order
 __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws, int k) {
   if (k == 0) return false;
+  if (P.stop_at) return k >= *P.stop_at - 2;  // the batch-global decision, taken by the caller
   const float *res = ws.res + (int64_t)((k - 1) & 1) * P.B * P.splits;
   for (int b = 0; b < P.B; ++b) {
     const double e0 = ws.rowc[b * 4];
@@ -423,7 +425,8 @@ extern "C" int64_t nfdpf_ot_workspace_bytes(int B, int N) {
 extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
                                  float scaling, float threshold, int max_iter, int64_t row_base,
                                  float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
-                                 void *workspace, const int32_t *gate, void *stream) {
+                                 void *workspace, const int32_t *gate, const int32_t *stop_at,
+                                 void *stream) {
   NFDPF_REQUIRE(x && w && x_out && w_out && idx_out && workspace,
                 "nfdpf_ot_resample: null pointer");
   NFDPF_REQUIRE(B >= 0 && N >= 1 && max_iter >= 1, "nfdpf_ot_resample: bad sizes");
@@ -434,7 +437,7 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
   const int splits = ot_splits(B, N);
   OtWs ws = carve(workspace, B, N, splits);
   OtParams P{B, N, splits, max_iter, (double)eps, (double)scaling * (double)scaling,
-             (double)threshold, gate};
+             (double)threshold, gate, stop_at};
   ot_setup_kernel<<<B, row_threads(N), 0, st>>>(x, w, N, ws, gate);
   const dim3 g(splits, B);
   ot_init_kernel<<<g, kOtThreads, 0, st>>>(P, ws);

@@ -269,12 +269,21 @@ class FilterEngine:
                 d.gate = gate_buf.data_ptr()
             if c.resampler == "ot":
                 contiguous = t == 0 or teacher is not None
-                xo, _, _, _ = ops.ot_resample(xp if contiguous else hx[:, t - 1].contiguous(),
-                                              pp if contiguous else hp[:, t - 1].contiguous(),
-                                              c.eps, c.scaling, c.threshold, c.max_iter, shard.row_base,
-                                              gate=gate_buf)
-                keep.append(xo)
-                d.ot_x = xo.data_ptr()
+                xin = xp if contiguous else hx[:, t - 1].contiguous()
+                pin = pp if contiguous else hp[:, t - 1].contiguous()
+                # The Sinkhorn loop is max_iter launches; when the gate is off they would all be
+                # no-ops, so read the gate (one sync, as the reference's `if ESS < ...` does,
+                # DPFs.py:165) and skip the call.  The gate is batch-global: same on every rank.
+                fire = fired[-1] if host_mode else bool(gate_buf.item())
+                if fire:
+                    xo, _, _, it = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,
+                                                   shard.row_base, gate=gate_buf)
+                    if shard.world > 1:
+                        xo = self._ot_global_stop(xin, pin, it, shard, gate_buf)
+                    keep.append(xo)
+                    d.ot_x = xo.data_ptr()
+                else:
+                    d.ot_x = xin.data_ptr()  # not read: the motion stage keeps the previous particles
             d.prof_events = None
             if self.step_events is not None and t == T // 2:
                 # one sampled step per pass: an event pair costs ~6 us of stream time
@@ -295,6 +304,16 @@ class FilterEngine:
         return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, obs, pred, fired)
 
     # -- helpers ----------------------------------------------------------------------------
+    def _ot_global_stop(self, xin, pin, it, shard: ShardInfo, gate_buf):
+        """Batch-coupled Sinkhorn stop across ranks (resamplers.py:126-129):
+        the loop ends when ANY row of the whole batch converges, i.e. at the MIN over ranks of
+        the local stop iteration; re-run this rank's rows for exactly that many iterations."""
+        c = self.cfg
+        dist.all_reduce(it, op=dist.ReduceOp.MIN, group=shard.group)
+        xo, _, _, _ = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter, shard.row_base,
+                                      gate=gate_buf, stop_at=it)
+        return xo
+
     @staticmethod
     def _global(t: torch.Tensor, shard: ShardInfo) -> torch.Tensor:
         """Host copy of a per-row tensor over the whole (sharded) batch."""

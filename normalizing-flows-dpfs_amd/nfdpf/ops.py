@@ -97,8 +97,13 @@ def _aligned_ptr(t: torch.Tensor) -> int:
     return (p + 255) // 256 * 256
 
 
-def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_base=0, gate=None):
-    """resampler_ot (resamplers.py:62-70) -> (x', w', flat idx, iterations int32[1])."""
+def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_base=0, gate=None,
+                stop_at=None):
+    """resampler_ot (resamplers.py:62-70) -> (x', w', flat idx, iterations int32[1]).
+
+    ``stop_at`` (device int32[1], iterations encoding): run exactly that many Sinkhorn
+    iterations instead of the batch-coupled stop rule (include/nfdpf.h) -- the second pass
+    of a batch sharded over ranks."""
     require_device(x, "ot_resample")
     B, N, D = x.shape
     if D != 2:
@@ -112,7 +117,8 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_b
     ws = workspace(nb, x.device)
     check(lib().nfdpf_ot_resample(ptr(x), ptr(w), B, N, float(eps), float(scaling), float(threshold),
                                   int(max_iter), int(row_base), ptr(xo), ptr(wo), ptr(idx), ptr(it),
-                                  _aligned_ptr(ws), ptr(gate), stream_ptr(x.device)), "nfdpf_ot_resample")
+                                  _aligned_ptr(ws), ptr(gate), ptr(stop_at), stream_ptr(x.device)),
+          "nfdpf_ot_resample")
     return xo, wo, idx, it
 
 

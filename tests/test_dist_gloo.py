@@ -1,6 +1,7 @@
 """world_size-2 rehearsal (gloo, CPU) of the batch-sharded exchange logic of nfdpf.engine:
 shard geometry, the per-step all-gather of per-row ESS terms feeding an identical gate on
-every rank, host-draw slicing in parity mode and the end-of-sequence obs-likelihood reduce.
+every rank, host-draw slicing in parity mode, the MIN of the Sinkhorn stop iteration and the
+end-of-sequence obs-likelihood reduce.
 The RCCL/GPU path uses the same code with device tensors."""
 import os
 import socket
@@ -41,7 +42,11 @@ def _worker(rank, world, port, q):
         lw = torch.full((B, 4), float(rank + 1))
         tot = lw.double().sum(0)
         dist.all_reduce(tot)
-        q.put((rank, sh.world, sh.B_global, sh.row_base, gathered.numpy(), gate, nz.numpy(), tot.numpy()))
+        # OT stop (engine._ot_global_stop): the MIN over ranks of the local iteration count
+        it = torch.tensor([31 + 7 * rank], dtype=torch.int32)
+        dist.all_reduce(it, op=dist.ReduceOp.MIN)
+        q.put((rank, sh.world, sh.B_global, sh.row_base, gathered.numpy(), gate, nz.numpy(), tot.numpy(),
+               int(it.item())))
     finally:
         dist.destroy_process_group()
 
@@ -66,7 +71,8 @@ def test_sharded_exchange_world2():
     inv_all = torch.rand(world * B, generator=torch.Generator().manual_seed(7)) * N
     ref_gate = FilterEngine._host_gate(inv_all, N, False)
     ref_noise = HostDraws(torch.Generator().manual_seed(11)).noise(world * B, N, 20.0)
-    for rank, w, bg, base, gathered, gate, nz, tot in res:
+    for rank, w, bg, base, gathered, gate, nz, tot, it in res:
+        assert it == 31
         assert (w, bg, base) == (world, world * B, rank * B)
         np.testing.assert_array_equal(gathered, inv_all.numpy())
         assert gate == ref_gate

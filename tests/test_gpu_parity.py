@@ -166,6 +166,28 @@ def test_ot_resampler_golden():
         np.testing.assert_array_equal(idx.cpu().numpy(), np.arange(B * N).reshape(B, N))
 
 
+def test_ot_sharded_stop_matches_unsharded():
+    """A batch split over two 'ranks' reproduces the unsharded Sinkhorn loop: each half runs
+    with the local stop rule, the MIN of the iteration counts is the batch-global stop
+    (resamplers.py:126-129), and each half re-runs to exactly that count (stop_at)."""
+    from nfdpf import ops
+    fx = load("ot.npz")
+    c = group(fx, "c1")
+    x, p = t(c["x"]).to(DEV), t(c["p"]).to(DEV)
+    B = x.shape[0]
+    full, _, _, it_full = ops.ot_resample(x, p)
+    h = B // 2
+    parts = [(x[:h].contiguous(), p[:h].contiguous(), 0), (x[h:].contiguous(), p[h:].contiguous(), h)]
+    its = [ops.ot_resample(xx, pp, row_base=rb)[3] for xx, pp, rb in parts]
+    stop = torch.minimum(its[0], its[1])
+    assert int(stop.item()) == int(it_full.item())
+    outs = [ops.ot_resample(xx, pp, row_base=rb, stop_at=stop) for xx, pp, rb in parts]
+    for o in outs:
+        assert int(o[3].item()) == int(it_full.item())
+    assert torch.equal(torch.cat([outs[0][0], outs[1][0]]), full)
+    assert torch.equal(torch.cat([outs[0][2], outs[1][2]]), ops.ot_resample(x, p)[2])
+
+
 @pytest.mark.parametrize("meas", ["cos", "CRNVP", "NN", "gaussian"])
 def test_measurement_golden(meas):
     from nfdpf import ops
