@@ -25,7 +25,8 @@
  *   RealNVP(_cond) flow     : coupling nets t1, s1, t2, s2                      (nf/flows.py:181-190)
  *   stack of n flows        : flow 0, flow 1, ... (model order, i.e. nf_dyn.flows[i])
  *   MAF flow (dim d)        : initial_param[2], then FCNN(i, 2, H) for i = 1..d-1 (nf/flows.py:247-254)
- *   particle encoder        : Linear(2,16) Linear(16,32) Linear(32,E): W,b each  (model/models.py:130-150)
+ *   particle encoder        : Linear(2,16) Linear(16,32) Linear(32,E): W,b each  (model/models.py:130-150),
+ *                             each W in row-pair order [out/2][in][2] (outputs 2m, 2m+1 adjacent)
  *   likelihood_est (NN)     : Linear(2E,64) Linear(64,64) Linear(64,1): W,b each (model/models.py:119-128)
  */
 #ifndef NFDPF_H
@@ -133,6 +134,18 @@ NFDPF_API int nfdpf_normalize_log_probs(const float *logw, int B, int N, float a
 NFDPF_API int nfdpf_measurement(int kind, const float *pe_params, const float *meas_params, int n_flows,
                       const float *enc, const float *x, int B, int N, int E, float prior_std,
                       float *lik, void *stream);
+
+/* Conditional-GLOW measurement (model/models.py:280-303; nf/cglow/CGlowModel.py with the
+ * default flow_depth K = 1, L = 1, x_size = y_size = (3,8,8)): particle (b,i) at
+ * x + b*x_rs + 2i, frame encoding of row b at enc + b*enc_rs (192 floats) -> the RAW
+ * likelihood -nll at lik + b*lik_rs + i (the row-max shift of :301-302 is the caller's:
+ * the filter's EXTERNAL-measurement phase 2, or measurement_model_cglow).
+ * pe_params: particle encoder 2->16->32->192 (row-paired MLP layout); glow_params:
+ * nfdpf_cglow_params_size(K) floats (layout: nfdpf.pack.cglow_tensors). */
+NFDPF_API int64_t nfdpf_cglow_params_size(int K);
+NFDPF_API int nfdpf_cglow_measurement(const float *pe_params, const float *glow_params, int K,
+                            const float *enc, int64_t enc_rs, const float *x, int64_t x_rs,
+                            int B, int N, float *lik, int64_t lik_rs, void *stream);
 
 /* particle_initialization (utils.py:46-62) in DEVICE rng mode:
  * uniform on [-width/2, width/2)^2 (or start + N(0,1) when true_state)        */

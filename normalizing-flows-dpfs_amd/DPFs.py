@@ -165,6 +165,8 @@ class DPF(nn.Module):
             dyn_flow=getattr(a, "NF_dyn_flow", "RealNVP"))
 
     def _fused_supported(self):
+        if self.measurement == "CGLOW":
+            return self.hidden_size == 192 and getattr(self.param, "flow_depth", 1) == 1
         return self.measurement in ("cos", "CRNVP", "NN", "gaussian") and self.hidden_size == 32
 
     def filtering_pos(self, obs, start_state_vs, vel_input):

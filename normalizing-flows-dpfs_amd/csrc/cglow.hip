@@ -1,0 +1,548 @@
+// cglow.hip -- the conditional-GLOW measurement (model/models.py:280-303 over
+// nf/cglow/CGlowModel.py:123-176 and nf/cglow/modules.py), BASELINE config 5.
+//
+// Per particle: x = particle_encoder(pos) reshaped (3,8,8); y = this row's frame encoding
+// (3,8,8), squeezed to (12,4,4); one CondGlowStep (K = 1, L = 1):
+//   cond-actnorm : (logs, bias) = tanh(MLP(convs(x)))          y = (y + bias) e^logs
+//   cond-1x1conv : W (12x12)    = tanh(MLP(convs(x)))          y = W y,  + 16 log|det W|
+//   cond-affine  : h = convs(x) (3->16->6->6 at 4x4); f([h, z1]) -> (shift, scale)
+//                  z2 = (z2 + shift) sigmoid(scale + 2)
+// then nll = -(logdet + Gaussian logp) / (192 log 2) and lik = -nll (raw; the row-max
+// shift of :301-302 is applied by the caller -- the filter's EXTERNAL-measurement phase or
+// measurement_model_cglow).
+//
+// Mapping (one workgroup = 4 waves = a tile of 16 particles, persistent over tiles):
+//   * layers whose outputs are per particle and wide (encoder 32->192, the conditioning
+//     MLPs, their 2x2-stride convs) run as f32 MFMA 16x16x4 GEMMs with the 16 particles as
+//     M; v_mfma_f32_16x16x4_f32 is an exact k-ordered fmaf chain;
+//   * layers over the 4x4 / 8x8 grids (the coupling's convolutions, actnorm, 1x1 conv,
+//     log-det) run on VALU with lane = (particle, 4x4 position): 16 lanes per particle, the
+//     same output channel in every lane, so weights are wave-uniform scalar loads; 3x3
+//     neighbourhoods are exchanged through LDS;
+//   * log|det W| of each particle's 12x12 matrix: Gaussian elimination with partial
+//     pivoting across the particle's 16 lanes (row r in lane r), rows exchanged by shuffles.
+#include <type_traits>
+
+#include "flows.hpp"
+
+namespace nfdpf {
+namespace cg {
+
+constexpr int kE = 192;       // particle / frame encoding (3 x 8 x 8)
+constexpr int kXH = 8;        // x_hidden_channels (arguments.py:63)
+constexpr int kXS = 16;       // x_hidden_size (arguments.py:64)
+constexpr int kC = 12;        // y channels after the squeeze
+constexpr int kCh = 6;        // coupling half
+constexpr int kYH = 8;        // y_hidden_channels
+constexpr int kTileP = 16;    // particles per workgroup tile
+constexpr int kThreads = 256;
+
+// ---- packed parameter layout (nfdpf.pack.cglow_tensors), floats, per CondGlowStep ----
+// conditioning net (x_Con: three 2x2-stride convs, x_Linear: 8->16->16->OUT)
+template <int OUT>
+struct Cond {
+  static constexpr int c0w = 0, c0b = c0w + kXH * 3 * 4, c2w = c0b + kXH, c2b = c2w + kXH * kXH * 4,
+                       c4w = c2b + kXH, c4b = c4w + kXH * kXH * 4, l0w = c4b + kXH, l0b = l0w + kXS * kXH,
+                       l2w = l0b + kXS, l2b = l2w + kXS * kXS, l4w = l2b + kXS, l4b = l4w + OUT * kXS,
+                       size = l4b + OUT;
+};
+using CondA = Cond<2 * kC>;    // actnorm: (logs, bias)
+using CondI = Cond<kC * kC>;   // 1x1 conv weight
+struct Aff {                   // CondAffineCoupling
+  static constexpr int r0w = 0, r0b = r0w + 16 * 3 * 9, r2w = r0b + 16, r2b = r2w + kCh * 16 * 4,
+                       r4w = r2b + kCh, r4b = r4w + kCh * kCh * 9, f0w = r4b + kCh,
+                       f0ab = f0w + kYH * kC * 9, f0al = f0ab + kYH, f2w = f0al + kYH,
+                       f2ab = f2w + kYH * kYH, f2al = f2ab + kYH, f4w = f2al + kYH,
+                       f4b = f4w + kC * kYH * 9, f4l = f4b + kC, f4nb = f4l + kC, size = f4nb + kC;
+};
+constexpr int kOffA = 0, kOffI = CondA::size, kOffF = kOffI + CondI::size;
+constexpr int kStep = kOffF + Aff::size;
+
+// ---- workgroup LDS ----
+struct Lds {
+  float pxy[kTileP][2];
+  float h1[kTileP][kPeH1 + 1];
+  float h2[kTileP][kPeH2 + 1];
+  float xs[kTileP][kE + 1];            // particle encoding, [c][8][8]
+  float cv1[kTileP][16][2 * kXH + 1];  // cond conv1 (A | I) at the 4x4 positions
+  float cv2[kTileP][4][2 * kXH + 1];   // cond conv2 at 2x2
+  float cv3[kTileP][2 * kXH + 1];
+  float v0[kTileP][2 * kXS + 1];
+  float v1[kTileP][2 * kXS + 1];
+  float an[kTileP][2 * kC + 1];        // actnorm (logs | bias)
+  float wm[kTileP][kC * kC + 1];       // 1x1 conv weight, row-major [out][in]
+  float ex[kTileP][16][kC + 1];        // 4x4-grid exchange
+  float yv[kTileP][16][kC + 1];        // y after actnorm + 1x1 conv, per position
+  float ld[kTileP];                    // per-particle log-det of actnorm + 1x1 conv
+  int row[kTileP];
+};
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__shared__ Lds S;  // one instance per workgroup, shared by the phase functions below
+
+// One 16x16 output tile of C = A B over K (zero-padded to 4*KSTEPS): lane l feeds A[l&15][k]
+// and B[k][l&15] for k = 4s + (l>>4), and gets C rows 4(l>>4)+i, column l&15.
+template <int KSTEPS, class FA, class FB>
+__device__ __forceinline__ f4 mfma_tile(const FA &fa, const FB &fb) {
+  const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa(r, 4 * s + kk), fb(4 * s + kk, r), acc, 0, 0, 0);
+  return acc;
+}
+template <class FE>
+__device__ __forceinline__ void mfma_store(const f4 &acc, const FE &epi) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) epi(4 * (l >> 4) + i, l & 15, acc[i]);
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+// A pointer argument of a non-inlined function arrives in VGPRs; it is wave-uniform, so move
+// it to SGPRs (readfirstlane) before making it a scalar-load weight pointer.
+__device__ __forceinline__ const float *sgpr_ptr(const float *p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const float *)(((uint64_t)hi << 32) | lo);
+}
+
+// log|det W| of the 12x12 matrix held one row per lane (lanes g*16 + r, r < 12), partial
+// pivoting by |value|; every lane of the group returns the same value.
+__device__ float logabsdet12(float (&a)[kC], int q) {
+  const int base = (threadIdx.x & 63) & ~15;  // first lane of this particle's group
+  float ld = 0.f;
+  bool done = q >= kC;                        // lanes 12..15 hold no row
+#pragma unroll
+  for (int k = 0; k < kC; ++k) {
+    // pivot: the undone row with the largest |a[r][k]|, ties to the lowest lane
+    float v = done ? -1.f : fabsf(a[k]);
+    int who = q;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(v, o, 16);
+      const int w2 = __shfl_xor(who, o, 16);
+      if (v2 > v || (v2 == v && w2 < who)) {
+        v = v2;
+        who = w2;
+      }
+    }
+    // pivot row to everyone
+    float prow[kC];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) prow[j] = __shfl(a[j], base + who, 64);
+    const float piv = prow[k];
+    ld += logf(fabsf(piv));
+    if (q == who) done = true;
+    if (!done) {
+      const float f = a[k] / piv;
+#pragma unroll
+      for (int j = 0; j < kC; ++j)
+        if (j > k) a[j] = fmaf(-f, prow[j], a[j]);
+    }
+  }
+  return ld;
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+// workgroup barrier that is also a scheduling fence
+#define SYNC()                            \
+  do {                                    \
+    __builtin_amdgcn_sched_barrier(0);    \
+    __syncthreads();                      \
+    __builtin_amdgcn_sched_barrier(0);    \
+  } while (0)
+
+// squeeze(y) at position q, cond-actnorm, cond-1x1 conv (-> S.yv), their log-dets (-> S.ld)
+__device__ __noinline__ void phase_y(const float *__restrict__ enc, int64_t enc_rs, int p, int q) {
+  const int qi = q >> 2, qj = q & 3;
+  const float *er = enc + (int64_t)S.row[p] * enc_rs;
+  float y[kC];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) y[c * 4 + f] = er[c * 64 + (2 * qi + (f >> 1)) * 8 + 2 * qj + (f & 1)];
+  float sl = 0.f;
+#pragma unroll
+  for (int c = 0; c < kC; ++c) {
+    const float ls = S.an[p][c];
+    y[c] = (y[c] + S.an[p][kC + c]) * expf(ls);
+    sl += ls;
+  }
+#pragma unroll
+  for (int o = 0; o < kC; ++o) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < kC; ++c) a = fmaf(S.wm[p][o * kC + c], y[c], a);
+    S.yv[p][q][o] = a;
+  }
+  float wr[kC];
+#pragma unroll
+  for (int j = 0; j < kC; ++j) wr[j] = q < kC ? S.wm[p][q * kC + j] : 0.f;
+  const float ldw = logabsdet12(wr, q);
+  if (q == 0) S.ld[p] = 16.0f * sl + 16.0f * ldw;  // dimensions (4x4) x (sum logs, log|det W|)
+}
+
+// resize_x = conv3x3(3->16, pad 1) ReLU, conv2x2/2(16->6) ReLU, fused per 4x4 position (the
+// 2x2 block of 8x8 conv1 outputs stays in registers) -> S.ex[p][q][0:6].  Weights are stored
+// tap-major, output channel fastest (nfdpf.pack.cglow_tensors), so each input value feeds a
+// contiguous run of output-channel pairs (v_pk_fma_f32 with an SGPR pair).
+__device__ __noinline__ void phase_resize(const float *glow_, int p, int q) {
+  const float *glow = sgpr_ptr(glow_);
+  const int qi = q >> 2, qj = q & 3;
+  float xp[3][4][4];  // rows 2qi-1 .. 2qi+2, cols 2qj-1 .. 2qj+2 of x, zero outside
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int rr = 2 * qi - 1 + r, ss = 2 * qj - 1 + s2;
+        xp[c][r][s2] = (rr >= 0 && rr < 8 && ss >= 0 && ss < 8) ? S.xs[p][c * 64 + rr * 8 + ss] : 0.f;
+      }
+  cf2 *F2 = (cf2 *)wptr(glow + kOffF);
+  f2 h62[kCh / 2];
+#pragma unroll
+  for (int m = 0; m < kCh / 2; ++m) h62[m] = F2[Aff::r2b / 2 + m];
+#pragma unroll
+  for (int ab = 0; ab < 4; ++ab) {
+    const int a = ab >> 1, b2 = ab & 1;
+    f2 hb[8];
+    F2 = (cf2 *)wptr(glow + kOffF);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) hb[m] = F2[Aff::r0b / 2 + m];
+#pragma unroll 3
+    for (int t = 0; t < 27; ++t) {  // taps (dr, ds, c) of the 3x3x3 window
+      F2 = (cf2 *)wptr(glow + kOffF);
+      const int dr = t / 9, ds = (t / 3) % 3, c = t % 3;
+      const float v = xp[c][a + dr][b2 + ds];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) hb[m] = pfma(F2[(Aff::r0w + t * 16) / 2 + m], splat(v), hb[m]);
+    }
+    F2 = (cf2 *)wptr(glow + kOffF);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const f2 hv = relu2(hb[m]);
+#pragma unroll
+      for (int n = 0; n < kCh / 2; ++n) {
+        h62[n] = pfma(F2[(Aff::r2w + (ab * 16 + 2 * m) * kCh) / 2 + n], splat(hv.x), h62[n]);
+        h62[n] = pfma(F2[(Aff::r2w + (ab * 16 + 2 * m + 1) * kCh) / 2 + n], splat(hv.y), h62[n]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < kCh / 2; ++m) {
+    S.ex[p][q][2 * m] = relu(h62[m].x);
+    S.ex[p][q][2 * m + 1] = relu(h62[m].y);
+  }
+}
+
+// 3x3 'same' conv on the 4x4 grid from the neighbours' channel vectors in S.ex; weights
+// [tap][c][o] with o fastest; acc holds NP output pairs
+template <int CIN, int NP>
+__device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int q, f2 (&acc)[NP]) {
+  const int qi = q >> 2, qj = q & 3;
+#pragma unroll 2
+  for (int tc = 0; tc < 9 * CIN; ++tc) {  // (tap, input channel), tap-major
+    const int t9 = tc / CIN, c = tc - CIN * (tc / CIN);
+    const int dr = t9 / 3, ds = t9 - 3 * (t9 / 3);
+    cf2 *F2 = (cf2 *)wptr(glow + kOffF);  // a few weights live at a time
+    const int rr = qi + dr - 1, ss = qj + ds - 1;
+    const bool in = rr >= 0 && rr < 4 && ss >= 0 && ss < 4;
+    const float v = in ? S.ex[p][rr * 4 + ss][c] : 0.f;
+#pragma unroll
+    for (int n = 0; n < NP; ++n) acc[n] = pfma(F2[(wofs + tc * (2 * NP)) / 2 + n], splat(v), acc[n]);
+  }
+}
+
+// resize conv3, the coupling net f, the affine update of z2 and the Gaussian log-prob;
+// returns this particle's sum (over its 16 positions) of log scale + logp
+__device__ __noinline__ float phase_f(const float *glow_, int p, int q) {
+  const float *glow = sgpr_ptr(glow_);
+  cfloat *F = wptr(glow + kOffF);
+  float fin[kC];  // cat(resize_x(x), z1)
+  {
+    f2 a3[kCh / 2];
+#pragma unroll
+    for (int m = 0; m < kCh / 2; ++m) a3[m] = ((cf2 *)F)[Aff::r4b / 2 + m];
+    conv3x3<kCh>(glow, Aff::r4w, p, q, a3);
+#pragma unroll
+    for (int m = 0; m < kCh / 2; ++m) {
+      fin[2 * m] = relu(a3[m].x);
+      fin[2 * m + 1] = relu(a3[m].y);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < kCh; ++c) fin[kCh + c] = S.yv[p][q][c];
+  SYNC();
+#pragma unroll
+  for (int c = 0; c < kC; ++c) S.ex[p][q][c] = fin[c];
+  SYNC();
+  // f: Conv2dNormy(12->8, 3x3) ReLU, Conv2dNormy(8->8, 1x1) ReLU, Conv2dZerosy(8->12) Tanh
+  float g8b[kYH];
+  {
+    f2 a0[kYH / 2];
+#pragma unroll
+    for (int m = 0; m < kYH / 2; ++m) a0[m] = splat(0.f);
+    conv3x3<kC>(glow, Aff::f0w, p, q, a0);
+    F = wptr(glow + kOffF);
+    float g8[kYH];
+#pragma unroll
+    for (int m = 0; m < kYH / 2; ++m) {
+      g8[2 * m] = relu((a0[m].x + F[Aff::f0ab + 2 * m]) * expf(F[Aff::f0al + 2 * m]));
+      g8[2 * m + 1] = relu((a0[m].y + F[Aff::f0ab + 2 * m + 1]) * expf(F[Aff::f0al + 2 * m + 1]));
+    }
+    f2 a1[kYH / 2];
+#pragma unroll
+    for (int m = 0; m < kYH / 2; ++m) a1[m] = splat(0.f);
+#pragma unroll
+    for (int c = 0; c < kYH; ++c)
+#pragma unroll
+      for (int m = 0; m < kYH / 2; ++m) a1[m] = pfma(((cf2 *)F)[(Aff::f2w + c * kYH) / 2 + m], splat(g8[c]), a1[m]);
+#pragma unroll
+    for (int m = 0; m < kYH / 2; ++m) {
+      g8b[2 * m] = relu((a1[m].x + F[Aff::f2ab + 2 * m]) * expf(F[Aff::f2al + 2 * m]));
+      g8b[2 * m + 1] = relu((a1[m].y + F[Aff::f2ab + 2 * m + 1]) * expf(F[Aff::f2al + 2 * m + 1]));
+    }
+  }
+  SYNC();
+#pragma unroll
+  for (int c = 0; c < kYH; ++c) S.ex[p][q][c] = g8b[c];
+  SYNC();
+  f2 a4[kC / 2];  // pair m = (shift_m, scale_m): channels 2m, 2m+1 (split_feature "cross")
+#pragma unroll
+  for (int m = 0; m < kC / 2; ++m) a4[m] = splat(0.f);
+  conv3x3<kYH>(glow, Aff::f4w, p, q, a4);
+  F = wptr(glow + kOffF);
+  float lsum = 0.f, lp = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCh; ++c) {
+    const float hs = tanhf((a4[c].x + F[Aff::f4b + 2 * c] + F[Aff::f4nb + 2 * c]) * expf(F[Aff::f4l + 2 * c] * 3.0f));
+    const float hc =
+        tanhf((a4[c].y + F[Aff::f4b + 2 * c + 1] + F[Aff::f4nb + 2 * c + 1]) * expf(F[Aff::f4l + 2 * c + 1] * 3.0f));
+    const float sc = sigmoidf_(hc + 2.0f);
+    const float z1 = S.yv[p][q][c];
+    const float z2 = (S.yv[p][q][kCh + c] + hs) * sc;
+    lsum += logf(sc);
+    lp += z2 * z2;
+    lp += z1 * z1;
+  }
+  // Gaussian logp over the 12 channels at this position, plus this position's log scale,
+  // summed over the particle's 16 positions (one DPP row)
+  float part = lsum - 0.5f * (lp + (float)kC * 1.8378770664093453f);
+  part += dpp_f<kDppXor1>(part);
+  part += dpp_f<kDppXor2>(part);
+  part += dpp_f<kDppHalfMirror>(part);
+  part += dpp_f<kDppMirror>(part);
+  return part;
+}
+
+
+
+// x: particle (b, i) at x + b * x_rs + 2 i;  enc: row b at enc + b * enc_rs (192 floats);
+// lik: (b, i) at lik + b * lik_rs + i.  Raw likelihood (no row-max shift).
+__global__ __launch_bounds__(kThreads, 2) void cglow_kernel(const float *__restrict__ pe,
+                                                            const float *__restrict__ glow,
+                                                            const float *__restrict__ enc,
+                                                            int64_t enc_rs, const float *__restrict__ x,
+                                                            int64_t x_rs, int B, int N,
+                                                            float *__restrict__ lik, int64_t lik_rs) {
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int64_t total = (int64_t)B * N;
+  const int64_t ntiles = (total + kTileP - 1) / kTileP;
+  auto PW = [](const float *w, int o, int i, int K) { return w[((o >> 1) * K + i) * 2 + (o & 1)]; };
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // weight pointers re-derived per tile behind an asm barrier, so the compiler re-reads
+    // weights from the caches instead of hoisting every one of them out of the tile loop
+    const float *gw = glow, *pe_ = pe;
+    asm volatile("" : "+s"(gw), "+s"(pe_));
+    const float *gA = gw + kOffA, *gI = gw + kOffI;
+    // encoder weights (nfdpf.pack.paired_mlp_tensors: row_pairs weights)
+    const float *pw1 = pe_, *pb1 = pe_ + kPeB1, *pw2 = pe_ + kPeW2, *pb2 = pe_ + kPeB2, *pw3 = pe_ + kPeW3,
+                *pb3 = pe_ + kPeW3 + kE * kPeH2;
+    auto W3 = [&](int n, int k) { return pw3[((n >> 1) * kPeH2 + k) * 2 + (n & 1)]; };
+    const int64_t g0 = tile * kTileP;
+    // ---- particles of the tile
+    if (tid < kTileP) {
+      const int64_t gi = g0 + tid;
+      float a = 0.f, c = 0.f;
+      int rb = 0;
+      if (gi < total) {
+        rb = (int)(gi / N);
+        const int i = (int)(gi - (int64_t)rb * N);
+        a = x[rb * x_rs + 2 * i];
+        c = x[rb * x_rs + 2 * i + 1];
+      }
+      S.pxy[tid][0] = a;
+      S.pxy[tid][1] = c;
+      S.row[tid] = rb;
+    }
+    SYNC();
+    // ---- particle encoder (model/models.py:141-150): 2 -> 16 -> 32 (ReLU), then 32 -> 192
+    {
+      const int p = tid >> 4, j = tid & 15;
+      const float h = fmaf(PW(pw1, j, 1, 2), S.pxy[p][1], fmaf(PW(pw1, j, 0, 2), S.pxy[p][0], pb1[j]));
+      S.h1[p][j] = relu(h);
+    }
+    SYNC();
+    {
+      const int p = tid >> 4, j = tid & 15;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int o = j + 16 * hh;
+        float a = pb2[o];
+#pragma unroll
+        for (int k = 0; k < kPeH1; ++k) a = fmaf(PW(pw2, o, k, kPeH1), S.h1[p][k], a);
+        S.h2[p][o] = relu(a);
+      }
+    }
+    SYNC();
+    for (int nt = w; nt < kE / 16; nt += 4) {
+      const int n0 = nt * 16;
+      const f4 acc = mfma_tile<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; },
+                                          [&](int k, int c) { return W3(n0 + c, k); });
+      mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + pb3[n0 + c]; });
+    }
+    SYNC();
+
+    // ---- conditioning nets, conv1 (3 -> 8, 2x2 stride 2, 8x8 -> 4x4) for actnorm (A) and
+    //      1x1-conv (I) nets: VALU, lane = (particle, 4x4 position)
+    const int p = w * 4 + (l >> 4), q = l & 15, qi = q >> 2, qj = q & 3;
+    {
+      float in[12];
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b2 = 0; b2 < 2; ++b2) in[c * 4 + a * 2 + b2] = S.xs[p][c * 64 + (2 * qi + a) * 8 + 2 * qj + b2];
+#pragma unroll
+      for (int net = 0; net < 2; ++net) {
+        cfloat *G = wptr(net ? gI : gA);
+#pragma unroll
+        for (int o = 0; o < kXH; ++o) {
+          float acc = G[CondA::c0b + o];
+#pragma unroll
+          for (int k = 0; k < 12; ++k) acc = fmaf(G[CondA::c0w + k * kXH + o], in[k], acc);
+          S.cv1[p][q][net * kXH + o] = relu(acc);
+        }
+      }
+    }
+    SYNC();
+    // conv2 (8 -> 8, 2x2 stride 2, 4x4 -> 2x2): GEMM, rows (particle, 2x2 pos), k (ci, a, b)
+    for (int job = w; job < 8; job += 4) {
+      const int net = job >> 2, mt = job & 3;  // 4 row tiles of 16 = 64 rows
+      const float *G = net ? gI : gA;
+      const f4 acc = mfma_tile<8>(
+          [&](int r, int k) {
+            const int row = mt * 16 + r, pp = row >> 2, pos = row & 3;
+            const int ci = k >> 2, a = (k >> 1) & 1, b2 = k & 1;
+            return S.cv1[pp][(2 * (pos >> 1) + a) * 4 + 2 * (pos & 1) + b2][net * kXH + ci];
+          },
+          [&](int k, int c) { return c < kXH ? G[CondA::c2w + c * 32 + k] : 0.f; });
+      mfma_store(acc, [&](int r, int c, float v) {
+        if (c < kXH) {
+          const int row = mt * 16 + r;
+          S.cv2[row >> 2][row & 3][net * kXH + c] = relu(v + G[CondA::c2b + c]);
+        }
+      });
+    }
+    SYNC();
+    // conv3 (8 -> 8, 2x2 stride 2, 2x2 -> 1x1): rows = particles, k = (ci, a, b)
+    if (w < 2) {
+      const int net = w;
+      const float *G = net ? gI : gA;
+      const f4 acc = mfma_tile<8>(
+          [&](int r, int k) { return S.cv2[r][k & 3][net * kXH + (k >> 2)]; },
+          [&](int k, int c) { return c < kXH ? G[CondA::c4w + c * 32 + k] : 0.f; });
+      mfma_store(acc, [&](int r, int c, float v) {
+        if (c < kXH) S.cv3[r][net * kXH + c] = relu(v + G[CondA::c4b + c]);
+      });
+    }
+    SYNC();
+    // x_Linear: 8 -> 16 -> 16 (ReLU)
+    if (w < 2) {
+      const int net = w;
+      const float *G = net ? gI : gA;
+      const f4 acc = mfma_tile<2>([&](int r, int k) { return S.cv3[r][net * kXH + k]; },
+                                  [&](int k, int c) { return G[CondA::l0w + c * kXH + k]; });
+      mfma_store(acc, [&](int r, int c, float v) { S.v0[r][net * kXS + c] = relu(v + G[CondA::l0b + c]); });
+    }
+    SYNC();
+    if (w < 2) {
+      const int net = w;
+      const float *G = net ? gI : gA;
+      const f4 acc = mfma_tile<4>([&](int r, int k) { return S.v0[r][net * kXS + k]; },
+                                  [&](int k, int c) { return G[CondA::l2w + c * kXS + k]; });
+      mfma_store(acc, [&](int r, int c, float v) { S.v1[r][net * kXS + c] = relu(v + G[CondA::l2b + c]); });
+    }
+    SYNC();
+    // last layer + tanh: actnorm (24 = 2 tiles) and 1x1 conv (144 = 9 tiles)
+    for (int job = w; job < 11; job += 4) {
+      const bool isI = job >= 2;
+      const int n0 = (isI ? job - 2 : job) * 16, nout = isI ? kC * kC : 2 * kC;
+      const float *G = isI ? gI : gA;
+      const int lw = isI ? CondI::l4w : CondA::l4w, lb = isI ? CondI::l4b : CondA::l4b;
+      const f4 acc = mfma_tile<4>([&](int r, int k) { return S.v1[r][(isI ? kXS : 0) + k]; },
+                                  [&](int k, int c) { return n0 + c < nout ? G[lw + (n0 + c) * kXS + k] : 0.f; });
+      mfma_store(acc, [&](int r, int c, float v) {
+        const int n = n0 + c;
+        if (n < nout) {
+          const float t = tanhf(v + G[lb + n]);
+          if (isI)
+            S.wm[r][n] = t;
+          else
+            S.an[r][n] = t;
+        }
+      });
+    }
+    SYNC();
+
+    // ---- squeeze(y) at position q, cond-actnorm, cond-1x1 conv, log|det W|
+    phase_y(enc, enc_rs, p, q);
+    SYNC();
+    phase_resize(gw, p, q);
+    SYNC();
+    const float part = phase_f(gw, p, q);
+    const int64_t gi = g0 + p;
+    if (q == 0 && gi < total) {
+      // logdet0 = -log(256) * 192, plus actnorm / 1x1-conv log-dets, plus this particle's sum
+      const float obj = (-5.545177444479562f * (float)kE + S.ld[p]) + part;
+      const int rb = S.row[p];
+      const int i = (int)(gi - (int64_t)rb * N);
+      lik[rb * lik_rs + i] = obj / (0.6931471805599453f * (float)kE);
+    }
+    SYNC();
+  }
+}
+
+}  // namespace nfdpf
+
+using namespace nfdpf;
+
+extern "C" int64_t nfdpf_cglow_params_size(int K) { return K == 1 ? (int64_t)kStep : -1; }
+
+extern "C" int nfdpf_cglow_measurement(const float *pe_params, const float *glow_params, int K,
+                                       const float *enc, int64_t enc_rs, const float *x, int64_t x_rs,
+                                       int B, int N, float *lik, int64_t lik_rs, void *stream) {
+  NFDPF_REQUIRE(pe_params && glow_params && enc && x && lik, "nfdpf_cglow_measurement: null pointer");
+  NFDPF_REQUIRE(K == 1, "nfdpf_cglow_measurement: built for flow_depth K = 1 (got %d)", K);
+  NFDPF_REQUIRE(B >= 0 && N >= 1, "nfdpf_cglow_measurement: bad sizes");
+  if (B == 0) return NFDPF_OK;
+  const int64_t tiles = ((int64_t)B * N + kTileP - 1) / kTileP;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
+  }
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 4);
+  cglow_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(pe_params, glow_params, enc, enc_rs, x, x_rs, B, N,
+                                                        lik, lik_rs);
+  return launch_status("nfdpf_cglow_measurement");
+}

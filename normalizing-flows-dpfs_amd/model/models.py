@@ -245,11 +245,14 @@ class measurement_model_cglow(nn.Module):
         self.CGLOW = CGLOW
 
     def forward(self, encodings, update_particles):
-        B, N, D = update_particles.shape
-        es = self.particle_encoder(update_particles.reshape(-1, D).float()).reshape(B * N, 3, 8, 8)
-        eo = encodings[:, None, ...].repeat(1, N, 1).reshape(B * N, 3, 8, 8)
-        _, nll = self.CGLOW(es, eo)
-        lik = -nll.reshape(B, N)
+        """One HIP kernel (csrc/cglow.hip: encoder, conditioning nets, actnorm, 1x1 conv with
+        its 12x12 log-determinant, affine coupling, Gaussian log-prob), then the row-max shift.
+        Forward only: gradients through CGLOW are SURVEY §8(f1) work."""
+        from nfdpf.pack import cglow_tensors
+        m = self
+        pe = blob(m, "pe", m.particle_encoder, lambda: paired_mlp_tensors(m.particle_encoder), update_particles.device)
+        glow = blob(m, "glow", m.CGLOW, lambda: cglow_tensors(m.CGLOW), update_particles.device)
+        lik = _ops.cglow_measurement(pe, glow, encodings.float(), update_particles.float())
         return lik - lik.max(dim=-1, keepdim=True)[0]
 
 

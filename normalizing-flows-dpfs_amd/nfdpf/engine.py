@@ -20,7 +20,7 @@ import torch.distributed as dist
 
 from . import _lib as L
 from . import ops
-from .pack import blob, flows_tensors, paired_mlp_tensors
+from .pack import blob, cglow_tensors, flows_tensors, paired_mlp_tensors
 
 
 @dataclass
@@ -136,6 +136,8 @@ class FilterEngine:
             meas = blob(m, "meas", m.cnf_measurement.flows, lambda: flows_tensors(m.cnf_measurement.flows), dev)
         elif c.measurement == "NN":
             meas = blob(m, "meas", m.likelihood_est, lambda: paired_mlp_tensors(m.likelihood_est), dev)
+        elif c.measurement == "CGLOW":
+            meas = blob(m, "glow", m.cglow_measurement, lambda: cglow_tensors(m.cglow_measurement), dev)
         return dyn, cond, pe, meas
 
     # -- main loop --------------------------------------------------------------------------
@@ -149,8 +151,12 @@ class FilterEngine:
         c = self.cfg
         dev = enc.device
         L.require_device(enc, "FilterEngine.run")
-        if c.measurement not in ("cos", "CRNVP", "NN", "gaussian"):
+        if c.measurement not in ("cos", "CRNVP", "NN", "gaussian", "CGLOW"):
             raise L.NfdpfError(f"measurement '{c.measurement}' has no HIP kernel in this build")
+        # CGLOW runs as its own kernel between the step's two phases: phase 1 ends with the
+        # proposal particles in hist_x slot t, the CGLOW kernel writes their raw likelihood,
+        # phase 2 takes it from there (row-max shift, weights, normalisation)
+        external = c.measurement == "CGLOW"
         enc = enc.float().contiguous()
         B, T, E = enc.shape
         N = c.N
@@ -210,7 +216,10 @@ class FilterEngine:
         d.B_global, d.phase, d.row_base = shard.B_global, 0, shard.row_base
         d.nf_dyn = (L.DYN_MAF if c.dyn_flow == "MAF" else L.DYN_REALNVP) if c.NF_dyn else L.DYN_NONE
         d.nf_cond = int(c.NF_cond)
-        d.measurement, d.resampler = L.MEAS[c.measurement], L.RESAMPLE[c.resampler]
+        d.measurement = L.MEAS_EXTERNAL if external else L.MEAS[c.measurement]
+        d.resampler = L.RESAMPLE[c.resampler]
+        lik_ext = torch.empty((B, N), **f32) if external else None
+        d.lik_ext = L.ptr(lik_ext)
         d.rng_mode = L.RNG_HOST if host_mode else L.RNG_DEVICE
         d.force_resample, d.n_flows, d.hidden = int(c.force_resample), c.n_flows, c.hidden
         d.alpha, d.pos_noise = c.alpha, c.pos_noise
@@ -291,10 +300,15 @@ class FilterEngine:
                 ev = EventPair()
                 self.step_events.append(ev)
                 d.prof_events = ev.ptr
-            if tiled:
-                ops.filter_step_tiled(d, ws, dev)
+            step = (lambda: ops.filter_step_tiled(d, ws, dev)) if tiled else (lambda: ops.filter_step(d, dev))
+            if external:
+                d.phase = 1
+                step()
+                ops.cglow_measurement(pe, meas, enc[:, t], hx[:, t], out=lik_ext)
+                d.phase = 2
+                step()
             else:
-                ops.filter_step(d, dev)
+                step()
             ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)

@@ -155,6 +155,27 @@ def measurement(kind: str, pe_blob, meas_blob, n_flows, enc, x, prior_std=2.5):
     return lik
 
 
+def cglow_measurement(pe_blob, glow_blob, enc, x, K=1, out=None):
+    """Conditional-GLOW likelihood (model/models.py:280-303) WITHOUT the row-max shift:
+    enc [B, 192] (or rows of a strided [B, T, 192] view), x [B, N, 2] (rows may be strided)
+    -> raw lik [B, N]."""
+    require_device(x, "cglow_measurement")
+    B, N, _ = x.shape
+    if x.stride(2) != 1 or x.stride(1) != 2:
+        x = x.contiguous()
+    if enc.stride(-1) != 1:
+        enc = enc.contiguous()
+    if enc.shape[-1] != 192:
+        raise L.NfdpfError("cglow_measurement: frame encodings must be 192 wide (--hiddensize 192)")
+    if int(glow_blob.numel()) != int(lib().nfdpf_cglow_params_size(int(K))):
+        raise L.NfdpfError("cglow_measurement: parameter blob does not match flow_depth K")
+    lik = out if out is not None else torch.empty((B, N), device=x.device, dtype=f32)
+    check(lib().nfdpf_cglow_measurement(ptr(pe_blob), ptr(glow_blob), int(K), ptr(enc), enc.stride(0), ptr(x),
+                                        x.stride(0), B, N, ptr(lik), lik.stride(0), stream_ptr(x.device)),
+          "nfdpf_cglow_measurement")
+    return lik
+
+
 def particle_init(start_xy, B, N, width, true_state, seed, row_base=0, device=None):
     """particle_initialization (utils.py:46-62), device RNG -> (x [B,N,2], logw [B,N])."""
     device = device if device is not None else start_xy.device

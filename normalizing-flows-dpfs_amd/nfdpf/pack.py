@@ -76,6 +76,39 @@ def paired_mlp_tensors(seq: nn.Module):
     return out
 
 
+def _taps_last(w: torch.Tensor) -> torch.Tensor:
+    """Conv weight [out][in][kh][kw] -> [kh][kw][in][out]: one tap's input channel feeds a
+    contiguous run of output channels (csrc/cglow.hip)."""
+    return w.permute(2, 3, 1, 0)
+
+
+def _cond_net_tensors(m: nn.Module):
+    """CondActNorm / Cond1x1Conv conditioning net (nf/cglow/modules.py:84-101, 145-162):
+    x_Con conv 0 as [k][out] (k = in, kh, kw), convs 2, 4 and the x_Linear layers as stored."""
+    c0, c2, c4 = [l for l in m.x_Con if isinstance(l, nn.Conv2d)]
+    l0, l2, l4 = _linears(m.x_Linear)
+    return [c0.weight.reshape(c0.weight.shape[0], -1).t(), c0.bias, c2.weight, c2.bias, c4.weight, c4.bias,
+            l0.weight, l0.bias, l2.weight, l2.bias, l4.weight, l4.bias]
+
+
+def cglow_tensors(glow: nn.Module):
+    """CondGlowModel (nf/cglow/CGlowModel.py) with K = 1, L = 1: the CondGlowStep's actnorm
+    net, 1x1-conv net, then the affine coupling (modules.py:258-303) in the kernel layout of
+    csrc/cglow.hip (Aff): resize_x / f convolutions tap-major, output channel fastest."""
+    steps = [l for l in glow.flow.layers if hasattr(l, "affine")]
+    if len(steps) != 1:
+        raise ValueError(f"the CGLOW kernel is built for flow_depth K = 1 (got {len(steps)} steps)")
+    st = steps[0]
+    a = st.affine
+    r0, r2, r4 = [l for l in a.resize_x if isinstance(l, nn.Conv2d)]
+    f0, f2, f4 = [l for l in a.f if isinstance(l, nn.Conv2d)]
+    return (_cond_net_tensors(st.actnorm) + _cond_net_tensors(st.invconv) +
+            [_taps_last(r0.weight), r0.bias, _taps_last(r2.weight), r2.bias, _taps_last(r4.weight), r4.bias,
+             _taps_last(f0.weight), f0.actnorm.bias, f0.actnorm.logs,
+             f2.weight.reshape(f2.weight.shape[0], -1).t(), f2.actnorm.bias, f2.actnorm.logs,
+             _taps_last(f4.weight), f4.bias, f4.logs, f4.newbias])
+
+
 def flows_tensors(flows):
     out = []
     for f in flows:

@@ -64,4 +64,4 @@ def e2e_cfg(fx):
     return dict(N=int(fx["N"]), NF_dyn=bool(flag("NF_dyn")), NF_cond=bool(flag("NF_cond")), measurement=m,
                 resampler=flag("resampler_type"), alpha=0.5, eps=0.1, scaling=0.75, threshold=1e-3,
                 max_iter=100, pos_noise=20.0, vel_noise=20.0, width=128, n_flows=2, cglow_K=1,
-                dyn_flow=str(flag("NF_dyn_flow")) if "flag/NF_dyn_flow" in fx else "RealNVP")
+                dyn_flow=str(flag("NF_dyn_flow")) if "flag/NF_dyn_flow" in fx else "RealNVP", H=int(fx["H"]))

@@ -203,15 +203,75 @@ def test_measurement_golden(meas):
     assert_close(lik.cpu(), fx["lik"], 1e-5, 2e-5, meas)
 
 
+def _glow_module(w, prefix="cglow_measurement."):
+    """CondGlowModel with the default arguments (K = 1, L = 1) holding the fixture weights."""
+    from arguments import parse_args
+    from nf.cglow.CGlowModel import CondGlowModel
+    m = CondGlowModel(parse_args([]))
+    sd = m.state_dict()
+    sd.update({k[len(prefix):]: v for k, v in w.items() if k.startswith(prefix)})
+    m.load_state_dict(sd)
+    return m
+
+
+def _oracle_cglow64(w, enc, x):
+    """The oracle's CGLOW likelihood in float64 (row-max shifted)."""
+    with O.precision(torch.float64):
+        p = O.cast_params(w, torch.float64)
+        return O.meas_cglow(O.sub(p, "particle_encoder"), O.sub(p, "cglow_measurement"), 1,
+                            enc.double(), x.double()).numpy()
+
+
+def test_cglow_measurement_golden():
+    """measurement_model_cglow (model/models.py:280-303) on the reference's golden vectors:
+    one HIP kernel (csrc/cglow.hip) vs the reference's float32 output, and both against the
+    oracle in float64 (the reference's own float32 error is the yardstick)."""
+    from nfdpf import ops
+    from nfdpf.pack import cglow_tensors
+    fx = group(load("meas.npz"), "CGLOW")
+    w = weights(fx)
+    pe = _mlp_blob(w, "particle_encoder")
+    glow = torch.cat([a.detach().reshape(-1) for a in cglow_tensors(_glow_module(w))]).to(DEV)
+    enc, x = t(fx["enc"]), t(fx["x"])
+    raw = ops.cglow_measurement(pe, glow, enc.to(DEV), x.to(DEV))
+    lik = (raw - raw.max(dim=-1, keepdim=True)[0]).cpu().numpy()
+    ref64 = _oracle_cglow64(w, enc, x)
+    e_ours = np.abs(lik - ref64)
+    e_ref = np.abs(fx["lik"] - ref64)
+    print(f"CGLOW: max |ours - f64| {e_ours.max():.3e} mean {e_ours.mean():.3e}; "
+          f"reference f32 max {e_ref.max():.3e} mean {e_ref.mean():.3e}")
+    assert e_ours.max() <= 4 * e_ref.max() + 1e-5
+    assert e_ours.mean() <= 2.5 * e_ref.mean() + 1e-6
+    assert_close(lik, fx["lik"], 1e-5, 5e-5, "CGLOW lik")
+
+
+def test_cglow_module_matches_kernel():
+    """measurement_model_cglow.forward (the reference module API) runs the same kernel."""
+    from model.models import build_particle_encoder_cglow, measurement_model_cglow
+    fx = group(load("meas.npz"), "CGLOW")
+    w = weights(fx)
+    pe = build_particle_encoder_cglow(192, 2)
+    pe.load_state_dict({k[len("particle_encoder."):]: v for k, v in w.items() if k.startswith("particle_encoder.")})
+    m = measurement_model_cglow(pe, _glow_module(w)).to(DEV)
+    lik = m(t(fx["enc"]).to(DEV), t(fx["x"]).to(DEV)).cpu()
+    assert_close(lik, fx["lik"], 1e-5, 5e-5, "CGLOW module")
+
+
 class _Models(torch.nn.Module):
     """Minimal holder with the DPF attribute names the engine reads."""
 
     def __init__(self, w, cfg):
         super().__init__()
-        from model.models import build_conditional_nf, build_likelihood, build_maf_dyn, build_particle_encoder
+        from model.models import (build_conditional_nf, build_likelihood, build_maf_dyn, build_particle_encoder,
+                                  build_particle_encoder_cglow)
+        H = cfg.get("H", 32)
         self.nf_dyn = build_maf_dyn(2, 2) if cfg.get("dyn_flow") == "MAF" else build_conditional_nf(2, 4, 2)
-        self.cond_model = build_conditional_nf(2, 36, 2)
-        self.particle_encoder = build_particle_encoder(32, 2)
+        self.cond_model = build_conditional_nf(2, 4 + H, 2)
+        if cfg["measurement"] == "CGLOW":
+            self.particle_encoder = build_particle_encoder_cglow(H, 2)
+            self.cglow_measurement = _glow_module(w)
+        else:
+            self.particle_encoder = build_particle_encoder(32, 2)
         if cfg["measurement"] == "CRNVP":
             self.cnf_measurement = build_conditional_nf(2, 32, 32, prior_std=2.5)
         if cfg["measurement"] == "NN":
@@ -244,7 +304,7 @@ class _TapeDraws:
         return self.tape.noise(B, N, std)
 
 
-E2E_FUSED = ["c1", "c2", "c2w", "c3", "c3n", "c4"]
+E2E_FUSED = ["c1", "c2", "c2w", "c3", "c3n", "c4", "c5"]
 
 
 def _oracle64_one_step(fx, monkeypatch):
@@ -333,7 +393,7 @@ def test_filter_step_one_step_parity(name, kernel, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4", "c5"])
 def test_filtering_free_running(name, kernel):
     """Whole sequences from the reference's initial state and draws."""
     fx = load(f"e2e_{name}.npz")
