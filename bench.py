@@ -38,6 +38,13 @@ CONFIGS = {
            13.1e3 * (5888 + 1792 + 3136) / 12608),
     "c3": (dict(NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler_type="ot"), 64, 1000, 50, 12.7e3,
            12.7e3),
+    # C4: B=256 over 8 GPUs -> 32 rows per GPU; MAF dynamic flow, OT (9.8k + OT)
+    "c4": (dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="ot", NF_dyn_flow="MAF"), 32, 4000,
+           50, 9.8e3, 9.8e3),
+    # C5: B=512 over 8 GPUs -> 64 rows per GPU, N=10000, T=100, CGLOW measurement (--hiddensize 192);
+    # 201k FLOP per particle-step, of which the CGLOW kernel (A13) 13,376 + 158,080
+    "c5": (dict(NF_dyn=True, NF_cond=True, measurement="CGLOW", resampler_type="soft", hiddensize=192), 64,
+           10000, 100, 201e3, 13376 + 158080),
 }
 B_ALG = 52.0            # algorithmic HBM bytes per particle-step
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
@@ -90,9 +97,12 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
     Bs, Ts = B, T
     if flags["resampler_type"] == "ot":
         Bs, Ts = max(1, B // 16), min(T, 10)   # one FP64 OT call is tens of seconds at B=64
+    if N >= 4000:
+        Bs, Ts = 4, 8                          # C4 / C5: 4 rows x 8 steps (dense N^2 resampler work)
     cfg = dict(N=N, NF_dyn=flags["NF_dyn"], NF_cond=flags["NF_cond"], measurement=flags["measurement"],
                resampler=flags["resampler_type"], alpha=0.5, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100,
-               pos_noise=20.0, vel_noise=20.0, width=128, n_flows=2)
+               pos_noise=20.0, vel_noise=20.0, width=128, n_flows=2, cglow_K=1,
+               dyn_flow=flags.get("NF_dyn_flow", "RealNVP"))
     run = lambda: O.filtering(cfg, params, enc[:Bs, :Ts], start[:Bs], vel[:Bs, :Ts], rng=O.HostRNG())
     with torch.no_grad():
         t0 = time.perf_counter()
@@ -135,7 +145,7 @@ def main():
     from nfdpf.engine import FilterEngine, ShardInfo
     flags, B, N, T, F_STEP, F_PROP = CONFIGS[args.config]
     B = args.batch or B
-    F_ALG = F_PROP if args.kernel == "tiled" else F_STEP
+    F_ALG = F_PROP if (args.kernel == "tiled" or flags["measurement"] == "CGLOW") else F_STEP
     torch.manual_seed(2)
     a = make_args(flags, B, N, T, {"force_resample": args.force_resample})
     dpf = DPF(a).to(dev).eval()
@@ -175,6 +185,8 @@ def main():
     for e in evs:
         e.close()
     kname = "tiled_prop_kernel" if args.kernel == "tiled" else "filter_step_kernel"
+    if flags["measurement"] == "CGLOW":
+        kname = "cglow_kernel"
     # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
     se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
     cnt = torch.tensor(float(res.pred.numel()), device=dev, dtype=torch.float64)

@@ -294,17 +294,23 @@ class FilterEngine:
                 else:
                     d.ot_x = xin.data_ptr()  # not read: the motion stage keeps the previous particles
             d.prof_events = None
+            ev = None
             if self.step_events is not None and t == T // 2:
                 # one sampled step per pass: an event pair costs ~6 us of stream time
                 from .prof import EventPair
                 ev = EventPair()
                 self.step_events.append(ev)
-                d.prof_events = ev.ptr
+                if not external:
+                    d.prof_events = ev.ptr  # around the step's dominant launch, inside the library
             step = (lambda: ops.filter_step_tiled(d, ws, dev)) if tiled else (lambda: ops.filter_step(d, dev))
             if external:
                 d.phase = 1
                 step()
+                if ev is not None:
+                    ev.record_start(dev)  # the CGLOW kernel is the step's dominant launch
                 ops.cglow_measurement(pe, meas, enc[:, t], hx[:, t], out=lik_ext)
+                if ev is not None:
+                    ev.record_end(dev)
                 d.phase = 2
                 step()
             else:

@@ -19,6 +19,7 @@ def hip():
         _hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
         _hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
         _hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+        _hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     return _hip
 
 
@@ -37,6 +38,19 @@ class EventPair:
     @property
     def ptr(self) -> int:
         return ctypes.addressof(self.arr)
+
+    def _record(self, k: int, device):
+        from ._lib import stream_ptr
+        rc = hip().hipEventRecord(self.arr[k], ctypes.c_void_p(stream_ptr(device)))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def record_start(self, device):
+        """Record event 0 on the stream the next nfdpf launch on ``device`` goes to."""
+        self._record(0, device)
+
+    def record_end(self, device):
+        self._record(1, device)
 
     def ms(self) -> float:
         hip().hipEventSynchronize(self.arr[1])
