@@ -92,7 +92,7 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
     a = make_args(flags, B, N, T, {})
     from DPFs import DPF
     dpf = DPF(a)
-    params = {k: v.detach().float() for k, v in dpf.state_dict().items()}
+    params = {k: v.detach().float().cpu() for k, v in dpf.state_dict().items()}
     start, state, vel, enc = synthetic_disk(B, T, 2, a.hiddensize)
     Bs, Ts = B, T
     if flags["resampler_type"] == "ot":
