@@ -140,70 +140,81 @@ __device__ __forceinline__ void store_sums4(double *dst, double a, double b, dou
   block_sum4_store(a, b, c, e, sh, dst);
 }
 
-// ---- K0: soft resampling of the rows where the gate fires (one workgroup per row)
-__global__ __launch_bounds__(512) void tiled_soft_kernel(const nfdpf_filter_desc d, TiledWs ws) {
-  extern __shared__ float Cbuf[];
-  __shared__ StepShared L;
-  __shared__ int fire_sh;
-  const int tiles = n_tiles(d.N);
-  const int b = blockIdx.x;
-  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh);
-  if (threadIdx.x == 0) ws.fire[b] = fire;  // the motion kernel's decision for this row
-  if (!fire) return;
-  const RowSlot S = row_slot(d, b);
-  const float *xprev = d.x_prev + b * d.x_prev_rs;
-  const float *pprev = d.p_prev + b * d.p_prev_rs;
-  SoftRow row{pprev, d.N, d.alpha, 1.0f / (float)d.N, (float)(1.0 - (double)d.alpha), 1.0f};
-  float off;
-  if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
-    off = d.host_offsets[b];
-  else
-    off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, d.row_base + b, 0u).x) * (1.0f / (float)d.N);
-  const int64_t flat0 = (int64_t)d.N * (d.row_base + b);
-  const int N = d.N;
-  soft_row_search(row, d.lin, off, Cbuf, L.d, L.f, [&](int i, int src) {
-    const float *xs;
-    float w;
-    if (src < N) {
-      xs = xprev + 2 * src;
-      w = row.w(src);
-    } else if (b + 1 < d.B) {
-      xs = xprev + d.x_prev_rs;
-      w = 0.f;
-    } else {
-      xs = xprev + 2 * (N - 1);
-      w = 0.f;
-    }
-    S.hx[2 * i] = xs[0];
-    S.hx[2 * i + 1] = xs[1];
-    S.hp[i] = w;
-    S.hidx[i] = flat0 + src;
-  });
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const float s = cascade_row_sum([&](int j) { return S.hp[j]; }, N);
-    if (threadIdx.x == 0) ws.S2[b] = s;
-  }
-}
-
-// ---- K1: motion
-__global__ __launch_bounds__(kTile) void tiled_motion_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+// ---- K1: ESS gate + resampling + motion, per (tile, row).  The gate (DPFs.py:163-165) is
+// evaluated block-parallel in every workgroup (same inputs, same order, same decision).  Soft
+// resampling (resamplers.py:20-60) of the row: every tile of the row builds the row's CDF in
+// LDS and searches all N markers (the renormaliser is a cascade sum over the whole row's
+// gathered weights), keeping its own particles' sources in registers -- so resampling and
+// motion share one launch and the resampled state never round-trips through HBM.
+// Dynamic LDS: C[max(N, B_global)] then w'[N].
+__global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  extern __shared__ float dyn_lds[];
   __shared__ double shd[16];
+  __shared__ float shf[16];
+  __shared__ int fire_sh;
+  __shared__ float xr_sh[kTile][2];
+  __shared__ int src_sh[kTile];
   TRACE(0, 0)
-  const int tiles = n_tiles(d.N);
+  const int tiles = n_tiles(d.N), N = d.N;
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
   const int64_t grow = d.row_base + b;
-  // soft: the decision K0 took for this row; OT: the gate launched before the resampler
-  const bool fire = d.resampler == NFDPF_RESAMPLE_SOFT ? ws.fire[b] != 0 : tiled_gate(d, tiles);
+  float *Cbuf = dyn_lds;
+  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh);
   const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
   const RowSlot S = row_slot(d, b);
+  const float *xprev = d.x_prev + b * d.x_prev_rs;
+  const float *pprev = d.p_prev + b * d.p_prev_rs;
+  float x0 = 0.f, x1 = 0.f, lr = 0.f;
+  if (mode == kSrcSoft) {
+    float *wbuf = dyn_lds + max(N, d.B_global);
+    SoftRow row{pprev, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
+    float off;
+    if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
+      off = d.host_offsets[b];
+    else
+      off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, grow, 0u).x) * (1.0f / (float)N);
+    const int i0 = tile * kTile;
+    soft_row_search(row, d.lin, off, Cbuf, shd, shf, [&](int j, int src) {
+      // src == N: the reference's out-of-range edge (next row's first particle, weight 0)
+      float w = 0.f;
+      if (src < N) w = row.w(src);
+      wbuf[j] = w;
+      if (j >= i0 && j < i0 + kTile) {
+        const float *xs = src < N ? xprev + 2 * src : (b + 1 < d.B ? xprev + d.x_prev_rs : xprev + 2 * (N - 1));
+        xr_sh[j - i0][0] = xs[0];
+        xr_sh[j - i0][1] = xs[1];
+        src_sh[j - i0] = src;
+      }
+    });
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const float s2 = cascade_row_sum([&](int j) { return wbuf[j]; }, N);
+      if (threadIdx.x == 0) shf[8] = s2;
+    }
+    __syncthreads();
+    if (i < N) {
+      x0 = xr_sh[threadIdx.x][0];
+      x1 = xr_sh[threadIdx.x][1];
+      lr = logf(wbuf[i] / shf[8]);
+      S.hidx[i] = (int64_t)N * grow + src_sh[threadIdx.x];
+    }
+  } else if (i < N) {
+    if (mode == kSrcOt) {
+      x0 = d.ot_x[((int64_t)b * N + i) * 2];
+      x1 = d.ot_x[((int64_t)b * N + i) * 2 + 1];
+      lr = logf(1.0f / (float)N);
+    } else {
+      x0 = xprev[2 * i];
+      x1 = xprev[2 * i + 1];
+      lr = logf(pprev[i]);
+    }
+    S.hidx[i] = (int64_t)N * grow + i;
+  }
   double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
-  if (i < d.N) {
+  if (i < N) {
     float p0, p1;
-    stage_motion(d, S, b, grow, i, mode, d.x_prev + b * d.x_prev_rs, d.p_prev + b * d.p_prev_rs,
-                 mode == kSrcSoft ? ws.S2[b] : 1.f, logf(1.0f / (float)d.N), d.vel[2 * b],
-                 d.vel[2 * b + 1], p0, p1);
+    motion_apply(d, S, b, grow, i, x0, x1, lr, d.vel[2 * b], d.vel[2 * b + 1], p0, p1);
     s0 = p0;
     s1 = p1;
     q0 = (double)p0 * p0;
@@ -524,9 +535,9 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
   TiledWs ws = tiled_carve(workspace, d.B, d.N, d.T);
   const dim3 g(n_tiles(d.N), d.B);
   if (d.phase != 2) {
-    if (d.resampler == NFDPF_RESAMPLE_SOFT)
-      tiled_soft_kernel<<<d.B, 512, std::max(d.N, d.B_global) * sizeof(float), st>>>(d, ws);
-    tiled_motion_kernel<<<g, kTile, 0, st>>>(d, ws);
+    const size_t lds = d.resampler == NFDPF_RESAMPLE_SOFT ? (size_t)(std::max(d.N, d.B_global) + d.N) * 4
+                                                         : (size_t)d.B_global * 4;
+    tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
     if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
     hipEvent_t *ev = (hipEvent_t *)d.prof_events;
     if (ev) (void)hipEventRecord(ev[0], st);

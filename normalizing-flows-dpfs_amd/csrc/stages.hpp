@@ -44,8 +44,36 @@ __device__ __forceinline__ Ctx4 ctx_from_sums(double a0, double a1, double b0, d
 // source of the particle before motion
 enum SrcMode { kSrcPrev = 0, kSrcSoft = 1, kSrcOt = 2 };
 
-// motion (model/models.py:191-204): x_phys = (x_res + vel) + eps, eps ~ N(0, pos_noise^2).
-// Writes hx = x_phys, hnoise = eps, hp = log p_res, hidx (pass-through / OT).
+// motion (model/models.py:191-204) of a particle whose resampled state (x0, x1, log p) is
+// known: x_phys = (x_res + vel) + eps, eps ~ N(0, pos_noise^2).  Writes hx = x_phys,
+// hnoise = eps, hp = log p_res.
+__device__ __forceinline__ void motion_apply(const nfdpf_filter_desc &d, const RowSlot &S, int b,
+                                             int64_t grow, int i, float x0, float x1, float lr,
+                                             float v0, float v1, float &p0, float &p1) {
+  const int N = d.N;
+  float e0, e1;
+  if (d.rng_mode == NFDPF_RNG_HOST) {
+    e0 = d.host_noise[((int64_t)b * N + i) * 2];
+    e1 = d.host_noise[((int64_t)b * N + i) * 2 + 1];
+  } else {
+    const U4 r = rng_draw(d.seed, kTagMotion, (uint32_t)d.t, grow, (uint32_t)i);
+    box_muller(r.x, r.y, e0, e1);
+    e0 *= d.pos_noise;
+    e1 *= d.pos_noise;
+  }
+  p0 = (x0 + v0) + e0;
+  p1 = (x1 + v1) + e1;
+  S.hnoise[2 * i] = e0;
+  S.hnoise[2 * i + 1] = e1;
+  S.hx[2 * i] = p0;
+  S.hx[2 * i + 1] = p1;
+  S.hp[i] = lr;
+}
+
+// motion from the particle's source: kSrcSoft = resampled into slot t by the fused step's
+// soft stage (hx = x_res, hp = unnormalised w', renormaliser S2); kSrcOt = the OT result;
+// kSrcPrev = the previous step's particle (no resampling).  Also writes hidx for the
+// non-soft modes (the soft stage wrote its own).
 __device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const RowSlot &S, int b,
                                              int64_t grow, int i, int mode, const float *xprev,
                                              const float *pprev, float S2, float lr_ot, float v0,
@@ -68,25 +96,8 @@ __device__ __forceinline__ void stage_motion(const nfdpf_filter_desc &d, const R
     }
     S.hidx[i] = (int64_t)N * grow + i;
   }
-  float e0, e1;
-  if (d.rng_mode == NFDPF_RNG_HOST) {
-    e0 = d.host_noise[((int64_t)b * N + i) * 2];
-    e1 = d.host_noise[((int64_t)b * N + i) * 2 + 1];
-  } else {
-    const U4 r = rng_draw(d.seed, kTagMotion, (uint32_t)d.t, grow, (uint32_t)i);
-    box_muller(r.x, r.y, e0, e1);
-    e0 *= d.pos_noise;
-    e1 *= d.pos_noise;
-  }
-  p0 = (x0 + v0) + e0;
-  p1 = (x1 + v1) + e1;
-  S.hnoise[2 * i] = e0;
-  S.hnoise[2 * i + 1] = e1;
-  S.hx[2 * i] = p0;
-  S.hx[2 * i + 1] = p1;
-  S.hp[i] = lr;
+  motion_apply(d, S, b, grow, i, x0, x1, lr, v0, v1, p0, p1);
 }
-
 
 constexpr int kOctxDyn = 4;  // nf_dyn context [mean(2), std(2)]
 constexpr int kNsDyn = net_size<1, kH>(kOctxDyn);  // pairs per coupling half
