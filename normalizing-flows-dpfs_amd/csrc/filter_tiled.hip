@@ -337,6 +337,73 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   TRACE(2, 3)
 }
 
+// ---- K3, two roles: 512 threads for a tile of 256 particles.  Waves 0-3 ("flows") run the
+// proposal inverse, hand the proposal to waves 4-7 ("measurement") through LDS, and go on with
+// the nf_dyn forward and densities while the measurement waves evaluate the likelihood of the
+// same particles -- two independent chains per SIMD instead of one, at a batch size where one
+// wave per SIMD is all the particles there are.
+template <bool NFD, bool NFC, int MEAS>
+__global__ __launch_bounds__(2 * kTile) void tiled_prop2_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ StepShared L;
+  __shared__ float qx[kTile][2];
+  __shared__ float lx[kTile];
+  TRACE(2, 0)
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int pl = threadIdx.x & (kTile - 1);
+  const bool flows = threadIdx.x < kTile;
+  const int i = tile * kTile + pl;
+  const RowSlot S = row_slot(d, b);
+  const bool valid = i < d.N;
+  PropIn in{};
+  float lr = 0.f;
+  if (valid && flows) {  // issued before the row prologue so they overlap it
+    in = load_prop_in<NFD>(S, i);
+    lr = S.hp[i];
+  }
+  measure_row_setup<MEAS>(S.enc, d.meas_params, L);
+  const int ncb = d.n_flows * 4 * kH;
+  if (NFD && threadIdx.x < ncb)
+    reinterpret_cast<float *>(L.cb_dyn)[threadIdx.x] = ws.cb_dyn[b * kCb + threadIdx.x];
+  if (threadIdx.x >= kTile && threadIdx.x - kTile < ncb) {
+    // finish the proposal fold: the encoding columns came from K1, add [mean, std] of x_dyn
+    const int k = threadIdx.x - kTile;
+    const Ctx4 cp = tiled_ctx(NFD ? ws.st_dyn : ws.st_phys, b, tiles, d.N);
+    const float c4[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), k);
+    reinterpret_cast<float *>(L.cb_cond)[k] = fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + k], c4, d.E, d.E + 4);
+  }
+  __syncthreads();
+  TRACE(2, 1)
+  float q0x = 0.f, q1x = 0.f, jp = 0.f;
+  if (flows && valid) {
+    jp = stage_propose_inverse<NFC>(d, in, L.cb_cond, q0x, q1x);
+    qx[pl][0] = q0x;
+    qx[pl][1] = q1x;
+  }
+  __syncthreads();
+  float lk = -INFINITY, u = 0.f, propose = 0.f, prior = 0.f;
+  if (valid) {
+    if (flows) {
+      stage_prior<NFD, NFC>(d, S, i, in, L.cb_dyn, q0x, q1x, jp, propose, prior);
+    } else {
+      lk = stage_measure<MEAS>(d, L, qx[pl][0], qx[pl][1]);
+      S.hlik[i] = lk;
+      lx[pl] = lk;
+    }
+  }
+  __syncthreads();
+  if (flows && valid) u = logw(lr, lx[pl], prior, propose);
+  TRACE(2, 2)
+  const int64_t bt = (int64_t)b * tiles + tile;
+  if (meas_shifted<MEAS>()) {
+    const float m = block_max(lk, L.f);  // the measurement waves hold lk, the others -inf
+    if (threadIdx.x == 0) ws.lmax[bt] = m;
+  }
+  store_softmax(u, valid && flows, ws.umax + bt, ws.usum + bt, L.f + 8, L.d);  // L.f[0:8] held block_max
+  TRACE(2, 3)
+}
+
 // ---- K3b (phase 2 of an EXTERNAL measurement): raw likelihood from lik_ext
 __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ float shf[16];
@@ -447,7 +514,11 @@ __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int t
 
 template <bool NFD, bool NFC, int MEAS>
 static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStream_t st) {
-  tiled_prop_kernel<NFD, NFC, MEAS><<<g, kTile, 0, st>>>(d, ws);
+  // the two-role kernel needs a flow chain to overlap with the measurement
+  if constexpr (NFC && MEAS != NFDPF_MEAS_EXTERNAL)
+    tiled_prop2_kernel<NFD, NFC, MEAS><<<g, 2 * kTile, 0, st>>>(d, ws);
+  else
+    tiled_prop_kernel<NFD, NFC, MEAS><<<g, kTile, 0, st>>>(d, ws);
 }
 
 template <int MEAS>

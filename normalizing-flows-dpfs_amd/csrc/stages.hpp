@@ -203,35 +203,41 @@ __device__ __forceinline__ PropIn load_prop_in(const RowSlot &S, int i) {
   return a;
 }
 
-// NF proposal + nf_dyn forward + densities (model/models.py:358-377) and the measurement.
-// Writes hx = proposal, scr propose/prior, hprior; returns the raw likelihood (0 for an
-// EXTERNAL measurement) and the (propose, prior) pair for the log-weight.
-template <bool NFD, bool NFC, int MEAS>
-__device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, const RowSlot &S,
-                                                const StepShared &L, int i, const PropIn &in,
-                                                const f2 *cb_dyn, const f2 *cb_cond, float &q0x,
-                                                float &q1x, float &propose, float &prior) {
+// NF proposal inverse (model/models.py:334-356): q = cond_model.inverse(x_dyn, [enc, mean, std]),
+// returns jac_prop = -log_det (0 and q = x_dyn without --NF-cond).
+template <bool NFC>
+__device__ __forceinline__ float stage_propose_inverse(const nfdpf_filter_desc &d, const PropIn &in,
+                                                       const f2 *cb_cond, float &q0x, float &q1x) {
+  q0x = in.xd0;
+  q1x = in.xd1;
+  if (!NFC) return 0.f;
+  const int oC = d.E + 4;
+  const int nsC = net_size<1, kH>(oC);
+  float lo[1] = {in.xd0}, up[1] = {in.xd1};
+  float ld = 0.f;
+#ifndef NFDPF_EXP_NOCOND
+  for (int f = d.n_flows - 1; f >= 0; --f)
+    ld += coupling_inverse<1, kH>(wptr2(d.cond_params) + f * 2 * nsC, oC, lo, up, cb_cond + f * 2 * kH);
+#endif
+  q0x = lo[0];
+  q1x = up[0];
+  return -ld;
+}
+
+// nf_dyn forward of the proposal + densities (model/models.py:358-377): (propose, prior);
+// writes hx = proposal, scr propose/prior, hprior.
+template <bool NFD, bool NFC>
+__device__ __forceinline__ void stage_prior(const nfdpf_filter_desc &d, const RowSlot &S, int i,
+                                            const PropIn &in, const f2 *cb_dyn, float q0x, float q1x,
+                                            float jac_prop, float &propose, float &prior) {
   const float K = d.dens_const;
   const float two_var = 2.0f * (d.pos_noise * d.pos_noise);
   const int nfl = d.n_flows;
   const float de = density(in.e0, in.e1, K, two_var);
-  q0x = in.xd0;
-  q1x = in.xd1;
   if (NFC) {
-    const int oC = d.E + 4;
-    const int nsC = net_size<1, kH>(oC);
-    float lo[1] = {in.xd0}, up[1] = {in.xd1};
-    float ld = 0.f;
-#ifndef NFDPF_EXP_NOCOND
-    for (int f = nfl - 1; f >= 0; --f)
-      ld += coupling_inverse<1, kH>(wptr2(d.cond_params) + f * 2 * nsC, oC, lo, up,
-                                    cb_cond + f * 2 * kH);
-#endif
-    q0x = lo[0];
-    q1x = up[0];
-    const float jac_prop = -ld;
     const float r0 = in.p0 - in.e0, r1 = in.p1 - in.e1;
     if (NFD) {
+      float lo[1] = {q0x}, up[1] = {q1x};
       float ld2 = 0.f;
 #ifndef NFDPF_EXP_NODYNF
       if (d.nf_dyn == NFDPF_DYN_MAF) {
@@ -260,13 +266,29 @@ __device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, cons
   S.scr[4 * i + 2] = propose;
   S.scr[4 * i + 3] = prior;
   if (S.hprior) S.hprior[i] = prior;
+}
+
+template <int MEAS>
+__device__ __forceinline__ float stage_measure(const nfdpf_filter_desc &d, const StepShared &L, float q0x,
+                                               float q1x) {
 #ifdef NFDPF_EXP_NOMEAS
   return q0x * 1e-3f;
 #endif
   if (MEAS != NFDPF_MEAS_EXTERNAL)
-    return measure<MEAS>(MeasArgs{d.pe_params, d.meas_params, d.n_flows, d.meas_prior_std}, L, q0x,
-                         q1x);
+    return measure<MEAS>(MeasArgs{d.pe_params, d.meas_params, d.n_flows, d.meas_prior_std}, L, q0x, q1x);
   return 0.f;
+}
+
+// The whole proposal stage for one particle: inverse, prior/propose, measurement.  Returns the
+// raw likelihood (0 for an EXTERNAL measurement).
+template <bool NFD, bool NFC, int MEAS>
+__device__ __forceinline__ float stage_proposal(const nfdpf_filter_desc &d, const RowSlot &S,
+                                                const StepShared &L, int i, const PropIn &in,
+                                                const f2 *cb_dyn, const f2 *cb_cond, float &q0x,
+                                                float &q1x, float &propose, float &prior) {
+  const float jp = stage_propose_inverse<NFC>(d, in, cb_cond, q0x, q1x);
+  stage_prior<NFD, NFC>(d, S, i, in, cb_dyn, q0x, q1x, jp, propose, prior);
+  return stage_measure<MEAS>(d, L, q0x, q1x);
 }
 
 // log-weight from registers: ((log p_res + lik) + prior) - propose
