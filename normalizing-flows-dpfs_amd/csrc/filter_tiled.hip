@@ -342,11 +342,16 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
 // the nf_dyn forward and densities while the measurement waves evaluate the likelihood of the
 // same particles -- two independent chains per SIMD instead of one, at a batch size where one
 // wave per SIMD is all the particles there are.
-template <bool NFD, bool NFC, int MEAS>
-__global__ __launch_bounds__(2 * kTile) void tiled_prop2_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+// With the cosine measurement a third role splits the encoder's output layer: waves 4-7 and
+// 8-11 each produce half of the 32 outputs and their partial (|e|^2, <e, v>).
+template <bool NFD, bool NFC, int MEAS, int ROLES>
+__global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;
   __shared__ float qx[kTile][2];
   __shared__ float lx[kTile];
+  __shared__ float ssx[ROLES][kTile], dotx[ROLES][kTile];
+  __shared__ float smf[16];   // per-wave softmax partials (up to 12 waves)
+  __shared__ double smd[16];
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -383,9 +388,18 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop2_kernel(const nfdpf_filt
   }
   __syncthreads();
   float lk = -INFINITY, u = 0.f, propose = 0.f, prior = 0.f;
+  const int role = threadIdx.x / kTile;
   if (valid) {
     if (flows) {
       stage_prior<NFD, NFC>(d, S, i, in, L.cb_dyn, q0x, q1x, jp, propose, prior);
+    } else if (ROLES == 3) {
+      // cosine measurement, half of the encoder outputs per role (model/models.py:206-219)
+      static_assert(ROLES != 3 || MEAS == NFDPF_MEAS_COS, "three roles: cosine measurement only");
+      constexpr int HP = kE / 4;  // output pairs per role
+      float ss, dot;
+      encode_dot<kE>(wptr(d.pe_params), qx[pl][0], qx[pl][1], L.encv, ss, dot, (role - 1) * HP, role * HP);
+      ssx[role][pl] = ss;
+      dotx[role][pl] = dot;
     } else {
       lk = stage_measure<MEAS>(d, L, qx[pl][0], qx[pl][1]);
       S.hlik[i] = lk;
@@ -393,14 +407,25 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop2_kernel(const nfdpf_filt
     }
   }
   __syncthreads();
-  if (flows && valid) u = logw(lr, lx[pl], prior, propose);
+  if (flows && valid) {
+    float lik;
+    if (ROLES == 3) {
+      const float ss = ssx[1][pl] + ssx[2][pl], dot = dotx[1][pl] + dotx[2][pl];
+      const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
+      lik = logf(1.0f / (1e-7f + cosd));
+      S.hlik[i] = lik;
+    } else {
+      lik = lx[pl];
+    }
+    u = logw(lr, lik, prior, propose);
+  }
   TRACE(2, 2)
   const int64_t bt = (int64_t)b * tiles + tile;
   if (meas_shifted<MEAS>()) {
     const float m = block_max(lk, L.f);  // the measurement waves hold lk, the others -inf
     if (threadIdx.x == 0) ws.lmax[bt] = m;
   }
-  store_softmax(u, valid && flows, ws.umax + bt, ws.usum + bt, L.f + 8, L.d);  // L.f[0:8] held block_max
+  store_softmax(u, valid && flows, ws.umax + bt, ws.usum + bt, smf, smd);
   TRACE(2, 3)
 }
 
@@ -515,8 +540,10 @@ __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int t
 template <bool NFD, bool NFC, int MEAS>
 static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStream_t st) {
   // the two-role kernel needs a flow chain to overlap with the measurement
+  // (a third role splitting the cosine encoder's output layer was measured slower: 16.7 vs
+  // 11.4 us for the compute phase at C2 -- the extra waves duplicate the encoder's first layers)
   if constexpr (NFC && MEAS != NFDPF_MEAS_EXTERNAL)
-    tiled_prop2_kernel<NFD, NFC, MEAS><<<g, 2 * kTile, 0, st>>>(d, ws);
+    tiled_prop2_kernel<NFD, NFC, MEAS, 2><<<g, 2 * kTile, 0, st>>>(d, ws);
   else
     tiled_prop_kernel<NFD, NFC, MEAS><<<g, kTile, 0, st>>>(d, ws);
 }

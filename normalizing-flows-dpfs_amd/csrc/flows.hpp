@@ -308,13 +308,14 @@ __device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, 
 // materialising e (model/models.py:130-139 then utils.py:8-15).
 template <int E>
 __device__ __forceinline__ void encode_dot(cfloat *pe, float x0, float x1, const float *v, float &ss,
-                                           float &dot) {
+                                           float &dot, int m0 = 0, int m1 = E / 2) {
+  // output pairs [m0, m1) only: a caller may split the E outputs over several waves
   f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
   ss = 0.f;
   dot = 0.f;
 #pragma unroll 2
-  for (int m = 0; m < E / 2; ++m) {
+  for (int m = m0; m < m1; ++m) {
     const f2 a = pe_out<E>(pe, h2, m);
     ss = fmaf(a.x, a.x, ss);
     dot = fmaf(a.x, v[2 * m], dot);
