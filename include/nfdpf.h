@@ -168,6 +168,9 @@ typedef struct nfdpf_filter_desc {
   /* configuration */
   int32_t nf_dyn, nf_cond, measurement, resampler, rng_mode, force_resample, n_flows,
       hidden;
+  int32_t defer_norm;       /* tiled step: normalise step t's weights inside step t+1's first
+                               launch (p_prev / x_prev = history slot t-1, not yet normalised);
+                               the caller clears it for the last step and to feed p_prev itself */
   float alpha, pos_noise, dens_const, meas_prior_std;
   uint64_t seed;
   /* packed parameters */
@@ -182,14 +185,14 @@ typedef struct nfdpf_filter_desc {
   const float *x_prev;      /* particles after the previous step, rows of x_prev_rs */
   const float *p_prev;      /* probabilities after the previous step, rows of p_prev_rs */
   int64_t x_prev_rs, p_prev_rs;
-  const float *ess_all;     /* [B_global] 1/sum(p_prev^2) per row */
+  const float *ess_all;     /* [B_global] 1/sum(p_prev^2) per row (tiled: see below) */
   const int32_t *gate;      /* optional [1]: precomputed gate (OT path), NULL = compute */
   const float *ot_x;        /* [B,N,2] OT-resampled particles (resampler OT, gate on) */
   const float *lik_ext;     /* [B,N] raw likelihood (measurement EXTERNAL) */
   /* outputs: history [B,T,...] slot t, plus per-step reductions */
   float *hist_x, *hist_p, *hist_noise, *hist_lik, *hist_jac, *hist_prior;
   int64_t *hist_idx;
-  float *ess_out;           /* [B] 1/sum(p^2) of this step */
+  float *ess_out;           /* [B] 1/sum(p^2) of this step (tiled: see below) */
   float *lw_sum;            /* [B,T] row sums of the unnormalised log-weights (obs likelihood) */
   float *pred;              /* [B,T,2] sum_n p*x (losses.py:18-31 prediction) */
   float *scratch;           /* [B,N,4] per-particle hand-off between stages (x_dyn, propose, prior) */
@@ -201,20 +204,23 @@ typedef struct nfdpf_filter_desc {
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
 
 /* The same step as a pipeline of launches over (particle tile of 256, batch row) workgroups
- * (soft-resample -> motion -> dyn inverse -> proposal+measurement -> normalise), so a small
- * batch fills every CU.  In this mode ess_all / ess_out hold per-(row, tile) sums of p^2
- * as doubles ([B_global][tiles] / [B][tiles]; nfdpf_filter_tiled_tiles(N) tiles per row),
- * and pred / lw_sum are written after the last step (t == T-1) for all steps at once.
+ * (gate + resample + motion -> dyn inverse -> proposal+measurement [-> normalise]), so a small
+ * batch fills every CU.  In this mode ess_out / ess_all hold the per-(row, tile) softmax
+ * partials of the step's log-weights u as 4 doubles {max u, sum e^(u-max), sum e^(2(u-max)),
+ * max raw likelihood} ([B][tiles][4] / [B_global][tiles][4]; nfdpf_filter_tiled_tiles(N)
+ * tiles per row): the next step's ESS gate and normalisation both derive from them.
+ * pred / lw_sum are written after the last step (t == T-1) for all steps at once.
  * workspace: nfdpf_filter_tiled_workspace_bytes(B, N, T) bytes, 256-B aligned, shared by
  * the T steps of one sequence.                                                        */
 NFDPF_API int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T);
 NFDPF_API int nfdpf_filter_tiled_tiles(int N);
-/* per-tile sums of p0^2 -> ess_parts [B][tiles] (the t = 0 gate input) */
+/* the t = 0 gate input from p0 [B,N] -> ess_parts [B][tiles][4] */
 NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
                             void *stream);
 NFDPF_API int nfdpf_filter_step_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);
-/* the ESS gate (DPFs.py:163-165) from per-(row, tile) sums of p^2 -> int32 [1] (OT path) */
-NFDPF_API int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int force, int32_t *gate,
+/* the ESS gate (DPFs.py:163-165) of step t from the [B][tiles][4] partials of step t-1
+ * -> int32 [1] (OT path) */
+NFDPF_API int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, int force, int32_t *gate,
                          void *stream);
 
 #ifdef __cplusplus

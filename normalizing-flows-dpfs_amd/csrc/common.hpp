@@ -171,6 +171,32 @@ __device__ __forceinline__ void block_sum4_store(double a, double b, double c, d
   }
 }
 
+// Eight workgroup sums with ONE barrier: (a0..a3) -> dst0[0..3], (b0..b3) -> dst1[0..3];
+// `sh` holds 8 doubles per wave.
+__device__ __forceinline__ void block_sum8_store(const double (&a)[4], double *dst0, const double (&c)[4],
+                                                 double *dst1, double *sh) {
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = wave_sum_dpp(a[k]);
+    v[4 + k] = wave_sum_dpp(c[k]);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[8 * w + k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int nw = (blockDim.x + 63) >> 6;
+    double r = sh[threadIdx.x];
+    for (int i = 1; i < nw; ++i) r += sh[8 * i + threadIdx.x];
+    if (threadIdx.x < 4)
+      dst0[threadIdx.x] = r;
+    else
+      dst1[threadIdx.x - 4] = r;
+  }
+}
+
 // Workgroup reductions.  `sh` is LDS scratch of >= 16 elements of T, reused across calls
 // (the leading barrier protects the previous use).  Every thread gets the result.
 template <typename T>

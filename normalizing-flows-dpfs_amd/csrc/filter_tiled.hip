@@ -37,15 +37,13 @@ __device__ unsigned long long g_trace[4][2048][8];
 struct TiledWs {
   double *st_phys;  // [B][tiles][4] sum x0, x1, x0^2, x1^2 of x_phys
   double *st_dyn;   // [B][tiles][4] same for x_dyn
-  float *lmax;      // [B][tiles] max raw likelihood
-  float *umax;      // [B][tiles] max of the unshifted log-weight u
-  double *usum;     // [B][tiles] sum exp(u - umax)
-  float *S2;        // [B] soft-resampling renormaliser
-  int *fire;        // [B] gate decision taken by K0 (soft resampler)
   float *cb_dyn;    // [B][kCb] folded nf_dyn biases of the row (K2, tile 0)
   float *cb_cond;   // [B][kCb] proposal fold over the encoding columns (K1, tile 0)
   double *fin;      // [B][T][tiles][4] sum p^2, sum p x0, sum p x1, sum logw
 };
+// The step's softmax partials live in the caller's ess_out / ess_all (include/nfdpf.h):
+// per (row, tile) {max u, sum e^(u-max), sum e^(2(u-max)), max raw likelihood}.
+constexpr int kSm = 4;
 
 constexpr int kCb = kMaxFlows * 4 * kH;  // floats of one row's folded-bias table
 
@@ -54,8 +52,7 @@ __host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / 
 
 static int64_t tiled_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(bt * 32) * 2 + al256(bt * 4) * 2 + al256(bt * 8) + al256((int64_t)B * 4) * 2 +
-         al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32);
+  return al256(bt * 32) * 2 + al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32);
 }
 
 static TiledWs tiled_carve(void *ws, int B, int N, int T) {
@@ -66,16 +63,6 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   p += al256(bt * 32);
   w.st_dyn = (double *)p;
   p += al256(bt * 32);
-  w.lmax = (float *)p;
-  p += al256(bt * 4);
-  w.umax = (float *)p;
-  p += al256(bt * 4);
-  w.usum = (double *)p;
-  p += al256(bt * 8);
-  w.S2 = (float *)p;
-  p += al256((int64_t)B * 4);
-  w.fire = (int *)p;
-  p += al256((int64_t)B * 4);
   w.cb_dyn = (float *)p;
   p += al256((int64_t)B * kCb * 4);
   w.cb_cond = (float *)p;
@@ -84,33 +71,68 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   return w;
 }
 
-// ESS gate from per-(row, tile) sums of p^2 (DPFs.py:163-165): torch.mean over the batch of
-// 1 / sum p^2, in ATen's cascade order.  Every wave evaluates it (lanes in parallel over
-// rows), so all workgroups take the same decision without a hand-off.
+// 1 / sum_n p_n^2 of one row from its per-tile softmax partials (DPFs.py:163).  With
+// e_n = e^(u_n - M) and S = sum e_n, p_n = e_n / S (+ 1e-12 after a filter step, DPFs.py:192):
+// sum p^2 = sum e^2 / S^2 + 2e-12 + N 1e-24.  fp64 throughout; the reference sums fp32 p^2 in
+// cascade order, so the two agree to ~1e-7 relative.
+__device__ __forceinline__ float row_inv_ess(const double *sm, int tiles, int N, bool eps) {
+  double M = -INFINITY;
+  for (int k = 0; k < tiles; ++k) M = sm[kSm * k] > M ? sm[kSm * k] : M;
+  double S = 0.0, Q = 0.0;
+  for (int k = 0; k < tiles; ++k) {
+    // the tile rescale factors in f32 (relative error ~1e-7, the gate's own resolution)
+    const float f = expf((float)(sm[kSm * k] - M));
+    S += sm[kSm * k + 1] * (double)f;
+    Q += sm[kSm * k + 2] * ((double)f * (double)f);
+  }
+  double sp2 = Q / (S * S);
+  if (eps) sp2 += 2e-12 + (double)N * 1e-24;
+  return 1.0f / (float)sp2;
+}
+
+// normalize_log_probs of a row (utils.py:39-44) from its softmax partials:
+// p = e^(lw - shift) / S + 1e-12, shift = max u (- max raw likelihood for the shifted models)
+struct RowNorm {
+  float shift, Ssum, Lmax;
+};
+__device__ __forceinline__ RowNorm row_norm(const double *sm, int tiles, bool shifted) {
+  float M = -INFINITY, Lmax = -INFINITY;
+  for (int k = 0; k < tiles; ++k) {
+    M = fmaxf(M, (float)sm[kSm * k]);
+    if (shifted) Lmax = fmaxf(Lmax, (float)sm[kSm * k + 3]);
+  }
+  double Sd = 0.0;
+  for (int k = 0; k < tiles; ++k) Sd += sm[kSm * k + 1] * (double)expf((float)sm[kSm * k] - M);
+  // u = logw + Lmax for the shifted models: normalise with the same shift
+  return RowNorm{shifted ? M - Lmax : M, (float)Sd, Lmax};
+}
+
+// ESS gate: torch.mean over the batch of the rows' 1/sum p^2 (ATen's cascade order),
+// evaluated by every wave (lanes in parallel over rows) -- the same decision everywhere.
 __device__ __forceinline__ bool tiled_gate(const nfdpf_filter_desc &d, int tiles) {
   if (d.gate) return d.gate[0] != 0;
   if (d.force_resample) return true;
   const double *parts = reinterpret_cast<const double *>(d.ess_all);
   const float s = cascade_row_sum(
-      [&](int r) {
-        double s2 = 0.0;
-        for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
-        return 1.0f / (float)s2;
-      },
-      d.B_global);
+      [&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, d.N, d.t > 0); }, d.B_global);
   return (s / (float)d.B_global) < 0.5f * (float)d.N;
 }
 
 // The same gate, block-parallel (all threads call): thread r stages row r's 1 / sum p^2 in
 // `buf` (one round trip for the whole batch), wave 0 folds them in cascade order.
-__device__ bool tiled_gate_block(const nfdpf_filter_desc &d, int tiles, float *buf, int *flag) {
-  if (d.gate) return d.gate[0] != 0;
-  if (d.force_resample) return true;
+// With `rn_row` >= 0 the thread that stages that row also leaves its RowNorm in *rn (LDS),
+// readable by every thread on return (the deferred normalisation needs it, same data).
+__device__ bool tiled_gate_block(const nfdpf_filter_desc &d, int tiles, float *buf, int *flag,
+                                 int64_t rn_row = -1, RowNorm *rn = nullptr, bool shifted = false) {
   const double *parts = reinterpret_cast<const double *>(d.ess_all);
+  if (d.gate || d.force_resample) {
+    if (rn_row >= 0 && threadIdx.x == 0) *rn = row_norm(parts + rn_row * tiles * kSm, tiles, shifted);
+    __syncthreads();
+    return d.gate ? d.gate[0] != 0 : true;
+  }
   for (int r = threadIdx.x; r < d.B_global; r += blockDim.x) {
-    double s2 = 0.0;
-    for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
-    buf[r] = 1.0f / (float)s2;
+    buf[r] = row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, d.N, d.t > 0);
+    if (r == rn_row) *rn = row_norm(parts + (int64_t)r * tiles * kSm, tiles, shifted);
   }
   __syncthreads();
   if (threadIdx.x < 64) {
@@ -119,6 +141,72 @@ __device__ bool tiled_gate_block(const nfdpf_filter_desc &d, int tiles, float *b
   }
   __syncthreads();
   return *flag != 0;
+}
+
+__host__ __device__ constexpr bool shifted_meas(int meas) {
+  return meas == NFDPF_MEAS_CRNVP || meas == NFDPF_MEAS_GAUSSIAN || meas == NFDPF_MEAS_EXTERNAL;
+}
+
+// the normalised weight of particle i of slot S (hp still holding log p_res, hlik the raw
+// likelihood): returns p, the log-weight lw and the (shifted) likelihood lk; writes nothing
+__device__ __forceinline__ float norm_value(const RowSlot &S, int i, const RowNorm &rn, bool shifted, float &lw,
+                                            float &lk) {
+  lk = S.hlik[i];
+  if (shifted) lk = lk - rn.Lmax;
+  lw = stage_logw(S, i, lk);
+  return expf(lw - rn.shift) / rn.Ssum + 1e-12f;
+}
+// ... and stores it: hp = p, hlik = shifted likelihood
+__device__ __forceinline__ float norm_particle(const RowSlot &S, int i, const RowNorm &rn, bool shifted,
+                                               float &lw) {
+  float lk;
+  const float p = norm_value(S, i, rn, shifted, lw, lk);
+  if (shifted) S.hlik[i] = lk;
+  S.hp[i] = p;
+  return p;
+}
+
+// The previous step's per-particle values a deferred normalisation needs, loaded up front.
+struct PrevIn {
+  float lr, lik, prop, prior, x0, x1;
+};
+__device__ __forceinline__ PrevIn load_prev_in(const RowSlot &Sp, int i) {
+  return PrevIn{Sp.hp[i], Sp.hlik[i], Sp.scr[4 * i + 2], Sp.scr[4 * i + 3], Sp.hx[2 * i], Sp.hx[2 * i + 1]};
+}
+// p of a prefetched particle (the arithmetic of norm_value)
+__device__ __forceinline__ float prev_p_of(const PrevIn &v, const RowNorm &rn, bool shifted, float &lw, float &lk) {
+  lk = shifted ? v.lik - rn.Lmax : v.lik;
+  lw = ((v.lr + lk) + v.prior) - v.prop;
+  return expf(lw - rn.shift) / rn.Ssum + 1e-12f;
+}
+// row b's softmax partials inside ess_all (global rows when the batch is sharded)
+__device__ __forceinline__ const double *prev_sm(const nfdpf_filter_desc &d, int b, int tiles) {
+  const int64_t r = d.row_base + d.B <= d.B_global ? d.row_base + b : b;
+  return reinterpret_cast<const double *>(d.ess_all) + r * tiles * kSm;
+}
+
+// Deferred normalisation of step t-1 (defer_norm, t > 0): slot t-1's weights are written by
+// the second launch of step t -- after every workgroup of the first launch has read slot t-1
+// (the gate / resampler / motion) and before anything overwrites the step-t-1 values of the
+// scratch (propose, prior).  All threads call (block reduction inside).
+__device__ __forceinline__ void finish_prev(const nfdpf_filter_desc &d, TiledWs ws, int b, int tile, int i,
+                                            bool own, const PrevIn &v, double *shd) {
+  const int tiles = n_tiles(d.N);
+  const bool shifted = shifted_meas(d.measurement);
+  const RowNorm rn = row_norm(prev_sm(d, b, tiles), tiles, shifted);
+  const RowSlot Sp = row_slot(d, b, d.t - 1);
+  double sp2 = 0, px = 0, py = 0, sw = 0;
+  if (own && i < d.N) {
+    float lw, lk;
+    const float p = prev_p_of(v, rn, shifted, lw, lk);
+    if (shifted) Sp.hlik[i] = lk;
+    Sp.hp[i] = p;
+    sp2 = (double)p * p;
+    px = (double)p * v.x0;
+    py = (double)p * v.x1;
+    sw = lw;
+  }
+  block_sum4_store(sp2, px, py, sw, shd, ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4);
 }
 
 // combine the 4-sum partials of row b -> context
@@ -160,14 +248,41 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   const int i = tile * kTile + threadIdx.x;
   const int64_t grow = d.row_base + b;
   float *Cbuf = dyn_lds;
-  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh);
+  PrevIn pv{};
+  const bool defer = d.defer_norm && d.t > 0;
+  if (defer && i < N) pv = load_prev_in(row_slot(d, b, d.t - 1), i);  // overlaps the gate
+  float e0 = 0.f, e1 = 0.f;
+  if (i < N) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: computed under its latency
+  __shared__ RowNorm rn_sh;
+  const int64_t my_row = d.row_base + d.B <= d.B_global ? d.row_base + b : b;
+  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh, defer ? my_row : -1, &rn_sh,
+                                     shifted_meas(d.measurement));
+  TRACE(0, 1)
   const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
   const RowSlot S = row_slot(d, b);
   const float *xprev = d.x_prev + b * d.x_prev_rs;
   const float *pprev = d.p_prev + b * d.p_prev_rs;
+  // defer_norm: step t-1 is not normalised yet; its weights are derived here on the fly from
+  // slot t-1 (read only -- the second launch of this step writes them, finish_prev)
+  RowNorm rn{0.f, 1.f, 0.f};
+  RowSlot Sp = S;
+  if (defer) {
+    rn = rn_sh;  // left by the gate staging (same partials)
+    Sp = row_slot(d, b, d.t - 1);
+  }
+  auto prev_p = [&](int j) {
+    float lw, lk;
+    return norm_value(Sp, j, rn, shifted_meas(d.measurement), lw, lk);
+  };
   float x0 = 0.f, x1 = 0.f, lr = 0.f;
   if (mode == kSrcSoft) {
     float *wbuf = dyn_lds + max(N, d.B_global);
+    if (defer) {  // the row's p_{t-1} into LDS for the resampler
+      float *pbuf = wbuf + N;
+      for (int j = threadIdx.x; j < N; j += blockDim.x) pbuf[j] = prev_p(j);
+      __syncthreads();
+      pprev = pbuf;
+    }
     SoftRow row{pprev, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
     float off;
     if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
@@ -205,16 +320,23 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
       x1 = d.ot_x[((int64_t)b * N + i) * 2 + 1];
       lr = logf(1.0f / (float)N);
     } else {
-      x0 = xprev[2 * i];
-      x1 = xprev[2 * i + 1];
-      lr = logf(pprev[i]);
+      if (defer) {
+        float lw, lk;
+        x0 = pv.x0;
+        x1 = pv.x1;
+        lr = logf(prev_p_of(pv, rn, shifted_meas(d.measurement), lw, lk));
+      } else {
+        x0 = xprev[2 * i];
+        x1 = xprev[2 * i + 1];
+        lr = logf(pprev[i]);
+      }
     }
     S.hidx[i] = (int64_t)N * grow + i;
   }
   double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
   if (i < N) {
     float p0, p1;
-    motion_apply(d, S, b, grow, i, x0, x1, lr, d.vel[2 * b], d.vel[2 * b + 1], p0, p1);
+    motion_apply_eps(S, i, x0, x1, lr, d.vel[2 * b], d.vel[2 * b + 1], e0, e1, p0, p1);
     s0 = p0;
     s1 = p1;
     q0 = (double)p0 * p0;
@@ -230,9 +352,10 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   TRACE(0, 3)
 }
 
-// ---- K2: nf_dyn inverse
+// ---- K2: nf_dyn inverse; with defer_norm also the normalisation of slot t-1 (finish_prev's
+// arithmetic, its sums reduced together with this launch's in one barrier)
 __global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   __shared__ f2 cb[kMaxFlows * 2 * kH];
   TRACE(1, 0)
   const int tiles = n_tiles(d.N);
@@ -240,50 +363,78 @@ __global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_des
   const int i = tile * kTile + threadIdx.x;
   const RowSlot S = row_slot(d, b);
   float p0 = 0.f, p1 = 0.f;
+  PrevIn pv{};
+  const bool defer = d.defer_norm && d.t > 0;
+  const bool shifted = shifted_meas(d.measurement);
   if (i < d.N) {  // before the fold, so the loads overlap it
     p0 = S.hx[2 * i];
     p1 = S.hx[2 * i + 1];
+    if (defer) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
   }
+  const RowNorm rn = defer ? row_norm(prev_sm(d, b, tiles), tiles, shifted) : RowNorm{0.f, 1.f, 0.f};
   fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb, d.nf_dyn);
   __syncthreads();
   if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
     ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
   TRACE(1, 1)
-  double s0 = 0, s1 = 0, q0 = 0, q1 = 0;
+  double sd[4] = {0, 0, 0, 0}, sf[4] = {0, 0, 0, 0};
   if (i < d.N) {
     float x0, x1;
     stage_dyn_inverse(d, S, i, p0, p1, cb, x0, x1);
-    s0 = x0;
-    s1 = x1;
-    q0 = (double)x0 * x0;
-    q1 = (double)x1 * x1;
+    sd[0] = x0;
+    sd[1] = x1;
+    sd[2] = (double)x0 * x0;
+    sd[3] = (double)x1 * x1;
+    if (defer) {
+      const RowSlot Sp = row_slot(d, b, d.t - 1);
+      float lw, lk;
+      const float p = prev_p_of(pv, rn, shifted, lw, lk);
+      if (shifted) Sp.hlik[i] = lk;
+      Sp.hp[i] = p;
+      sf[0] = (double)p * p;
+      sf[1] = (double)p * pv.x0;
+      sf[2] = (double)p * pv.x1;
+      sf[3] = lw;
+    }
   }
   TRACE(1, 2)
-  store_sums4(ws.st_dyn + ((int64_t)b * tiles + tile) * 4, s0, s1, q0, q1, shd);
+  double *dst = ws.st_dyn + ((int64_t)b * tiles + tile) * 4;
+  if (defer)
+    block_sum8_store(sd, dst, sf, ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4, shd);
+  else
+    store_sums4(dst, sd[0], sd[1], sd[2], sd[3], shd);
   TRACE(1, 3)
 }
 
 // softmax partials of the unshifted log-weight u over this tile
-__device__ __forceinline__ void store_softmax(float u, bool valid, float *umax, double *usum, float *shf,
-                                              double *shd) {
-  // per wave (max, sum exp(u - max)), merged over the waves with one barrier
+__device__ __forceinline__ void store_softmax(float u, bool valid, double *sm, float *shf, double *shd) {
+  // per wave (max, sum e^(u - max), sum e^(2(u - max))), merged over the waves with one
+  // barrier into this tile's {max, sum, sum of squares} (sm[0..2])
   const float mw = wave_max_dpp(valid ? u : -INFINITY);
-  const double ew = wave_sum_dpp(valid ? (double)expf(u - mw) : 0.0);
+  const float ev = valid ? expf(u - mw) : 0.f;
+  const double ew = wave_sum_dpp((double)ev);
+  const double qw = wave_sum_dpp((double)ev * ev);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     shf[w] = mw;
-    shd[w] = ew;
+    shd[2 * w] = ew;
+    shd[2 * w + 1] = qw;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nw = (blockDim.x + 63) >> 6;
     float m = shf[0];
     for (int k = 1; k < nw; ++k) m = fmaxf(m, shf[k]);
-    double sum = 0.0;
+    double sum = 0.0, sq = 0.0;
     for (int k = 0; k < nw; ++k)
-      if (shf[k] > -INFINITY) sum += shd[k] * (double)expf(shf[k] - m);
-    *umax = m;
-    *usum = sum;
+      if (shf[k] > -INFINITY) {
+        const double f = (double)expf(shf[k] - m);
+        sum += shd[2 * k] * f;
+        sq += shd[2 * k + 1] * f * f;
+      }
+    sm[0] = m;
+    sm[1] = sum;
+    sm[2] = sq;
   }
 }
 
@@ -316,6 +467,8 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
         fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + threadIdx.x], c4, d.E, d.E + 4);
   }
   __syncthreads();
+  if (!NFD && d.defer_norm && d.t > 0)  // no K2 in this config
+    finish_prev(d, ws, b, tile, i, true, i < d.N ? load_prev_in(row_slot(d, b, d.t - 1), i) : PrevIn{}, L.d);
   TRACE(2, 1)
   float lk = -INFINITY, u = 0.f;
   if (valid) {
@@ -328,12 +481,11 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   }
   TRACE(2, 2)
   if (MEAS == NFDPF_MEAS_EXTERNAL) return;  // phase 1: the external likelihood comes next
-  const int64_t bt = (int64_t)b * tiles + tile;
-  if (meas_shifted<MEAS>()) {
-    const float m = block_max(lk, L.f);
-    if (threadIdx.x == 0) ws.lmax[bt] = m;
-  }
-  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, L.f + 8, L.d);  // L.f[0:8] held block_max
+  double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
+  const float lm = meas_shifted<MEAS>() ? block_max(lk, L.f) : 0.f;
+  if (threadIdx.x == 0) sm[3] = lm;
+  __shared__ double smd[32];
+  store_softmax(u, valid, sm, L.f + 8, smd);  // L.f[0:8] held block_max
   TRACE(2, 3)
 }
 
@@ -351,7 +503,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   __shared__ float lx[kTile];
   __shared__ float ssx[ROLES][kTile], dotx[ROLES][kTile];
   __shared__ float smf[16];   // per-wave softmax partials (up to 12 waves)
-  __shared__ double smd[16];
+  __shared__ double smd[32];
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -379,6 +531,9 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
     reinterpret_cast<float *>(L.cb_cond)[k] = fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + k], c4, d.E, d.E + 4);
   }
   __syncthreads();
+  if (!NFD && d.defer_norm && d.t > 0)  // no K2 in this config
+    finish_prev(d, ws, b, tile, i, flows, flows && i < d.N ? load_prev_in(row_slot(d, b, d.t - 1), i) : PrevIn{},
+                L.d);
   TRACE(2, 1)
   float q0x = 0.f, q1x = 0.f, jp = 0.f;
   if (flows && valid) {
@@ -420,19 +575,18 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
     u = logw(lr, lik, prior, propose);
   }
   TRACE(2, 2)
-  const int64_t bt = (int64_t)b * tiles + tile;
-  if (meas_shifted<MEAS>()) {
-    const float m = block_max(lk, L.f);  // the measurement waves hold lk, the others -inf
-    if (threadIdx.x == 0) ws.lmax[bt] = m;
-  }
-  store_softmax(u, valid && flows, ws.umax + bt, ws.usum + bt, smf, smd);
+  double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
+  // the measurement waves hold lk, the others -inf
+  const float lm = meas_shifted<MEAS>() ? block_max(lk, L.f) : 0.f;
+  if (threadIdx.x == 0) sm[3] = lm;
+  store_softmax(u, valid && flows, sm, smf, smd);
   TRACE(2, 3)
 }
 
 // ---- K3b (phase 2 of an EXTERNAL measurement): raw likelihood from lik_ext
 __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ double shd2[32];
   __shared__ float shf[16];
-  __shared__ double shd[16];
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
@@ -444,13 +598,15 @@ __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_
     S.hlik[i] = lk;
     u = stage_logw(S, i, lk);
   }
-  const int64_t bt = (int64_t)b * tiles + tile;
+  double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
   const float m = block_max(lk, shf);
-  if (threadIdx.x == 0) ws.lmax[bt] = m;
-  store_softmax(u, valid, ws.umax + bt, ws.usum + bt, shf + 8, shd);  // shf[0:8] held block_max
+  if (threadIdx.x == 0) sm[3] = m;
+  store_softmax(u, valid, sm, shf + 8, shd2);  // shf[0:8] held block_max
 }
 
-// ---- K4: log-weights, normalisation, per-tile sums for the gate / prediction / obs-likelihood
+// ---- K4: log-weights, normalisation, per-tile sums for the prediction / obs-likelihood, for
+// the step's own slot (every step with OT or a caller-fed p_prev; otherwise only after the
+// last step -- the front kernel of the next step does it, see tiled_front_kernel)
 template <bool SHIFT>
 __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   TRACE(3, 0)
@@ -458,28 +614,12 @@ __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_de
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
   const int i = tile * kTile + threadIdx.x;
-  const int64_t rb = (int64_t)b * tiles;
-  float M = -INFINITY, Lmax = -INFINITY;
-  for (int k = 0; k < tiles; ++k) {
-    M = fmaxf(M, ws.umax[rb + k]);
-    if (SHIFT) Lmax = fmaxf(Lmax, ws.lmax[rb + k]);
-  }
-  double Sd = 0.0;
-  for (int k = 0; k < tiles; ++k) Sd += ws.usum[rb + k] * (double)expf(ws.umax[rb + k] - M);
-  const float Ssum = (float)Sd;
-  // u = logw + Lmax for the shifted models: normalise with the same shift
-  const float shift = SHIFT ? M - Lmax : M;
+  const RowNorm rn = row_norm(reinterpret_cast<const double *>(d.ess_out) + (int64_t)b * tiles * kSm, tiles, SHIFT);
   const RowSlot S = row_slot(d, b);
   double sp2 = 0, px = 0, py = 0, sw = 0;
   if (i < d.N) {
-    float lk = S.hlik[i];
-    if (SHIFT) {
-      lk = lk - Lmax;
-      S.hlik[i] = lk;
-    }
-    const float lw = stage_logw(S, i, lk);
-    const float p = expf(lw - shift) / Ssum + 1e-12f;
-    S.hp[i] = p;
+    float lw;
+    const float p = norm_particle(S, i, rn, SHIFT, lw);
     sp2 = (double)p * p;
     px = (double)p * S.hx[2 * i];
     py = (double)p * S.hx[2 * i + 1];
@@ -488,7 +628,6 @@ __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_de
   double *fin = ws.fin + (((int64_t)b * d.T + d.t) * tiles + tile) * 4;
   TRACE(3, 2)
   store_sums4(fin, sp2, px, py, sw, shd);
-  if (threadIdx.x == 0) reinterpret_cast<double *>(d.ess_out)[rb + tile] = fin[0];
   TRACE(3, 3)
 }
 
@@ -522,18 +661,20 @@ __global__ __launch_bounds__(kTile) void tiled_ess_init_kernel(const float *__re
     v = (double)x * x;
   }
   v = block_sum(v, shd);
-  if (threadIdx.x == 0) parts[(int64_t)b * tiles + tile] = v;
+  if (threadIdx.x == 0) {
+    // partials of p0 itself: max 0, sum 1 (tile 0 only), sum p0^2 -> row_inv_ess = 1/sum p0^2
+    double *sm = parts + ((int64_t)b * tiles + tile) * kSm;
+    sm[0] = 0.0;
+    sm[1] = tile == 0 ? 1.0 : 0.0;
+    sm[2] = v;
+    sm[3] = 0.0;
+  }
 }
 
-__global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int tiles, int N, int force,
+__global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int tiles, int N, int t, int force,
                                   int32_t *gate) {
-  const float s = cascade_row_sum(
-      [&](int r) {
-        double s2 = 0.0;
-        for (int k = 0; k < tiles; ++k) s2 += parts[(int64_t)r * tiles + k];
-        return 1.0f / (float)s2;
-      },
-      force ? 0 : B);
+  const float s = cascade_row_sum([&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, N, t > 0); },
+                                  force ? 0 : B);
   if (threadIdx.x == 0) gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 
@@ -570,10 +711,10 @@ extern "C" int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T) {
 
 extern "C" int nfdpf_filter_tiled_tiles(int N) { return N <= 0 ? 0 : n_tiles(N); }
 
-extern "C" int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int force, int32_t *gate,
+extern "C" int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, int force, int32_t *gate,
                                     void *stream) {
   NFDPF_REQUIRE(gate && (force || parts) && B >= 1 && N >= 1, "nfdpf_ess_gate_tiled: bad arguments");
-  tiled_gate_kernel<<<1, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, force, gate);
+  tiled_gate_kernel<<<1, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, t, force, gate);
   return launch_status("nfdpf_ess_gate_tiled");
 }
 
@@ -618,6 +759,8 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_step_tiled: EXTERNAL measurement runs as phase 1 + phase 2");
   NFDPF_REQUIRE(d.measurement != NFDPF_MEAS_EXTERNAL || d.phase != 2 || d.lik_ext,
                 "nfdpf_filter_step_tiled: phase 2 needs lik_ext");
+  NFDPF_REQUIRE(!d.defer_norm || d.resampler == NFDPF_RESAMPLE_SOFT,
+                "nfdpf_filter_step_tiled: defer_norm needs the soft resampler (OT reads p_prev before the step)");
   if (d.resampler == NFDPF_RESAMPLE_SOFT) {
     NFDPF_REQUIRE(d.N <= kStepMaxN, "nfdpf_filter_step_tiled: soft resampling supports N <= %d", kStepMaxN);
     NFDPF_REQUIRE(d.lin || d.phase == 2, "nfdpf_filter_step_tiled: soft resampling needs lin");
@@ -633,7 +776,8 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
   TiledWs ws = tiled_carve(workspace, d.B, d.N, d.T);
   const dim3 g(n_tiles(d.N), d.B);
   if (d.phase != 2) {
-    const size_t lds = d.resampler == NFDPF_RESAMPLE_SOFT ? (size_t)(std::max(d.N, d.B_global) + d.N) * 4
+    // C / gate staging [max(N, B_global)], gathered weights [N], deferred p_{t-1} [N]
+    const size_t lds = d.resampler == NFDPF_RESAMPLE_SOFT ? (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4
                                                          : (size_t)d.B_global * 4;
     tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
     if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
@@ -653,10 +797,12 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
   if (d.measurement == NFDPF_MEAS_EXTERNAL) tiled_extlik_kernel<<<g, kTile, 0, st>>>(d, ws);
   const bool shift = d.measurement == NFDPF_MEAS_CRNVP || d.measurement == NFDPF_MEAS_GAUSSIAN ||
                      d.measurement == NFDPF_MEAS_EXTERNAL;
-  if (shift)
-    tiled_norm_kernel<true><<<g, kTile, 0, st>>>(d, ws);
-  else
-    tiled_norm_kernel<false><<<g, kTile, 0, st>>>(d, ws);
+  if (!d.defer_norm || d.t == d.T - 1) {  // deferred: the next step's launches normalise slot t
+    if (shift)
+      tiled_norm_kernel<true><<<g, kTile, 0, st>>>(d, ws);
+    else
+      tiled_norm_kernel<false><<<g, kTile, 0, st>>>(d, ws);
+  }
   if (d.t == d.T - 1 && d.pred && d.lw_sum) {
     const int BT = d.B * d.T;
     tiled_finalize_kernel<<<(BT + 255) / 256, 256, 0, st>>>(ws.fin, BT, n_tiles(d.N), d.pred, d.lw_sum);

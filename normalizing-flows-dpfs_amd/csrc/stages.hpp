@@ -19,8 +19,8 @@ struct RowSlot {
   const float *enc;
 };
 
-__device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) {
-  const int64_t hrow = ((int64_t)b * d.T + d.t) * d.N;
+__device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b, int t) {
+  const int64_t hrow = ((int64_t)b * d.T + t) * d.N;
   RowSlot s;
   s.hx = d.hist_x + hrow * 2;
   s.hp = d.hist_p + hrow;
@@ -30,9 +30,10 @@ __device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) {
   s.hjac = d.hist_jac ? d.hist_jac + hrow : nullptr;
   s.hprior = d.hist_prior ? d.hist_prior + hrow : nullptr;
   s.scr = d.scratch + (int64_t)b * d.N * 4;
-  s.enc = d.enc + ((int64_t)b * d.T + d.t) * d.E;
+  s.enc = d.enc + ((int64_t)b * d.T + t) * d.E;
   return s;
 }
+__device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) { return row_slot(d, b, d.t); }
 
 // context from (sum x, sum y, sum x^2, sum y^2) over N particles
 __device__ __forceinline__ Ctx4 ctx_from_sums(double a0, double a1, double b0, double b1, int N) {
@@ -47,20 +48,37 @@ enum SrcMode { kSrcPrev = 0, kSrcSoft = 1, kSrcOt = 2 };
 // motion (model/models.py:191-204) of a particle whose resampled state (x0, x1, log p) is
 // known: x_phys = (x_res + vel) + eps, eps ~ N(0, pos_noise^2).  Writes hx = x_phys,
 // hnoise = eps, hp = log p_res.
-__device__ __forceinline__ void motion_apply(const nfdpf_filter_desc &d, const RowSlot &S, int b,
-                                             int64_t grow, int i, float x0, float x1, float lr,
-                                             float v0, float v1, float &p0, float &p1) {
-  const int N = d.N;
-  float e0, e1;
+// the motion noise eps of particle i (model/models.py:200-202): device Philox or the
+// uploaded parity-mode draw
+__device__ __forceinline__ void motion_noise(const nfdpf_filter_desc &d, int b, int64_t grow, int i, float &e0,
+                                             float &e1) {
   if (d.rng_mode == NFDPF_RNG_HOST) {
-    e0 = d.host_noise[((int64_t)b * N + i) * 2];
-    e1 = d.host_noise[((int64_t)b * N + i) * 2 + 1];
+    e0 = d.host_noise[((int64_t)b * d.N + i) * 2];
+    e1 = d.host_noise[((int64_t)b * d.N + i) * 2 + 1];
   } else {
     const U4 r = rng_draw(d.seed, kTagMotion, (uint32_t)d.t, grow, (uint32_t)i);
     box_muller(r.x, r.y, e0, e1);
     e0 *= d.pos_noise;
     e1 *= d.pos_noise;
   }
+}
+
+__device__ __forceinline__ void motion_apply_eps(const RowSlot &S, int i, float x0, float x1, float lr, float v0,
+                                                 float v1, float e0, float e1, float &p0, float &p1) {
+  p0 = (x0 + v0) + e0;
+  p1 = (x1 + v1) + e1;
+  S.hnoise[2 * i] = e0;
+  S.hnoise[2 * i + 1] = e1;
+  S.hx[2 * i] = p0;
+  S.hx[2 * i + 1] = p1;
+  S.hp[i] = lr;
+}
+
+__device__ __forceinline__ void motion_apply(const nfdpf_filter_desc &d, const RowSlot &S, int b,
+                                             int64_t grow, int i, float x0, float x1, float lr,
+                                             float v0, float v1, float &p0, float &p1) {
+  float e0, e1;
+  motion_noise(d, b, grow, i, e0, e1);
   p0 = (x0 + v0) + e0;
   p1 = (x1 + v1) + e1;
   S.hnoise[2 * i] = e0;

@@ -194,10 +194,12 @@ class FilterEngine:
         if tiled:
             # per-(row, tile) sums of p^2 (double) feed the next step's gate
             tiles = ops.tiled_tiles(N)
-            ess_bufs = [torch.empty((B, tiles), device=dev, dtype=torch.float64) for _ in range(2)]
-            ess0 = ops.tiled_init(p0, torch.empty((B, tiles), device=dev, dtype=torch.float64))
+            # per-(row, tile) softmax partials {max u, sum e, sum e^2, max lik} of each step:
+            # the next step's gate and (deferred) normalisation derive from them
+            ess_bufs = [torch.empty((B, tiles, 4), device=dev, dtype=torch.float64) for _ in range(2)]
+            ess0 = ops.tiled_init(p0, torch.empty((B, tiles, 4), device=dev, dtype=torch.float64))
             ws = ops.tiled_workspace(B, N, T, dev)
-            gather_buf = torch.empty((shard.B_global, tiles), device=dev, dtype=torch.float64) \
+            gather_buf = torch.empty((shard.B_global, tiles, 4), device=dev, dtype=torch.float64) \
                 if shard.world > 1 else None
         else:
             ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
@@ -222,6 +224,9 @@ class FilterEngine:
         d.lik_ext = L.ptr(lik_ext)
         d.rng_mode = L.RNG_HOST if host_mode else L.RNG_DEVICE
         d.force_resample, d.n_flows, d.hidden = int(c.force_resample), c.n_flows, c.hidden
+        # tiled + soft: step t's weights are normalised inside step t+1 (one launch fewer per
+        # step); not when the caller feeds p_prev itself (teacher forcing) or OT reads it first
+        d.defer_norm = int(tiled and c.resampler == "soft" and teacher is None)
         d.alpha, d.pos_noise = c.alpha, c.pos_noise
         d.dens_const, d.meas_prior_std = density_const(c.pos_noise), c.meas_prior_std
         d.seed = int(c.seed) & (2 ** 64 - 1)
@@ -256,7 +261,7 @@ class FilterEngine:
                     pc = teacher["p"][:, t - 1].cpu().float()
                     fire = bool(c.force_resample or torch.mean(1 / torch.sum(pc ** 2, dim=-1)) < 0.5 * N)
                 elif tiled:
-                    fire = self._host_gate_parts(ess_all, N, c.force_resample)
+                    fire = self._host_gate_parts(ess_all, N, c.force_resample, t)
                 else:
                     fire = self._host_gate(ess_all, N, c.force_resample)
                 fired.append(fire)
@@ -272,7 +277,7 @@ class FilterEngine:
                 d.host_noise = nz.data_ptr()
             elif c.resampler == "ot":
                 if tiled:
-                    ops.ess_gate_tiled(ess_all, N, c.force_resample, out=gate_buf)
+                    ops.ess_gate_tiled(ess_all, N, t, c.force_resample, out=gate_buf)
                 else:
                     ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
                 d.gate = gate_buf.data_ptr()
@@ -353,15 +358,21 @@ class FilterEngine:
         return out
 
     @staticmethod
-    def _host_gate_parts(parts: torch.Tensor, N: int, force: bool) -> bool:
-        """Tiled-mode gate on the host: per row sum the per-tile p^2 sums (double, in order),
-        1/sum in float32, then torch.mean over rows (csrc/filter_tiled.hip)."""
+    def _host_gate_parts(parts: torch.Tensor, N: int, force: bool, t: int) -> bool:
+        """Tiled-mode gate of step t on the host, from the [B, tiles, 4] softmax partials of
+        step t-1 (csrc/filter_tiled.hip row_inv_ess): sum p^2 = sum e^2 / S^2 (+ the +1e-12
+        terms after a filter step), 1/sum in float32, then torch.mean over rows."""
         if force:
             return True
-        rows = parts.double().cpu().numpy()
-        inv = np.array([np.float32(1.0) / np.float32(sum(float(v) for v in row)) for row in rows],
-                       dtype=np.float32)
-        return bool(torch.from_numpy(inv).mean() < np.float32(0.5 * N))
+        inv = []
+        for row in parts.double().cpu().numpy():
+            M = row[:, 0].max()
+            f = np.exp((row[:, 0] - M).astype(np.float32)).astype(np.float64)  # f32 factors, as the kernel
+            S = float(np.sum(row[:, 1] * f))
+            Q = float(np.sum(row[:, 2] * f * f))
+            sp2 = Q / (S * S) + ((2e-12 + N * 1e-24) if t > 0 else 0.0)
+            inv.append(np.float32(1.0) / np.float32(sp2))
+        return bool(torch.from_numpy(np.array(inv, dtype=np.float32)).mean() < np.float32(0.5 * N))
 
     @staticmethod
     def _host_gate(ess_all: torch.Tensor, N: int, force: bool) -> bool:

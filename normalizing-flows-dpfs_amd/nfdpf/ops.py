@@ -205,11 +205,12 @@ def tiled_init(p0: torch.Tensor, out: torch.Tensor):
     return out
 
 
-def ess_gate_tiled(parts, N, force=False, out=None):
+def ess_gate_tiled(parts, N, t, force=False, out=None):
+    """Gate of step ``t`` from the [B, tiles, 4] softmax partials of step t-1 (include/nfdpf.h)."""
     B = parts.shape[0]
     g = out if out is not None else torch.empty(1, device=parts.device, dtype=torch.int32)
-    check(lib().nfdpf_ess_gate_tiled(ptr(parts), B, N, int(bool(force)), ptr(g), stream_ptr(parts.device)),
-          "nfdpf_ess_gate_tiled")
+    check(lib().nfdpf_ess_gate_tiled(ptr(parts), B, N, int(t), int(bool(force)), ptr(g),
+                                     stream_ptr(parts.device)), "nfdpf_ess_gate_tiled")
     return g
 
 
