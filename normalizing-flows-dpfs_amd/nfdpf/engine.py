@@ -10,6 +10,7 @@ same batch-global gate decision (DPFs.py:163-165), and nothing else is exchanged
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass, field
 from typing import Optional
@@ -239,21 +240,35 @@ class FilterEngine:
 
         fired = [] if host_mode else None
         keep = []  # host uploads must outlive their kernels
+        # per-step pointers precomputed as integers: the loop below is the launch path of every
+        # time step, so it stays free of tensor slicing and per-call lookups
+        hx_p, hp_p, vel_p = hx.data_ptr(), hp.data_ptr(), vel_steps.data_ptr()
+        ess_out_p = [b.data_ptr() for b in ess_bufs]
+        stream = ops.stream_ptr(dev)
+        launch = L.lib().nfdpf_filter_step_tiled if tiled else L.lib().nfdpf_filter_step
+        ws_p = ops._aligned_ptr(ws) if tiled else None
+        d_ref = ctypes.byref(d)
+
+        def step():
+            rc = launch(d_ref, ws_p, stream) if tiled else launch(d_ref, stream)
+            if rc != L.NFDPF_OK:
+                L.check(rc, "nfdpf_filter_step_tiled" if tiled else "nfdpf_filter_step")
+
         for t in range(T):
             if t == 0:
-                xp, pp, xrs, prs = x0, p0, N * 2, N
+                d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = x0.data_ptr(), p0.data_ptr(), N * 2, N
             elif teacher is not None:
                 xp = teacher["x"][:, t - 1].to(dev).float().contiguous()
                 pp = teacher["p"][:, t - 1].to(dev).float().contiguous()
                 keep += [xp, pp]
-                xrs, prs = N * 2, N
-            else:
-                xp, pp, xrs, prs = hx[:, t - 1], hp[:, t - 1], T * N * 2, T * N
+                d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = xp.data_ptr(), pp.data_ptr(), N * 2, N
+            else:  # history slot t-1, rows of T*N
+                d.x_prev, d.p_prev = hx_p + (t - 1) * N * 8, hp_p + (t - 1) * N * 4
+                d.x_prev_rs, d.p_prev_rs = T * N * 2, T * N
             d.t = t
-            d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = xp.data_ptr(), pp.data_ptr(), xrs, prs
-            d.vel = vel_steps[t].data_ptr()
+            d.vel = vel_p + t * B * 8
             d.ess_all = ess_all.data_ptr()
-            d.ess_out = ess_bufs[t & 1].data_ptr()
+            d.ess_out = ess_out_p[t & 1]
             d.gate = None
             d.host_noise = d.host_offsets = None
             if host_mode:
@@ -282,9 +297,12 @@ class FilterEngine:
                     ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
                 d.gate = gate_buf.data_ptr()
             if c.resampler == "ot":
-                contiguous = t == 0 or teacher is not None
-                xin = xp if contiguous else hx[:, t - 1].contiguous()
-                pin = pp if contiguous else hp[:, t - 1].contiguous()
+                if t == 0:
+                    xin, pin = x0, p0
+                elif teacher is not None:
+                    xin, pin = xp, pp
+                else:
+                    xin, pin = hx[:, t - 1].contiguous(), hp[:, t - 1].contiguous()
                 # The Sinkhorn loop is max_iter launches; when the gate is off they would all be
                 # no-ops, so read the gate (one sync, as the reference's `if ESS < ...` does,
                 # DPFs.py:165) and skip the call.  The gate is batch-global: same on every rank.
@@ -307,7 +325,6 @@ class FilterEngine:
                 self.step_events.append(ev)
                 if not external:
                     d.prof_events = ev.ptr  # around the step's dominant launch, inside the library
-            step = (lambda: ops.filter_step_tiled(d, ws, dev)) if tiled else (lambda: ops.filter_step(d, dev))
             if external:
                 d.phase = 1
                 step()
@@ -320,7 +337,10 @@ class FilterEngine:
                 step()
             else:
                 step()
-            ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
+            if shard.world > 1:
+                ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
+            else:
+                ess_all = ess_bufs[t & 1]
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)
         if shard.world > 1:
