@@ -120,6 +120,24 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
                       f"host {platform.processor() or platform.machine()}"}
 
 
+def pmc_traffic(cfg_name, kname):
+    """HBM bytes per launch of ``kname`` from the committed PMC summary of this workload
+    (scripts/pmc.sh + scripts/pmc_summary.py -> profiles/pmc_<config>.csv): FETCH_SIZE and
+    WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts half the bytes of a streaming read
+    (MI355X_MICROARCH.md, HBM / rocprofv3), so it is doubled.  None when no summary exists."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.csv")
+    if not os.path.exists(path):
+        return None, None
+    vals = {}
+    for line in open(path).read().splitlines()[1:]:
+        k, c, _, v = line.split(",")
+        if k.split("::")[-1] == kname:
+            vals[c] = float(v)
+    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
+        return None, None
+    return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,9 +226,12 @@ def main():
     kernel_ms = float(np.mean([e.ms() for e in evs]))
     for e in evs:
         e.close()
-    kname = "tiled_prop_kernel" if args.kernel == "tiled" else "filter_step_kernel"
+    kname = "filter_step_kernel"
+    if args.kernel == "tiled":  # the proposal launch: two roles (flow, measurement) with NF_cond
+        kname = "tiled_prop2_kernel" if flags["NF_cond"] else "tiled_prop_kernel"
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
+    traffic, traffic_src = pmc_traffic(args.config, kname)
     # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
     se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
     cnt = torch.tensor(float(res.pred.numel()), device=dev, dtype=torch.float64)
@@ -238,7 +259,8 @@ def main():
                        "parallelism": f"batch-sharded x{world}"},
             "rmse": rmse,
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": kname, "kernel_avg_ms": kernel_ms,
                          "flop_per_unit": F_ALG, "units_per_launch": per_launch_units,
                          "hbm_achieved_GBs": hbm_gbs, "hbm_frac": hbm_gbs / PEAK_HBM_GBS},

@@ -22,11 +22,17 @@
  *   coupling net            : FCNN(h + O, h, H) of a RealNVP(_cond) flow, h = dim/2, O = obser_dim,
  *                             stored core-first: W1[:, :h] W2 b2 W3 b3, then W1[:, h:] b1
  *                             (the context columns are folded into a bias once per row)
- *   RealNVP(_cond) flow     : coupling nets t1, s1, t2, s2                      (nf/flows.py:181-190)
+ *   RealNVP(_cond) flow     : coupling halves (t1, s1), (t2, s2), the two nets of a half
+ *                             interleaved elementwise ({t, s} float pairs)     (nf/flows.py:181-190)
  *   stack of n flows        : flow 0, flow 1, ... (model order, i.e. nf_dyn.flows[i])
+ *   split suffix (optional) : behind a stack of RealNVP_cond(2, O) flows, for each flow and net
+ *                             t1, s1, t2, s2 ninety floats: W1[:, 0], W2, b2, W3 with hidden
+ *                             units 2m, 2m+1 adjacent, then {b3, 0} (csrc/split.hpp); the tiled
+ *                             step reads it when split_nets is set
  *   MAF flow (dim d)        : initial_param[2], then FCNN(i, 2, H) for i = 1..d-1 (nf/flows.py:247-254)
  *   particle encoder        : Linear(2,16) Linear(16,32) Linear(32,E): W,b each  (model/models.py:130-150),
- *                             each W in row-pair order [out/2][in][2] (outputs 2m, 2m+1 adjacent)
+ *                             W1 in row-pair order [out/2][in][2], W2 and W3 in col-pair order
+ *                             [in][out/2][2] (outputs 2m, 2m+1 adjacent in both)
  *   likelihood_est (NN)     : Linear(2E,64) Linear(64,64) Linear(64,1): W,b each (model/models.py:119-128)
  */
 #ifndef NFDPF_H
@@ -140,7 +146,7 @@ NFDPF_API int nfdpf_measurement(int kind, const float *pe_params, const float *m
  * x + b*x_rs + 2i, frame encoding of row b at enc + b*enc_rs (192 floats) -> the RAW
  * likelihood -nll at lik + b*lik_rs + i (the row-max shift of :301-302 is the caller's:
  * the filter's EXTERNAL-measurement phase 2, or measurement_model_cglow).
- * pe_params: particle encoder 2->16->32->192 (row-paired MLP layout); glow_params:
+ * pe_params: particle encoder 2->16->32->192 (encoder layout above); glow_params:
  * nfdpf_cglow_params_size(K) floats (layout: nfdpf.pack.cglow_tensors). */
 NFDPF_API int64_t nfdpf_cglow_params_size(int K);
 NFDPF_API int nfdpf_cglow_measurement(const float *pe_params, const float *glow_params, int K,
@@ -171,6 +177,9 @@ typedef struct nfdpf_filter_desc {
   int32_t defer_norm;       /* tiled step: normalise step t's weights inside step t+1's first
                                launch (p_prev / x_prev = history slot t-1, not yet normalised);
                                the caller clears it for the last step and to feed p_prev itself */
+  int32_t split_nets;       /* tiled step: dyn_params / cond_params carry the split suffix
+                               (below) and nf_dyn is RealNVP -- the coupling nets then run on
+                               wave pairs (t-nets and s-nets on separate waves) */
   float alpha, pos_noise, dens_const, meas_prior_std;
   uint64_t seed;
   /* packed parameters */

@@ -363,10 +363,11 @@ __global__ __launch_bounds__(kThreads, 2) void cglow_kernel(const float *__restr
     const float *gw = glow, *pe_ = pe;
     asm volatile("" : "+s"(gw), "+s"(pe_));
     const float *gA = gw + kOffA, *gI = gw + kOffI;
-    // encoder weights (nfdpf.pack.paired_mlp_tensors: row_pairs weights)
+    // encoder weights (nfdpf.pack.encoder_tensors)
     const float *pw1 = pe_, *pb1 = pe_ + kPeB1, *pw2 = pe_ + kPeW2, *pb2 = pe_ + kPeB2, *pw3 = pe_ + kPeW3,
                 *pb3 = pe_ + kPeW3 + kE * kPeH2;
-    auto W3 = [&](int n, int k) { return pw3[((n >> 1) * kPeH2 + k) * 2 + (n & 1)]; };
+    // W2 / W3 in col_pairs order (nfdpf.pack.encoder_tensors): {W[2m, k], W[2m+1, k]} at [k][m]
+    auto W3 = [&](int n, int k) { return pw3[(k * (kE / 2) + (n >> 1)) * 2 + (n & 1)]; };
     const int64_t g0 = tile * kTileP;
     // ---- particles of the tile
     if (tid < kTileP) {
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(kThreads, 2) void cglow_kernel(const float *__restr
         const int o = j + 16 * hh;
         float a = pb2[o];
 #pragma unroll
-        for (int k = 0; k < kPeH1; ++k) a = fmaf(PW(pw2, o, k, kPeH1), S.h1[p][k], a);
+        for (int k = 0; k < kPeH1; ++k) a = fmaf(pw2[(k * (kPeH2 / 2) + (o >> 1)) * 2 + (o & 1)], S.h1[p][k], a);
         S.h2[p][o] = relu(a);
       }
     }

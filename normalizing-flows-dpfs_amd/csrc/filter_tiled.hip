@@ -18,7 +18,7 @@
 // ess_all / ess_out of the descriptor hold per-(row, tile) sums of p^2 as doubles
 // ([B_global][tiles] / [B][tiles]); everything else has the fused kernel's meaning.
 #include "soft.hpp"
-#include "stages.hpp"
+#include "split.hpp"
 
 namespace nfdpf {
 
@@ -353,39 +353,91 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
 }
 
 // ---- K2: nf_dyn inverse; with defer_norm also the normalisation of slot t-1 (finish_prev's
-// arithmetic, its sums reduced together with this launch's in one barrier)
-__global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
-  __shared__ double shd[32];
+// arithmetic, its sums reduced together with this launch's in one barrier).  SPLIT: the
+// RealNVP nets on wave pairs (split.hpp) -- role 0 = t-nets (and the stores), role 1 =
+// s-nets (and the deferred normalisation).
+// Each role's waves reduce their own four sums; thread k < 8 adds the wave partials of role
+// k / 4 in particle-group order (waves k / 4, 2 + k / 4, ...) -- the order of block_sum8_store
+// over the same particles.
+__device__ __forceinline__ void block_sum_roles_store(const double (&v)[4], double *dst0, double *dst1,
+                                                      double *sh) {
+  double w4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w4[k] = wave_sum_dpp(v[k]);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh[4 * w + k] = w4[k];
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int r = threadIdx.x >> 2, k = threadIdx.x & 3;
+    double *dst = r ? dst1 : dst0;
+    if (dst) {
+      double a = sh[4 * r + k];
+      for (int q = 1; q < 4; ++q) a += sh[4 * (2 * q + r) + k];
+      dst[k] = a;
+    }
+  }
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 2 * kTile : kTile) void tiled_dyn_kernel(const nfdpf_filter_desc d,
+                                                                               TiledWs ws) {
+  __shared__ double shd[64];
   __shared__ f2 cb[kMaxFlows * 2 * kH];
+  __shared__ f2 cbs[SPLIT ? kMaxFlows * 2 * kH : 1];  // split order (split_cb_index)
+  __shared__ float xbuf[SPLIT ? 4 * kTile : 1];
+  __shared__ int xflag[16];
   TRACE(1, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
-  const int i = tile * kTile + threadIdx.x;
+  const SplitLane sl = SPLIT ? split_lane(8) : SplitLane{0, (int)threadIdx.x};
+  const int role = sl.role, slot = sl.slot;
+  const int i = tile * kTile + slot;
   const RowSlot S = row_slot(d, b);
   float p0 = 0.f, p1 = 0.f;
   PrevIn pv{};
   const bool defer = d.defer_norm && d.t > 0;
+  const bool defer_here = defer && role == (SPLIT ? 1 : 0);
   const bool shifted = shifted_meas(d.measurement);
   if (i < d.N) {  // before the fold, so the loads overlap it
     p0 = S.hx[2 * i];
     p1 = S.hx[2 * i + 1];
-    if (defer) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
+    if (defer_here) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
   }
-  const RowNorm rn = defer ? row_norm(prev_sm(d, b, tiles), tiles, shifted) : RowNorm{0.f, 1.f, 0.f};
-  fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb, d.nf_dyn);
+  const RowNorm rn = defer_here ? row_norm(prev_sm(d, b, tiles), tiles, shifted) : RowNorm{0.f, 1.f, 0.f};
+  if (SPLIT) {
+    if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+    if (threadIdx.x < d.n_flows * 4 * kH) {
+      const Ctx4 c = tiled_ctx(ws.st_phys, b, tiles, d.N);
+      const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
+      const float v = fold_one(d.dyn_params, kNsDyn, kOctxDyn, threadIdx.x, cv);
+      reinterpret_cast<float *>(cb)[threadIdx.x] = v;
+      reinterpret_cast<float *>(cbs)[split_cb_index(threadIdx.x)] = v;
+    }
+  } else {
+    fold_dyn(d.dyn_params, d.n_flows, tiled_ctx(ws.st_phys, b, tiles, d.N), cb, d.nf_dyn);
+  }
   __syncthreads();
   if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
     ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
   TRACE(1, 1)
   double sd[4] = {0, 0, 0, 0}, sf[4] = {0, 0, 0, 0};
   if (i < d.N) {
-    float x0, x1;
-    stage_dyn_inverse(d, S, i, p0, p1, cb, x0, x1);
-    sd[0] = x0;
-    sd[1] = x1;
-    sd[2] = (double)x0 * x0;
-    sd[3] = (double)x1 * x1;
-    if (defer) {
+    float x0 = 0.f, x1 = 0.f;
+    if (SPLIT) {
+      PairX x = pair_of(xbuf, xflag, role, slot);
+      stage_dyn_inverse_split(d, S, i, p0, p1, cbs, x, kTile, x0, x1);
+    } else {
+      stage_dyn_inverse(d, S, i, p0, p1, cb, x0, x1);
+    }
+    if (role == 0) {
+      sd[0] = x0;
+      sd[1] = x1;
+      sd[2] = (double)x0 * x0;
+      sd[3] = (double)x1 * x1;
+    }
+    if (defer_here) {
       const RowSlot Sp = row_slot(d, b, d.t - 1);
       float lw, lk;
       const float p = prev_p_of(pv, rn, shifted, lw, lk);
@@ -399,8 +451,11 @@ __global__ __launch_bounds__(kTile) void tiled_dyn_kernel(const nfdpf_filter_des
   }
   TRACE(1, 2)
   double *dst = ws.st_dyn + ((int64_t)b * tiles + tile) * 4;
-  if (defer)
-    block_sum8_store(sd, dst, sf, ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4, shd);
+  double *dfin = defer ? ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4 : nullptr;
+  if (SPLIT)
+    block_sum_roles_store(role ? sf : sd, dst, dfin, shd);
+  else if (defer)
+    block_sum8_store(sd, dst, sf, dfin, shd);
   else
     store_sums4(dst, sd[0], sd[1], sd[2], sd[3], shd);
   TRACE(1, 3)
@@ -542,6 +597,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
     qx[pl][1] = q1x;
   }
   __syncthreads();
+  TRACE(2, 4)
   float lk = -INFINITY, u = 0.f, propose = 0.f, prior = 0.f;
   const int role = threadIdx.x / kTile;
   if (valid) {
@@ -552,7 +608,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
       static_assert(ROLES != 3 || MEAS == NFDPF_MEAS_COS, "three roles: cosine measurement only");
       constexpr int HP = kE / 4;  // output pairs per role
       float ss, dot;
-      encode_dot<kE>(wptr(d.pe_params), qx[pl][0], qx[pl][1], L.encv, ss, dot, (role - 1) * HP, role * HP);
+      encode_dot<kE, HP>(wptr(d.pe_params), qx[pl][0], qx[pl][1], L.encv, ss, dot, (role - 1) * HP);
       ssx[role][pl] = ss;
       dotx[role][pl] = dot;
     } else {
@@ -580,6 +636,73 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   const float lm = meas_shifted<MEAS>() ? block_max(lk, L.f) : 0.f;
   if (threadIdx.x == 0) sm[3] = lm;
   store_softmax(u, valid && flows, sm, smf, smd);
+  TRACE(2, 3)
+}
+
+// ---- K3 on wave pairs (split.hpp; --NF-dyn RealNVP, --NF-cond, cosine measurement): the
+// t-wave and the s-wave of a particle group run the proposal inverse and the nf_dyn forward
+// net by net, then split the particle encoder's output layer (each computes the hidden
+// layers, then half of the 32 outputs) and exchange their partial |e|^2 and <e, v>.  No
+// wave idles and no workgroup barrier separates the stages.  512 threads per tile.
+__global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ StepShared L;  // cb_dyn / cb_cond in split order
+  __shared__ float xbuf[4 * kTile];
+  __shared__ int xflag[16];
+  __shared__ float smf[16];
+  __shared__ double smd[32];
+  TRACE(2, 0)
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const SplitLane sl = split_lane(8);
+  const int role = sl.role, slot = sl.slot;
+  const int i = tile * kTile + slot;
+  const RowSlot S = row_slot(d, b);
+  const bool valid = i < d.N;
+  PropIn in{};
+  float lr = 0.f;
+  if (valid) {  // issued before the row prologue so they overlap it
+    in = load_prop_in<true>(S, i);
+    if (role == 0) lr = S.hp[i];
+  }
+  measure_row_setup<NFDPF_MEAS_COS>(S.enc, d.meas_params, L);
+  if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+  const int ncb = d.n_flows * 4 * kH;
+  if (threadIdx.x < ncb)
+    reinterpret_cast<float *>(L.cb_dyn)[split_cb_index(threadIdx.x)] = ws.cb_dyn[b * kCb + threadIdx.x];
+  if (threadIdx.x >= kTile && threadIdx.x - kTile < ncb) {
+    // finish the proposal fold: the encoding columns came from K1, add [mean, std] of x_dyn
+    const int k = threadIdx.x - kTile;
+    const Ctx4 cp = tiled_ctx(ws.st_dyn, b, tiles, d.N);
+    const float c4[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), k);
+    reinterpret_cast<float *>(L.cb_cond)[split_cb_index(k)] =
+        fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + k], c4, d.E, d.E + 4);
+  }
+  __syncthreads();
+  TRACE(2, 1)
+  PairX x = pair_of(xbuf, xflag, role, slot);
+  float u = 0.f;
+  if (valid) {
+    float q0x, q1x, propose, prior;
+    const float jp = stage_propose_inverse_split(d, in, L.cb_cond, x, kTile, q0x, q1x);
+    stage_prior_split(d, S, i, in, L.cb_dyn, q0x, q1x, jp, x, kTile, propose, prior);
+    // cosine measurement (model/models.py:206-219): outputs [16 role, 16 role + 16) here
+    float ss, dot;
+    encode_dot<kE, kE / 4>(wptr(d.pe_params), q0x, q1x, L.encv, ss, dot, role * (kE / 4));
+    const float ss_o = pair_swap(x, ss, kTile), dot_o = pair_swap(x, dot, kTile);
+    ss = role ? ss_o + ss : ss + ss_o;
+    dot = role ? dot_o + dot : dot + dot_o;
+    const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
+    const float lk = logf(1.0f / (1e-7f + cosd));
+    if (role == 0) {
+      S.hlik[i] = lk;
+      u = logw(lr, lk, prior, propose);
+    }
+  }
+  TRACE(2, 2)
+  double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
+  if (threadIdx.x == 0) sm[3] = 0.f;
+  store_softmax(u, valid && role == 0, sm, smf, smd);
   TRACE(2, 3)
 }
 
@@ -678,11 +801,20 @@ __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int t
   if (threadIdx.x == 0) gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 
+// the flows run on wave pairs when the blobs carry the split suffix (RealNVP nf_dyn)
+static bool use_split(const nfdpf_filter_desc &d) { return d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP; }
+
 template <bool NFD, bool NFC, int MEAS>
 static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStream_t st) {
   // the two-role kernel needs a flow chain to overlap with the measurement
   // (a third role splitting the cosine encoder's output layer was measured slower: 16.7 vs
   // 11.4 us for the compute phase at C2 -- the extra waves duplicate the encoder's first layers)
+  if constexpr (NFD && NFC && MEAS == NFDPF_MEAS_COS) {
+    if (use_split(d)) {
+      tiled_prop_split_kernel<<<g, 2 * kTile, 0, st>>>(d, ws);
+      return;
+    }
+  }
   if constexpr (NFC && MEAS != NFDPF_MEAS_EXTERNAL)
     tiled_prop2_kernel<NFD, NFC, MEAS, 2><<<g, 2 * kTile, 0, st>>>(d, ws);
   else
@@ -780,7 +912,10 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
     const size_t lds = d.resampler == NFDPF_RESAMPLE_SOFT ? (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4
                                                          : (size_t)d.B_global * 4;
     tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
-    if (d.nf_dyn) tiled_dyn_kernel<<<g, kTile, 0, st>>>(d, ws);
+    if (use_split(d))
+      tiled_dyn_kernel<true><<<g, 2 * kTile, 0, st>>>(d, ws);
+    else if (d.nf_dyn)
+      tiled_dyn_kernel<false><<<g, kTile, 0, st>>>(d, ws);
     hipEvent_t *ev = (hipEvent_t *)d.prof_events;
     if (ev) (void)hipEventRecord(ev[0], st);
     switch (d.measurement) {

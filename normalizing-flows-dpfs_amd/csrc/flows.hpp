@@ -257,8 +257,11 @@ __device__ __forceinline__ float maf_inverse(cfloat *fw, float (&v)[D]) {
 
 // ----------------------------------------------------------------------------------------
 // particle encoder (model/models.py:130-150): Linear(2,16) ReLU Linear(16,32) ReLU Linear(32,E)
-// Weights in row_pairs layout (nfdpf.pack.paired_mlp_tensors): outputs 2m, 2m+1 advance
-// together, W[m][k] = {W[2m, k], W[2m+1, k]}; biases as stored by nn.Linear.
+// Layout (nfdpf.pack.encoder_tensors): W1 in row_pairs order ({W[2m, k], W[2m+1, k]} at
+// [m][k]); W2 and W3 in col_pairs order ({W[2m, k], W[2m+1, k]} at [k][m]), so the layers run
+// input-major: each input's weight run (16 pairs = 128 B, two s_load_dwordx16) feeds
+// independent accumulators for every output pair -- full ILP instead of one long dependent
+// chain per output.  Biases as stored by nn.Linear.
 // ----------------------------------------------------------------------------------------
 constexpr int kPeH1 = 16, kPeH2 = 32;
 __host__ __device__ constexpr int pe_size(int E) {
@@ -267,6 +270,8 @@ __host__ __device__ constexpr int pe_size(int E) {
 constexpr int kPeB1 = kPeH1 * 2, kPeW2 = kPeB1 + kPeH1, kPeB2 = kPeW2 + kPeH2 * kPeH1,
               kPeW3 = kPeB2 + kPeH2;
 
+__device__ __forceinline__ float pick(const f2 *h, int k) { return (k & 1) ? h[k >> 1].y : h[k >> 1].x; }
+
 __device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, f2 (&h2)[kPeH2 / 2]) {
   cf2 *w1 = (cf2 *)pe, *b1 = (cf2 *)(pe + kPeB1);
   f2 h1[kPeH1 / 2];
@@ -274,53 +279,65 @@ __device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, f2 (&h
   for (int m = 0; m < kPeH1 / 2; ++m)
     h1[m] = relu2(pfma(w1[2 * m + 1], splat(x1), pfma(w1[2 * m], splat(x0), b1[m])));
   cf2 *w2 = (cf2 *)(pe + kPeW2), *b2 = (cf2 *)(pe + kPeB2);
+  constexpr int M = kPeH2 / 2;
 #pragma unroll
-  for (int m = 0; m < kPeH2 / 2; ++m) {
-    f2 a = b2[m];
+  for (int m = 0; m < M; ++m) h2[m] = b2[m];
 #pragma unroll
-    for (int k = 0; k < kPeH1; ++k) a = pfma(w2[m * kPeH1 + k], splat(k & 1 ? h1[k >> 1].y : h1[k >> 1].x), a);
-    h2[m] = relu2(a);
+  for (int k = 0; k < kPeH1; ++k) {
+    const float hk = pick(h1, k);
+#pragma unroll
+    for (int m = 0; m < M; ++m) h2[m] = pfma(w2[k * M + m], splat(hk), h2[m]);
   }
+#pragma unroll
+  for (int m = 0; m < M; ++m) h2[m] = relu2(h2[m]);
 }
 
-template <int E>
-__device__ __forceinline__ f2 pe_out(cfloat *pe, const f2 (&h2)[kPeH2 / 2], int m) {
-  cf2 *w3 = (cf2 *)(pe + kPeW3), *b3 = (cf2 *)(pe + kPeW3 + E * kPeH2);
-  f2 a = b3[m];
+// output pairs [m0, m0 + MP) of the last layer, input-major
+template <int E, int MP>
+__device__ __forceinline__ void pe_out(cfloat *pe, const f2 (&h2)[kPeH2 / 2], int m0, f2 (&a)[MP]) {
+  constexpr int M = E / 2;
+  cf2 *w3 = (cf2 *)(pe + kPeW3) + m0, *b3 = (cf2 *)(pe + kPeW3 + E * kPeH2) + m0;
 #pragma unroll
-  for (int k = 0; k < kPeH2; ++k) a = pfma(w3[m * kPeH2 + k], splat(k & 1 ? h2[k >> 1].y : h2[k >> 1].x), a);
-  return a;
+  for (int m = 0; m < MP; ++m) a[m] = b3[m];
+#pragma unroll
+  for (int k = 0; k < kPeH2; ++k) {
+    const float hk = pick(h2, k);
+#pragma unroll
+    for (int m = 0; m < MP; ++m) a[m] = pfma(w3[k * M + m], splat(hk), a[m]);
+  }
 }
 
 template <int E>
 __device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, float (&e)[E]) {
   f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
+  f2 a[E / 2];
+  pe_out<E, E / 2>(pe, h2, 0, a);
 #pragma unroll
   for (int m = 0; m < E / 2; ++m) {
-    const f2 a = pe_out<E>(pe, h2, m);
-    e[2 * m] = a.x;
-    e[2 * m + 1] = a.y;
+    e[2 * m] = a[m].x;
+    e[2 * m + 1] = a[m].y;
   }
 }
 
-// Cosine-distance pieces for the particle encoder output, streamed: (|e|^2, <e, v>) without
-// materialising e (model/models.py:130-139 then utils.py:8-15).
-template <int E>
+// Cosine-distance pieces for the particle encoder output (|e|^2, <e, v>) over output pairs
+// [m0, m0 + MP) (model/models.py:130-139 then utils.py:8-15); a caller may split the E
+// outputs over several waves.
+template <int E, int MP = E / 2>
 __device__ __forceinline__ void encode_dot(cfloat *pe, float x0, float x1, const float *v, float &ss,
-                                           float &dot, int m0 = 0, int m1 = E / 2) {
-  // output pairs [m0, m1) only: a caller may split the E outputs over several waves
+                                           float &dot, int m0 = 0) {
   f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
+  f2 a[MP];
+  pe_out<E, MP>(pe, h2, m0, a);
   ss = 0.f;
   dot = 0.f;
-#pragma unroll 2
-  for (int m = m0; m < m1; ++m) {
-    const f2 a = pe_out<E>(pe, h2, m);
-    ss = fmaf(a.x, a.x, ss);
-    dot = fmaf(a.x, v[2 * m], dot);
-    ss = fmaf(a.y, a.y, ss);
-    dot = fmaf(a.y, v[2 * m + 1], dot);
+#pragma unroll
+  for (int m = 0; m < MP; ++m) {
+    ss = fmaf(a[m].x, a[m].x, ss);
+    dot = fmaf(a[m].x, v[2 * (m0 + m)], dot);
+    ss = fmaf(a[m].y, a[m].y, ss);
+    dot = fmaf(a[m].y, v[2 * (m0 + m) + 1], dot);
   }
 }
 

@@ -1,0 +1,208 @@
+// split.hpp -- a coupling flow on two waves per particle group: the t-net of every particle
+// runs on one wave, its s-net on a partner wave, and the two exchange their single output
+// through LDS once per coupling half.
+//
+// Why: at the C2 workload (64 rows x 1000 particles) one particle per lane is ONE wave per
+// SIMD across the chip, where a VALU instruction issues at half rate and nothing hides the
+// scalar weight loads or the exp/rcp latencies of the tanh chains.  Splitting the nets
+// halves each wave's chain and doubles the waves in flight without adding arithmetic (the
+// only duplicated work is the coupling update itself, a handful of VALU ops).
+//
+// Weight layout (the "split suffix" of a dynamic / proposal flow blob, nfdpf.pack
+// split_flow_tensors, include/nfdpf.h): for each flow, coupling half n (t1/s1, t2/s2) and
+// net r (t, s), kSplitNet floats
+//   [ W1[:, 0] as hidden pairs (4) | W2 rows as hidden pairs [4][8] | b2 pairs (4) |
+//     W3 pairs (4) | {b3, 0} ]
+// so one v_pk_fma_f32 advances hidden units 2m and 2m+1 of ONE net (HALF = 1, H = 8: the
+// 2-D particle flows of the filter).  The folded first-layer biases are re-ordered the same
+// way in LDS: [flow][half][net][j] (split_cb_index).
+#pragma once
+
+#include "stages.hpp"
+
+namespace nfdpf {
+
+constexpr int kSplitNet = 90;              // floats per net (45 pairs)
+constexpr int kSplitFlow = 4 * kSplitNet;  // t1, s1, t2, s2
+static_assert(kH == 8, "split nets are laid out for hidden width 8");
+
+// offset (floats) of the split suffix behind the pair layout of an n_flows stack of
+// RealNVP_cond(2, O) flows
+__host__ __device__ constexpr int split_suffix_offset(int n_flows, int O) {
+  return n_flows * 2 * net_size<1, kH>(O) * 2;
+}
+
+// position of float `tid` of a pair-order fold table ([flow][half][j][t|s], fold_ref) in the
+// split order [flow][half][net][j]
+__device__ __forceinline__ int split_cb_index(int tid) {
+  const int f = tid / (4 * kH), r = tid % (4 * kH);
+  const int n = r / (2 * kH), j = (r >> 1) % kH, w = r & 1;
+  return ((f * 2 + n) * 2 + w) * kH + j;
+}
+
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Pairwise hand-off between the t-wave and the s-wave of one particle group, through LDS,
+// with no workgroup barrier: each side writes its value, publishes a per-wave counter and
+// spins (s_sleep) until the partner's counter reaches the same exchange.  Values are double
+// buffered by exchange parity, so a fast side never overwrites one its partner has not read
+// (it would first need the partner's NEXT counter, published only after that read).  Both
+// waves of a pair cover the same particles, so they execute the same exchanges.
+typedef __attribute__((address_space(3))) float lds_float;
+typedef volatile __attribute__((address_space(3))) int lds_vint;
+
+struct PairX {
+  lds_float *buf;  // [2 parities][2 nets][kTile]
+  lds_vint *mine;  // this wave's counter
+  lds_vint *theirs;
+  int role, slot, k;
+};
+
+// Wave roles of a split workgroup: waves 2g and 2g + 1 are the t-net and the s-net of
+// particle group g (adjacent waves sit on different SIMDs, so a pair computes side by side
+// rather than taking turns on one SIMD); waves from `flow_waves` on take role 2.
+struct SplitLane {
+  int role, slot;
+};
+__device__ __forceinline__ SplitLane split_lane(int flow_waves) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (w < flow_waves) return SplitLane{w & 1, (w >> 1) * 64 + l};
+  return SplitLane{2, (w - flow_waves) * 64 + l};
+}
+
+// the PairX of a flow wave (role 0 / 1): its partner is the adjacent wave
+__device__ __forceinline__ PairX pair_of(float *buf, int *flags, int role, int slot) {
+  const int w = (threadIdx.x >> 6) & 15;
+  return PairX{(lds_float *)buf, (lds_vint *)(flags + w), (lds_vint *)(flags + (w ^ 1)), role, slot, 0};
+}
+
+constexpr int kSpinCap = 1 << 22;  // ~0.1 s of s_sleep: a safety exit, never reached in a correct run
+
+__device__ __forceinline__ float pair_swap(PairX &x, float v, int tile_len) {
+  const int k = ++x.k;
+  lds_float *b = x.buf + (k & 1) * 2 * tile_len;
+  b[x.role * tile_len + x.slot] = v;
+#ifndef NFDPF_EXP_NOWAIT
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the value lands before the counter
+  *x.mine = k;
+  for (int it = 0; __builtin_amdgcn_readfirstlane(*x.theirs) < k && it < kSpinCap; ++it)
+    __builtin_amdgcn_s_sleep(1);
+#endif
+  asm volatile("" ::: "memory");
+  return b[(1 - x.role) * tile_len + x.slot];
+}
+
+// One net (t or s) of a coupling half on input u; cb = this net's 4 folded bias pairs.
+__device__ __forceinline__ float net_split(cf2 *w, float u, const f2 *cb) {
+  constexpr int P = kH / 2;
+  f2 h[P];
+#pragma unroll
+  for (int m = 0; m < P; ++m) h[m] = tanh2(pfma(w[m], splat(u), cb[m]));
+  cf2 *w2 = w + P;
+  f2 g[P];
+#pragma unroll
+  for (int m = 0; m < P; ++m) {
+    f2 a = w2[P * kH + m];
+#pragma unroll
+    for (int k = 0; k < kH; ++k) a = pfma(w2[m * kH + k], splat((k & 1) ? h[k >> 1].y : h[k >> 1].x), a);
+    g[m] = tanh2(a);
+  }
+  cf2 *w3 = w2 + P * kH + P;
+  f2 a = w3[0] * g[0];
+#pragma unroll
+  for (int m = 1; m < P; ++m) a = pfma(w3[m], g[m], a);
+  return (a.x + a.y) + w3[P].x;
+}
+
+// RealNVP_cond flow, forward (nf/flows.py:215-226) / inverse (:228-239), split over a wave
+// pair.  fw = the flow's split block (kSplitFlow floats, wave-uniform), cbs = its folded
+// biases in split order (16 pairs).  Both waves end with identical lo, up and log-det.
+__device__ __forceinline__ float coupling_forward_split(const float *fw, float &lo, float &up, const f2 *cbs,
+                                                        PairX &x, int tile_len) {
+  const int r = x.role;
+  float v = net_split(wptr2(fw + r * kSplitNet), lo, cbs + r * 4);
+  float o = pair_swap(x, v, tile_len);
+  float t = r ? o : v, s = r ? v : o;
+  up = t + up * expf(s);
+  const float l1 = s;
+  v = net_split(wptr2(fw + (2 + r) * kSplitNet), up, cbs + (2 + r) * 4);
+  o = pair_swap(x, v, tile_len);
+  t = r ? o : v;
+  s = r ? v : o;
+  lo = t + lo * expf(s);
+  return l1 + s;
+}
+
+__device__ __forceinline__ float coupling_inverse_split(const float *fw, float &lo, float &up, const f2 *cbs,
+                                                        PairX &x, int tile_len) {
+  const int r = x.role;
+  float v = net_split(wptr2(fw + (2 + r) * kSplitNet), up, cbs + (2 + r) * 4);
+  float o = pair_swap(x, v, tile_len);
+  float t = r ? o : v, s = r ? v : o;
+  lo = (lo - t) * expf(-s);
+  const float l2 = -s;
+  v = net_split(wptr2(fw + r * kSplitNet), lo, cbs + r * 4);
+  o = pair_swap(x, v, tile_len);
+  t = r ? o : v;
+  s = r ? v : o;
+  up = (up - t) * expf(-s);
+  return -s + l2;
+}
+
+// ---- the filter stages on a wave pair (stages.hpp restated for the split nets) ----
+
+// nf_dyn inverse (model/models.py:305-332) of x_phys; role 0 writes scr x_dyn and hjac.
+__device__ __forceinline__ void stage_dyn_inverse_split(const nfdpf_filter_desc &d, const RowSlot &S, int i,
+                                                        float x0, float x1, const f2 *cbs, PairX &x, int tile_len,
+                                                        float &xd0, float &xd1) {
+  const float *base = d.dyn_params + split_suffix_offset(d.n_flows, kOctxDyn);
+  float lo = x0, up = x1, ld = 0.f;
+  for (int f = d.n_flows - 1; f >= 0; --f)
+    ld += coupling_inverse_split(base + f * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
+  if (x.role == 0) {
+    S.scr[4 * i] = lo;
+    S.scr[4 * i + 1] = up;
+    if (S.hjac) S.hjac[i] = -ld;
+  }
+  xd0 = lo;
+  xd1 = up;
+}
+
+// NF proposal inverse (model/models.py:334-356): returns jac_prop = -log_det.
+__device__ __forceinline__ float stage_propose_inverse_split(const nfdpf_filter_desc &d, const PropIn &in,
+                                                             const f2 *cbs, PairX &x, int tile_len, float &q0x,
+                                                             float &q1x) {
+  const float *base = d.cond_params + split_suffix_offset(d.n_flows, d.E + 4);
+  float lo = in.xd0, up = in.xd1, ld = 0.f;
+  for (int f = d.n_flows - 1; f >= 0; --f)
+    ld += coupling_inverse_split(base + f * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
+  q0x = lo;
+  q1x = up;
+  return -ld;
+}
+
+// nf_dyn forward of the proposal + densities (model/models.py:358-377) with --NF-dyn and
+// --NF-cond; role 0 writes hx = proposal, scr propose/prior and hprior.
+__device__ __forceinline__ void stage_prior_split(const nfdpf_filter_desc &d, const RowSlot &S, int i,
+                                                  const PropIn &in, const f2 *cbs, float q0x, float q1x,
+                                                  float jac_prop, PairX &x, int tile_len, float &propose,
+                                                  float &prior) {
+  const float K = d.dens_const;
+  const float two_var = 2.0f * (d.pos_noise * d.pos_noise);
+  const float de = density(in.e0, in.e1, K, two_var);
+  const float r0 = in.p0 - in.e0, r1 = in.p1 - in.e1;
+  const float *base = d.dyn_params + split_suffix_offset(d.n_flows, kOctxDyn);
+  float lo = q0x, up = q1x, ld2 = 0.f;
+  for (int f = 0; f < d.n_flows; ++f) ld2 += coupling_forward_split(base + f * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
+  prior = density(lo - r0, up - r1, K, two_var) - (-ld2);
+  propose = (de + in.jac) + jac_prop;
+  if (x.role == 0) {
+    S.hx[2 * i] = q0x;
+    S.hx[2 * i + 1] = q1x;
+    S.scr[4 * i + 2] = propose;
+    S.scr[4 * i + 3] = prior;
+    if (S.hprior) S.hprior[i] = prior;
+  }
+}
+
+}  // namespace nfdpf

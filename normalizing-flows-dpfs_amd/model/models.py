@@ -15,7 +15,7 @@ from nf.flows import FCNN, RealNVP, RealNVP_cond, MAF  # noqa: F401  (reference 
 from nf.models import NormalizingFlowModel, NormalizingFlowModel_cond
 from nfdpf import autograd as _ag
 from nfdpf import ops as _ops
-from nfdpf.pack import blob, flows_tensors, paired_mlp_tensors
+from nfdpf.pack import blob, encoder_tensors, flows_tensors, paired_mlp_tensors
 from utils import et_distance
 
 device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
@@ -139,7 +139,7 @@ class _MeasRunner:
 
     def hip(self, enc, x):
         m = self.model
-        pe = blob(m, "pe", m.particle_encoder, lambda: paired_mlp_tensors(m.particle_encoder), x.device)
+        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
         meas, nfl, pstd = None, 0, 2.5
         if self.kind == "CRNVP":
             meas = blob(m, "meas", m.CNF.flows, lambda: flows_tensors(m.CNF.flows), x.device)
@@ -250,7 +250,7 @@ class measurement_model_cglow(nn.Module):
         Forward only: gradients through CGLOW are SURVEY §8(f1) work."""
         from nfdpf.pack import cglow_tensors
         m = self
-        pe = blob(m, "pe", m.particle_encoder, lambda: paired_mlp_tensors(m.particle_encoder), update_particles.device)
+        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), update_particles.device)
         glow = blob(m, "glow", m.CGLOW, lambda: cglow_tensors(m.CGLOW), update_particles.device)
         lik = _ops.cglow_measurement(pe, glow, encodings.float(), update_particles.float())
         return lik - lik.max(dim=-1, keepdim=True)[0]

@@ -32,7 +32,7 @@ class FilterDesc(Structure):
         ("row_base", c_int64),
         ("nf_dyn", c_int32), ("nf_cond", c_int32), ("measurement", c_int32), ("resampler", c_int32),
         ("rng_mode", c_int32), ("force_resample", c_int32), ("n_flows", c_int32), ("hidden", c_int32),
-        ("defer_norm", c_int32),
+        ("defer_norm", c_int32), ("split_nets", c_int32),
         ("alpha", c_float), ("pos_noise", c_float), ("dens_const", c_float), ("meas_prior_std", c_float),
         ("seed", c_uint64),
         ("dyn_params", c_void_p), ("cond_params", c_void_p), ("pe_params", c_void_p), ("meas_params", c_void_p),

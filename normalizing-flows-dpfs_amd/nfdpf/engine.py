@@ -21,7 +21,8 @@ import torch.distributed as dist
 
 from . import _lib as L
 from . import ops
-from .pack import blob, cglow_tensors, flows_tensors, paired_mlp_tensors
+from .pack import (blob, cglow_tensors, encoder_tensors, filter_flow_tensors, flows_tensors,
+                   paired_mlp_tensors, splittable)
 
 
 @dataclass
@@ -48,6 +49,7 @@ class FilterConfig:
     seed: int = 2
     force_resample: bool = False
     kernel: str = "tiled"        # "tiled" (multi-CU pipeline per step) | "fused" (one launch per step)
+    split_nets: bool = True      # tiled: coupling nets on wave pairs (csrc/split.hpp) where the flows allow
 
 
 @dataclass
@@ -129,9 +131,11 @@ class FilterEngine:
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
         c, m = self.cfg, self.m
-        dyn = blob(m, "dyn", m.nf_dyn.flows, lambda: flows_tensors(m.nf_dyn.flows), dev) if c.NF_dyn else None
-        cond = blob(m, "cond", m.cond_model.flows, lambda: flows_tensors(m.cond_model.flows), dev) if c.NF_cond else None
-        pe = blob(m, "pe", m.particle_encoder, lambda: paired_mlp_tensors(m.particle_encoder), dev)
+        # the dynamic / proposal stacks carry the split suffix when every flow allows it
+        dyn = blob(m, "dyn", m.nf_dyn.flows, lambda: filter_flow_tensors(m.nf_dyn.flows), dev) if c.NF_dyn else None
+        cond = (blob(m, "cond", m.cond_model.flows, lambda: filter_flow_tensors(m.cond_model.flows), dev)
+                if c.NF_cond else None)
+        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), dev)
         meas = None
         if c.measurement == "CRNVP":
             meas = blob(m, "meas", m.cnf_measurement.flows, lambda: flows_tensors(m.cnf_measurement.flows), dev)
@@ -228,6 +232,8 @@ class FilterEngine:
         # tiled + soft: step t's weights are normalised inside step t+1 (one launch fewer per
         # step); not when the caller feeds p_prev itself (teacher forcing) or OT reads it first
         d.defer_norm = int(tiled and c.resampler == "soft" and teacher is None)
+        d.split_nets = int(tiled and c.split_nets and c.NF_dyn and splittable(self.m.nf_dyn.flows)
+                           and (not c.NF_cond or splittable(self.m.cond_model.flows)))
         d.alpha, d.pos_noise = c.alpha, c.pos_noise
         d.dens_const, d.meas_prior_std = density_const(c.pos_noise), c.meas_prior_std
         d.seed = int(c.seed) & (2 ** 64 - 1)

@@ -34,6 +34,21 @@ def row_pairs(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(o // 2, 2, i).transpose(1, 2)
 
 
+def col_pairs(w: torch.Tensor) -> torch.Tensor:
+    """nn.Linear weight [out, in] -> [in][out/2][2]: for each input, the weights of output
+    rows 2m and 2m+1 adjacent, all output pairs contiguous -- an input-major layer reads one
+    contiguous run per input (csrc/flows.hpp, particle encoder)."""
+    o, i = w.shape
+    return w.t().reshape(i, o // 2, 2)
+
+
+def encoder_tensors(seq: nn.Module):
+    """Particle encoder Linear(2,16) Linear(16,32) Linear(32,E) (model/models.py:130-150) in
+    the kernel layout: W1 row_pairs, W2 and W3 col_pairs, biases as they are."""
+    l1, l2, l3 = _linears(seq)
+    return [row_pairs(l1.weight), l1.bias, col_pairs(l2.weight), l2.bias, col_pairs(l3.weight), l3.bias]
+
+
 def coupling_pair_tensors(t_net: nn.Module, s_net: nn.Module, half: int):
     """Nets t and s of one coupling half, FCNN(half + O, half, H) each (nf/flows.py:101-114,
     183-190), interleaved t/s elementwise (csrc/flows.hpp ts_pair): core
@@ -67,7 +82,7 @@ def mlp_tensors(seq: nn.Module):
 
 
 def paired_mlp_tensors(seq: nn.Module):
-    """Particle encoder / likelihood_est MLPs (model/models.py:119-150): W in row_pairs
+    """likelihood_est MLP (model/models.py:119-128): W in row_pairs
     layout wherever the layer has an even number of outputs, biases as they are."""
     out = []
     for lin in _linears(seq):
@@ -117,6 +132,41 @@ def flows_tensors(flows):
         else:
             out += realnvp_tensors(f)
     return out
+
+
+def splittable(flows) -> bool:
+    """True when every flow is a RealNVP(_cond) on 2-D particles with hidden width 8: the
+    layout of the split suffix (csrc/split.hpp)."""
+    for f in flows:
+        if hasattr(f, "initial_param") or getattr(f, "dim", None) != 2:
+            return False
+        if _linears(f.t1.network)[1].weight.shape != (8, 8):
+            return False
+    return True
+
+
+def split_net_tensors(net: nn.Module):
+    """One coupling net FCNN(1 + O, 1, 8) in the split layout (csrc/split.hpp): W1[:, 0],
+    W2 and b2 with hidden units 2m, 2m+1 adjacent, W3 likewise, then {b3, 0} -- 90 floats."""
+    (w1, _), (w2, b2), (w3, b3) = [(m.weight, m.bias) for m in _linears(net.network)]
+    h = w2.shape[0]
+    return [row_pairs(w1[:, :1]), row_pairs(w2), b2.reshape(h // 2, 2), w3.reshape(h // 2, 2),
+            torch.cat([b3.reshape(1), b3.new_zeros(1)])]
+
+
+def split_flow_tensors(flows):
+    """The split suffix of a flow stack: per flow the nets t1, s1, t2, s2."""
+    out = []
+    for f in flows:
+        for net in (f.t1, f.s1, f.t2, f.s2):
+            out += split_net_tensors(net)
+    return out
+
+
+def filter_flow_tensors(flows):
+    """The filter's dynamic / proposal stack: the pair layout (flows_tensors), then the
+    split suffix when the stack allows it (include/nfdpf.h)."""
+    return flows_tensors(flows) + (split_flow_tensors(flows) if splittable(flows) else [])
 
 
 class BlobCache:

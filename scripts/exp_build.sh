@@ -1,0 +1,10 @@
+#!/bin/bash
+# Experiment builds of libnfdpf.so with -D flags (never shipped): exp/lib_<TAG>.so
+#   scripts/exp_build.sh TRACE -DNFDPF_EXP_TRACE
+set -e
+TAG=$1; shift
+cd "$(dirname "$0")/../normalizing-flows-dpfs_amd/csrc"
+mkdir -p ../../exp
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fvisibility=hidden --offload-arch=gfx950 -w "$@" -shared \
+  capi.hip flows.hip resample_soft.hip filter_step.hip filter_tiled.hip resample_ot.hip measure.hip misc.hip \
+  cglow.hip -o ../../exp/lib_${TAG}.so

@@ -13,6 +13,7 @@ import bench  # noqa: E402
 from nfdpf import _lib  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+SPLIT = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 flags, _, N, T, _, _ = bench.CONFIGS["c2"]
 torch.manual_seed(2)
 a = bench.make_args(flags, B, N, T, {})
@@ -21,22 +22,25 @@ from nfdpf.engine import FilterEngine, ShardInfo  # noqa: E402
 dev = torch.device("cuda", 0)
 dpf = DPF(a).to(dev).eval()
 start, state, vel, enc = (t.to(dev) for t in bench.synthetic_disk(B, T, 2, a.hiddensize))
-eng = FilterEngine(dpf.filter_config(), dpf)
+cfg = dpf.filter_config()
+cfg.split_nets = bool(SPLIT)
+eng = FilterEngine(cfg, dpf)
 for _ in range(3):
     eng.run(enc, start, vel, shard=ShardInfo.from_env(B))
 torch.cuda.synchronize()
 buf = np.zeros((4, 2048, 8), dtype=np.uint64)
 assert _lib.lib().nfdpf_exp_trace_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 nwg = B * ((N + 255) // 256)
-tr = buf[:, :nwg, :4].astype(np.int64)
+tr = buf[:, :nwg, :8].astype(np.int64)
 t0 = tr[:, :, 0][tr[:, :, 0] > 0].min()
 for k, name in enumerate(["motion", "dyn", "prop", "norm"]):
     x = (tr[k] - t0) / 100.0  # 100 MHz -> us
     st = x[:, 0]
     print(f"{name:7s} start min {st.min():7.2f} med {np.median(st):7.2f} max {st.max():7.2f} | end max "
           f"{x[:, 3].max():7.2f}", end="")
-    for p in range(1, 4):
-        if (tr[k][:, p] > 0).all():
-            dd = x[:, p] - x[:, p - 1]
-            print(f" | ph{p} med {np.median(dd):6.2f} max {dd.max():6.2f}", end="")
+    order = [0, 1, 4, 2, 3] if (tr[k][:, 4] > 0).all() else [0, 1, 2, 3]
+    for a, p in zip(order[:-1], order[1:]):
+        if (tr[k][:, p] > 0).all() and (tr[k][:, a] > 0).all():
+            dd = x[:, p] - x[:, a]
+            print(f" | {a}->{p} med {np.median(dd):6.2f} max {dd.max():6.2f}", end="")
     print()

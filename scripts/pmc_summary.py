@@ -5,6 +5,7 @@
 import csv
 import glob
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -12,7 +13,8 @@ acc = defaultdict(lambda: defaultdict(list))
 for d in sys.argv[1:]:
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            # base name only: template arguments hold commas, which would break the CSV
+            name = re.split(r"[<(]", r["Kernel_Name"].replace("void ", ""), maxsplit=1)[0].strip()
             acc[name][r["Counter_Name"]].append((r["Dispatch_Id"], float(r["Counter_Value"])))
 print("kernel,counter,dispatches,mean_per_dispatch")
 for k in sorted(acc):

@@ -46,6 +46,15 @@ def _maf_blob(w, n_flows, D):
     return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
 
 
+def _enc_blob(w, prefix="particle_encoder"):
+    """Particle encoder in the kernel layout (W1 row_pairs, W2 / W3 col_pairs)."""
+    from nfdpf.pack import col_pairs, row_pairs
+    W = [w[f"{prefix}.{layer}.weight"] for layer in (0, 2, 4)]
+    b = [w[f"{prefix}.{layer}.bias"] for layer in (0, 2, 4)]
+    parts = [row_pairs(W[0]), b[0], col_pairs(W[1]), b[1], col_pairs(W[2]), b[2]]
+    return torch.cat([p.reshape(-1) for p in parts]).to(DEV)
+
+
 def _mlp_blob(w, prefix):
     """Particle encoder / likelihood_est in the kernel layout: weights with an even number of
     outputs in row_pairs order, biases plain."""
@@ -193,7 +202,7 @@ def test_measurement_golden(meas):
     from nfdpf import ops
     fx = group(load("meas.npz"), meas)
     w = weights(fx)
-    pe = _mlp_blob(w, "particle_encoder")
+    pe = _enc_blob(w)
     mb = None
     if meas == "CRNVP":
         mb = _flow_blob({k[len("cnf_measurement."):]: v for k, v in w.items() if k.startswith("cnf_measurement.")}, 2)
@@ -230,7 +239,7 @@ def test_cglow_measurement_golden():
     from nfdpf.pack import cglow_tensors
     fx = group(load("meas.npz"), "CGLOW")
     w = weights(fx)
-    pe = _mlp_blob(w, "particle_encoder")
+    pe = _enc_blob(w)
     glow = torch.cat([a.detach().reshape(-1) for a in cglow_tensors(_glow_module(w))]).to(DEV)
     enc, x = t(fx["enc"]), t(fx["x"])
     raw = ops.cglow_measurement(pe, glow, enc.to(DEV), x.to(DEV))
@@ -481,6 +490,37 @@ def test_tiled_matches_fused(gated):
     a, b = out["fused"], out["tiled"]
     assert torch.equal(a.noise, b.noise)
     agree = (a.index == b.index).float().mean().item()
-    assert agree > 0.999, agree
+    # resampling every step: a marker within rounding of a CDF step flips one index and the
+    # row's later steps then follow different particles -- rounding-level differences
+    # compound (the teacher-forced one-step tests pin each step exactly)
+    assert agree > (0.999 if gated else 0.99), agree
     assert torch.allclose(a.particles[:, :2], b.particles[:, :2], rtol=1e-4, atol=1e-2)
+    assert torch.allclose(a.pred[:, :2], b.pred[:, :2], rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("gated", [True, False])
+def test_split_nets_match_pair_layout(gated):
+    """Coupling nets on wave pairs (csrc/split.hpp: t-nets and s-nets on partner waves, LDS
+    hand-off) against the one-wave pair layout: same device-RNG draws, only the order of the
+    output layer's sum differs."""
+    from nfdpf.engine import FilterConfig, FilterEngine
+    fx = load("e2e_c2.npz")
+    models = _Models(weights(fx), e2e_cfg(fx))
+    B, N, T = 6, 1000, 8
+    g = torch.Generator().manual_seed(18)
+    enc = torch.randn(B, T, 32, generator=g).to(DEV)
+    start = (torch.randn(B, 4, generator=g) * 10).to(DEV)
+    vel = (torch.randn(B, T, 2, generator=g) * 3).to(DEV)
+    out = {}
+    for split in (False, True):
+        cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft",
+                           force_resample=not gated, seed=31, kernel="tiled", split_nets=split)
+        out[split] = FilterEngine(cfg, models).run(enc, start, vel)
+    a, b = out[False], out[True]
+    assert torch.equal(a.noise, b.noise)
+    agree = (a.index == b.index).float().mean().item()
+    assert agree > (0.999 if gated else 0.99), agree  # see test_tiled_matches_fused
+    assert torch.allclose(a.particles[:, :2], b.particles[:, :2], rtol=1e-4, atol=1e-2)
+    assert torch.allclose(a.jac[:, :2], b.jac[:, :2], rtol=1e-4, atol=1e-4)
+    assert torch.allclose(a.prior[:, :2], b.prior[:, :2], rtol=1e-4, atol=1e-3)
     assert torch.allclose(a.pred[:, :2], b.pred[:, :2], rtol=1e-4, atol=1e-2)
