@@ -227,8 +227,14 @@ def main():
     for e in evs:
         e.close()
     kname = "filter_step_kernel"
-    if args.kernel == "tiled":  # the proposal launch: two roles (flow, measurement) with NF_cond
-        kname = "tiled_prop2_kernel" if flags["NF_cond"] else "tiled_prop_kernel"
+    if args.kernel == "tiled":  # the proposal launch (csrc/filter_tiled.hip launch_prop)
+        if fcfg.split_nets and flags["NF_dyn"] and flags["NF_cond"] and flags["measurement"] == "cos" \
+                and flags.get("NF_dyn_flow", "RealNVP") == "RealNVP":
+            kname = "tiled_prop_split_kernel"  # coupling nets on wave pairs
+        elif flags["NF_cond"] and flags["measurement"] != "CGLOW":
+            kname = "tiled_prop2_kernel"       # two roles: flow chain, measurement
+        else:
+            kname = "tiled_prop_kernel"
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
     traffic, traffic_src = pmc_traffic(args.config, kname)
