@@ -125,6 +125,11 @@ NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, fl
  *         once with NULL, taking the MIN of iters_out over ranks (the first row to converge
  *         anywhere), and running again with stop_at = that minimum.                      */
 
+/* Diagnostics of the last nfdpf_ot_resample on `workspace` (synchronous device read):
+ *   host_out[0] = iterations in the iters_out encoding (-1: ran to max_iter), host_out[1] =
+ *   softmin evaluations that left the shifted fast path and were recomputed exactly. */
+NFDPF_API int nfdpf_ot_stats(const void *workspace, int32_t *host_out);
+
 /* ESS gate of DPFs.py:163-165: gate = mean_b(inv_ess[b]) < 0.5 N (or force) -> int32 [1] */
 NFDPF_API int nfdpf_ess_gate(const float *inv_ess, int B, int N, int force, int32_t *gate,
                    void *stream);

@@ -6,80 +6,457 @@
 // transport matrix (:194-210) and multiply it with the particles (:254-264).
 //
 // What runs here:
-//   * costs are recomputed on the fly from the 2-D points (||x_i - x_j||^2 / 2), never stored;
 //   * only the two potentials that reach the output (a_y, b_x) are iterated: a_x / b_y are
 //     computed by the reference but read by nothing (:139-147, :177-178);
-//   * every softmin is a streamed log-sum-exp over j tiles staged in LDS, in base 2
-//     (v_exp_f32 is 2^x), with a tile-wise running max;
+//   * costs are recomputed on the fly from the 2-D points, never stored;
+//   * potentials, exponents and shifts are fp64 per particle (the reference iterates in fp64;
+//     at eps = 0.1 a potential of 100 is an exponent of 1400, whose fp32 ulp would already be a
+//     1e-4 relative error of a transport weight); the O(N^2) pair work is fp32 on exponents
+//     that are small by construction:
+//   * every softmin is a log-sum-exp with a PER-LANE shift m_i predicted from the potentials
+//     (no running max per pair).  In base 2, with h_j the softmin's exponent, c_ij = C_ij / e
+//     and the row cut into slices s of 256 j with maxima M_s,
+//       LSE_j(h_j - c_ij) = m_i + log2 sum_s sum_{j in s} 2^((h_j - M_s) + (M_s - m_i) - c_ij),
+//     h_j - M_s <= 0 stored per j (fp32), M_s - m_i formed in fp64 once per slice and lane.
+//     m_i = -a_i / (e ln 2) is the lane's current potential (the fixed point of the iteration),
+//     so the sum stays near 1; a lane whose sum leaves [2^-60, 2^60] recomputes its softmin
+//     exactly with a streamed max-shifted LSE (a diagnostic counter records how often);
+//   * the two softmins of an iteration share c_ij, so a slice is summed as
+//       2^(M_s - m_i) sum_j alpha_j 2^(-c_ij),   alpha_j = 2^(h_j - M_s)   (stored per j),
+//     ONE v_exp_f32 per pair for both softmins -- unless, for some lane of the wave,
+//     M_s - m_i > 60 (a heavy particle of the slice far from i: the near terms would underflow
+//     in alpha_j K_ij before the factor lifts them); the wave then takes the two-exp form;
+//   * the per-j operands form a per-row TABLE of planes written by the launch that produced
+//     them (workgroup s writes j in [256 s, 256 s + 256) and its slice maximum: no
+//     cross-workgroup hand-off inside a launch);
+//   * a workgroup owns 256 i; its 4 waves split the row's slices and every lane carries 4 of
+//     the 256 i, so each table word a wave loads (a wave-uniform vector load, software-
+//     pipelined one block of 8 j ahead) serves 4 pairs per lane; partial sums meet in LDS in
+//     wave order (deterministic);
 //   * the transport matrix is never formed: column log-normalisers r_j first, then
-//     x'_i = sum_j 2^(...) x_j;
+//     x'_i = sum_j T_ij x_j with T_ij = 2^(f_i/e + r_j - c_ij) summed directly;
 //   * the loop keeps the reference's batch-coupled stop rule -- it ends at the first
 //     iteration after which ANY row has converged (torch.all(continue_), :126-129) -- with
 //     one launch per iteration that first reads the previous iteration's per-row residuals
-//     (identical decision in every workgroup, no host sync, no atomics);
-//   * rows are split over `splits` workgroups along i so that a small batch still fills
-//     the 256 CUs.
-// Precision: Real = float (default) or double (parity mode, --ot-fp64).
+//     (identical decision in every workgroup, no atomics).
 #include "common.hpp"
 
 namespace nfdpf {
 
-constexpr int kOtThreads = 256;  // i per workgroup
-constexpr int kOtTile = 512;     // j per LDS tile
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
+constexpr int kOtThreads = 256;  // i (or j) per workgroup = the table slice length
+constexpr double kLog2ed = 1.4426950408889634;
+constexpr double kLn2d = 0.6931471805599453;
+constexpr float kLo = 0x1.0p-60f, kHi = 0x1.0p60f;  // outside: the lane recomputes exactly
+constexpr float kRisky = 60.f;                      // M_s - m_i above: two-exp form
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 sp2(float v) { return f2{v, v}; }
+__device__ __forceinline__ f2 pfma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 struct OtState {
-  int32_t stopped;  // set by the iteration that observes a converged row
-  int32_t K;        // total_iter of the reference
+  int32_t stopped;    // set by the iteration that observes a converged row
+  int32_t K;          // total_iter of the reference
+  int32_t fallbacks;  // softmins recomputed exactly (diagnostic, nfdpf_ot_stats)
 };
 
+// A table of one row: P planes of Np = splits * 256 floats, plane-major, plus the slice maxima
+// (fp64, [splits][NM]).  Exponent planes hold h_j - M_s (fp32, <= 0; -inf on the padding).
 struct OtWs {  // carve of the caller's workspace
   OtState *st;
-  float *xs;     // [B,N,2] centred / scaled particles
+  float *xs;     // [B,N,2] centred / scaled particles x~
   float *logw;   // [B,N]
-  double *rowc;  // [B,4]: eps0, logu, unused, unused
-  float *pot;    // [2 buffers][2 (a_y,b_x)][B,N]
-  float *res;    // [2 parity][B][splits] max |delta| of the iteration
-  float *fg;     // [2][B,N] final potentials f (=a_y), g (=b_x)
-  float *r;      // [B,N] column terms r_j
+  double *rowc;  // [B,4]: eps0, logu, max logw, unused
+  double *pot;   // [2 buffers][2 (a_y,b_x)][B,N]
+  double *res;   // [2 parity][B][splits] max |delta| of the iteration
+  double *fg;    // [B,N] final potential f (= a_y after the post-loop softmin)
+  float *tabI;   // [2][B][6][Np] X, Y, h_a - M, h_b - M, alpha, beta (iteration consuming a state)
+  double *mI;    // [2][B][splits][2]
+  float *tabF;   // [B][4][Np] X, Y, h_a - M, h_b - M at the final epsilon (rows still annealing)
+  double *mF;    // [B][splits][2]
+  float *tabC;   // [B][3][Np] column pass: X, Y, f_i / eps - M
+  double *mC;    // [B][splits]
+  float *tabA;   // [B][5][Np] apply pass: X, Y, r_j - M, x_j, y_j (x = the input particles)
+  double *mA;    // [B][splits]
 };
 
 static inline int64_t align256(int64_t v) { return (v + 255) / 256 * 256; }
 
-static inline int ot_splits(int B, int N) {
-  // enough workgroups to cover the chip, at most one per 256 i
-  int s = (N + kOtThreads - 1) / kOtThreads;
-  return s < 1 ? 1 : s;
-}
+static inline int ot_splits(int N) { return (N + kOtThreads - 1) / kOtThreads; }
 
-static OtWs carve(void *ws, int B, int N, int splits) {
-  char *p = (char *)ws;
+struct Carver {
+  char *p;
+  int64_t used = 0;
+  template <class T>
+  T *take(int64_t n) {
+    T *r = (T *)(p ? p + used : nullptr);
+    used += align256(n * (int64_t)sizeof(T));
+    return r;
+  }
+};
+
+static OtWs carve(void *ws, int B, int N, int64_t *bytes = nullptr) {
+  const int S = ot_splits(N);
+  const int64_t Np = (int64_t)S * kOtThreads;
+  Carver c{(char *)ws};
   OtWs w;
-  w.st = (OtState *)p;
-  p += 256;
-  w.xs = (float *)p;
-  p += align256((int64_t)B * N * 2 * 4);
-  w.logw = (float *)p;
-  p += align256((int64_t)B * N * 4);
-  w.rowc = (double *)p;
-  p += align256((int64_t)B * 4 * 8);
-  w.pot = (float *)p;
-  p += align256((int64_t)4 * B * N * 4);
-  w.res = (float *)p;
-  p += align256((int64_t)2 * B * splits * 4);
-  w.fg = (float *)p;
-  p += align256((int64_t)2 * B * N * 4);
-  w.r = (float *)p;
+  w.st = c.take<OtState>(1);
+  w.xs = c.take<float>((int64_t)B * N * 2);
+  w.logw = c.take<float>((int64_t)B * N);
+  w.rowc = c.take<double>((int64_t)B * 4);
+  w.pot = c.take<double>((int64_t)4 * B * N);
+  w.res = c.take<double>((int64_t)2 * B * S);
+  w.fg = c.take<double>((int64_t)B * N);
+  // + a padding block: the pair loop prefetches 8 floats past the last plane of the last row
+  w.tabI = c.take<float>(2 * B * 6 * Np + 64);
+  w.mI = c.take<double>((int64_t)2 * B * S * 2);
+  w.tabF = c.take<float>(B * 4 * Np + 64);
+  w.mF = c.take<double>((int64_t)B * S * 2);
+  w.tabC = c.take<float>(B * 3 * Np + 64);
+  w.mC = c.take<double>((int64_t)B * S);
+  w.tabA = c.take<float>(B * 5 * Np + 64);
+  w.mA = c.take<double>((int64_t)B * S);
+  if (bytes) *bytes = c.used;
   return w;
 }
 
 static int64_t ws_bytes(int B, int N) {
-  const int s = ot_splits(B, N);
-  return 256 + align256((int64_t)B * N * 8) + align256((int64_t)B * N * 4) +
-         align256((int64_t)B * 32) + align256((int64_t)16 * B * N) +
-         align256((int64_t)8 * B * s) + align256((int64_t)8 * B * N) +
-         align256((int64_t)4 * B * N);
+  int64_t n = 0;
+  carve(nullptr, B, N, &n);
+  return n;
+}
+
+struct OtParams {
+  int B, N, splits, max_iter;
+  double eps, sf, thr;
+  const int32_t *gate;     // optional: skip everything when *gate == 0
+  const int32_t *stop_at;  // optional: total_iter + 2 to run (sharded batches), else the rule
+};
+
+__device__ __forceinline__ bool ot_off(const OtParams &P) { return P.gate && *P.gate == 0; }
+
+__device__ __forceinline__ int64_t np_of(const OtParams &P) { return (int64_t)P.splits * kOtThreads; }
+
+__device__ __forceinline__ double *pot_ptr(const OtWs &ws, const OtParams &P, int buf, int which, int b) {
+  return ws.pot + (((int64_t)buf * 2 + which) * P.B + b) * P.N;
+}
+__device__ __forceinline__ float *tabI_row(const OtWs &ws, const OtParams &P, int buf, int b) {
+  return ws.tabI + ((int64_t)buf * P.B + b) * 6 * np_of(P);
+}
+__device__ __forceinline__ double *mI_row(const OtWs &ws, const OtParams &P, int buf, int b) {
+  return ws.mI + ((int64_t)buf * P.B + b) * P.splits * 2;
+}
+
+// running epsilon at iteration k: eps_{k+1} = max(eps_k * s^2, eps) in double (:158)
+__device__ __forceinline__ double run_eps(double eps0, int k, double sf, double eps) {
+  double e = eps0;
+  for (int t = 0; t < k; ++t) e = fmax(e * sf, eps);
+  return e;
+}
+
+// sc with sc |dx|^2 = |dx|^2 / (2 e) * log2(e): C_ij / e in base 2
+__device__ __forceinline__ float cost_scale(double inv_e) { return (float)(0.5 * inv_e * kLog2ed); }
+
+// ------------------------------------------------------------------------------------------
+// Pair loops.  A workgroup owns 256 i (i = 256 s0 + t); its 4 waves split the row's slices
+// (wave w takes slices w, w + 4, ...) and every lane carries kR = 4 of the workgroup's i
+// (lane + 64 r), so each table word a wave loads serves 4 pairs per lane.  (The table words
+// are wave-uniform; a vector load returns them to every lane, and at one i per lane the L1
+// return path, not the VALU, bounds the loop.)  Partial sums meet in LDS in wave order.
+// ------------------------------------------------------------------------------------------
+constexpr int kR = 4;
+constexpr int kWaves = kOtThreads / 64;
+constexpr int kLdsPart = kWaves * 3 * kOtThreads;  // floats: wave partials of <= 3 sums per i
+
+template <int NP>
+struct TBlock {  // 8 consecutive j of NP planes
+  float4 v[NP][2];
+};
+
+// load block j of the planes pl[0..NP) of a row table
+template <int NP>
+__device__ __forceinline__ void tload(TBlock<NP> &B, const float *tab, int64_t Np, int j, const int (&pl)[NP]) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const float4 *X = reinterpret_cast<const float4 *>(tab + pl[p] * Np + j);
+    B.v[p][0] = X[0];
+    B.v[p][1] = X[1];
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ f2 tpair(const TBlock<NP> &B, int p, int q) {
+  const float4 &c = B.v[p][q >> 1];
+  return (q & 1) ? f2{c.z, c.w} : f2{c.x, c.y};
+}
+
+// Software pipeline over blocks of 8 j in [j0, j1) (a multiple of 16) with vector loads of the
+// wave-uniform table words (vmcnt is in order, so a wait covers exactly the block about to be
+// used -- scalar loads return out of order and every wait on them is lgkmcnt(0)).  Two named
+// buffers; the scheduling barriers keep each block's loads one compute block ahead of their
+// use.  Past the end a prefetch reads the next plane / the allocation's padding block and is
+// discarded.
+template <int NP, class Body>
+__device__ __forceinline__ void pipelined(const float *tab, int64_t Np, int j0, int j1, const int (&pl)[NP],
+                                          const Body &body) {
+  TBlock<NP> A, Bk;
+  tload(A, tab, Np, j0, pl);
+  for (int j = j0; j < j1; j += 16) {
+    tload(Bk, tab, Np, j + 8, pl);
+    __builtin_amdgcn_sched_barrier(0);
+    body(A);
+    __builtin_amdgcn_sched_barrier(0);
+    tload(A, tab, Np, j + 16, pl);
+    __builtin_amdgcn_sched_barrier(0);
+    body(Bk);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+struct LaneI {  // the kR points of a lane, as packed splats
+  f2 x[kR], y[kR];
+};
+
+// Shifted-exponent block (planes X, Y, E_0..E_{NH-1}, V_0..V_{NV-1}; E = h - M_s):
+//   acc[r][w] += 2^(E_w[j] + o[r][w] - sc |p_i - p_j|^2),  accv[r][v] += (w = 0 term) V_v[j]
+template <int NH, int NV, int NP>
+__device__ __forceinline__ void hblock(const TBlock<NP> &B, const LaneI &L, f2 nsc2, const f2 (&o)[kR][NH],
+                                       f2 (&acc)[kR][NH], f2 (&accv)[kR][NV > 0 ? NV : 1]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const f2 dx = L.x[r] - tpair(B, 0, q);
+      const f2 dy = L.y[r] - tpair(B, 1, q);
+      const f2 d2 = pfma2(dy, dy, dx * dx);
+#pragma unroll
+      for (int w = 0; w < NH; ++w) {
+        const f2 a = pfma2(nsc2, d2, tpair(B, 2 + w, q) + o[r][w]);
+        const f2 t = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+        acc[r][w] += t;
+        if (w == 0)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) accv[r][v] = pfma2(tpair(B, 2 + NH + v, q), t, accv[r][v]);
+      }
+    }
+  }
+}
+
+// Shared-kernel block of the two iteration softmins (planes X, Y, alpha, beta): one
+// v_exp_f32 per pair, K = 2^(-sc |p_i - p_j|^2);  acc[r][0] += alpha_j K,  acc[r][1] += beta_j K
+__device__ __forceinline__ void kblock(const TBlock<4> &B, const LaneI &L, f2 nsc2, f2 (&acc)[kR][2]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const f2 dx = L.x[r] - tpair(B, 0, q);
+      const f2 dy = L.y[r] - tpair(B, 1, q);
+      const f2 a = pfma2(dy, dy, dx * dx) * nsc2;
+      const f2 k = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+      acc[r][0] = pfma2(tpair(B, 2, q), k, acc[r][0]);
+      acc[r][1] = pfma2(tpair(B, 3, q), k, acc[r][1]);
+    }
+  }
+}
+
+__device__ __forceinline__ float hsum2(f2 a) { return a.x + a.y; }
+
+// slice offset M_s - m_i in fp32 (-inf: the slice carries no weight)
+__device__ __forceinline__ float slice_off(double Ms, double m) {
+  return Ms > -INFINITY ? (float)(Ms - m) : -INFINITY;
+}
+
+// The lane's kR points and shifts: pt(i, x, y, m[NH]) for i = 256 s0 + lane + 64 r (i < N).
+template <int NH, class Pt>
+__device__ __forceinline__ void lane_points(int N, const Pt &pt, LaneI &L, double (&m)[kR][NH]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int i = blockIdx.x * kOtThreads + lane + 64 * r;
+    float x = 0.f, y = 0.f;
+    double mm[NH];
+#pragma unroll
+    for (int w = 0; w < NH; ++w) mm[w] = 0.0;
+    if (i < N) pt(i, x, y, mm);
+    L.x[r] = sp2(x);
+    L.y[r] = sp2(y);
+#pragma unroll
+    for (int w = 0; w < NH; ++w) m[r][w] = mm[w];
+  }
+}
+
+// Combine the waves' partials through LDS: thread t gets out[k] for its i (wave order).
+template <int NK>
+__device__ __forceinline__ void combine(float *lds, const float (&mine)[kR][NK], float (&out)[NK]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < kR; ++r)
+#pragma unroll
+    for (int k = 0; k < NK; ++k) lds[(w * NK + k) * kOtThreads + lane + 64 * r] = mine[r][k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    float a = lds[k * kOtThreads + threadIdx.x];
+    for (int u = 1; u < kWaves; ++u) a += lds[(u * NK + k) * kOtThreads + threadIdx.x];
+    out[k] = a;
+  }
+}
+
+// Workgroup sums over the whole row with the shifted-exponent block (table planes 0, 1,
+// 2 .. 2+NH+NV, slice maxima msh[s * MS + w]): thread t gets, for i = 256 s0 + t,
+//   S[w] = sum_j 2^(h_w[j] - sc |p_i - p_j|^2 - m_i[w]),  SV[v] = sum_j (w = 0 term) V_v[j].
+template <int NH, int NV, int MS, class Pt>
+__device__ __forceinline__ void wg_table_sums(const float *tab, const double *msh, int splits, int64_t Np, int N,
+                                              float sc, const Pt &pt, float *lds, float (&S)[NH], float *SV) {
+  constexpr int NP = 2 + NH + NV;
+  int pl[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) pl[p] = p;
+  LaneI L;
+  double m[kR][NH];
+  lane_points<NH>(N, pt, L, m);
+  const f2 nsc2 = sp2(-sc);
+  f2 acc[kR][NH], accv[kR][NV > 0 ? NV : 1];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+#pragma unroll
+    for (int w = 0; w < NH; ++w) acc[r][w] = sp2(0.f);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) accv[r][v] = sp2(0.f);
+  }
+  for (int s = threadIdx.x >> 6; s < splits; s += kWaves) {
+    f2 o[kR][NH];
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+#pragma unroll
+      for (int w = 0; w < NH; ++w) o[r][w] = sp2(slice_off(msh[s * MS + w], m[r][w]));
+    pipelined<NP>(tab, Np, s * kOtThreads, (s + 1) * kOtThreads, pl,
+                  [&](const TBlock<NP> &B) { hblock<NH, NV>(B, L, nsc2, o, acc, accv); });
+  }
+  float mine[kR][NH + NV], out[NH + NV];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+#pragma unroll
+    for (int w = 0; w < NH; ++w) mine[r][w] = hsum2(acc[r][w]);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) mine[r][NH + v] = hsum2(accv[r][v]);
+  }
+  combine<NH + NV>(lds, mine, out);
+#pragma unroll
+  for (int w = 0; w < NH; ++w) S[w] = out[w];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) SV[v] = out[NH + v];
+}
+
+// The two softmins of an iteration over an iteration table (planes X, Y, h_a - M, h_b - M,
+// alpha, beta; maxima msh[2 s], msh[2 s + 1]): one exp per pair for both unless some lane of
+// the wave is "risky" for the slice (see the file header).
+template <class Pt>
+__device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh, int splits, int64_t Np, int N,
+                                             float sc, const Pt &pt, float *lds, float (&S)[2]) {
+  const int plk[4] = {0, 1, 4, 5}, plh[4] = {0, 1, 2, 3};
+  LaneI L;
+  double m[kR][2];
+  lane_points<2>(N, pt, L, m);
+  const f2 nsc2 = sp2(-sc);
+  float Sk[kR][2];
+  f2 hacc[kR][2];
+  f2 none[kR][1];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    Sk[r][0] = Sk[r][1] = 0.f;
+    hacc[r][0] = hacc[r][1] = sp2(0.f);
+  }
+  for (int s = threadIdx.x >> 6; s < splits; s += kWaves) {
+    const double Ma = msh[2 * s], Mb = msh[2 * s + 1];
+    float oa[kR], ob[kR];
+    bool risky = false;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      oa[r] = slice_off(Ma, m[r][0]);
+      ob[r] = slice_off(Mb, m[r][1]);
+      risky |= (oa[r] > kRisky) || (ob[r] > kRisky);
+    }
+    const int j0 = s * kOtThreads, j1 = j0 + kOtThreads;
+    if (__builtin_amdgcn_ballot_w64(risky) == 0) {
+      f2 acc[kR][2];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) acc[r][0] = acc[r][1] = sp2(0.f);
+      pipelined<4>(tab, Np, j0, j1, plk, [&](const TBlock<4> &B) { kblock(B, L, nsc2, acc); });
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        Sk[r][0] = fmaf(exp2f(oa[r]), hsum2(acc[r][0]), Sk[r][0]);
+        Sk[r][1] = fmaf(exp2f(ob[r]), hsum2(acc[r][1]), Sk[r][1]);
+      }
+    } else {
+      f2 o[kR][2];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        o[r][0] = sp2(oa[r]);
+        o[r][1] = sp2(ob[r]);
+      }
+      pipelined<4>(tab, Np, j0, j1, plh, [&](const TBlock<4> &B) { hblock<2, 0>(B, L, nsc2, o, hacc, none); });
+    }
+  }
+  float mine[kR][2], out[2];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    mine[r][0] = Sk[r][0] + hsum2(hacc[r][0]);
+    mine[r][1] = Sk[r][1] + hsum2(hacc[r][1]);
+  }
+  combine<2>(lds, mine, out);
+  S[0] = out[0];
+  S[1] = out[1];
+}
+
+__device__ __forceinline__ bool sum_ok(float s) { return s >= kLo && s <= kHi; }
+
+// exact base-2 LSE_j(h(j) - sc * |x_i - x_j|^2) over the row (h in fp64, streamed max shift,
+// global reads) -- the fallback of a lane whose shifted sum left the safe range
+template <class H>
+__device__ double lse2_exact(const float *xs, int N, float xi, float yi, float sc, const H &h) {
+  double m = -INFINITY, s = 0.0;
+  for (int j = 0; j < N; ++j) {
+    const float dx = xi - xs[2 * j], dy = yi - xs[2 * j + 1];
+    const double v = h(j) - (double)(fmaf(dx, dx, dy * dy) * sc);
+    if (v > m) {
+      s = s * exp2(m - v) + 1.0;
+      m = v;
+    } else {
+      s += exp2(v - m);
+    }
+  }
+  return m + log2(s);
+}
+
+// base-2 LSE from a shifted sum, or exactly when the sum left the safe range
+template <class H>
+__device__ __forceinline__ double lse2_from(float S, double m, const float *xs, int N, float xi, float yi, float sc,
+                                            const H &h, int32_t *fallbacks) {
+  if (sum_ok(S)) return m + log2((double)S);
+  atomicAdd(fallbacks, 1);
+  return lse2_exact(xs, N, xi, yi, sc, h);
+}
+
+// Thread's column of a table (j = 256 blockIdx.x + threadIdx.x): planes X, Y, then NE exponent
+// planes stored as h - M_s (slice maxima to msh[blockIdx.x * NE + e]), then NV value planes.
+// With ALPHA, planes 2 + NE + e hold 2^(h_e - M_s) (the iteration table's alpha / beta).
+template <int NE, int NV, bool ALPHA>
+__device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, bool valid, float X, float Y,
+                                          const double (&h)[NE], const float *vals, double *shd) {
+  const int64_t j = (int64_t)blockIdx.x * kOtThreads + threadIdx.x;
+  tab[j] = valid ? X : 0.f;
+  tab[Np + j] = valid ? Y : 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const double he = valid ? h[e] : -INFINITY;
+    const double M = block_max(he, shd);
+    const float E = (he > -INFINITY) ? (float)(he - M) : -INFINITY;
+    tab[(2 + e) * Np + j] = E;
+    if (ALPHA) tab[(2 + NE + e) * Np + j] = E > -INFINITY ? __builtin_amdgcn_exp2f(E) : 0.f;
+    if (threadIdx.x == 0) msh[blockIdx.x * NE + e] = M;
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) tab[(2 + NE + (ALPHA ? NE : 0) + v) * Np + j] = valid ? vals[v] : 0.f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -114,7 +491,7 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
   const float dm = fmaxf(d0, d1);
   const double diam = dm == 0.0f ? 1.0 : (double)dm;
   const double scale = diam * (double)sqrtf(2.0f);
-  float mx = -INFINITY, mn = INFINITY;
+  float mx = -INFINITY, mn = INFINITY, lwmax = -INFINITY;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     const float a = (float)((double)(xr[2 * i] - m0) / scale);
     const float c = (float)((double)(xr[2 * i + 1] - m1) / scale);
@@ -122,125 +499,105 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
     ws.xs[((int64_t)b * N + i) * 2 + 1] = c;
     mx = fmaxf(mx, fmaxf(a, c));
     mn = fminf(mn, fminf(a, c));
-    ws.logw[(int64_t)b * N + i] = logf(w[(int64_t)b * N + i]);
+    const float lw = logf(w[(int64_t)b * N + i]);
+    ws.logw[(int64_t)b * N + i] = lw;
+    lwmax = fmaxf(lwmax, lw);
   }
   mx = block_max(mx, shf);
   mn = -block_max(-mn, shf);
+  lwmax = block_max(lwmax, shf);
   if (threadIdx.x == 0) {
     const double mm = (double)mx - (double)mn;
     ws.rowc[b * 4 + 0] = mm * mm;                        // epsilon_0 = diameter^2 (:117)
     ws.rowc[b * 4 + 1] = -(double)logf((float)N);       // uniform log weight (:214-215)
+    ws.rowc[b * 4 + 2] = (double)lwmax;                 // shift of the first a-softmin
     if (b == 0) {
       ws.st->stopped = 0;
       ws.st->K = 0;
+      ws.st->fallbacks = 0;
     }
   }
 }
 
-// running epsilon at iteration k: eps_{k+1} = max(eps_k * s^2, eps) in double (:158)
-__device__ __forceinline__ double run_eps(double eps0, int k, double sf, double eps) {
-  double e = eps0;
-  for (int t = 0; t < k; ++t) e = fmax(e * sf, eps);
-  return e;
+// table of the initial softmins at eps0 (:120-121): h_a = logw, h_b = logu (base 2)
+__global__ __launch_bounds__(kOtThreads) void ot_prep_kernel(OtParams P, OtWs ws) {
+  if (ot_off(P)) return;
+  __shared__ double shd[16];
+  const int b = blockIdx.y, N = P.N, i = blockIdx.x * kOtThreads + threadIdx.x;
+  const bool v = i < N;
+  const float *xs = ws.xs + (int64_t)b * N * 2;
+  const double h[2] = {v ? (double)ws.logw[(int64_t)b * N + i] * kLog2ed : 0.0, ws.rowc[b * 4 + 1] * kLog2ed};
+  write_col<2, 0, true>(tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), np_of(P), v, v ? xs[2 * i] : 0.f,
+                        v ? xs[2 * i + 1] : 0.f, h, nullptr, shd);
 }
 
-// Two softmins of one i against all j of the row (base-2 streamed LSE):
-//   A_i = -e * LSE_j(ha_j - C_ij/e),  B_i = -e * LSE_j(hb_j - C_ij/e),  C_ij = |x_i-x_j|^2/2
-// ha/hb are produced tile by tile by `fill(j, &ha, &hb)`.
-template <class Fill>
-__device__ void softmin_pair(const float *xs, int N, int i, bool active, float inv_e, float e,
-                             const Fill &fill, float *tx, float *ty, float *tha, float *thb,
-                             float &A, float &Bv) {
-  const float xi = active ? xs[2 * i] : 0.f, yi = active ? xs[2 * i + 1] : 0.f;
-  const float c2 = 0.5f * inv_e * kLog2e;  // C_ij / e in base 2
-  float ma = -INFINITY, sa = 0.f, mb = -INFINITY, sb = 0.f;
-  for (int j0 = 0; j0 < N; j0 += kOtTile) {
-    const int nt = min(kOtTile, N - j0);
-    __syncthreads();
-    for (int j = threadIdx.x; j < nt; j += blockDim.x) {
-      float ha, hb;
-      fill(j0 + j, ha, hb);
-      tx[j] = xs[2 * (j0 + j)];
-      ty[j] = xs[2 * (j0 + j) + 1];
-      tha[j] = ha * kLog2e;
-      thb[j] = hb * kLog2e;
-    }
-    __syncthreads();
-    if (active) {
-      for (int j = 0; j < nt; j += 16) {
-        const int jn = min(16, nt - j);
-        float va[16], vb[16];
-        float la = -INFINITY, lb = -INFINITY;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          if (q < jn) {
-            const float dx = xi - tx[j + q], dy = yi - ty[j + q];
-            const float c = fmaf(dx, dx, dy * dy) * c2;
-            va[q] = tha[j + q] - c;
-            vb[q] = thb[j + q] - c;
-          } else {
-            va[q] = -INFINITY;
-            vb[q] = -INFINITY;
-          }
-          la = fmaxf(la, va[q]);
-          lb = fmaxf(lb, vb[q]);
-        }
-        if (la > ma) {
-          sa = sa * exp2f(ma - la);
-          ma = la;
-        }
-        if (lb > mb) {
-          sb = sb * exp2f(mb - lb);
-          mb = lb;
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          sa += exp2f(va[q] - ma);
-          sb += exp2f(vb[q] - mb);
-        }
-      }
-    }
+// Table columns of state `ks` (the potentials a_y, b_x of thread i just produced): for the
+// iteration that consumes it (epsilon e_ks) and, for a row whose epsilon is still annealing,
+// at the final epsilon (the post-loop softmin :173-176, should the batch stop right here).
+__device__ __forceinline__ void emit_state_tables(const OtParams &P, const OtWs &ws, int b, int ks, bool v,
+                                                  float xi, float yi, float lw, double logu, double ay,
+                                                  double bx, double *shd) {
+  const int64_t Np = np_of(P);
+  const double e = run_eps(ws.rowc[b * 4], ks, P.sf, P.eps);
+  {
+    const double inv = 1.0 / e;
+    const double h[2] = {((double)lw + bx * inv) * kLog2ed, (logu + ay * inv) * kLog2ed};
+    write_col<2, 0, true>(tabI_row(ws, P, ks & 1, b), mI_row(ws, P, ks & 1, b), Np, v, xi, yi, h, nullptr, shd);
   }
-  A = -e * (ma + log2f(sa)) * kLn2;
-  Bv = -e * (mb + log2f(sb)) * kLn2;
+  if (e != P.eps) {
+    const double inv = 1.0 / P.eps;
+    const double h[2] = {((double)lw + bx * inv) * kLog2ed, (logu + ay * inv) * kLog2ed};
+    write_col<2, 0, false>(ws.tabF + (int64_t)b * 4 * Np, ws.mF + (int64_t)b * P.splits * 2, Np, v, xi, yi, h,
+                           nullptr, shd);
+  }
 }
 
-struct OtParams {
-  int B, N, splits, max_iter;
-  double eps, sf, thr;
-  const int32_t *gate;     // optional: skip everything when *gate == 0
-  const int32_t *stop_at;  // optional: total_iter + 2 to run (sharded batches), else the rule
-};
-
-__device__ __forceinline__ bool ot_off(const OtParams &P) { return P.gate && *P.gate == 0; }
-
-__device__ __forceinline__ float *pot_ptr(const OtWs &ws, const OtParams &P, int buf, int which,
-                                          int b) {
-  return ws.pot + (((int64_t)buf * 2 + which) * P.B + b) * P.N;
+// the two softmins of an iteration for thread t's i (shifts ma / mb, base 2), from the
+// workgroup sums with the lanes' shifts pt(i) -> (x, y, {m_a, m_b}); exact when a sum left
+// the safe range.  Returns the softmins -e ln2 LSE2 in fp64.
+template <class Pt, class HA, class HB>
+__device__ __forceinline__ void softmin_pair(const OtParams &P, const float *tab, const double *msh,
+                                             const float *xs, bool v, float xi, float yi, double e, double ma,
+                                             double mb, const Pt &pt, const HA &ha, const HB &hb, float *lds,
+                                             double &A, double &Bv, int32_t *fb) {
+  const float sc = cost_scale(1.0 / e);
+  float S[2];
+  wg_iter_sums(tab, msh, P.splits, np_of(P), P.N, sc, pt, lds, S);
+  if (v) {
+    A = -e * lse2_from(S[0], ma, xs, P.N, xi, yi, sc, ha, fb) * kLn2d;
+    Bv = -e * lse2_from(S[1], mb, xs, P.N, xi, yi, sc, hb, fb) * kLn2d;
+  }
 }
 
 // initial potentials at eps0 (:120-121): a_y = softmin(eps0, C, logw), b_x = softmin(eps0, C, logu)
 __global__ __launch_bounds__(kOtThreads) void ot_init_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
-  __shared__ float tx[kOtTile], ty[kOtTile], tha[kOtTile], thb[kOtTile];
+  __shared__ double shd[16];
+  __shared__ float lds[kLdsPart];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
+  const bool v = i < N;
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
-  const double e = ws.rowc[b * 4];
-  const float logu = (float)ws.rowc[b * 4 + 1];
-  float A, Bv;
+  const double e = ws.rowc[b * 4], logu = ws.rowc[b * 4 + 1];
+  const float xi = v ? xs[2 * i] : 0.f, yi = v ? xs[2 * i + 1] : 0.f;
+  // shifts: the largest exponent of the row (the costs are <= 1/2 here: eps0 = diameter^2)
+  const double ma = ws.rowc[b * 4 + 2] * kLog2ed, mb = logu * kLog2ed;
+  double A = 0.0, Bv = 0.0;
   softmin_pair(
-      xs, N, i, i < N, (float)(1.0 / e), (float)e,
-      [&](int j, float &ha, float &hb) {
-        ha = lw[j];
-        hb = logu;
+      P, tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), xs, v, xi, yi, e, ma, mb,
+      [&](int ii, float &x, float &y, double (&m)[2]) {
+        x = xs[2 * ii];
+        y = xs[2 * ii + 1];
+        m[0] = ma;
+        m[1] = mb;
       },
-      tx, ty, tha, thb, A, Bv);
-  if (i < N) {
+      [&](int j) { return (double)lw[j] * kLog2ed; }, [&](int) { return mb; }, lds, A, Bv, &ws.st->fallbacks);
+  if (v) {
     pot_ptr(ws, P, 0, 0, b)[i] = A;
     pot_ptr(ws, P, 0, 1, b)[i] = Bv;
   }
+  emit_state_tables(P, ws, b, 0, v, xi, yi, v ? lw[i] : 0.f, logu, A, Bv, shd);
 }
 
 // does the loop stop before iteration k?  (stop_condition :126-129) -- every workgroup
@@ -248,13 +605,13 @@ __global__ __launch_bounds__(kOtThreads) void ot_init_kernel(OtParams P, OtWs ws
 __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws, int k) {
   if (k == 0) return false;
   if (P.stop_at) return k >= *P.stop_at - 2;  // the batch-global decision, taken by the caller
-  const float *res = ws.res + (int64_t)((k - 1) & 1) * P.B * P.splits;
+  const double *res = ws.res + (int64_t)((k - 1) & 1) * P.B * P.splits;
   for (int b = 0; b < P.B; ++b) {
     const double e0 = ws.rowc[b * 4];
     const double re = run_eps(e0, k - 1, P.sf, P.eps);
     const double ne = fmax(re * P.sf, P.eps);
     bool cont = ne < re;
-    for (int s = 0; s < P.splits && !cont; ++s) cont = (double)res[b * P.splits + s] > P.thr;
+    for (int s = 0; s < P.splits && !cont; ++s) cont = res[b * P.splits + s] > P.thr;
     if (!cont) return true;  // some row converged -> torch.all(continue_) is False
   }
   return false;
@@ -263,8 +620,8 @@ __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws
 // iteration k: state k (buffer k&1) -> state k+1 (buffer (k+1)&1)  (apply_one :131-153)
 __global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
   if (ot_off(P)) return;
-  __shared__ float tx[kOtTile], ty[kOtTile], tha[kOtTile], thb[kOtTile];
-  __shared__ float shf[16];
+  __shared__ double shd[16];
+  __shared__ float lds[kLdsPart];
   __shared__ int s_stop;
   if (threadIdx.x == 0) {
     int st = ws.st->stopped;
@@ -281,88 +638,130 @@ __global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws
   if (s_stop) return;
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const double re = run_eps(ws.rowc[b * 4], k, P.sf, P.eps);
-  const float ref = (float)re, inv = (float)(1.0 / re);
+  const bool v = i < N;
+  const double re = run_eps(ws.rowc[b * 4], k, P.sf, P.eps), inv = 1.0 / re;
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
-  const float logu = (float)ws.rowc[b * 4 + 1];
-  const float *ay = pot_ptr(ws, P, k & 1, 0, b), *bx = pot_ptr(ws, P, k & 1, 1, b);
-  float A, Bv;
-  // at_y = softmin(e, C, logw + b_x/e);  bt_x = softmin(e, C, logu + a_y/e)
+  const double logu = ws.rowc[b * 4 + 1];
+  const double *ay = pot_ptr(ws, P, k & 1, 0, b), *bx = pot_ptr(ws, P, k & 1, 1, b);
+  const float xi = v ? xs[2 * i] : 0.f, yi = v ? xs[2 * i + 1] : 0.f;
+  // at_y = softmin(e, C, logw + b_x/e);  bt_x = softmin(e, C, logu + a_y/e); shifts from the
+  // current potentials (softmin = -e ln2 LSE2)
+  const double sh = -inv * kLog2ed;
+  const double oa = v ? ay[i] : 0.0, ob = v ? bx[i] : 0.0;
+  double A = 0.0, Bv = 0.0;
   softmin_pair(
-      xs, N, i, i < N, inv, ref,
-      [&](int j, float &ha, float &hb) {
-        ha = lw[j] + bx[j] * inv;
-        hb = logu + ay[j] * inv;
+      P, tabI_row(ws, P, k & 1, b), mI_row(ws, P, k & 1, b), xs, v, xi, yi, re, oa * sh, ob * sh,
+      [&](int ii, float &x, float &y, double (&m)[2]) {
+        x = xs[2 * ii];
+        y = xs[2 * ii + 1];
+        m[0] = ay[ii] * sh;
+        m[1] = bx[ii] * sh;
       },
-      tx, ty, tha, thb, A, Bv);
-  float dmax = 0.f;
-  if (i < N) {
-    const float na = 0.5f * (ay[i] + A), nb = 0.5f * (bx[i] + Bv);
+      [&](int j) { return ((double)lw[j] + bx[j] * inv) * kLog2ed; },
+      [&](int j) { return (logu + ay[j] * inv) * kLog2ed; }, lds, A, Bv, &ws.st->fallbacks);
+  double na = 0.0, nb = 0.0, dmax = 0.0;
+  if (v) {
+    na = 0.5 * (oa + A);
+    nb = 0.5 * (ob + Bv);
     pot_ptr(ws, P, (k + 1) & 1, 0, b)[i] = na;
     pot_ptr(ws, P, (k + 1) & 1, 1, b)[i] = nb;
-    dmax = fmaxf(fabsf(na - ay[i]), fabsf(nb - bx[i]));
+    dmax = fmax(fabs(na - oa), fabs(nb - ob));
   }
-  dmax = block_max(dmax, shf);
+  dmax = block_max(dmax, shd);
   if (threadIdx.x == 0) ws.res[((int64_t)(k & 1) * P.B + b) * P.splits + blockIdx.x] = dmax;
+  emit_state_tables(P, ws, b, k + 1, v, xi, yi, v ? lw[i] : 0.f, logu, na, nb, shd);
 }
 
 __device__ __forceinline__ int ot_total_iter(const OtParams &P, const OtWs &ws) {
   return ws.st->stopped ? ws.st->K : max(P.max_iter - 1, 0);
 }
 
-// final potentials at eps (:173-176): f = softmin(eps, C, logw + b_x/eps), g = softmin(eps, C, logu + a_y/eps)
+// final potential at eps (:173-176): f = softmin(eps, C, logw + b_x/eps).  (g = softmin(eps,
+// C, logu + a_y/eps) cancels in the column normalisation of the transport matrix: not formed.)
+// Writes the column table: X, Y, f_i / eps (base 2).
 __global__ __launch_bounds__(kOtThreads) void ot_final_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
-  __shared__ float tx[kOtTile], ty[kOtTile], tha[kOtTile], thb[kOtTile];
+  __shared__ double shd[16];
+  __shared__ float lds[kLdsPart];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
+  const bool v = i < N;
+  const int64_t Np = np_of(P);
   const int K = ot_total_iter(P, ws);
-  const float e = (float)P.eps, inv = (float)(1.0 / P.eps);
+  const double e = P.eps, inv = 1.0 / P.eps;
+  const float sc = cost_scale(inv);
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
-  const float logu = (float)ws.rowc[b * 4 + 1];
-  const float *ay = pot_ptr(ws, P, K & 1, 0, b), *bx = pot_ptr(ws, P, K & 1, 1, b);
-  float A, Bv;
-  softmin_pair(
-      xs, N, i, i < N, inv, e,
-      [&](int j, float &ha, float &hb) {
-        ha = lw[j] + bx[j] * inv;
-        hb = logu + ay[j] * inv;
-      },
-      tx, ty, tha, thb, A, Bv);
-  if (i < N) {
-    ws.fg[(int64_t)b * N + i] = A;
-    ws.fg[((int64_t)P.B + b) * N + i] = Bv;
+  const double *ay = pot_ptr(ws, P, K & 1, 0, b), *bx = pot_ptr(ws, P, K & 1, 1, b);
+  // the state's iteration table is at eps unless the row was still annealing at the stop
+  const bool annealing = run_eps(ws.rowc[b * 4], K, P.sf, P.eps) != P.eps;
+  const float *tab = annealing ? ws.tabF + (int64_t)b * 4 * Np : tabI_row(ws, P, K & 1, b);
+  const double *msh = annealing ? ws.mF + (int64_t)b * P.splits * 2 : mI_row(ws, P, K & 1, b);
+  const float xi = v ? xs[2 * i] : 0.f, yi = v ? xs[2 * i + 1] : 0.f;
+  const double sh = -inv * kLog2ed;  // f is the softmin that a_y converged to
+  float S[1];
+  wg_table_sums<1, 0, 2>(tab, msh, P.splits, Np, N, sc,
+                         [&](int ii, float &x, float &y, double (&m)[1]) {
+                           x = xs[2 * ii];
+                           y = xs[2 * ii + 1];
+                           m[0] = ay[ii] * sh;
+                         },
+                         lds, S, nullptr);
+  double fe = 0.0;
+  if (v) {
+    const double L = lse2_from(S[0], ay[i] * sh, xs, N, xi, yi, sc,
+                               [&](int j) { return ((double)lw[j] + bx[j] * inv) * kLog2ed; }, &ws.st->fallbacks);
+    const double f = -e * L * kLn2d;
+    ws.fg[(int64_t)b * N + i] = f;
+    fe = f * inv * kLog2ed;
   }
+  const double h[1] = {fe};
+  write_col<1, 0, false>(ws.tabC + (int64_t)b * 3 * Np, ws.mC + (int64_t)b * P.splits, Np, v, xi, yi, h, nullptr,
+                         shd);
 }
 
 // r_j = log N + logw_j - LSE_i(f_i/eps - C_ij/eps)   (transport_from_potentials :200-207,
-// with the column log-normaliser; g_j cancels)
-__global__ __launch_bounds__(kOtThreads) void ot_col_kernel(OtParams P, OtWs ws) {
+// with the column log-normaliser; g_j cancels).  Writes the apply table: X, Y, r_j, x_j, y_j.
+__global__ __launch_bounds__(kOtThreads) void ot_col_kernel(OtParams P, OtWs ws, const float *__restrict__ x) {
   if (ot_off(P)) return;
-  __shared__ float tx[kOtTile], ty[kOtTile], tha[kOtTile], thb[kOtTile];
+  __shared__ double shd[16];
+  __shared__ float lds[kLdsPart];
   const int b = blockIdx.y, N = P.N;
   const int j = blockIdx.x * kOtThreads + threadIdx.x;
-  const float e = (float)P.eps, inv = (float)(1.0 / P.eps);
+  const bool v = j < N;
+  const int64_t Np = np_of(P);
+  const int K = ot_total_iter(P, ws);
+  const double inv = 1.0 / P.eps;
+  const float sc = cost_scale(inv);
   const float *xs = ws.xs + (int64_t)b * N * 2;
-  const float *f = ws.fg + (int64_t)b * N;
-  float A, Bv;
-  // softmin_pair returns -e * LSE(...); reuse it with ha = f_i / eps (the second lane unused)
-  softmin_pair(
-      xs, N, j, j < N, inv, e,
-      [&](int i, float &ha, float &hb) {
-        ha = f[i] * inv;
-        hb = 0.f;
-      },
-      tx, ty, tha, thb, A, Bv);
-  if (j < N) {
-    const float lse = -A * inv;
-    ws.r[(int64_t)b * N + j] = -(float)ws.rowc[b * 4 + 1] + ws.logw[(int64_t)b * N + j] - lse;
+  const double *f = ws.fg + (int64_t)b * N;
+  const double *bx = pot_ptr(ws, P, K & 1, 1, b);
+  const double logu = ws.rowc[b * 4 + 1];
+  const float xj = v ? xs[2 * j] : 0.f, yj = v ? xs[2 * j + 1] : 0.f;
+  // LSE_i(f_i/eps - C_ij/eps) = -b_x_j/eps - logu at the Sinkhorn fixed point
+  auto shift = [&](int jj) { return (-bx[jj] * inv - logu) * kLog2ed; };
+  float S[1];
+  wg_table_sums<1, 0, 1>(ws.tabC + (int64_t)b * 3 * Np, ws.mC + (int64_t)b * P.splits, P.splits, Np, N, sc,
+                         [&](int jj, float &xx, float &yy, double (&m)[1]) {
+                           xx = xs[2 * jj];
+                           yy = xs[2 * jj + 1];
+                           m[0] = shift(jj);
+                         },
+                         lds, S, nullptr);
+  double rj = 0.0;
+  if (v) {
+    const double L = lse2_from(S[0], shift(j), xs, N, xj, yj, sc, [&](int i) { return f[i] * inv * kLog2ed; },
+                               &ws.st->fallbacks);
+    rj = -logu + (double)ws.logw[(int64_t)b * N + j] - L * kLn2d;
   }
+  const double h[1] = {rj * kLog2ed};
+  const float vals[2] = {v ? x[((int64_t)b * N + j) * 2] : 0.f, v ? x[((int64_t)b * N + j) * 2 + 1] : 0.f};
+  write_col<1, 2, false>(ws.tabA + (int64_t)b * 5 * Np, ws.mA + (int64_t)b * P.splits, Np, v, xj, yj, h, vals, shd);
 }
 
-// x'_i = sum_j exp(f_i/eps - C_ij/eps + r_j) x_j  (apply_transport_matrix :254-264)
+// x'_i = sum_j T_ij x_j with T_ij = exp(f_i/eps - C_ij/eps + r_j)  (apply_transport_matrix
+// :254-264): the terms are the matrix entries themselves (shift -f_i/eps, sum ~ 1)
 __global__ __launch_bounds__(kOtThreads) void ot_apply_kernel(OtParams P, OtWs ws,
                                                              const float *__restrict__ x,
                                                              int64_t row_base,
@@ -370,44 +769,54 @@ __global__ __launch_bounds__(kOtThreads) void ot_apply_kernel(OtParams P, OtWs w
                                                              float *__restrict__ w_out,
                                                              int64_t *__restrict__ idx_out) {
   if (ot_off(P)) return;
-  __shared__ float tx[kOtTile], ty[kOtTile], tr[kOtTile], px[kOtTile], py[kOtTile];
+  __shared__ float lds[kLdsPart];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const float inv = (float)(1.0 / P.eps);
+  const bool v = i < N;
+  const int64_t Np = np_of(P);
+  const double inv = 1.0 / P.eps;
+  const float sc = cost_scale(inv);
   const float *xs = ws.xs + (int64_t)b * N * 2;
-  const float *xr = x + (int64_t)b * N * 2;
-  const bool act = i < N;
-  const float xi = act ? xs[2 * i] : 0.f, yi = act ? xs[2 * i + 1] : 0.f;
-  const float fi = act ? ws.fg[(int64_t)b * N + i] * inv * kLog2e : 0.f;
-  const float c2 = 0.5f * inv * kLog2e;
-  float ax = 0.f, ay = 0.f;
-  for (int j0 = 0; j0 < N; j0 += kOtTile) {
-    const int nt = min(kOtTile, N - j0);
-    __syncthreads();
-    for (int j = threadIdx.x; j < nt; j += blockDim.x) {
-      tx[j] = xs[2 * (j0 + j)];
-      ty[j] = xs[2 * (j0 + j) + 1];
-      tr[j] = ws.r[(int64_t)b * N + j0 + j] * kLog2e;
-      px[j] = xr[2 * (j0 + j)];
-      py[j] = xr[2 * (j0 + j) + 1];
+  const double *fg = ws.fg + (int64_t)b * N;
+  const double fsh = inv * kLog2ed;
+  float S[1], SV[2];
+  wg_table_sums<1, 2, 1>(ws.tabA + (int64_t)b * 5 * Np, ws.mA + (int64_t)b * P.splits, P.splits, Np, N, sc,
+                         [&](int ii, float &xx, float &yy, double (&m)[1]) {
+                           xx = xs[2 * ii];
+                           yy = xs[2 * ii + 1];
+                           m[0] = -fg[ii] * fsh;
+                         },
+                         lds, S, SV);
+  if (!v) return;
+  float ax = SV[0], ay = SV[1];
+  if (!sum_ok(S[0])) {  // exact: max shift first, then the weighted sums (fp64 exponents)
+    atomicAdd(&ws.st->fallbacks, 1);
+    const float xi = xs[2 * i], yi = xs[2 * i + 1];
+    const double fi = fg[i] * fsh;
+    const float *xr = x + (int64_t)b * N * 2;
+    const float *E = ws.tabA + (int64_t)b * 5 * Np + 2 * Np;  // r_j - M_s
+    const double *ms = ws.mA + (int64_t)b * P.splits;
+    auto expo = [&](int j) {
+      const float dx = xi - xs[2 * j], dy = yi - xs[2 * j + 1];
+      return fi + (double)E[j] + ms[j / kOtThreads] - (double)(fmaf(dx, dx, dy * dy) * sc);
+    };
+    double mx = -INFINITY;
+    for (int j = 0; j < N; ++j) mx = fmax(mx, expo(j));
+    double sx = 0.0, sy = 0.0;
+    for (int j = 0; j < N; ++j) {
+      const double t = exp2(expo(j) - mx);
+      sx += t * xr[2 * j];
+      sy += t * xr[2 * j + 1];
     }
-    __syncthreads();
-    if (act) {
-      for (int j = 0; j < nt; ++j) {
-        const float dx = xi - tx[j], dy = yi - ty[j];
-        const float t = exp2f(fi + tr[j] - fmaf(dx, dx, dy * dy) * c2);
-        ax = fmaf(t, px[j], ax);
-        ay = fmaf(t, py[j], ay);
-      }
-    }
+    const double R = exp2(mx);
+    ax = (float)(sx * R);
+    ay = (float)(sy * R);
   }
-  if (act) {
-    const int64_t o = (int64_t)b * N + i;
-    x_out[2 * o] = ax;
-    x_out[2 * o + 1] = ay;
-    w_out[o] = 1.0f / (float)N;
-    idx_out[o] = (int64_t)N * (row_base + b) + i;
-  }
+  const int64_t o = (int64_t)b * N + i;
+  x_out[2 * o] = ax;
+  x_out[2 * o + 1] = ay;
+  w_out[o] = 1.0f / (float)N;
+  idx_out[o] = (int64_t)N * (row_base + b) + i;
 }
 
 __global__ void ot_iters_kernel(OtParams P, OtWs ws, int32_t *out) {
@@ -422,6 +831,16 @@ extern "C" int64_t nfdpf_ot_workspace_bytes(int B, int N) {
   return (B <= 0 || N <= 0) ? 256 : ws_bytes(B, N);
 }
 
+extern "C" int nfdpf_ot_stats(const void *workspace, int32_t *host_out) {
+  NFDPF_REQUIRE(workspace && host_out, "nfdpf_ot_stats: null pointer");
+  OtState st;
+  if (hipMemcpy(&st, workspace, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess)
+    return launch_status("nfdpf_ot_stats");
+  host_out[0] = st.stopped ? st.K + 2 : -1;
+  host_out[1] = st.fallbacks;
+  return NFDPF_OK;
+}
+
 extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
                                  float scaling, float threshold, int max_iter, int64_t row_base,
                                  float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
@@ -434,16 +853,17 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
   NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_ot_resample: workspace not 256-B aligned");
   if (B == 0) return NFDPF_OK;
   hipStream_t st = as_stream(stream);
-  const int splits = ot_splits(B, N);
-  OtWs ws = carve(workspace, B, N, splits);
+  const int splits = ot_splits(N);
+  OtWs ws = carve(workspace, B, N);
   OtParams P{B, N, splits, max_iter, (double)eps, (double)scaling * (double)scaling,
              (double)threshold, gate, stop_at};
   ot_setup_kernel<<<B, row_threads(N), 0, st>>>(x, w, N, ws, gate);
   const dim3 g(splits, B);
+  ot_prep_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
   ot_init_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
   for (int k = 0; k < max_iter - 1; ++k) ot_iter_kernel<<<g, kOtThreads, 0, st>>>(P, ws, k);
   ot_final_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
-  ot_col_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
+  ot_col_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x);
   ot_apply_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);
   if (iters_out) ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
   return launch_status("nfdpf_ot_resample");

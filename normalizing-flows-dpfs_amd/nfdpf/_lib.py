@@ -58,6 +58,7 @@ SIGNATURES = {
     "nfdpf_soft_resample": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int64,
                                     c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_ot_workspace_bytes": (c_int64, [c_int, c_int]),
+    "nfdpf_ot_stats": (c_int, [c_void_p, c_void_p]),
     "nfdpf_ot_resample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),

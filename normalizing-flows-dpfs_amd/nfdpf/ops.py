@@ -122,6 +122,20 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_b
     return xo, wo, idx, it
 
 
+def ot_stats(device=None):
+    """(iterations or -1, exact-fallback count) of the last ot_resample on ``device``
+    (synchronous; diagnostics for tests and benchmarks)."""
+    import ctypes
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ws = _ws.get(("ot", str(dev)))
+    if ws is None:
+        raise L.NfdpfError("ot_stats: no ot_resample has run on this device")
+    out = (ctypes.c_int32 * 2)()
+    torch.cuda.synchronize(dev)
+    check(lib().nfdpf_ot_stats(_aligned_ptr(ws), ctypes.addressof(out)), "nfdpf_ot_stats")
+    return int(out[0]), int(out[1])
+
+
 def ess_gate(inv_ess, N, force=False, out=None):
     """DPFs.py:163-165 gate as a device int32[1] (no host sync)."""
     B = inv_ess.shape[0]
