@@ -115,7 +115,7 @@ NFDPF_API int64_t nfdpf_ot_workspace_bytes(int B, int N);
 NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps, float scaling,
                       float threshold, int max_iter, int64_t row_base, float *x_out,
                       float *w_out, int64_t *idx_out, int32_t *iters_out, void *workspace,
-                      const int32_t *gate, const int32_t *stop_at, void *stream);
+                      const int32_t *gate, const int32_t *stop_at, int poll, void *stream);
 /*   gate: optional device flag; when non-NULL and *gate == 0 every kernel is a no-op (the
  *         ESS gate of DPFs.py:165 decided not to resample this step, without a host sync)
  *   stop_at: optional device int32, in the iters_out encoding (total_iter + 2).  NULL: the
@@ -123,7 +123,13 @@ NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, fl
  *         has converged (resamplers.py:126-129).  Non-NULL: run exactly that many
  *         iterations.  A batch sharded over ranks reproduces the unsharded loop by running
  *         once with NULL, taking the MIN of iters_out over ranks (the first row to converge
- *         anywhere), and running again with stop_at = that minimum.                      */
+ *         anywhere), and running again with stop_at = that minimum.
+ *   poll: 0 -- enqueue max_iter - 1 iteration launches (iterations after the stop exit at
+ *         once; stream-ordered, graph-capturable, returns immediately).  1 -- the calling
+ *         thread follows the device's progress through library-owned mapped host flags and
+ *         stops enqueueing once the loop has stopped (at most 2 early-exit launches past the
+ *         stop; the call returns when the last iteration has been enqueued, not capturable;
+ *         the reference's own loop syncs the host every iteration, resamplers.py:126-129). */
 
 /* Diagnostics of the last nfdpf_ot_resample on `workspace` (synchronous device read):
  *   host_out[0] = iterations in the iters_out encoding (-1: ran to max_iter), host_out[1] =

@@ -39,6 +39,11 @@
 //     iteration after which ANY row has converged (torch.all(continue_), :126-129) -- with
 //     one launch per iteration that first reads the previous iteration's per-row residuals
 //     (identical decision in every workgroup, no atomics).
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <thread>
+
 #include "common.hpp"
 
 namespace nfdpf {
@@ -130,7 +135,15 @@ struct OtParams {
   double eps, sf, thr;
   const int32_t *gate;     // optional: skip everything when *gate == 0
   const int32_t *stop_at;  // optional: total_iter + 2 to run (sharded batches), else the rule
+  int32_t *host;           // optional (poll mode): mapped host flags {stop seq, seq * 4096 + k}
+  int32_t seq;             // call sequence number for the host flags
 };
+
+// progress of the Sinkhorn loop to the polling host thread (system-scope stores into
+// fine-grained host memory; vector stores)
+__device__ __forceinline__ void host_flag(int32_t *h, int idx, int32_t v) {
+  __hip_atomic_store(h + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ bool ot_off(const OtParams &P) { return P.gate && *P.gate == 0; }
 
@@ -619,7 +632,11 @@ __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws
 
 // iteration k: state k (buffer k&1) -> state k+1 (buffer (k+1)&1)  (apply_one :131-153)
 __global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
-  if (ot_off(P)) return;
+  const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+  if (ot_off(P)) {
+    if (lead && P.host) host_flag(P.host, 0, P.seq);  // nothing to iterate: stop enqueueing
+    return;
+  }
   __shared__ double shd[16];
   __shared__ float lds[kLdsPart];
   __shared__ int s_stop;
@@ -627,12 +644,16 @@ __global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws
     int st = ws.st->stopped;
     if (!st && ot_stop_before(P, ws, k)) {
       st = 1;
-      if (blockIdx.x == 0 && blockIdx.y == 0) {
+      if (lead) {
         ws.st->stopped = 1;
         ws.st->K = k;
       }
     }
     s_stop = st;
+    if (lead && P.host) {
+      host_flag(P.host, 1, P.seq * 4096 + k);
+      if (st) host_flag(P.host, 0, P.seq);
+    }
   }
   __syncthreads();
   if (s_stop) return;
@@ -841,27 +862,80 @@ extern "C" int nfdpf_ot_stats(const void *workspace, int32_t *host_out) {
   return NFDPF_OK;
 }
 
+// poll mode: library-owned flags in fine-grained (coherent, mapped) host memory, allocated on
+// first use and kept for the process; one polled call at a time
+static std::mutex g_poll_mu;
+static int32_t g_poll_seq = 0;
+static bool poll_flags(volatile int32_t **host, int32_t **dev) {
+  static int32_t *h = nullptr, *d = nullptr;
+  if (!h) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return false;
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) return false;
+    h = (int32_t *)p;
+    d = (int32_t *)dp;
+    h[0] = h[1] = -1;
+  }
+  *host = h;
+  *dev = d;
+  return true;
+}
+
 extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
                                  float scaling, float threshold, int max_iter, int64_t row_base,
                                  float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
                                  void *workspace, const int32_t *gate, const int32_t *stop_at,
-                                 void *stream) {
+                                 int poll, void *stream) {
   NFDPF_REQUIRE(x && w && x_out && w_out && idx_out && workspace,
                 "nfdpf_ot_resample: null pointer");
   NFDPF_REQUIRE(B >= 0 && N >= 1 && max_iter >= 1, "nfdpf_ot_resample: bad sizes");
   NFDPF_REQUIRE(eps > 0.f && scaling > 0.f, "nfdpf_ot_resample: eps and scaling must be > 0");
   NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_ot_resample: workspace not 256-B aligned");
+  NFDPF_REQUIRE(max_iter <= 4096, "nfdpf_ot_resample: max_iter <= 4096");
   if (B == 0) return NFDPF_OK;
   hipStream_t st = as_stream(stream);
   const int splits = ot_splits(N);
   OtWs ws = carve(workspace, B, N);
   OtParams P{B, N, splits, max_iter, (double)eps, (double)scaling * (double)scaling,
-             (double)threshold, gate, stop_at};
+             (double)threshold, gate, stop_at, nullptr, 0};
+  std::unique_lock<std::mutex> lock;
+  volatile int32_t *hf = nullptr;
+  if (poll) {
+    lock = std::unique_lock<std::mutex>(g_poll_mu);
+    if (!poll_flags(&hf, &P.host)) return launch_status("nfdpf_ot_resample (poll flags)");
+    P.seq = (g_poll_seq = (g_poll_seq + 1) & 0x7ffff);
+  }
   ot_setup_kernel<<<B, row_threads(N), 0, st>>>(x, w, N, ws, gate);
   const dim3 g(splits, B);
   ot_prep_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
   ot_init_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
-  for (int k = 0; k < max_iter - 1; ++k) ot_iter_kernel<<<g, kOtThreads, 0, st>>>(P, ws, k);
+  if (!poll) {
+    for (int k = 0; k < max_iter - 1; ++k) ot_iter_kernel<<<g, kOtThreads, 0, st>>>(P, ws, k);
+  } else {
+    // Keep at most kAhead iterations queued past the one the device has started, and stop
+    // enqueueing once an iteration has observed the stop (or the gate is off): the loop then
+    // costs (iterations run) + <= kAhead early-exit launches instead of max_iter - 1.  A
+    // device that reports nothing for 2 s (should not happen) gets the remaining launches.
+    constexpr int kAhead = 2;
+    bool blind = false;
+    for (int k = 0; k < max_iter - 1; ++k) {
+      if (!blind && hf[0] == P.seq) break;
+      ot_iter_kernel<<<g, kOtThreads, 0, st>>>(P, ws, k);
+      if (blind) continue;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        if (hf[0] == P.seq) break;
+        const int32_t pr = hf[1];
+        if (pr / 4096 == P.seq && k - pr % 4096 < kAhead) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+          blind = true;
+          break;
+        }
+        std::this_thread::yield();
+      }
+    }
+  }
   ot_final_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
   ot_col_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x);
   ot_apply_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);

@@ -61,7 +61,7 @@ SIGNATURES = {
     "nfdpf_ot_stats": (c_int, [c_void_p, c_void_p]),
     "nfdpf_ot_resample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                  c_void_p]),
+                                  c_int, c_void_p]),
     "nfdpf_ess_gate": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_normalize_log_probs": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "nfdpf_cglow_params_size": (c_int64, [c_int]),

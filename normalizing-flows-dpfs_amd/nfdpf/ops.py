@@ -98,12 +98,14 @@ def _aligned_ptr(t: torch.Tensor) -> int:
 
 
 def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_base=0, gate=None,
-                stop_at=None):
+                stop_at=None, poll=None):
     """resampler_ot (resamplers.py:62-70) -> (x', w', flat idx, iterations int32[1]).
 
     ``stop_at`` (device int32[1], iterations encoding): run exactly that many Sinkhorn
     iterations instead of the batch-coupled stop rule (include/nfdpf.h) -- the second pass
-    of a batch sharded over ranks."""
+    of a batch sharded over ranks.  ``poll`` (default: unless the stream is being captured
+    into a graph): follow the loop's progress from the host and stop enqueueing iteration
+    launches once it has stopped."""
     require_device(x, "ot_resample")
     B, N, D = x.shape
     if D != 2:
@@ -113,11 +115,14 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_b
     wo = torch.empty_like(w)
     idx = torch.empty((B, N), device=x.device, dtype=torch.int64)
     it = torch.zeros(1, device=x.device, dtype=torch.int32)
+    if poll is None:
+        poll = not torch.cuda.is_current_stream_capturing()
     nb = int(lib().nfdpf_ot_workspace_bytes(B, N))
     ws = workspace(nb, x.device)
     check(lib().nfdpf_ot_resample(ptr(x), ptr(w), B, N, float(eps), float(scaling), float(threshold),
                                   int(max_iter), int(row_base), ptr(xo), ptr(wo), ptr(idx), ptr(it),
-                                  _aligned_ptr(ws), ptr(gate), ptr(stop_at), stream_ptr(x.device)),
+                                  _aligned_ptr(ws), ptr(gate), ptr(stop_at), int(bool(poll)),
+                                  stream_ptr(x.device)),
           "nfdpf_ot_resample")
     return xo, wo, idx, it
 

@@ -199,6 +199,21 @@ def test_ot_resampler_vs_oracle_stress(B, N, kind):
     assert torch.all(wo.cpu() == 1.0 / N)
 
 
+def test_ot_poll_matches_enqueue_all():
+    """poll=1 (host follows the loop and stops enqueueing) gives the bit-identical result of
+    poll=0 (all max_iter - 1 launches enqueued, graph-capturable), gate on and off."""
+    from nfdpf import ops
+    c = group(load("ot.npz"), "c1")
+    x, p = t(c["x"]).to(DEV), t(c["p"]).to(DEV)
+    a = ops.ot_resample(x, p, poll=False)
+    b = ops.ot_resample(x, p, poll=True)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+    off = torch.zeros(1, dtype=torch.int32, device=DEV)
+    z = ops.ot_resample(x, p, gate=off, poll=True)
+    assert int(z[3].item()) == 0
+
+
 def test_ot_sharded_stop_matches_unsharded():
     """A batch split over two 'ranks' reproduces the unsharded Sinkhorn loop: each half runs
     with the local stop rule, the MIN of the iteration counts is the batch-global stop
