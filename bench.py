@@ -98,11 +98,23 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
     if flags["resampler_type"] == "ot":
         Bs, Ts = max(1, B // 16), min(T, 10)   # one FP64 OT call is tens of seconds at B=64
     if N >= 4000:
-        Bs, Ts = 4, 8                          # C4 / C5: 4 rows x 8 steps (dense N^2 resampler work)
+        Bs, Ts = 4, 8                          # C5: 4 rows x 8 steps (dense N^2 resampler work)
+        if flags["resampler_type"] == "ot":
+            # C4: one row; the ESS gate first fires after ~12 steps, so 16 steps hold a few
+            # FP64 Sinkhorn calls (~10 s each at N=4000) -- 8 rows x 8 steps would hold none
+            Bs, Ts = 1, 16
     cfg = dict(N=N, NF_dyn=flags["NF_dyn"], NF_cond=flags["NF_cond"], measurement=flags["measurement"],
                resampler=flags["resampler_type"], alpha=0.5, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100,
                pos_noise=20.0, vel_noise=20.0, width=128, n_flows=2, cglow_K=1,
                dyn_flow=flags.get("NF_dyn_flow", "RealNVP"))
+    ot_calls = []
+    ot_orig = O.ot_resample
+
+    def ot_counted(*a, **k):
+        ot_calls.append(1)
+        return ot_orig(*a, **k)
+
+    O.ot_resample = ot_counted
     run = lambda: O.filtering(cfg, params, enc[:Bs, :Ts], start[:Bs], vel[:Bs, :Ts], rng=O.HostRNG())
     with torch.no_grad():
         t0 = time.perf_counter()
@@ -114,10 +126,42 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
             t0 = time.perf_counter()
             run()
             times.append(time.perf_counter() - t0)
+    O.ot_resample = ot_orig
     med = float(np.median(times))
+    ot_note = ""
+    if flags["resampler_type"] == "ot":
+        ot_note = f", OT resampling in {len(ot_calls) // (reps + 1)} of {Ts} steps"
     return {"value": Bs * N * Ts / med, "unit": "particle-steps/s", "cores": cores, "kind": "port",
-            "sample": f"oracle filtering B={Bs} N={N} T={Ts} (ESS-gated), median of {reps} after 1 warm-up; "
-                      f"host {platform.processor() or platform.machine()}"}
+            "sample": f"oracle filtering B={Bs} N={N} T={Ts} (ESS-gated{ot_note}), median of {reps} after 1 "
+                      f"warm-up; host {platform.processor() or platform.machine()}"}
+
+
+# Sinkhorn iteration (resamplers.py:131-153): per particle pair (i, j) of a row, the cost
+# |x~_i - x~_j|^2 / 2 (4 FLOP) and the two live softmins' f_j - C_ij / eps, max-shift, exp,
+# sum (5 each, the exp counted as one) -- the reference's algorithm, a_x / b_y excluded
+F_OT_PAIR = 14.0
+
+
+def ot_iteration_ms(res, T):
+    """Average duration of one Sinkhorn iteration launch (ot_iter_kernel) on this workload's
+    particles (history slot T/2): two stream-ordered OT calls forced to 10 and 20 iterations
+    (stop_at), hipEvents around each; the difference / 10 leaves the fixed launches out."""
+    from nfdpf import ops
+    x = res.particles[:, T // 2].contiguous()
+    w = res.probs[:, T // 2].contiguous()
+    out = {}
+    for k in (10, 20):
+        stop = torch.full((1,), k + 2, dtype=torch.int32, device=x.device)
+        best = None
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ops.ot_resample(x, w, stop_at=stop, poll=False)
+            b.record()
+            torch.cuda.synchronize()
+            best = a.elapsed_time(b) if best is None else min(best, a.elapsed_time(b))
+        out[k] = best
+    return (out[20] - out[10]) / 10.0
 
 
 def pmc_traffic(cfg_name, kname):
@@ -167,6 +211,8 @@ def main():
     flags, B, N, T, F_STEP, F_PROP = CONFIGS[args.config]
     B = args.batch or B
     F_ALG = F_PROP if (args.kernel == "tiled" or flags["measurement"] == "CGLOW") else F_STEP
+    launch_units = B * N  # particle-steps per launch of the step kernels
+    launch_bytes = B_ALG * B * N
     torch.manual_seed(2)
     a = make_args(flags, B, N, T, {"force_resample": args.force_resample})
     dpf = DPF(a).to(dev).eval()
@@ -237,6 +283,14 @@ def main():
             kname = "tiled_prop_kernel"
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
+    ot_iter_ms = None
+    if flags["resampler_type"] == "ot" and eng.last_ot_calls:
+        ot_iter_ms = ot_iteration_ms(res, T)
+        if ot_iter_ms * eng.last_ot_calls * 10 > kernel_ms * T:  # the Sinkhorn loop dominates
+            kname, kernel_ms = "ot_iter_kernel", ot_iter_ms
+            F_ALG, launch_units = F_OT_PAIR, B * N * N
+            # per particle: x~ (8 B) + logw (4) + both potentials read and written (fp64, 32)
+            launch_bytes = 44.0 * B * N
     traffic, traffic_src = pmc_traffic(args.config, kname)
     # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
     se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
@@ -245,13 +299,20 @@ def main():
         dist.all_reduce(se)
         dist.all_reduce(cnt)
     rmse = float(torch.sqrt(se / cnt))
+    # steps whose ESS gate fired (DPFs.py:165) in the last pass: OT calls are counted on the
+    # host by the engine; a soft resample leaves a non-identity index row
+    if flags["resampler_type"] == "ot":
+        resampled = eng.last_ot_calls
+    else:
+        ident = (torch.arange(N, device=dev) + N * (shard.row_base + torch.arange(B, device=dev))[:, None])
+        resampled = int((res.index != ident[:, None, :]).flatten(2).any(-1).any(0).sum())
 
     if rank == 0:
         units = B * world * N * T * args.steps
         value = units / elapsed
-        per_launch_units = B * N
+        per_launch_units = launch_units
         achieved_tf = F_ALG * per_launch_units / (kernel_ms * 1e-3) / 1e12
-        hbm_gbs = B_ALG * per_launch_units / (kernel_ms * 1e-3) / 1e9
+        hbm_gbs = launch_bytes / (kernel_ms * 1e-3) / 1e9
         out = {
             "metric": "particle-steps/sec (batch x N x T / s) + filtering RMSE, disk-tracking task",
             "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps,
@@ -264,6 +325,7 @@ def main():
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
                        "parallelism": f"batch-sharded x{world}"},
             "rmse": rmse,
+            "resampled_steps": resampled,
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "traffic_source": traffic_src,

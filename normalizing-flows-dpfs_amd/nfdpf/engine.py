@@ -245,6 +245,7 @@ class FilterEngine:
         d.lw_sum, d.pred, d.scratch = lw_sum.data_ptr(), pred.data_ptr(), scratch.data_ptr()
 
         fired = [] if host_mode else None
+        self.last_ot_calls = 0
         keep = []  # host uploads must outlive their kernels
         # per-step pointers precomputed as integers: the loop below is the launch path of every
         # time step, so it stays free of tensor slicing and per-call lookups
@@ -314,6 +315,7 @@ class FilterEngine:
                 # DPFs.py:165) and skip the call.  The gate is batch-global: same on every rank.
                 fire = fired[-1] if host_mode else bool(gate_buf.item())
                 if fire:
+                    self.last_ot_calls += 1
                     xo, _, _, it = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,
                                                    shard.row_base, gate=gate_buf)
                     if shard.world > 1:
