@@ -215,7 +215,9 @@ typedef struct nfdpf_filter_desc {
   float *ess_out;           /* [B] 1/sum(p^2) of this step (tiled: see below) */
   float *lw_sum;            /* [B,T] row sums of the unnormalised log-weights (obs likelihood) */
   float *pred;              /* [B,T,2] sum_n p*x (losses.py:18-31 prediction) */
-  float *scratch;           /* [B,N,4] per-particle hand-off between stages (x_dyn, propose, prior) */
+  float *scratch;           /* [2][B,N,4] per-particle hand-off between stages (x_dyn, propose, prior),
+                               indexed by step parity: step t's values must not overwrite step t-1's,
+                               which the deferred normalisation of slot t-1 reads during step t */
   void *prof_events;        /* optional hipEvent_t[2]: recorded around the dominant launch
                                (the whole step for nfdpf_filter_step, the proposal+measurement
                                launch for nfdpf_filter_step_tiled) -- live kernel timing */

@@ -461,6 +461,232 @@ __global__ __launch_bounds__(SPLIT ? 2 * kTile : kTile) void tiled_dyn_kernel(co
   TRACE(1, 3)
 }
 
+// ---- K1+K2 merged (the split-net path of --NF-dyn RealNVP with --NF-cond and the cosine
+// measurement; tiled_prop_split_kernel finishes the step).  The nf_dyn context is the row's
+// mean / std of the particles AFTER motion, a row reduction that otherwise costs a launch
+// boundary: here every workgroup of a row runs the gate, the resampling source selection and
+// the motion of the WHOLE row (the motion is a Philox draw and two adds per particle; soft
+// resampling already builds the row's CDF in every tile), reduces the row's x, x^2 sums
+// itself (same inputs, same order in every workgroup of the row -> the same context) and then
+// runs the nf_dyn inverse of its own 256 particles on wave pairs.  Slot t-1 is read only here;
+// its deferred normalisation moves to the proposal launch (the scratch row is double-
+// buffered by step parity, so step t's propose / prior do not overwrite step t-1's).
+// Dynamic LDS: C[max(N, B_global)], w'[N], p_{t-1}[N].
+__global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  extern __shared__ float dyn_lds[];
+  __shared__ double shd[64];
+  __shared__ float shf[16];
+  __shared__ int fire_sh;
+  __shared__ RowNorm rn_sh;
+  __shared__ float xr_sh[kTile][2];
+  __shared__ int src_sh[kTile];
+  __shared__ float w_sh[kTile];
+  __shared__ f2 cb[kMaxFlows * 2 * kH];
+  __shared__ f2 cbs[kMaxFlows * 2 * kH];
+  __shared__ float xbuf[4 * kTile];
+  __shared__ int xflag[16];
+  TRACE(0, 0)
+  const int tiles = n_tiles(d.N), N = d.N;
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const SplitLane sl = split_lane(8);
+  const int role = sl.role, slot = sl.slot;
+  const int i = tile * kTile + slot;
+  const bool valid = i < N;
+  const int64_t grow = d.row_base + b;
+  const bool defer = d.defer_norm && d.t > 0;
+  const bool shifted = shifted_meas(d.measurement);
+  float *Cbuf = dyn_lds;
+  if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+  float e0 = 0.f, e1 = 0.f;
+  if (valid) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: under its latency
+  const int64_t my_row = d.row_base + d.B <= d.B_global ? d.row_base + b : b;
+  const RowSlot S = row_slot(d, b);
+  const float *xprev = d.x_prev + b * d.x_prev_rs;
+  const float *pprev = d.p_prev + b * d.p_prev_rs;
+  const RowSlot Sp = defer ? row_slot(d, b, d.t - 1) : S;
+  const float v0 = d.vel[2 * b], v1 = d.vel[2 * b + 1];
+  // the row's sums over x_phys = (x_src + vel) + eps (motion_apply_eps's arithmetic)
+  double a0 = 0, a1 = 0, c0 = 0, c1 = 0;
+  auto acc = [&](int j, float xs0, float xs1) {
+    float n0, n1;
+    motion_noise(d, b, grow, j, n0, n1);
+    const float p0 = (xs0 + v0) + n0, p1 = (xs1 + v1) + n1;
+    a0 += p0;
+    a1 += p1;
+    c0 += (double)p0 * p0;
+    c1 += (double)p1 * p1;
+  };
+  // The ESS gate (DPFs.py:163-165) is a chain of dependent loads and fp64 arithmetic on one
+  // wave: wave 0 evaluates it (tiled_gate_block's arithmetic) while waves 1..7 run the
+  // no-resampling motion of the row speculatively -- kept when the gate stays off (every
+  // step of the C2 bench), recomputed from the resampled sources when it fires.
+  const double *parts = reinterpret_cast<const double *>(d.ess_all);
+  const bool spec = !d.force_resample && !(d.gate && d.gate[0] != 0);
+  if (threadIdx.x < 64) {
+    if (d.gate || d.force_resample) {
+      if (threadIdx.x == 0) {
+        fire_sh = d.gate ? d.gate[0] != 0 : 1;
+        if (defer) rn_sh = row_norm(parts + my_row * tiles * kSm, tiles, shifted);
+      }
+    } else {
+      for (int r = threadIdx.x; r < d.B_global; r += 64) {
+        Cbuf[r] = row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, N, d.t > 0);
+        if (defer && r == my_row) rn_sh = row_norm(parts + (int64_t)r * tiles * kSm, tiles, shifted);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
+      __builtin_amdgcn_wave_barrier();
+      const float s = cascade_row_sum([&](int r) { return Cbuf[r]; }, d.B_global);
+      if (threadIdx.x == 0) fire_sh = (s / (float)d.B_global) < 0.5f * (float)N;
+    }
+  } else if (spec) {
+    for (int j = threadIdx.x - 64; j < N; j += blockDim.x - 64) {
+      if (defer)
+        acc(j, Sp.hx[2 * j], Sp.hx[2 * j + 1]);
+      else
+        acc(j, xprev[2 * j], xprev[2 * j + 1]);
+    }
+  }
+  __syncthreads();
+  const bool fire = fire_sh != 0;
+  TRACE(0, 1)
+  const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
+  const RowNorm rn = defer ? rn_sh : RowNorm{0.f, 1.f, 0.f};
+  auto prev_p = [&](int j) {
+    float lw, lk;
+    return norm_value(Sp, j, rn, shifted, lw, lk);
+  };
+  if (mode != kSrcPrev || !spec) a0 = a1 = c0 = c1 = 0;  // the speculation does not apply
+  const int i0 = tile * kTile;
+  float x0 = 0.f, x1 = 0.f, lr = 0.f;
+  int src = i;
+  if (mode == kSrcSoft) {
+    float *wbuf = dyn_lds + max(N, d.B_global);
+    if (defer) {  // the row's p_{t-1} into LDS for the resampler
+      float *pbuf = wbuf + N;
+      for (int j = threadIdx.x; j < N; j += blockDim.x) pbuf[j] = prev_p(j);
+      __syncthreads();
+      pprev = pbuf;
+    }
+    SoftRow row{pprev, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
+    float off;
+    if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
+      off = d.host_offsets[b];
+    else
+      off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, grow, 0u).x) * (1.0f / (float)N);
+    soft_row_search(row, d.lin, off, Cbuf, shd, shf, [&](int j, int sj) {
+      // sj == N: the reference's out-of-range edge (next row's first particle, weight 0)
+      float w = 0.f;
+      if (sj < N) w = row.w(sj);
+      wbuf[j] = w;
+      const float *xs = sj < N ? xprev + 2 * sj : (b + 1 < d.B ? xprev + d.x_prev_rs : xprev + 2 * (N - 1));
+      const float xs0 = xs[0], xs1 = xs[1];
+      acc(j, xs0, xs1);
+      if (j >= i0 && j < i0 + kTile) {
+        xr_sh[j - i0][0] = xs0;
+        xr_sh[j - i0][1] = xs1;
+        src_sh[j - i0] = sj;
+        w_sh[j - i0] = w;
+      }
+    });
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const float s2 = cascade_row_sum([&](int j) { return wbuf[j]; }, N);
+      if (threadIdx.x == 0) shf[8] = s2;
+    }
+    __syncthreads();
+    if (valid) {
+      x0 = xr_sh[slot][0];
+      x1 = xr_sh[slot][1];
+      lr = logf(w_sh[slot] / shf[8]);
+      src = src_sh[slot];
+    }
+  } else {
+    if (mode == kSrcOt || !spec) {
+      for (int j = threadIdx.x; j < N; j += blockDim.x) {
+        if (mode == kSrcOt)
+          acc(j, d.ot_x[((int64_t)b * N + j) * 2], d.ot_x[((int64_t)b * N + j) * 2 + 1]);
+        else if (defer)
+          acc(j, Sp.hx[2 * j], Sp.hx[2 * j + 1]);
+        else
+          acc(j, xprev[2 * j], xprev[2 * j + 1]);
+      }
+    }
+    if (valid) {
+      if (mode == kSrcOt) {
+        x0 = d.ot_x[((int64_t)b * N + i) * 2];
+        x1 = d.ot_x[((int64_t)b * N + i) * 2 + 1];
+        lr = logf(1.0f / (float)N);
+      } else if (defer) {
+        x0 = Sp.hx[2 * i];
+        x1 = Sp.hx[2 * i + 1];
+        lr = logf(prev_p(i));
+      } else {
+        x0 = xprev[2 * i];
+        x1 = xprev[2 * i + 1];
+        lr = logf(pprev[i]);
+      }
+    }
+  }
+  // the row context: wave sums (DPP), then the 8 wave partials in wave order, in every thread
+  {
+    const double w4[4] = {wave_sum_dpp(a0), wave_sum_dpp(a1), wave_sum_dpp(c0), wave_sum_dpp(c1)};
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) shd[4 * w + k] = w4[k];
+    __syncthreads();
+    a0 = shd[0];
+    a1 = shd[1];
+    c0 = shd[2];
+    c1 = shd[3];
+    for (int q = 1; q < 8; ++q) {
+      a0 += shd[4 * q];
+      a1 += shd[4 * q + 1];
+      c0 += shd[4 * q + 2];
+      c1 += shd[4 * q + 3];
+    }
+  }
+  const Ctx4 c = ctx_from_sums(a0, a1, c0, c1, N);
+  if (threadIdx.x < d.n_flows * 4 * kH) {
+    const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
+    const float v = fold_one(d.dyn_params, kNsDyn, kOctxDyn, threadIdx.x, cv);
+    reinterpret_cast<float *>(cb)[threadIdx.x] = v;
+    reinterpret_cast<float *>(cbs)[split_cb_index(threadIdx.x)] = v;
+  }
+  if (d.nf_cond && tile == 0 && threadIdx.x >= kTile && threadIdx.x - kTile < d.n_flows * 4 * kH) {
+    // proposal fold over the encoding columns (model/models.py:338-346); K3 adds mean/std
+    const int k = threadIdx.x - kTile;
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), k);
+    ws.cb_cond[b * kCb + k] = fold_acc(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
+  }
+  __syncthreads();
+  if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
+    ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
+  TRACE(0, 2)
+  double sd[4] = {0, 0, 0, 0};
+  if (valid) {
+    float p0, p1;
+    if (role == 0) {
+      motion_apply_eps(S, i, x0, x1, lr, v0, v1, e0, e1, p0, p1);
+      S.hidx[i] = (int64_t)N * grow + (mode == kSrcSoft ? src : i);
+    } else {
+      p0 = (x0 + v0) + e0;
+      p1 = (x1 + v1) + e1;
+    }
+    PairX x = pair_of(xbuf, xflag, role, slot);
+    float xd0, xd1;
+    stage_dyn_inverse_split(d, S, i, p0, p1, cbs, x, kTile, xd0, xd1);
+    if (role == 0) {
+      sd[0] = xd0;
+      sd[1] = xd1;
+      sd[2] = (double)xd0 * xd0;
+      sd[3] = (double)xd1 * xd1;
+    }
+  }
+  block_sum_roles_store(sd, ws.st_dyn + ((int64_t)b * tiles + tile) * 4, nullptr, shd);
+  TRACE(0, 3)
+}
+
 // softmax partials of the unshifted log-weight u over this tile
 __device__ __forceinline__ void store_softmax(float u, bool valid, double *sm, float *shf, double *shd) {
   // per wave (max, sum e^(u - max), sum e^(2(u - max))), merged over the waves with one
@@ -490,6 +716,49 @@ __device__ __forceinline__ void store_softmax(float u, bool valid, double *sm, f
     sm[0] = m;
     sm[1] = sum;
     sm[2] = sq;
+  }
+}
+
+// store_softmax (role-0 lanes carry u) plus, with the same barrier, the four deferred-
+// normalisation sums of the role-1 waves (block_sum_roles_store's order) into fin.
+// smd >= 48 doubles.
+__device__ __forceinline__ void store_softmax_fin(float u, bool valid, double *sm, const double (&sf)[4],
+                                                  double *fin, float *shf, double *shd) {
+  const float mw = wave_max_dpp(valid ? u : -INFINITY);
+  const float ev = valid ? expf(u - mw) : 0.f;
+  const double ew = wave_sum_dpp((double)ev);
+  const double qw = wave_sum_dpp((double)ev * ev);
+  double f4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) f4[k] = wave_sum_dpp(sf[k]);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    shf[w] = mw;
+    shd[2 * w] = ew;
+    shd[2 * w + 1] = qw;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) shd[16 + 4 * w + k] = f4[k];
+  }
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+  if (threadIdx.x == 0) {
+    float m = shf[0];
+    for (int k = 1; k < nw; ++k) m = fmaxf(m, shf[k]);
+    double sum = 0.0, sq = 0.0;
+    for (int k = 0; k < nw; ++k)
+      if (shf[k] > -INFINITY) {
+        const double f = (double)expf(shf[k] - m);
+        sum += shd[2 * k] * f;
+        sq += shd[2 * k + 1] * f * f;
+      }
+    sm[0] = m;
+    sm[1] = sum;
+    sm[2] = sq;
+  } else if (threadIdx.x >= 64 && threadIdx.x < 68) {  // role-1 waves 1, 3, 5, 7 in order
+    const int k = threadIdx.x - 64;
+    double a = shd[16 + 4 * 1 + k];
+    for (int q = 1; q < 4; ++q) a += shd[16 + 4 * (2 * q + 1) + k];
+    fin[k] = a;
   }
 }
 
@@ -539,7 +808,7 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
   const float lm = meas_shifted<MEAS>() ? block_max(lk, L.f) : 0.f;
   if (threadIdx.x == 0) sm[3] = lm;
-  __shared__ double smd[32];
+  __shared__ double smd[48];
   store_softmax(u, valid, sm, L.f + 8, smd);  // L.f[0:8] held block_max
   TRACE(2, 3)
 }
@@ -558,7 +827,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   __shared__ float lx[kTile];
   __shared__ float ssx[ROLES][kTile], dotx[ROLES][kTile];
   __shared__ float smf[16];   // per-wave softmax partials (up to 12 waves)
-  __shared__ double smd[32];
+  __shared__ double smd[48];
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -644,12 +913,13 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
 // net by net, then split the particle encoder's output layer (each computes the hidden
 // layers, then half of the 32 outputs) and exchange their partial |e|^2 and <e, v>.  No
 // wave idles and no workgroup barrier separates the stages.  512 threads per tile.
+template <bool MERGED>
 __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;  // cb_dyn / cb_cond in split order
   __shared__ float xbuf[4 * kTile];
   __shared__ int xflag[16];
   __shared__ float smf[16];
-  __shared__ double smd[32];
+  __shared__ double smd[48];
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -660,9 +930,13 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
   const bool valid = i < d.N;
   PropIn in{};
   float lr = 0.f;
+  // with the merged front + dyn launch, slot t-1's deferred normalisation runs here (role 1)
+  const bool defer_here = MERGED && d.defer_norm && d.t > 0 && role == 1;
+  PrevIn pv{};
   if (valid) {  // issued before the row prologue so they overlap it
     in = load_prop_in<true>(S, i);
     if (role == 0) lr = S.hp[i];
+    if (defer_here) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
   }
   measure_row_setup<NFDPF_MEAS_COS>(S.enc, d.meas_params, L);
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
@@ -702,7 +976,28 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
   TRACE(2, 2)
   double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
   if (threadIdx.x == 0) sm[3] = 0.f;
-  store_softmax(u, valid && role == 0, sm, smf, smd);
+  if (MERGED && d.defer_norm && d.t > 0) {
+    // finish_prev's arithmetic for slot t-1 on role 1; its four sums and this step's softmax
+    // partials share one barrier
+    double sf[4] = {0, 0, 0, 0};
+    if (defer_here && valid) {
+      const bool shifted = shifted_meas(d.measurement);
+      const RowNorm rn = row_norm(prev_sm(d, b, tiles), tiles, shifted);
+      const RowSlot Sp = row_slot(d, b, d.t - 1);
+      float lw, lk;
+      const float p = prev_p_of(pv, rn, shifted, lw, lk);
+      if (shifted) Sp.hlik[i] = lk;
+      Sp.hp[i] = p;
+      sf[0] = (double)p * p;
+      sf[1] = (double)p * pv.x0;
+      sf[2] = (double)p * pv.x1;
+      sf[3] = lw;
+    }
+    store_softmax_fin(u, valid && role == 0, sm, sf, ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4,
+                      smf, smd);
+  } else {
+    store_softmax(u, valid && role == 0, sm, smf, smd);
+  }
   TRACE(2, 3)
 }
 
@@ -803,6 +1098,13 @@ __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int t
 
 // the flows run on wave pairs when the blobs carry the split suffix (RealNVP nf_dyn)
 static bool use_split(const nfdpf_filter_desc &d) { return d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP; }
+// front + dyn in one launch (tiled_fdyn_kernel), the deferred normalisation in the proposal
+// launch: the split-net path with the cosine measurement, rows short enough for LDS
+constexpr int kMergedMaxN = 4096;
+static bool use_merged(const nfdpf_filter_desc &d) {
+  return use_split(d) && d.nf_cond && d.measurement == NFDPF_MEAS_COS && d.N <= kMergedMaxN &&
+         d.B_global <= kMergedMaxN;
+}
 
 template <bool NFD, bool NFC, int MEAS>
 static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStream_t st) {
@@ -810,8 +1112,12 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
   // (a third role splitting the cosine encoder's output layer was measured slower: 16.7 vs
   // 11.4 us for the compute phase at C2 -- the extra waves duplicate the encoder's first layers)
   if constexpr (NFD && NFC && MEAS == NFDPF_MEAS_COS) {
+    if (use_merged(d)) {
+      tiled_prop_split_kernel<true><<<g, 2 * kTile, 0, st>>>(d, ws);
+      return;
+    }
     if (use_split(d)) {
-      tiled_prop_split_kernel<<<g, 2 * kTile, 0, st>>>(d, ws);
+      tiled_prop_split_kernel<false><<<g, 2 * kTile, 0, st>>>(d, ws);
       return;
     }
   }
@@ -911,8 +1217,15 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
     // C / gate staging [max(N, B_global)], gathered weights [N], deferred p_{t-1} [N]
     const size_t lds = d.resampler == NFDPF_RESAMPLE_SOFT ? (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4
                                                          : (size_t)d.B_global * 4;
-    tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
-    if (use_split(d))
+    if (use_merged(d)) {
+      const size_t mlds = (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4;
+      tiled_fdyn_kernel<<<g, 2 * kTile, mlds, st>>>(d, ws);
+    } else {
+      tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
+    }
+    if (use_merged(d))
+      ;  // nf_dyn ran in tiled_fdyn_kernel
+    else if (use_split(d))
       tiled_dyn_kernel<true><<<g, 2 * kTile, 0, st>>>(d, ws);
     else if (d.nf_dyn)
       tiled_dyn_kernel<false><<<g, kTile, 0, st>>>(d, ws);

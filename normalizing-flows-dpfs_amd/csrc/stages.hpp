@@ -29,7 +29,7 @@ __device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b, i
   s.hidx = d.hist_idx + hrow;
   s.hjac = d.hist_jac ? d.hist_jac + hrow : nullptr;
   s.hprior = d.hist_prior ? d.hist_prior + hrow : nullptr;
-  s.scr = d.scratch + (int64_t)b * d.N * 4;
+  s.scr = d.scratch + ((int64_t)(t & 1) * d.B + b) * d.N * 4;  // double-buffered by step parity
   s.enc = d.enc + ((int64_t)b * d.T + t) * d.E;
   return s;
 }

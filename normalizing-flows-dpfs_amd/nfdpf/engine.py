@@ -193,7 +193,7 @@ class FilterEngine:
         hi = torch.empty((B, T, N), device=dev, dtype=torch.int64)
         hj = torch.empty((B, T, N), **f32) if c.NF_dyn else None
         hr = torch.empty((B, T, N), **f32) if c.NF_dyn else None
-        scratch = torch.empty((B, N, 4), **f32)
+        scratch = torch.empty((2, B, N, 4), **f32)  # by step parity (include/nfdpf.h)
         lw_sum = torch.empty((B, T), **f32)
         pred = torch.empty((B, T, 2), **f32)
         if tiled:
