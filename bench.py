@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--graph", type=int, default=1,
                     help="1: capture the whole T-step pass (all launches of filtering_pos) in a hipGraph and "
                          "replay it per step (device RNG, soft resampler, one GPU); 0: launch from Python")
+    ap.add_argument("--speculate", type=int, default=-1,
+                    help="speculative ESS gate (one exchange per pass, engine.FilterConfig.speculate_gate): "
+                         "-1 auto (on when sharded), 0 off (per-step exchange), 1 on (also at one GPU)")
     ap.add_argument("--kernel", default="tiled", choices=["tiled", "fused"],
                     help="tiled: multi-CU pipeline per step; fused: one workgroup per batch row")
     args = ap.parse_args()
@@ -222,6 +225,8 @@ def main():
     shard = ShardInfo.from_env(B)
     fcfg = dpf.filter_config()
     fcfg.kernel = args.kernel
+    if args.speculate >= 0:
+        fcfg.speculate_gate = bool(args.speculate)
     eng = FilterEngine(fcfg, dpf)
 
     def step():
@@ -231,18 +236,27 @@ def main():
         res = step()
     torch.cuda.synchronize()
     graph = None
-    if args.graph and world == 1 and flags["resampler_type"] == "soft":
+    spec_on = (world > 1) if args.speculate < 0 else bool(args.speculate)
+    spec = spec_on and args.kernel == "tiled" and flags["resampler_type"] == "soft" and not args.force_resample
+    if args.graph and flags["resampler_type"] == "soft" and (world == 1 or spec):
         # the pass has no host synchronisation in this mode: capture it once, replay per step
-        # (every launch of every time step runs on each replay; only the Python launch path goes)
+        # (every launch of every time step runs on each replay; only the Python launch path goes).
+        # Sharded: the speculative-gate pass (engine.run(finish=False): no exchange inside) is
+        # captured; after each replay finish_pending() gathers all steps' partials once,
+        # verifies the T gates and reduces the obs-likelihood -- a fired gate (never at the
+        # bench's init weights) reruns the pass with the per-step exchange, inside the timing.
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            res = step()
+            res = eng.run(enc, start, vel_in, shard=shard, finish=not spec)
         graph.replay()
         torch.cuda.synchronize()
+        cap = res
 
         def step():  # noqa: F811
             graph.replay()
-            return res
+            if spec and not eng.finish_pending():
+                return eng.run(enc, start, vel_in, shard=shard, speculate=False)
+            return cap
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -321,7 +335,8 @@ def main():
             "config": {"workload": f"{args.config}: DPF.filtering_pos, " + ", ".join(f"{k}={v}" for k, v in flags.items())
                        + f", N={N}, batch={B} per GPU, seq_len={T}, state_dim=4 (2-D particles), "
                          f"{'forced' if args.force_resample else 'ESS-gated'} resampling, device RNG, "
-                         f"{'hipGraph replay of the pass' if graph is not None else 'Python launches'}",
+                         f"{'hipGraph replay of the pass' if graph is not None else 'Python launches'}"
+                         + (", speculative ESS gate verified once per pass" if spec else ""),
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
                        "parallelism": f"batch-sharded x{world}"},
             "rmse": rmse,

@@ -221,6 +221,9 @@ typedef struct nfdpf_filter_desc {
   void *prof_events;        /* optional hipEvent_t[2]: recorded around the dominant launch
                                (the whole step for nfdpf_filter_step, the proposal+measurement
                                launch for nfdpf_filter_step_tiled) -- live kernel timing */
+  int32_t ess_local;        /* tiled: 1 = ess_all holds this shard's B rows only (row b at b), the
+                               gate coming from `gate` -- the speculative-gate mode of a sharded
+                               batch (nfdpf_ess_gate_tiled_batch verifies it after the pass) */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
@@ -244,6 +247,11 @@ NFDPF_API int nfdpf_filter_step_tiled(const nfdpf_filter_desc *d, void *workspac
  * -> int32 [1] (OT path) */
 NFDPF_API int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, int force, int32_t *gate,
                          void *stream);
+/* The tiled gate of T steps at once: parts [T][B_global][tiles][4] (step t's input partials,
+ * i.e. the previous step's outputs gathered over the shards) -> gates [T] int32 (step t uses
+ * the +1e-12 terms iff t0 + t > 0).  Verifies a speculative pass (every gate assumed off). */
+NFDPF_API int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int N, int t0, int force,
+                                         int32_t *gates, void *stream);
 
 #ifdef __cplusplus
 }

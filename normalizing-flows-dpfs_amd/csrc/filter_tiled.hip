@@ -180,9 +180,13 @@ __device__ __forceinline__ float prev_p_of(const PrevIn &v, const RowNorm &rn, b
   return expf(lw - rn.shift) / rn.Ssum + 1e-12f;
 }
 // row b's softmax partials inside ess_all (global rows when the batch is sharded)
+// row of ess_all holding local row b: the global row of a sharded batch, unless the
+// speculative-gate mode keeps only this shard's rows (ess_local)
+__device__ __forceinline__ int64_t ess_row(const nfdpf_filter_desc &d, int b) {
+  return (!d.ess_local && d.row_base + d.B <= d.B_global) ? d.row_base + b : b;
+}
 __device__ __forceinline__ const double *prev_sm(const nfdpf_filter_desc &d, int b, int tiles) {
-  const int64_t r = d.row_base + d.B <= d.B_global ? d.row_base + b : b;
-  return reinterpret_cast<const double *>(d.ess_all) + r * tiles * kSm;
+  return reinterpret_cast<const double *>(d.ess_all) + ess_row(d, b) * tiles * kSm;
 }
 
 // Deferred normalisation of step t-1 (defer_norm, t > 0): slot t-1's weights are written by
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   float e0 = 0.f, e1 = 0.f;
   if (i < N) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: computed under its latency
   __shared__ RowNorm rn_sh;
-  const int64_t my_row = d.row_base + d.B <= d.B_global ? d.row_base + b : b;
+  const int64_t my_row = ess_row(d, b);
   const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh, defer ? my_row : -1, &rn_sh,
                                      shifted_meas(d.measurement));
   TRACE(0, 1)
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
   float e0 = 0.f, e1 = 0.f;
   if (valid) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: under its latency
-  const int64_t my_row = d.row_base + d.B <= d.B_global ? d.row_base + b : b;
+  const int64_t my_row = ess_row(d, b);
   const RowSlot S = row_slot(d, b);
   const float *xprev = d.x_prev + b * d.x_prev_rs;
   const float *pprev = d.p_prev + b * d.p_prev_rs;
@@ -1096,6 +1100,16 @@ __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int t
   if (threadIdx.x == 0) gate[0] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 
+// the same for T steps, one wave each (block = step)
+__global__ void tiled_gate_batch_kernel(const double *__restrict__ parts, int B, int tiles, int N, int t0,
+                                        int force, int32_t *gates) {
+  const int k = blockIdx.x;
+  const double *p = parts + (int64_t)k * B * tiles * kSm;
+  const float s = cascade_row_sum([&](int r) { return row_inv_ess(p + (int64_t)r * tiles * kSm, tiles, N, t0 + k > 0); },
+                                  force ? 0 : B);
+  if (threadIdx.x == 0) gates[k] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
+}
+
 // the flows run on wave pairs when the blobs carry the split suffix (RealNVP nf_dyn)
 static bool use_split(const nfdpf_filter_desc &d) { return d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP; }
 // front + dyn in one launch (tiled_fdyn_kernel), the deferred normalisation in the proposal
@@ -1154,6 +1168,15 @@ extern "C" int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, in
   NFDPF_REQUIRE(gate && (force || parts) && B >= 1 && N >= 1, "nfdpf_ess_gate_tiled: bad arguments");
   tiled_gate_kernel<<<1, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, t, force, gate);
   return launch_status("nfdpf_ess_gate_tiled");
+}
+
+extern "C" int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int N, int t0, int force,
+                                          int32_t *gates, void *stream) {
+  NFDPF_REQUIRE(gates && (force || parts) && T >= 0 && B >= 1 && N >= 1 && t0 >= 0,
+                "nfdpf_ess_gate_tiled_batch: bad arguments");
+  if (T == 0) return NFDPF_OK;
+  tiled_gate_batch_kernel<<<T, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, t0, force, gates);
+  return launch_status("nfdpf_ess_gate_tiled_batch");
 }
 
 extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,

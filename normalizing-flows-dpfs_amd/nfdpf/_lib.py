@@ -44,6 +44,7 @@ class FilterDesc(Structure):
         ("hist_jac", c_void_p), ("hist_prior", c_void_p), ("hist_idx", c_void_p),
         ("ess_out", c_void_p), ("lw_sum", c_void_p), ("pred", c_void_p), ("scratch", c_void_p),
         ("prof_events", c_void_p),
+        ("ess_local", c_int32),
     ]
 
 
@@ -77,6 +78,7 @@ SIGNATURES = {
     "nfdpf_filter_tiled_init": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_filter_step_tiled": (c_int, [POINTER(FilterDesc), c_void_p, c_void_p]),
     "nfdpf_ess_gate_tiled": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_ess_gate_tiled_batch": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None

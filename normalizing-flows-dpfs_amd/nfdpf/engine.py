@@ -50,6 +50,10 @@ class FilterConfig:
     force_resample: bool = False
     kernel: str = "tiled"        # "tiled" (multi-CU pipeline per step) | "fused" (one launch per step)
     split_nets: bool = True      # tiled: coupling nets on wave pairs (csrc/split.hpp) where the flows allow
+    # sharded tiled soft pass: run every step with the ESS gate assumed off and no per-step
+    # exchange, then gather all steps' softmax partials once and verify the gates (a fired
+    # gate reruns the pass with the per-step exchange); None = on when the batch is sharded
+    speculate_gate: Optional[bool] = None
 
 
 @dataclass
@@ -149,10 +153,17 @@ class FilterEngine:
     @torch.no_grad()
     def run(self, enc: torch.Tensor, start_state: torch.Tensor, vel_input: torch.Tensor,
             shard: Optional[ShardInfo] = None, host: Optional[HostDraws] = None, init=None,
-            teacher=None) -> FilterResult:
+            teacher=None, finish: bool = True, speculate: Optional[bool] = None) -> FilterResult:
         """``teacher`` (tests only): dict with the reference's own history ``x`` (B,T,N,2) and
         ``p`` (B,T,N); step t then starts from the reference's step t-1 state and its gate
-        is the reference's own torch expression (one-step parity)."""
+        is the reference's own torch expression (one-step parity).
+
+        Speculative-gate mode (``cfg.speculate_gate``): the pass runs with every ESS gate
+        assumed off and no exchange between the shards; with ``finish`` the gates are then
+        verified from all steps' gathered partials (one all-gather) and a fired gate reruns
+        the pass with the per-step exchange -- the result is the reference's either way.
+        ``finish=False`` leaves the verification to ``finish_pending()`` (the pass itself is
+        then free of collectives and host syncs: capturable in a graph)."""
         c = self.cfg
         dev = enc.device
         L.require_device(enc, "FilterEngine.run")
@@ -184,6 +195,10 @@ class FilterEngine:
                                           c.seed, shard.row_base, dev)
         p0, ie0 = ops.normalize_log_probs(logw0)
         tiled = c.kernel == "tiled"
+        if speculate is None:
+            speculate = c.speculate_gate if c.speculate_gate is not None else shard.world > 1
+        spec = bool(speculate and tiled and c.resampler == "soft" and not host_mode and teacher is None
+                    and not c.force_resample and not external)
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)
@@ -201,17 +216,23 @@ class FilterEngine:
             tiles = ops.tiled_tiles(N)
             # per-(row, tile) softmax partials {max u, sum e, sum e^2, max lik} of each step:
             # the next step's gate and (deferred) normalisation derive from them
-            ess_bufs = [torch.empty((B, tiles, 4), device=dev, dtype=torch.float64) for _ in range(2)]
-            ess0 = ops.tiled_init(p0, torch.empty((B, tiles, 4), device=dev, dtype=torch.float64))
+            if spec:  # every step's partials kept for the verification
+                ess_hist = torch.empty((T + 1, B, tiles, 4), device=dev, dtype=torch.float64)
+                ess_bufs = [ess_hist[t] for t in range(1, T + 1)]
+                ess0 = ops.tiled_init(p0, ess_hist[0])
+            else:
+                ess_bufs = [torch.empty((B, tiles, 4), device=dev, dtype=torch.float64) for _ in range(2)]
+                ess0 = ops.tiled_init(p0, torch.empty((B, tiles, 4), device=dev, dtype=torch.float64))
             ws = ops.tiled_workspace(B, N, T, dev)
             gather_buf = torch.empty((shard.B_global, tiles, 4), device=dev, dtype=torch.float64) \
-                if shard.world > 1 else None
+                if shard.world > 1 and not spec else None
         else:
             ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
             ess0 = ie0
             gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
-        ess_all = self._gather(ess0, shard)
+        ess_all = ess0 if spec else self._gather(ess0, shard)
         gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
+        spec_gate = torch.zeros(1, device=dev, dtype=torch.int32) if spec else None
         # velocity used by each step's motion: start velocity, then vel_input[:, t-1] (DPFs.py:158,173)
         vel_steps = torch.cat([start_state[:, None, 2:4].to(dev), vel_input[:, :T - 1].to(dev)], 1)
         vel_steps = vel_steps.transpose(0, 1).contiguous()  # (T, B, 2)
@@ -243,6 +264,7 @@ class FilterEngine:
         d.hist_x, d.hist_p, d.hist_noise, d.hist_lik = hx.data_ptr(), hp.data_ptr(), hn.data_ptr(), hl.data_ptr()
         d.hist_jac, d.hist_prior, d.hist_idx = L.ptr(hj), L.ptr(hr), hi.data_ptr()
         d.lw_sum, d.pred, d.scratch = lw_sum.data_ptr(), pred.data_ptr(), scratch.data_ptr()
+        d.ess_local = int(spec)
 
         fired = [] if host_mode else None
         self.last_ot_calls = 0
@@ -251,6 +273,8 @@ class FilterEngine:
         # time step, so it stays free of tensor slicing and per-call lookups
         hx_p, hp_p, vel_p = hx.data_ptr(), hp.data_ptr(), vel_steps.data_ptr()
         ess_out_p = [b.data_ptr() for b in ess_bufs]
+        ess_in_p = [ess0.data_ptr()] + ess_out_p[:-1] if spec else None
+        spec_gate_p = spec_gate.data_ptr() if spec else None
         stream = ops.stream_ptr(dev)
         launch = L.lib().nfdpf_filter_step_tiled if tiled else L.lib().nfdpf_filter_step
         ws_p = ops._aligned_ptr(ws) if tiled else None
@@ -274,9 +298,12 @@ class FilterEngine:
                 d.x_prev_rs, d.p_prev_rs = T * N * 2, T * N
             d.t = t
             d.vel = vel_p + t * B * 8
-            d.ess_all = ess_all.data_ptr()
-            d.ess_out = ess_out_p[t & 1]
-            d.gate = None
+            if spec:  # this shard's own partials; the gate assumed off (verified after the pass)
+                d.ess_all, d.ess_out, d.gate = ess_in_p[t], ess_out_p[t], spec_gate_p
+            else:
+                d.ess_all = ess_all.data_ptr()
+                d.ess_out = ess_out_p[t & 1]
+                d.gate = None
             d.host_noise = d.host_offsets = None
             if host_mode:
                 if teacher is not None and t > 0:
@@ -345,16 +372,44 @@ class FilterEngine:
                 step()
             else:
                 step()
-            if shard.world > 1:
+            if spec:
+                pass
+            elif shard.world > 1:
                 ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
             else:
                 ess_all = ess_bufs[t & 1]
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)
+        if spec:
+            res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
+            self._pending = (ess_hist[:T], tot, shard, N, res)
+            if not finish:
+                return res
+            if self.finish_pending():
+                return res
+            # a gate fired: the pass again, with the per-step exchange
+            return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, speculate=False)
         if shard.world > 1:
             dist.all_reduce(tot, group=shard.group)
         obs = (tot / (shard.B_global * N)).sum().float()
         return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, obs, pred, fired)
+
+    def finish_pending(self) -> bool:
+        """Verify the speculative pass of the last ``run`` (its buffers, so also after a graph
+        replay of it): gather every step's softmax partials over the shards (one all-gather),
+        evaluate all T gates (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the
+        obs-likelihood into the result.  False: some gate fired -- the pass is not the
+        reference's and must be rerun without speculation (run(..., speculate=False))."""
+        parts, tot, shard, N, res = self._pending
+        tot = tot.clone()
+        parts = self._gather_steps(parts, shard)
+        if shard.world > 1:
+            dist.all_reduce(tot, group=shard.group)
+        gates = ops.ess_gate_tiled_batch(parts, N, 0, False)
+        if bool(gates.any()):
+            return False
+        res.obs_likelihood = (tot / (shard.B_global * N)).sum().float()
+        return True
 
     # -- helpers ----------------------------------------------------------------------------
     def _ot_global_stop(self, xin, pin, it, shard: ShardInfo, gate_buf):
@@ -376,6 +431,19 @@ class FilterEngine:
         out = torch.empty((shard.B_global,) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
         dist.all_gather_into_tensor(out, t.contiguous(), group=shard.group)
         return out.cpu()
+
+    @staticmethod
+    def _gather_steps(parts: torch.Tensor, shard: ShardInfo) -> torch.Tensor:
+        """[T, B, tiles, 4] per-shard step partials -> [T, B_global, tiles, 4] (rows in rank
+        order = global row order), one all-gather."""
+        if shard.world == 1:
+            return parts
+        T, B = parts.shape[0], parts.shape[1]
+        # concatenated along dim 0 (the layout every backend accepts), then rank-major -> row order
+        g = torch.empty((shard.world * T,) + tuple(parts.shape[1:]), device=parts.device, dtype=parts.dtype)
+        dist.all_gather_into_tensor(g, parts.contiguous(), group=shard.group)
+        g = g.view((shard.world, T) + tuple(parts.shape[1:]))
+        return g.transpose(0, 1).reshape((T, shard.world * B) + tuple(parts.shape[2:]))
 
     @staticmethod
     def _gather(ie: torch.Tensor, shard: ShardInfo, buf=None) -> torch.Tensor:

@@ -233,5 +233,16 @@ def ess_gate_tiled(parts, N, t, force=False, out=None):
     return g
 
 
+def ess_gate_tiled_batch(parts, N, t0=0, force=False, out=None):
+    """Gates of T consecutive steps from [T, B_global, tiles, 4] input partials -> int32 [T]
+    (the verification of a speculative sharded pass, include/nfdpf.h)."""
+    T, B = parts.shape[0], parts.shape[1]
+    g = out if out is not None else torch.empty(T, device=parts.device, dtype=torch.int32)
+    parts = parts.to(torch.float64).contiguous()
+    check(lib().nfdpf_ess_gate_tiled_batch(ptr(parts), T, B, N, int(t0), int(bool(force)), ptr(g),
+                                           stream_ptr(parts.device)), "nfdpf_ess_gate_tiled_batch")
+    return g
+
+
 def filter_step_tiled(desc: L.FilterDesc, ws: torch.Tensor, device):
     check(lib().nfdpf_filter_step_tiled(desc, _aligned_ptr(ws), stream_ptr(device)), "nfdpf_filter_step_tiled")

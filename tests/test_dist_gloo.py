@@ -42,11 +42,14 @@ def _worker(rank, world, port, q):
         lw = torch.full((B, 4), float(rank + 1))
         tot = lw.double().sum(0)
         dist.all_reduce(tot)
+        # speculative-gate verification: every step's [B, tiles, 4] partials gathered at once
+        steps = torch.arange(5 * B * 3 * 4, dtype=torch.float64).reshape(5, B, 3, 4) + 1000 * rank
+        allsteps = FilterEngine._gather_steps(steps, sh)
         # OT stop (engine._ot_global_stop): the MIN over ranks of the local iteration count
         it = torch.tensor([31 + 7 * rank], dtype=torch.int32)
         dist.all_reduce(it, op=dist.ReduceOp.MIN)
         q.put((rank, sh.world, sh.B_global, sh.row_base, gathered.numpy(), gate, nz.numpy(), tot.numpy(),
-               int(it.item())))
+               int(it.item()), allsteps.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -71,7 +74,10 @@ def test_sharded_exchange_world2():
     inv_all = torch.rand(world * B, generator=torch.Generator().manual_seed(7)) * N
     ref_gate = FilterEngine._host_gate(inv_all, N, False)
     ref_noise = HostDraws(torch.Generator().manual_seed(11)).noise(world * B, N, 20.0)
-    for rank, w, bg, base, gathered, gate, nz, tot, it in res:
+    steps = [torch.arange(5 * B * 3 * 4, dtype=torch.float64).reshape(5, B, 3, 4) + 1000 * r for r in range(world)]
+    ref_steps = torch.cat(steps, 1).numpy()  # [T, B_global, tiles, 4], rows in rank order
+    for rank, w, bg, base, gathered, gate, nz, tot, it, allsteps in res:
+        np.testing.assert_array_equal(allsteps, ref_steps)
         assert it == 31
         assert (w, bg, base) == (world, world * B, rank * B)
         np.testing.assert_array_equal(gathered, inv_all.numpy())

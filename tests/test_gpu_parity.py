@@ -563,3 +563,56 @@ def test_split_nets_match_pair_layout(gated):
     assert torch.allclose(a.jac[:, :2], b.jac[:, :2], rtol=1e-4, atol=1e-4)
     assert torch.allclose(a.prior[:, :2], b.prior[:, :2], rtol=1e-4, atol=1e-3)
     assert torch.allclose(a.pred[:, :2], b.pred[:, :2], rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("aligned", [False, True])
+def test_speculative_gate_matches_exchange(aligned):
+    """Speculative-gate mode (every gate assumed off, verified after the pass from all steps'
+    partials, rerun on a fired gate) returns exactly the per-step-gate pass: bit-identical
+    histories and obs-likelihood.  aligned=True uses the fixture's encodings aligned with the
+    true state, on which the gate fires -- the verification must catch it and rerun."""
+    from nfdpf.engine import FilterConfig, FilterEngine
+    fx = load("e2e_c2.npz")
+    c = e2e_cfg(fx)
+    models = _Models(weights(fx), c)
+    if aligned:
+        enc, start, vel = t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV)
+        N = int(fx["N"])
+    else:
+        g = torch.Generator().manual_seed(5)
+        B, T, N = 6, 8, 1000
+        enc = torch.randn(B, T, 32, generator=g).to(DEV)
+        start = (torch.randn(B, 4, generator=g) * 10).to(DEV)
+        vel = (torch.randn(B, T, 2, generator=g) * 3).to(DEV)
+    out = {}
+    for spec in (False, True):
+        cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=77,
+                           kernel="tiled", speculate_gate=spec)
+        out[spec] = FilterEngine(cfg, models).run(enc, start, vel)
+    a, b = out[False], out[True]
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert torch.equal(a.obs_likelihood, b.obs_likelihood)
+    B, T = enc.shape[0], enc.shape[1]
+    ident = torch.arange(N, device=DEV) + N * torch.arange(B, device=DEV)[:, None]
+    fired = int((a.index != ident[:, None, :]).any(-1).any(0).sum())
+    assert (fired > 0) == aligned, fired
+
+
+def test_gate_batch_matches_single():
+    """nfdpf_ess_gate_tiled_batch == nfdpf_ess_gate_tiled step by step (both branches)."""
+    from nfdpf import ops
+    g = torch.Generator().manual_seed(6)
+    T, B, N = 7, 5, 1000
+    tiles = ops.tiled_tiles(N)
+    parts = torch.zeros(T, B, tiles, 4, dtype=torch.float64)
+    parts[..., 0] = torch.randn(T, B, tiles, generator=g, dtype=torch.float64) * 0.01
+    parts[..., 1] = 250.0 * (1 + 0.1 * torch.rand(T, B, tiles, generator=g, dtype=torch.float64))
+    # sum e^2 ~ sum e (spread weights, 1/sum p^2 ~ N: gate off) or ~ (sum e)^2 (peaked: on)
+    peak = (torch.arange(T) % 2 == 1)[:, None, None]
+    parts[..., 2] = torch.where(peak, parts[..., 1] ** 2, parts[..., 1])
+    parts = parts.to(DEV)
+    batch = ops.ess_gate_tiled_batch(parts, N, 0, False).cpu()
+    single = torch.stack([ops.ess_gate_tiled(parts[k].contiguous(), N, k).cpu()[0] for k in range(T)])
+    assert torch.equal(batch, single)
+    assert 0 < int(batch.sum()) < T
