@@ -204,10 +204,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # more ranks than devices (a rehearsal on a one-GPU box) share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # "nccl" is RCCL over xGMI; NFDPF_DIST_BACKEND=gloo only for rehearsing several ranks on
+        # one device (RCCL refuses two ranks on one GPU)
+        backend = os.environ.get("NFDPF_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from DPFs import DPF
     from nfdpf.engine import FilterEngine, ShardInfo

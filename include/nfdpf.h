@@ -93,6 +93,26 @@ NFDPF_API int nfdpf_cond_stack(const float *params, int n_flows, int dim, int ob
                      int inverse, float prior_mean, float prior_std,
                      float *out, float *logdet, float *prior_logprob, void *stream);
 
+/* Backward of nfdpf_cond_stack (training); replaces the autograd graph the
+ * reference builds over nf/flows.py:215-239 (RealNVP_cond.forward/.inverse) and
+ * nf/models.py:45-61 (NormalizingFlowModel_cond.forward/.inverse, prior log-prob :51).
+ * Per-row condition only (cond_group = 1: the reference's materialised obser).
+ *   g_out [rows, dim], g_logdet [rows]: dL/d(out, logdet); g_prior_logprob [rows] or NULL
+ *   (forward only)
+ *   g_x [rows, dim]; g_cond [rows, obser_dim] (may be NULL); g_params [blob floats] in the
+ *   blob layout of params (every entry a {t, s} pair, as nfdpf_cond_stack reads it)
+ *   workspace: nfdpf_cond_stack_backward_workspace() bytes (per-workgroup parameter partials,
+ *   summed in a fixed order: the result is deterministic)
+ * Built for dim in {2, 4, 32}, hidden 8, n_flows 1..4, LDS-bound obser_dim (<= ~400 at dim 2). */
+NFDPF_API int64_t nfdpf_cond_stack_backward_workspace(int n_flows, int dim, int obser_dim, int hidden,
+                                                      int64_t rows);
+NFDPF_API int nfdpf_cond_stack_backward(const float *params, int n_flows, int dim, int obser_dim,
+                                        int hidden, const float *x, const float *cond, int64_t rows,
+                                        int inverse, float prior_mean, float prior_std,
+                                        const float *g_out, const float *g_logdet,
+                                        const float *g_prior_logprob, float *g_x, float *g_cond,
+                                        float *g_params, void *workspace, void *stream);
+
 /* NormalizingFlowModel.forward / .inverse over MAF flows (nf/models.py:13-30,
  * nf/flows.py:259-284; forward flips the output).  x/out [rows, dim], logdet [rows]. */
 NFDPF_API int nfdpf_maf_stack(const float *params, int n_flows, int dim, int hidden, const float *x,

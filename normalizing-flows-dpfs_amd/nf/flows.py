@@ -111,6 +111,35 @@ class CouplingStack:
                                       obser, 1, self.inverse, pm, ps, want_prior=self.prior is not None)
         return (out, ld) if lp is None else (out, ld, lp)
 
+    def hip_backward(self, x, obser, gouts):
+        """d/d(x, obser, parameters) by nfdpf_cond_stack_backward (csrc/flows_bwd.hip); None when
+        the kernel does not cover the case (autograd then differentiates ``torch``)."""
+        rows = x.shape[0]
+        if (self.dim not in (2, 4, 32) or self.hidden != 8 or not 1 <= len(self.flows) <= 4
+                or (self.obser_dim and (obser is None or obser.dim() != 2 or obser.shape[0] != rows))):
+            return None
+        b = blob(self.owner, "stack", self.flows, lambda: flows_tensors(self.flows), x.device)
+        g_out = gouts[0] if gouts[0] is not None else torch.zeros_like(x, dtype=torch.float32)
+        g_ld = gouts[1] if gouts[1] is not None else torch.zeros(rows, device=x.device)
+        g_lp = gouts[2] if len(gouts) > 2 else None
+        pm, ps = self.prior if self.prior is not None else (0.0, 1.0)
+        gx, gc, gb = _ops.cond_stack_backward(b, len(self.flows), self.dim, self.obser_dim, self.hidden,
+                                              x.float(), obser.float() if self.obser_dim else None,
+                                              self.inverse, g_out.float(), g_ld.float(),
+                                              None if g_lp is None else g_lp.float(), pm, ps)
+        # blob -> parameters: the packed blob is a fixed gather of the parameters (nfdpf.pack)
+        params = _params(self.flows)
+        gp = [None] * len(params)
+        req = [i for i, p in enumerate(params) if p.requires_grad]
+        if req:
+            with torch.enable_grad():
+                flat = torch.cat([t.reshape(-1) for t in flows_tensors(self.flows)])
+                g = torch.autograd.grad(flat, [params[i] for i in req], gb, allow_unused=True)
+            for i, gi in zip(req, g):
+                gp[i] = gi
+        gobs = None if gc is None else gc.to(obser.dtype)
+        return (gx.to(x.dtype), gobs), gp
+
     def torch(self, x, obser):
         ld = torch.zeros(x.shape[0], device=x.device)
         seq = self.flows[::-1] if self.inverse else self.flows

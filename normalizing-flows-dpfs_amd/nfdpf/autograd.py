@@ -1,13 +1,18 @@
-"""HIP forward + recompute backward for the standalone flow / measurement ops.
+"""Autograd for the HIP flow / measurement ops (training).
 
-Training (autograd) is §8(f1) "next" in SURVEY.md: the forward value always comes from the
-HIP kernel; the backward re-runs the same math as PyTorch ops on the saved inputs and
-differentiates that (activation-recompute style).  Dedicated HIP backward kernels replace
-this in a later round.
+The forward value always comes from the HIP kernel.  Backward: a runner with a HIP backward
+(``runner.hip_backward``: the RealNVP(_cond) coupling stacks, csrc/flows_bwd.hip) returns the
+input and parameter gradients from the kernel; the other runners (MAF, measurements) re-run
+the same math as PyTorch ops on the saved inputs and differentiate that (activation-recompute
+style).  ``NFDPF_HIP_BACKWARD=0`` sends every runner down the recompute path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+HIP_BACKWARD = os.environ.get("NFDPF_HIP_BACKWARD", "1") != "0"
 
 
 class _RecomputeFn(torch.autograd.Function):
@@ -26,6 +31,14 @@ class _RecomputeFn(torch.autograd.Function):
         saved = ctx.saved_tensors
         n_in = ctx.n_in
         ins, params = saved[:n_in], saved[n_in:]
+        hb = getattr(ctx.runner, "hip_backward", None)
+        if HIP_BACKWARD and hb is not None:
+            got = hb(*ins, gouts)
+            if got is not None:
+                gin, gpar = got
+                gin = [g if (t is not None and t.requires_grad) else None for g, t in zip(gin, ins)]
+                gpar = [g if p.requires_grad else None for g, p in zip(gpar, params)]
+                return (None, None) + tuple(gin) + tuple(gpar)
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(t.requires_grad) if t is not None and t.is_floating_point() else t
                       for t in ins]

@@ -37,6 +37,31 @@ def cond_stack(blob, n_flows, dim, obser_dim, hidden, x, cond, cond_group=1, inv
     return out, ld, lp
 
 
+def cond_stack_backward(blob, n_flows, dim, obser_dim, hidden, x, cond, inverse, g_out, g_logdet,
+                        g_prior=None, prior_mean=0.0, prior_std=1.0):
+    """Backward of cond_stack with a per-row condition -> (g_x, g_cond or None, g_blob)
+    (include/nfdpf.h nfdpf_cond_stack_backward)."""
+    require_device(x, "cond_stack_backward")
+    x, g_out, g_logdet = _c(x), _c(g_out), _c(g_logdet)
+    rows = x.shape[0]
+    cond = _c(cond) if cond is not None and obser_dim > 0 else None
+    if cond is not None and cond.shape[0] != rows:
+        raise ValueError(f"cond_stack_backward: cond has {cond.shape[0]} rows, x has {rows} (per-row condition only)")
+    g_prior = _c(g_prior) if g_prior is not None and not inverse else None
+    gx = torch.empty_like(x)
+    gc = torch.empty_like(cond) if cond is not None else None
+    gb = torch.empty_like(blob)
+    nbytes = lib().nfdpf_cond_stack_backward_workspace(n_flows, dim, obser_dim, hidden, rows)
+    if nbytes < 0:
+        raise L.NfdpfError(f"cond_stack_backward: bad sizes (n_flows={n_flows}, dim={dim}, hidden={hidden})")
+    ws = torch.empty(max(1, nbytes // 4), device=x.device, dtype=f32)
+    check(lib().nfdpf_cond_stack_backward(ptr(blob), n_flows, dim, obser_dim, hidden, ptr(x), ptr(cond), rows,
+                                          int(bool(inverse)), float(prior_mean), float(prior_std), ptr(g_out),
+                                          ptr(g_logdet), ptr(g_prior), ptr(gx), ptr(gc), ptr(gb), ptr(ws),
+                                          stream_ptr(x.device)), "nfdpf_cond_stack_backward")
+    return gx, gc, gb
+
+
 def maf_stack(blob, n_flows, dim, hidden, x, inverse=False):
     """NormalizingFlowModel over MAF flows (nf/models.py:13-30, nf/flows.py:259-284)."""
     require_device(x, "maf_stack")

@@ -1,0 +1,187 @@
+"""HIP backward of the coupling-flow stacks (csrc/flows_bwd.hip, nfdpf_cond_stack_backward)
+against PyTorch autograd of the same math in float64 (and float32 to size the tolerance).
+GPU box only.
+
+The reference's training path differentiates NormalizingFlowModel_cond.forward / .inverse
+(nf/models.py:45-61) over RealNVP_cond (nf/flows.py:215-239) with autograd; the module API
+here routes that backward through the HIP kernel (nfdpf.autograd).
+
+Tolerance: per tensor, |d| <= 4 * |err32| + 1e-6 * max|ref|, elementwise, where err32 is the
+float32 autograd's own error against float64 on the same inputs, plus a global cap
+|d| <= 2e-4 |ref| + 2e-5 max|ref| -- the parameter gradients are sums over every row, so
+their accumulation order (per-64-row partials, then per-workgroup) differs from ATen's.
+"""
+import copy
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _ref_stack(flows, x, c, inverse, prior, dtype):
+    """RealNVP_cond stack (nf/flows.py:215-239, nf/models.py:45-61) in plain torch ops."""
+    def net(m, a):
+        l0, l2, l4 = [l for l in m.network if isinstance(l, torch.nn.Linear)]
+        h = torch.tanh(F.linear(a, l0.weight.to(dtype), l0.bias.to(dtype)))
+        h = torch.tanh(F.linear(h, l2.weight.to(dtype), l2.bias.to(dtype)))
+        return F.linear(h, l4.weight.to(dtype), l4.bias.to(dtype))
+
+    cat = (lambda a: torch.cat([a, c], -1)) if c is not None else (lambda a: a)
+    ld = torch.zeros(x.shape[0], dtype=dtype, device=x.device)
+    for f in (flows[::-1] if inverse else flows):
+        half = x.shape[1] // 2
+        lo, up = x[:, :half], x[:, half:]
+        if not inverse:
+            t1, s1 = net(f.t1, cat(lo)), net(f.s1, cat(lo))
+            up = t1 + up * torch.exp(s1)
+            t2, s2 = net(f.t2, cat(up)), net(f.s2, cat(up))
+            lo = t2 + lo * torch.exp(s2)
+            ld = ld + s1.sum(1) + s2.sum(1)
+        else:
+            t2, s2 = net(f.t2, cat(up)), net(f.s2, cat(up))
+            lo = (lo - t2) * torch.exp(-s2)
+            t1, s1 = net(f.t1, cat(lo)), net(f.s1, cat(lo))
+            up = (up - t1) * torch.exp(-s1)
+            ld = ld - s1.sum(1) - s2.sum(1)
+        x = torch.cat([lo, up], 1)
+    if prior is None or inverse:
+        return x, ld, None
+    pm, ps = prior
+    d = x.shape[1]
+    z = (x - pm) / ps
+    lp = -0.5 * (z * z).sum(-1) - d * math.log(ps) - 0.5 * d * math.log(2 * math.pi)
+    return x, ld, lp
+
+
+def _build(D, O, n_flows, std, seed):
+    from nf.flows import RealNVP_cond, RealNVP
+    torch.manual_seed(seed)
+    flows = []
+    for _ in range(n_flows):
+        f = RealNVP_cond(D, 8, obser_dim=O) if O else RealNVP(D, 8)
+        f.zero_initialization(std)
+        # non-zero biases, so every bias gradient path is exercised
+        with torch.no_grad():
+            for p in f.parameters():
+                if p.dim() == 1:
+                    p.normal_(0, std)
+        flows.append(f)
+    return flows
+
+
+def _grads(loss, tensors):
+    return torch.autograd.grad(loss, tensors, allow_unused=True)
+
+
+def _check(ours, r32, r64, what, rel_cap=2e-4, abs_cap=2e-5):
+    ours, r32, r64 = ours.double().cpu(), r32.double().cpu(), r64.double().cpu()
+    scale = float(r64.abs().max()) + 1e-30
+    d = (ours - r64).abs()
+    e32 = (r32 - r64).abs()
+    env = 4 * e32 + 1e-6 * scale
+    cap = rel_cap * r64.abs() + abs_cap * scale
+    bad = (d > torch.maximum(env, cap))
+    assert not bool(bad.any()), (
+        f"{what}: {int(bad.sum())}/{d.numel()} outside; max |d| {float(d.max()):.3g} "
+        f"(fp32 err max {float(e32.max()):.3g}, scale {scale:.3g})")
+
+
+CASES = [  # (D, O, n_flows, std, rows)
+    (2, 4, 2, 0.01, 5000),     # nf_dyn, reference init (nf/flows.py:191-211)
+    (2, 4, 2, 0.3, 4097),
+    (2, 36, 2, 0.3, 3001),     # NF proposal context (model/models.py:334-356)
+    (2, 196, 2, 0.1, 777),     # CGLOW-size context
+    (32, 32, 2, 0.3, 1000),    # CRNVP measurement flow
+    (4, 0, 2, 0.3, 2048),      # unconditional RealNVP
+    (2, 36, 1, 0.3, 1),        # one row, one flow
+    (2, 4, 4, 0.3, 65),        # four flows, ragged last wave
+]
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("D,O,n_flows,std,rows", CASES)
+def test_cond_stack_backward_vs_autograd(D, O, n_flows, std, rows, inverse, monkeypatch):
+    from nf.models import NormalizingFlowModel, NormalizingFlowModel_cond
+    from nfdpf import ops
+    calls = []
+    real = ops.cond_stack_backward
+    monkeypatch.setattr(ops, "cond_stack_backward", lambda *a, **k: calls.append(1) or real(*a, **k))
+    flows = _build(D, O, n_flows, std, seed=D * 1000 + O * 10 + n_flows)
+    ref_flows = copy.deepcopy(flows)
+    g = torch.Generator().manual_seed(rows)
+    x = (torch.randn(rows, D, generator=g) * 3).to(DEV).requires_grad_(True)
+    c = torch.randn(rows, O, generator=g).to(DEV).requires_grad_(True) if O else None
+    w_out = torch.randn(rows, D, generator=g)
+    w_ld = torch.randn(rows, generator=g)
+    w_lp = torch.randn(rows, generator=g)
+    prior = (0.0, 2.5)
+    if O:
+        prior_d = torch.distributions.MultivariateNormal(torch.zeros(D, device=DEV), 6.25 * torch.eye(D, device=DEV))
+        model = NormalizingFlowModel_cond(prior_d, flows, device=DEV)
+    else:
+        model = NormalizingFlowModel(None, flows, device=DEV)
+
+    if inverse:
+        out, ld = model.inverse(x, c) if O else model.inverse(x)
+        lp = None
+    elif O:
+        out, lp, ld = model.forward(x, c)
+    else:
+        out, _, ld = model.forward(x)
+        lp = None
+    loss = (out * w_out.to(DEV)).sum() + (ld * w_ld.to(DEV)).sum()
+    if lp is not None:
+        loss = loss + (lp * w_lp.to(DEV)).sum()
+    params = [p for f in flows for p in f.parameters()]
+    ins = [x] + ([c] if O else [])
+    ours = _grads(loss, ins + params)
+    assert len(calls) == 1, "the backward did not run through nfdpf_cond_stack_backward"
+
+    refs = []
+    for dt in (torch.float32, torch.float64):
+        rf = copy.deepcopy(ref_flows)
+        for p in rf:
+            p.to(dtype=dt)
+        xr = x.detach().cpu().to(dt).requires_grad_(True)
+        cr = c.detach().cpu().to(dt).requires_grad_(True) if O else None
+        o_, l_, p_ = _ref_stack(rf, xr, cr, inverse, prior if O else None, dt)
+        lr = (o_ * w_out.to(dt)).sum() + (l_ * w_ld.to(dt)).sum()
+        if p_ is not None:
+            lr = lr + (p_ * w_lp.to(dt)).sum()
+        rp = [p for f in rf for p in f.parameters()]
+        refs.append(_grads(lr, [xr] + ([cr] if O else []) + rp))
+    names = ["x"] + (["cond"] if O else []) + [f"param{i}" for i in range(len(params))]
+    for name, a, r32, r64 in zip(names, ours, refs[0], refs[1]):
+        assert a is not None, name
+        _check(a, r32, r64, f"{name} (D={D} O={O} flows={n_flows} inv={inverse})")
+
+
+def test_cond_stack_backward_deterministic():
+    """Fixed-order partial sums: two backward calls give identical bits."""
+    from nfdpf import ops
+    from nfdpf.pack import flows_tensors
+    flows = _build(2, 36, 2, 0.3, 7)
+    b = torch.cat([t.detach().reshape(-1) for t in flows_tensors(flows)]).to(DEV)
+    x = torch.randn(10000, 2, device=DEV)
+    c = torch.randn(10000, 36, device=DEV)
+    go, gl = torch.randn(10000, 2, device=DEV), torch.randn(10000, device=DEV)
+    a = ops.cond_stack_backward(b, 2, 2, 36, 8, x, c, True, go, gl)
+    bb = ops.cond_stack_backward(b, 2, 2, 36, 8, x, c, True, go, gl)
+    for u, v in zip(a, bb):
+        assert torch.equal(u, v)
+
+
+def test_cond_stack_backward_zero_rows():
+    from nfdpf import ops
+    from nfdpf.pack import flows_tensors
+    flows = _build(2, 4, 2, 0.3, 3)
+    b = torch.cat([t.detach().reshape(-1) for t in flows_tensors(flows)]).to(DEV)
+    x = torch.zeros(0, 2, device=DEV)
+    c = torch.zeros(0, 4, device=DEV)
+    gx, gc, gb = ops.cond_stack_backward(b, 2, 2, 4, 8, x, c, False, torch.zeros(0, 2, device=DEV),
+                                         torch.zeros(0, device=DEV))
+    assert gx.shape == (0, 2) and gc.shape == (0, 4) and bool((gb == 0).all())
