@@ -34,8 +34,12 @@ struct BwdLds {
   static __host__ __device__ size_t xin_off(int nf, int O) {
     return sf_off(nf) + sizeof(float) * (size_t)kBwdRows * sfs(O);
   }
-  static __host__ __device__ size_t bytes(int nf, int O) {
+  static __host__ __device__ size_t cbs_off(int nf, int O) {
     return xin_off(nf, O) + sizeof(float) * (size_t)nf * D * kBwdRows;
+  }
+  // folded first-layer biases of every flow ([flow][2H][row] f2), kept from the recompute
+  static __host__ __device__ size_t bytes(int nf, int O) {
+    return cbs_off(nf, O) + sizeof(f2) * (size_t)nf * 2 * H * kBwdRows;
   }
 };
 
@@ -171,6 +175,7 @@ __global__ __launch_bounds__(kBwdRows) void cond_stack_bwd_kernel(
   f2 *gzall = (f2 *)(lds + L::gz_off());
   float *sf = (float *)(lds + L::sf_off(n_flows));
   float *xin = (float *)(lds + L::xin_off(n_flows, O));
+  f2 *cbs = (f2 *)(lds + L::cbs_off(n_flows, O));
   const int SF = L::sfs(O);
   const int lane = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * kBwdRows;
@@ -205,7 +210,10 @@ __global__ __launch_bounds__(kBwdRows) void cond_stack_bwd_kernel(
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int j = 0; j < H; ++j) cb[n * H + j] = fold_pair<HALF, H>(fw + n * ns, O, j, c_row);
+      for (int j = 0; j < H; ++j) {
+        cb[n * H + j] = fold_pair<HALF, H>(fw + n * ns, O, j, c_row);
+        cbs[(q * 2 * H + n * H + j) * kBwdRows + lane] = cb[n * H + j];
+      }
     if (INV)
       coupling_inverse<HALF, H>(fw, O, lo, up, cb);
     else
@@ -242,9 +250,7 @@ __global__ __launch_bounds__(kBwdRows) void cond_stack_bwd_kernel(
       a_up[k] = xin[(q * D + HALF + k) * kBwdRows + lane];
     }
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int j = 0; j < H; ++j) cb[n * H + j] = fold_pair<HALF, H>(fw + n * ns, O, j, c_row);
+    for (int j = 0; j < 2 * H; ++j) cb[j] = cbs[(q * 2 * H + j) * kBwdRows + lane];
     // the half applied first (pair 0 forward, pair 1 inverse) and the intermediate it made
     float mid[HALF], gu[HALF];
     {

@@ -19,7 +19,7 @@ import torch.nn.init as init
 
 from nfdpf import autograd as _ag
 from nfdpf import ops as _ops
-from nfdpf.pack import blob, flows_tensors
+from nfdpf.pack import blob, blob_grad_to_params, flows_tensors
 
 device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
 
@@ -129,14 +129,8 @@ class CouplingStack:
                                               None if g_lp is None else g_lp.float(), pm, ps)
         # blob -> parameters: the packed blob is a fixed gather of the parameters (nfdpf.pack)
         params = _params(self.flows)
-        gp = [None] * len(params)
-        req = [i for i, p in enumerate(params) if p.requires_grad]
-        if req:
-            with torch.enable_grad():
-                flat = torch.cat([t.reshape(-1) for t in flows_tensors(self.flows)])
-                g = torch.autograd.grad(flat, [params[i] for i in req], gb, allow_unused=True)
-            for i, gi in zip(req, g):
-                gp[i] = gi
+        gp = blob_grad_to_params(self.owner, "stack", params, lambda get: flows_tensors(self.flows, get), gb)
+        gp = [g if p.requires_grad else None for g, p in zip(gp, params)]
         gobs = None if gc is None else gc.to(obser.dtype)
         return (gx.to(x.dtype), gobs), gp
 

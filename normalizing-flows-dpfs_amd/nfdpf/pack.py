@@ -13,11 +13,15 @@ def _linears(seq: nn.Module):
     return [m for m in seq.modules() if isinstance(m, nn.Linear)]
 
 
-def fcnn_tensors(fcnn: nn.Module):
+def _same(p):
+    return p
+
+
+def fcnn_tensors(fcnn: nn.Module, get=_same):
     """FCNN(in, out, H): W1 b1 W2 b2 W3 b3 (nf/flows.py:101-114)."""
     out = []
     for lin in _linears(fcnn.network):
-        out += [lin.weight, lin.bias]
+        out += [get(lin.weight), get(lin.bias)]
     return out
 
 
@@ -49,27 +53,28 @@ def encoder_tensors(seq: nn.Module):
     return [row_pairs(l1.weight), l1.bias, col_pairs(l2.weight), l2.bias, col_pairs(l3.weight), l3.bias]
 
 
-def coupling_pair_tensors(t_net: nn.Module, s_net: nn.Module, half: int):
+def coupling_pair_tensors(t_net: nn.Module, s_net: nn.Module, half: int, get=_same):
     """Nets t and s of one coupling half, FCNN(half + O, half, H) each (nf/flows.py:101-114,
     183-190), interleaved t/s elementwise (csrc/flows.hpp ts_pair): core
     [W1[:, :half], W2, b2, W3, b3] then context [W1[:, half:], b1]."""
-    (tw1, tb1), (tw2, tb2), (tw3, tb3) = [(m.weight, m.bias) for m in _linears(t_net.network)]
-    (sw1, sb1), (sw2, sb2), (sw3, sb3) = [(m.weight, m.bias) for m in _linears(s_net.network)]
+    (tw1, tb1), (tw2, tb2), (tw3, tb3) = [(get(m.weight), get(m.bias)) for m in _linears(t_net.network)]
+    (sw1, sb1), (sw2, sb2), (sw3, sb3) = [(get(m.weight), get(m.bias)) for m in _linears(s_net.network)]
     return [pair(tw1[:, :half], sw1[:, :half]), pair(tw2, sw2), pair(tb2, sb2), pair(tw3, sw3),
             pair(tb3, sb3), pair(tw1[:, half:], sw1[:, half:]), pair(tb1, sb1)]
 
 
-def realnvp_tensors(flow: nn.Module):
+def realnvp_tensors(flow: nn.Module, get=_same):
     """RealNVP / RealNVP_cond flow (nf/flows.py:123-129, 183-190): pair (t1, s1), pair (t2, s2)."""
     half = flow.dim // 2
-    return coupling_pair_tensors(flow.t1, flow.s1, half) + coupling_pair_tensors(flow.t2, flow.s2, half)
+    return (coupling_pair_tensors(flow.t1, flow.s1, half, get) +
+            coupling_pair_tensors(flow.t2, flow.s2, half, get))
 
 
-def maf_tensors(flow: nn.Module):
+def maf_tensors(flow: nn.Module, get=_same):
     """MAF flow: initial_param[2] then FCNN(i, 2, H) for i = 1..dim-1 (nf/flows.py:247-254)."""
-    out = [flow.initial_param]
+    out = [get(flow.initial_param)]
     for layer in flow.layers:
-        out += fcnn_tensors(layer)
+        out += fcnn_tensors(layer, get)
     return out
 
 
@@ -124,13 +129,41 @@ def cglow_tensors(glow: nn.Module):
              _taps_last(f4.weight), f4.bias, f4.logs, f4.newbias])
 
 
-def flows_tensors(flows):
+def flows_tensors(flows, get=_same):
+    """``get`` maps each parameter to the tensor packed in its place (default: itself)."""
     out = []
     for f in flows:
         if hasattr(f, "initial_param"):
-            out += maf_tensors(f)
+            out += maf_tensors(f, get)
         else:
-            out += realnvp_tensors(f)
+            out += realnvp_tensors(f, get)
+    return out
+
+
+def blob_source_index(params, build) -> torch.Tensor:
+    """For every entry of the blob ``build(get)`` packs, the index of its source element in the
+    concatenation of ``params`` (flattened, in order).  The packing is a gather, so a blob
+    gradient maps back to the parameters by one scatter with this index."""
+    ids, off = {}, 0
+    for p in params:
+        ids[id(p)] = torch.arange(off, off + p.numel(), dtype=torch.int64).view(p.shape)
+        off += p.numel()
+    return torch.cat([t.reshape(-1) for t in build(lambda p: ids[id(p)])])
+
+
+def blob_grad_to_params(owner: nn.Module, name: str, params, build, g_blob: torch.Tensor):
+    """Scatter a gradient in blob layout back to per-parameter gradients (cached index)."""
+    caches = owner.__dict__.setdefault("_nfdpf_blob_index", {})
+    key = (name, str(g_blob.device)) + tuple(id(p) for p in params)
+    idx = caches.get(key)
+    if idx is None:
+        idx = caches[key] = blob_source_index(params, build).to(g_blob.device)
+    flat = torch.empty(sum(p.numel() for p in params), device=g_blob.device, dtype=g_blob.dtype)
+    flat[idx] = g_blob
+    out, off = [], 0
+    for p in params:
+        out.append(flat[off:off + p.numel()].view(p.shape).to(p.dtype))
+        off += p.numel()
     return out
 
 

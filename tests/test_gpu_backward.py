@@ -185,3 +185,45 @@ def test_cond_stack_backward_zero_rows():
     gx, gc, gb = ops.cond_stack_backward(b, 2, 2, 4, 8, x, c, False, torch.zeros(0, 2, device=DEV),
                                          torch.zeros(0, device=DEV))
     assert gx.shape == (0, 2) and gc.shape == (0, 4) and bool((gb == 0).all())
+
+
+@pytest.mark.parametrize("meas", ["cos", "CRNVP"])
+def test_training_step_hip_backward_matches_recompute(meas):
+    """One training pass of the reference loop (DPFs.py:144-216 under autograd, as e2e_train
+    runs it): parameter gradients with the HIP flow backward == with the PyTorch-recompute
+    backward (same HIP forward, so only the backward differs)."""
+    import sys
+    import os
+    import torch.nn as nn
+    from nfdpf import autograd as ag
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import make_args, synthetic_disk
+    from DPFs import DPF
+    B, N, T = 4, 200, 4
+    flags = dict(NF_dyn=True, NF_cond=True, measurement=meas, resampler_type="soft", force_resample=True)
+    torch.manual_seed(5)
+    a = make_args(flags, B, N, T, {})
+    dpf = DPF(a).to(DEV)
+    dpf.encoder = nn.Identity()
+    start, state, vel_in, enc = (x.to(DEV) for x in synthetic_disk(B, T, 3, a.hiddensize))
+    grads = {}
+    for mode in (True, False):
+        ag.HIP_BACKWARD = mode
+        try:
+            dpf.zero_grad(set_to_none=True)
+            torch.manual_seed(11)
+            out = dpf.filtering_pos(enc, start, vel_in)
+            xs, ps = out[0], out[1]
+            pred = (xs * ps[..., None]).sum(2)
+            loss = ((pred - state[:, :, :2]) ** 2).mean() + 0.01 * out[-1]
+            loss.backward()
+        finally:
+            ag.HIP_BACKWARD = True
+        grads[mode] = {n: p.grad.detach().clone() for n, p in dpf.named_parameters() if p.grad is not None}
+    flow_keys = [k for k in grads[False] if k.startswith(("nf_dyn.", "cond_model."))]
+    assert flow_keys and set(grads[True]) == set(grads[False])
+    for k in grads[False]:
+        a_, b_ = grads[True][k].double(), grads[False][k].double()
+        scale = float(b_.abs().max()) + 1e-30
+        d = float((a_ - b_).abs().max())
+        assert d <= 2e-3 * scale + 1e-7, f"{k}: max |d| {d:.3g} vs scale {scale:.3g}"

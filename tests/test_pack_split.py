@@ -50,3 +50,22 @@ def test_split_suffix_reproduces_nets():
 def test_maf_stack_not_split():
     from nf.flows import MAF
     assert not splittable([MAF(dim=2, hidden_dim=8)])
+
+
+def test_blob_grad_scatter_matches_autograd_of_pack():
+    """The HIP backward returns d/d(blob); nfdpf.pack.blob_grad_to_params maps it back to the
+    parameters by one scatter -- equal to differentiating the packing itself."""
+    import torch
+    from nf.flows import RealNVP_cond, RealNVP
+    from nfdpf.pack import blob_grad_to_params, flows_tensors
+    torch.manual_seed(0)
+    for fl in ([RealNVP_cond(2, 8, obser_dim=36) for _ in range(2)], [RealNVP(32, 8) for _ in range(3)]):
+        for f in fl:
+            f.zero_initialization(0.3)
+        params = [p for f in fl for p in f.parameters()]
+        flat = torch.cat([t.reshape(-1) for t in flows_tensors(fl)])
+        assert flat.numel() == sum(p.numel() for p in params)
+        g = torch.randn_like(flat)
+        ref = torch.autograd.grad(flat, params, g)
+        ours = blob_grad_to_params(fl[0], "t", params, lambda get: flows_tensors(fl, get), g)
+        assert all(torch.equal(a, b) for a, b in zip(ref, ours))
