@@ -136,6 +136,16 @@ NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, fl
                       float threshold, int max_iter, int64_t row_base, float *x_out,
                       float *w_out, int64_t *idx_out, int32_t *iters_out, void *workspace,
                       const int32_t *gate, const int32_t *stop_at, int poll, void *stream);
+
+/* Backward of nfdpf_ot_resample for training: the reference's gradient
+ * reaches the particles only through x' = bmm(T, x) with T treated as a constant (its
+ * transport Function discards the autograd.grad it computes, resamplers.py:234-245), so
+ *   g_x[b, j] = sum_i T[b, i, j] g_out[b, i]      (g_out, g_x [B, N, 2])
+ * T is not formed: column j is summed over i from the forward's potentials and column
+ * normalisers.  workspace = the forward call's workspace, untouched since that call (its
+ * iteration tables are reused); gate = the forward's gate (off: g_x = g_out). */
+NFDPF_API int nfdpf_ot_transport_backward(const float *g_out, int B, int N, float eps, float *g_x,
+                                          void *workspace, const int32_t *gate, void *stream);
 /*   gate: optional device flag; when non-NULL and *gate == 0 every kernel is a no-op (the
  *         ESS gate of DPFs.py:165 decided not to resample this step, without a host sync)
  *   stop_at: optional device int32, in the iters_out encoding (total_iter + 2).  NULL: the

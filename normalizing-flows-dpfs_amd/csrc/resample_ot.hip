@@ -840,6 +840,98 @@ __global__ __launch_bounds__(kOtThreads) void ot_apply_kernel(OtParams P, OtWs w
   idx_out[o] = (int64_t)N * (row_base + b) + i;
 }
 
+// ---- backward (training) ----------------------------------------------
+// The reference differentiates x' = bmm(T, x) with T a constant (its transport Function's own
+// autograd.grad result is discarded, resamplers.py:234-245), so dL/dx_j = sum_i T_ij g_i.
+// Column j:  T_ij = 2^(F_i + R_j - c_ij) (F = f/eps, R = r log2 e as in the apply pass) and
+// sum_i T_ij = N w_j exactly (r_j is the column log-normaliser), so with the shift
+// L_j = log2 N + log2 w_j - R_j the shifted sum over i is 1 and dL/dx_j = N w_j * SV_j.
+// The forward's workspace must be untouched since its call; the iteration tables (free after
+// the loop) hold the backward's table: X, Y, F_i - M, g_x, g_y.
+__global__ __launch_bounds__(kOtThreads) void ot_bwd_table_kernel(OtParams P, OtWs ws,
+                                                                 const float *__restrict__ g) {
+  if (ot_off(P)) return;
+  __shared__ double shd[16];
+  const int b = blockIdx.y, N = P.N;
+  const int i = blockIdx.x * kOtThreads + threadIdx.x;
+  const bool v = i < N;
+  const int64_t Np = np_of(P);
+  const float *xs = ws.xs + (int64_t)b * N * 2;
+  const double fsh = (1.0 / P.eps) * kLog2ed;
+  const double h[1] = {v ? ws.fg[(int64_t)b * N + i] * fsh : 0.0};
+  const float vals[2] = {v ? g[((int64_t)b * N + i) * 2] : 0.f, v ? g[((int64_t)b * N + i) * 2 + 1] : 0.f};
+  write_col<1, 2, false>(tabI_row(ws, P, 0, b), mI_row(ws, P, 0, b), Np, v, v ? xs[2 * i] : 0.f,
+                         v ? xs[2 * i + 1] : 0.f, h, vals, shd);
+}
+
+__global__ __launch_bounds__(kOtThreads) void ot_bwd_apply_kernel(OtParams P, OtWs ws,
+                                                                 const float *__restrict__ g,
+                                                                 float *__restrict__ g_x) {
+  const int b = blockIdx.y, N = P.N;
+  const int j = blockIdx.x * kOtThreads + threadIdx.x;
+  const bool v = j < N;
+  const int64_t o = (int64_t)b * N + j;
+  if (ot_off(P)) {  // no resampling happened: x' = x
+    if (v) {
+      g_x[2 * o] = g[2 * o];
+      g_x[2 * o + 1] = g[2 * o + 1];
+    }
+    return;
+  }
+  __shared__ float lds[kLdsPart];
+  const int64_t Np = np_of(P);
+  const float sc = cost_scale(1.0 / P.eps);
+  const float *xs = ws.xs + (int64_t)b * N * 2;
+  const float *EA = ws.tabA + (int64_t)b * 5 * Np + 2 * Np;  // R_j - M_s
+  const double *mA = ws.mA + (int64_t)b * P.splits;
+  const double log2N = log2((double)N);
+  auto shift = [&](int jj) {  // L_j (0 for a column of zero weight: it carries nothing)
+    const double lw = (double)ws.logw[(int64_t)b * N + jj];
+    return lw > -INFINITY ? log2N + lw * kLog2ed - ((double)EA[jj] + mA[jj / kOtThreads]) : 0.0;
+  };
+  const float *tab = tabI_row(ws, P, 0, b);
+  const double *msh = mI_row(ws, P, 0, b);
+  float S[1], SV[2];
+  wg_table_sums<1, 2, 1>(tab, msh, P.splits, Np, N, sc,
+                         [&](int jj, float &xx, float &yy, double (&m)[1]) {
+                           xx = xs[2 * jj];
+                           yy = xs[2 * jj + 1];
+                           m[0] = shift(jj);
+                         },
+                         lds, S, SV);
+  if (!v) return;
+  const double lw = (double)ws.logw[o];
+  if (!(lw > -INFINITY)) {
+    g_x[2 * o] = 0.f;
+    g_x[2 * o + 1] = 0.f;
+    return;
+  }
+  const double Nw = (double)N * exp(lw);
+  double gx = SV[0], gy = SV[1];
+  if (!sum_ok(S[0])) {  // exact: max shift first, then the weighted sums (fp64 exponents)
+    atomicAdd(&ws.st->fallbacks, 1);
+    const float xj = xs[2 * j], yj = xs[2 * j + 1];
+    const double Lj = shift(j), fsh = (1.0 / P.eps) * kLog2ed;
+    const float *gr = g + (int64_t)b * N * 2;
+    auto expo = [&](int i) {
+      const float dx = xs[2 * i] - xj, dy = xs[2 * i + 1] - yj;
+      return ws.fg[(int64_t)b * N + i] * fsh - Lj - (double)(fmaf(dx, dx, dy * dy) * sc);
+    };
+    double mx = -INFINITY;
+    for (int i = 0; i < N; ++i) mx = fmax(mx, expo(i));
+    double sx = 0.0, sy = 0.0;
+    for (int i = 0; i < N; ++i) {
+      const double t = exp2(expo(i) - mx);
+      sx += t * gr[2 * i];
+      sy += t * gr[2 * i + 1];
+    }
+    gx = sx * exp2(mx);
+    gy = sy * exp2(mx);
+  }
+  g_x[2 * o] = (float)(Nw * gx);
+  g_x[2 * o + 1] = (float)(Nw * gy);
+}
+
 __global__ void ot_iters_kernel(OtParams P, OtWs ws, int32_t *out) {
   out[0] = ot_off(P) ? 0 : ot_total_iter(P, ws) + 2;
 }
@@ -941,6 +1033,23 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
   ot_apply_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);
   if (iters_out) ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
   return launch_status("nfdpf_ot_resample");
+}
+
+extern "C" int nfdpf_ot_transport_backward(const float *g_out, int B, int N, float eps, float *g_x,
+                                           void *workspace, const int32_t *gate, void *stream) {
+  NFDPF_REQUIRE(g_out && g_x && workspace, "nfdpf_ot_transport_backward: null pointer");
+  NFDPF_REQUIRE(B >= 0 && N >= 1, "nfdpf_ot_transport_backward: bad sizes");
+  NFDPF_REQUIRE(eps > 0.f, "nfdpf_ot_transport_backward: eps must be > 0");
+  NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_ot_transport_backward: workspace not 256-B aligned");
+  if (B == 0) return NFDPF_OK;
+  hipStream_t st = as_stream(stream);
+  const int splits = ot_splits(N);
+  OtWs ws = carve(workspace, B, N);
+  OtParams P{B, N, splits, 1, (double)eps, 1.0, 0.0, gate, nullptr, nullptr, 0};
+  const dim3 g(splits, B);
+  ot_bwd_table_kernel<<<g, kOtThreads, 0, st>>>(P, ws, g_out);
+  ot_bwd_apply_kernel<<<g, kOtThreads, 0, st>>>(P, ws, g_out, g_x);
+  return launch_status("nfdpf_ot_transport_backward");
 }
 
 namespace nfdpf {

@@ -58,6 +58,8 @@ SIGNATURES = {
     "nfdpf_cond_stack_backward": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int,
                                           c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_void_p]),
+    "nfdpf_ot_transport_backward": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                            c_void_p]),
     "nfdpf_maf_stack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                 c_void_p]),
     "nfdpf_soft_resample": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int64,

@@ -123,14 +123,15 @@ def _aligned_ptr(t: torch.Tensor) -> int:
 
 
 def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_base=0, gate=None,
-                stop_at=None, poll=None):
+                stop_at=None, poll=None, keep=None):
     """resampler_ot (resamplers.py:62-70) -> (x', w', flat idx, iterations int32[1]).
 
     ``stop_at`` (device int32[1], iterations encoding): run exactly that many Sinkhorn
     iterations instead of the batch-coupled stop rule (include/nfdpf.h) -- the second pass
     of a batch sharded over ranks.  ``poll`` (default: unless the stream is being captured
     into a graph): follow the loop's progress from the host and stop enqueueing iteration
-    launches once it has stopped."""
+    launches once it has stopped.  ``keep``: a private workspace (ot_workspace) to run in
+    instead of the shared one -- it then holds the state ot_transport_backward needs."""
     require_device(x, "ot_resample")
     B, N, D = x.shape
     if D != 2:
@@ -143,13 +144,31 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_b
     if poll is None:
         poll = not torch.cuda.is_current_stream_capturing()
     nb = int(lib().nfdpf_ot_workspace_bytes(B, N))
-    ws = workspace(nb, x.device)
+    ws = workspace(nb, x.device) if keep is None else keep
     check(lib().nfdpf_ot_resample(ptr(x), ptr(w), B, N, float(eps), float(scaling), float(threshold),
                                   int(max_iter), int(row_base), ptr(xo), ptr(wo), ptr(idx), ptr(it),
                                   _aligned_ptr(ws), ptr(gate), ptr(stop_at), int(bool(poll)),
                                   stream_ptr(x.device)),
           "nfdpf_ot_resample")
     return xo, wo, idx, it
+
+
+def ot_workspace(B, N, device) -> torch.Tensor:
+    """A private OT workspace (the forward state of one call, for its backward)."""
+    nb = int(lib().nfdpf_ot_workspace_bytes(B, N))
+    return torch.empty(max(nb, 256) + 256, dtype=torch.uint8, device=device)
+
+
+def ot_transport_backward(ws, g_out, eps, gate=None):
+    """dL/dx of ot_resample's x' = T x with T constant (resamplers.py:234-264): T^T g_out,
+    from the state the forward left in ``ws`` (include/nfdpf.h nfdpf_ot_transport_backward)."""
+    require_device(g_out, "ot_transport_backward")
+    B, N, D = g_out.shape
+    g_out = _c(g_out)
+    gx = torch.empty_like(g_out)
+    check(lib().nfdpf_ot_transport_backward(ptr(g_out), B, N, float(eps), ptr(gx), _aligned_ptr(ws), ptr(gate),
+                                            stream_ptr(g_out.device)), "nfdpf_ot_transport_backward")
+    return gx
 
 
 def ot_stats(device=None):

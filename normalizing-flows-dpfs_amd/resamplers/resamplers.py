@@ -7,7 +7,7 @@
 * ``resampler_ot`` (resamplers.py:62-277): streamed Sinkhorn with the reference's
   batch-coupled stop rule; the transport matrix is never materialised.  As in the
   reference, the particles' gradient is T^T g with T treated as a constant (its own
-  autograd.grad result is discarded, :241-245).
+  autograd.grad result is discarded, :241-245) -- nfdpf_ot_transport_backward.
 """
 import torch
 import torch.nn as nn
@@ -58,9 +58,31 @@ def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, 
     return (xo, wo, idx) if index else (xo, wo)
 
 
+class _OtTransport(torch.autograd.Function):
+    """x' = T x with the Sinkhorn plan T held constant in backward (resamplers.py:234-264):
+    dL/dx = T^T g by nfdpf_ot_transport_backward from this call's own workspace; no gradient
+    to the weights (the reference returns None for them)."""
+
+    @staticmethod
+    def forward(ctx, particles, weights, eps, scaling, threshold, max_iter):
+        B, N, _ = particles.shape
+        ws = _ops.ot_workspace(B, N, particles.device)
+        xo, wo, idx, _ = _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=ws)
+        ctx.ws, ctx.eps = ws, eps
+        ctx.mark_non_differentiable(wo, idx)
+        return xo, wo, idx
+
+    @staticmethod
+    def backward(ctx, g, _gw, _gi):
+        gx = _ops.ot_transport_backward(ctx.ws, g, ctx.eps)
+        return gx, None, None, None, None, None
+
+
 def resampler_ot(particles, weights, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, device="cuda",
                  flag=None):
     """OT resampling -> (x', uniform weights, identity flat index) (resamplers.py:62-70)."""
+    if torch.is_grad_enabled() and particles.requires_grad:
+        return _OtTransport.apply(particles, weights.detach(), eps, scaling, threshold, max_iter)
     xo, wo, idx, _ = _ops.ot_resample(particles.detach(), weights.detach(), eps, scaling, threshold, max_iter)
     return xo, wo, idx
 

@@ -542,7 +542,7 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, retur
     wr = torch.ones_like(w) / _f(torch.tensor(N))
     idx = (torch.arange(N) + N * torch.arange(B)[:, None].repeat((1, N))).long()
     if return_info:
-        return xr, wr, idx, {"iters": it + 2, "a_y": f, "b_x": g}
+        return xr, wr, idx, {"iters": it + 2, "a_y": f, "b_x": g, "T": T}
     return xr, wr, idx
 
 

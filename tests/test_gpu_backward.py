@@ -227,3 +227,30 @@ def test_training_step_hip_backward_matches_recompute(meas):
         scale = float(b_.abs().max()) + 1e-30
         d = float((a_ - b_).abs().max())
         assert d <= 2e-3 * scale + 1e-7, f"{k}: max |d| {d:.3g} vs scale {scale:.3g}"
+
+
+@pytest.mark.parametrize("B,N,kind", [(4, 128, "random"), (3, 1000, "peaked"), (2, 257, "zero_w")])
+def test_ot_transport_backward_vs_oracle(B, N, kind):
+    """dL/dx through resampler_ot under autograd == T^T g with the oracle's float64 transport
+    matrix (the reference treats T as a constant in backward, resamplers.py:234-245)."""
+    from oracle import dpf_oracle as O
+    from resamplers.resamplers import resampler_ot
+    g = torch.Generator().manual_seed(N)
+    x = torch.randn(B, N, 2, generator=g) * 20
+    logits = torch.randn(B, N, generator=g) * (4.0 if kind == "peaked" else 1.0)
+    w = torch.softmax(logits, -1)
+    if kind == "zero_w":
+        w[:, ::7] = 0.0
+        w = w / w.sum(-1, keepdim=True)
+    gout = torch.randn(B, N, 2, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    xo, wo, idx = resampler_ot(xd, w.to(DEV))
+    (xo * gout.to(DEV)).sum().backward()
+    _, _, _, info = O.ot_resample(x.double(), w.double(), return_info=True)
+    ref = torch.einsum("bij,bic->bjc", info["T"].double(), gout.double())
+    d = (xd.grad.double().cpu() - ref).abs()
+    scale = float(ref.abs().max())
+    tol = 1e-4 * ref.abs() + 5e-5 * scale
+    assert bool((d <= tol).all()), f"max |d| {float(d.max()):.3g} (scale {scale:.3g})"
+    if kind == "zero_w":
+        assert bool((xd.grad[:, ::7].abs() == 0).all())
