@@ -25,6 +25,7 @@ from model.models import (build_conditional_glow, build_conditional_nf, build_de
                           measurement_model_Gaussian, measurement_model_NN, motion_update, nf_dynamic_model,
                           proposal_likelihood)
 from nfdpf.engine import FilterConfig, FilterEngine, ShardInfo
+from nfdpf.gradsync import GradBucket, global_mean, world_size
 from resamplers.resamplers import resampler
 from utils import (checkpoint_state, compute_normal_density, load_model, normalize_log_probs,
                    particle_initialization)
@@ -193,7 +194,9 @@ class DPF(nn.Module):
         hist = {k: [] for k in ("x", "p", "n", "l", "i", "j", "r")}
         for step in range(self.seq_len):
             index_p = (torch.arange(N) + N * torch.arange(B)[:, None].repeat((1, N))).long().to(particles.device)
-            ess = torch.mean(1 / torch.sum(probs ** 2, dim=-1))
+            inv_ess = 1 / torch.sum(probs ** 2, dim=-1)
+            # batch-global gate (DPFs.py:163-165); sharded: the mean over every rank's rows
+            ess = torch.mean(inv_ess) if world_size() == 1 else global_mean(inv_ess.sum(), inv_ess.numel())
             if force or ess < 0.5 * N:
                 xr, pr, index_p = self.resampler(particles, probs)
                 lr = pr.log()
@@ -218,6 +221,14 @@ class DPF(nn.Module):
                 st("r") if self.NF else None, obs_likelihood)
 
     # ------------------------------------------------------------------------------------
+    def _sync_grads(self):
+        """Average the gradients over the ranks of a batch-sharded run (one all-reduce of one
+        flat bucket, nfdpf.gradsync); a no-op on one process."""
+        if world_size() > 1:
+            if getattr(self, "_grad_bucket", None) is None:
+                self._grad_bucket = GradBucket(self)
+            self._grad_bucket.sync()
+
     def get_mask(self):
         """Random labelled mask with labeledRatio ones (DPFs.py:218-229)."""
         n1 = int(self.batch_size * self.seq_len * self.labeledRatio)
@@ -237,6 +248,7 @@ class DPF(nn.Module):
                 loss = F.mse_loss(self.decoder(self.encoder(img)), img)
                 self.zero_grad()
                 loss.backward()
+                self._sync_grads()
                 self.optim.step()
                 losses.append(loss.detach().cpu().numpy())
             print(f"Train AE: Epoch: {epoch}, loss: {np.mean(losses)}")
@@ -270,6 +282,7 @@ class DPF(nn.Module):
                 out = self.forward(inputs, train=True)
                 self.zero_grad()
                 out[0].backward()
+                self._sync_grads()
                 self.optim.step()
                 sup.append(out[1].detach().cpu().numpy())
                 ae.append(out[3].detach().cpu().numpy())

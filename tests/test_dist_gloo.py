@@ -93,3 +93,55 @@ def test_single_process_shard_is_identity():
     from nfdpf.engine import ShardInfo
     sh = ShardInfo.from_env(5)
     assert (sh.world, sh.B_global, sh.row_base) == (1, 5, 0)
+
+
+def _grad_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf.gradsync import GradBucket, global_mean
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Tanh(), torch.nn.Linear(4, 2))
+        x = torch.randn(5, 3, generator=torch.Generator().manual_seed(100 + rank))
+        m(x).pow(2).mean().backward()
+        m[2].bias.grad = None if rank == 1 else m[2].bias.grad  # a gradient missing on one rank
+        GradBucket(m).sync()
+        inv = torch.arange(3, dtype=torch.float32) + 10 * rank
+        ess = global_mean(inv.sum(), inv.numel())
+        q.put((rank, [p.grad.clone().numpy() for p in m.parameters()], float(ess)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_bucket_world2():
+    """nfdpf.gradsync: one all-reduce averages the ranks' gradients (== the gradient of the
+    mean loss over both shards); global_mean is the batch-global ESS mean."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Tanh(), torch.nn.Linear(4, 2))
+    grads = []
+    for r in range(world):
+        m.zero_grad()
+        m(torch.randn(5, 3, generator=torch.Generator().manual_seed(100 + r))).pow(2).mean().backward()
+        g = [p.grad.clone() for p in m.parameters()]
+        if r == 1:
+            g[3] = torch.zeros_like(g[3])
+        grads.append(g)
+    ref = [(a + b) / 2 for a, b in zip(*grads)]
+    for rank, gs, ess in res:
+        for a, b in zip(gs, ref):
+            np.testing.assert_allclose(a, b.numpy(), rtol=1e-6, atol=1e-7)
+        assert abs(ess - (0 + 1 + 2 + 10 + 11 + 12) / 6) < 1e-6
