@@ -126,6 +126,21 @@ NFDPF_API int nfdpf_soft_resample(const float *x, const float *p, const float *l
                         int B, int N, int D, float alpha, int64_t row_base, float *x_out,
                         float *w_out, int64_t *idx_out, void *stream);
 
+/* Backward of nfdpf_soft_resample (training): the gradient the reference's
+ * autograd takes through resamplers.py:28-56 (q = (a p + (1-a)/N) / S, w = p / q, gather by
+ * idx, w' normalised), without its B x N x N tensor.
+ *   p [B, N]: the forward's input probabilities; idx [B, N], w_out [B, N]: its outputs
+ *   g_x_out [B, N, D] / g_w_out [B, N]: dL/d(x', w') (either may be NULL: zero)
+ *   g_x [B, N, D], g_p [B, N]: dL/d(x, p)
+ *   workspace: nfdpf_soft_resample_backward_workspace(B, N) bytes
+ * Each source's gradient is the in-order sum over its run of equal indices (idx is sorted):
+ * deterministic, no atomics. */
+NFDPF_API int64_t nfdpf_soft_resample_backward_workspace(int B, int N);
+NFDPF_API int nfdpf_soft_resample_backward(const float *p, const int64_t *idx, const float *w_out,
+                                           const float *g_x_out, const float *g_w_out, int B, int N,
+                                           int D, float alpha, int64_t row_base, float *g_x,
+                                           float *g_p, void *workspace, void *stream);
+
 /* resampler_ot (resamplers.py:62-277): entropy-regularised OT, Sinkhorn in fp32 with the
  * reference's batch-coupled stop rule (the loop ends when ANY row converges, :126-129).
  *   x [B,N,2], w [B,N] -> x_out [B,N,2], w_out [B,N] (= 1/N), idx_out [B,N] (identity)

@@ -60,6 +60,9 @@ SIGNATURES = {
                                           c_void_p, c_void_p, c_void_p]),
     "nfdpf_ot_transport_backward": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
                                             c_void_p]),
+    "nfdpf_soft_resample_backward_workspace": (c_int64, [c_int, c_int]),
+    "nfdpf_soft_resample_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                             c_float, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_maf_stack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                 c_void_p]),
     "nfdpf_soft_resample": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int64,

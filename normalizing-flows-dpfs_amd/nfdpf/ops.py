@@ -106,6 +106,24 @@ def soft_resample(x, p, alpha, offsets, row_base=0):
     return xo, wo, idx
 
 
+def soft_resample_backward(p, idx, w_out, g_x_out, g_w_out, alpha, D, row_base=0):
+    """Backward of soft_resample -> (g_x [B, N, D], g_p [B, N]) (include/nfdpf.h)."""
+    require_device(p, "soft_resample_backward")
+    B, N = p.shape
+    p, w_out = _c(p), _c(w_out)
+    idx = idx.to(torch.int64).contiguous()
+    gxo = _c(g_x_out) if g_x_out is not None else None
+    gwo = _c(g_w_out) if g_w_out is not None else None
+    gx = torch.empty((B, N, D), device=p.device, dtype=f32)
+    gp = torch.empty((B, N), device=p.device, dtype=f32)
+    ws = torch.empty(max(1, int(lib().nfdpf_soft_resample_backward_workspace(B, N))), device=p.device,
+                     dtype=torch.uint8)
+    check(lib().nfdpf_soft_resample_backward(ptr(p), ptr(idx), ptr(w_out), ptr(gxo), ptr(gwo), B, N, D,
+                                             float(alpha), int(row_base), ptr(gx), ptr(gp), ptr(ws),
+                                             stream_ptr(p.device)), "nfdpf_soft_resample_backward")
+    return gx, gp
+
+
 _ws = {}
 
 

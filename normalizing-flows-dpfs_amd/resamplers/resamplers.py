@@ -3,7 +3,7 @@
 * ``soft_resampler`` (resamplers.py:20-60): the HIP kernel reproduces the reference's
   indices bit for bit (same reduction orders, exact f64 prefix, lower-bound search) without
   the B x N x N comparison tensor; gradients (training) flow through the gathered weights
-  p/q as in the reference.
+  p/q as in the reference, computed by nfdpf_soft_resample_backward.
 * ``resampler_ot`` (resamplers.py:62-277): streamed Sinkhorn with the reference's
   batch-coupled stop rule; the transport matrix is never materialised.  As in the
   reference, the particles' gradient is T^T g with T treated as a constant (its own
@@ -35,6 +35,25 @@ class resampler(nn.Module):
         return self.resampling(particles, particle_probs, **self.kargs)
 
 
+class _SoftResample(torch.autograd.Function):
+    """soft_resampler with the HIP backward (nfdpf_soft_resample_backward): dL/dx by in-order
+    run sums over the sorted indices, dL/dp through w = p / q and the output normalisation."""
+
+    @staticmethod
+    def forward(ctx, particles, particle_probs, alpha, offsets):
+        xo, wo, idx = _ops.soft_resample(particles, particle_probs, alpha, offsets)
+        ctx.save_for_backward(particle_probs, idx, wo)
+        ctx.alpha, ctx.D, ctx.dtypes = alpha, particles.shape[-1], (particles.dtype, particle_probs.dtype)
+        ctx.mark_non_differentiable(idx)
+        return xo, wo, idx
+
+    @staticmethod
+    def backward(ctx, g_xo, g_wo, _g_idx):
+        p, idx, wo = ctx.saved_tensors
+        gx, gp = _ops.soft_resample_backward(p, idx, wo, g_xo, g_wo, ctx.alpha, ctx.D)
+        return gx.to(ctx.dtypes[0]), gp.to(ctx.dtypes[1]), None, None
+
+
 def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, device="cuda", offsets=None):
     """Soft resampling with q = alpha p + (1 - alpha)/N; the CPU-generator offset draw of
     the reference (:43) is kept (pass ``offsets`` to supply it)."""
@@ -42,19 +61,10 @@ def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, 
     B, N = particle_probs.shape
     if offsets is None:
         offsets = torch.FloatTensor(B).uniform_(0.0, 1.0 / num_resampled)
-    xo, wo, idx = _ops.soft_resample(particles.detach(), particle_probs.detach(), alpha, offsets)
     if torch.is_grad_enabled() and (particles.requires_grad or particle_probs.requires_grad):
-        # differentiable gather with the kernel's indices (resamplers.py:52-56)
-        if alpha < 1.0:
-            uni = torch.ones((B, N), device=particle_probs.device) / N
-            q = torch.stack((particle_probs * alpha, uni * (1.0 - alpha)), dim=-1).sum(dim=-1)
-            q = q / q.sum(dim=-1, keepdim=True)
-            w = particle_probs / q
-        else:
-            w = torch.ones_like(particle_probs) / N
-        xo = particles.reshape(B * N, -1)[idx, :]
-        wo = w.reshape(B * N)[idx]
-        wo = wo / wo.sum(dim=-1, keepdim=True)
+        xo, wo, idx = _SoftResample.apply(particles, particle_probs, alpha, offsets)
+    else:
+        xo, wo, idx = _ops.soft_resample(particles.detach(), particle_probs.detach(), alpha, offsets)
     return (xo, wo, idx) if index else (xo, wo)
 
 

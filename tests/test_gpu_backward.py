@@ -254,3 +254,77 @@ def test_ot_transport_backward_vs_oracle(B, N, kind):
     assert bool((d <= tol).all()), f"max |d| {float(d.max()):.3g} (scale {scale:.3g})"
     if kind == "zero_w":
         assert bool((xd.grad[:, ::7].abs() == 0).all())
+
+
+def _soft_ref(x, p, idx, alpha):
+    """resamplers.py:28-56 in float64 with the given indices (and this library's edge rule:
+    an index past the row reads the next row's first particle with weight 0; past the batch,
+    the row's own last particle)."""
+    B, N = p.shape
+    M = B * N
+    if alpha < 1.0:
+        q = p * alpha + (1.0 - alpha) / N
+        q = q / q.sum(-1, keepdim=True)
+        w = p / q
+    else:
+        w = torch.ones_like(p) / N
+    tg = idx.clamp(max=M - 1)
+    xo = x.reshape(M, -1)[tg]
+    same = (tg // N) == torch.arange(B)[:, None]
+    a = torch.where(same, w.reshape(M)[tg], torch.zeros_like(p))
+    return xo, a / a.sum(-1, keepdim=True)
+
+
+def _soft_check(ours, ref, what):
+    ours, ref = ours.double().cpu(), ref.double().cpu()
+    scale = float(ref.abs().max()) + 1e-30
+    d = (ours - ref).abs()
+    ok = d <= 1e-4 * ref.abs() + 2e-5 * scale
+    assert bool(ok.all()), f"{what}: max |d| {float(d.max()):.3g} (scale {scale:.3g})"
+
+
+@pytest.mark.parametrize("B,N,alpha,kind", [(4, 100, 0.5, "random"), (3, 1000, 0.5, "peaked"), (2, 7, 1.0, "random"),
+                                            (5, 333, 0.3, "random"), (3, 1, 0.5, "random")])
+def test_soft_resampler_backward_vs_autograd(B, N, alpha, kind):
+    """dL/d(x, p) through resampler.soft_resampler under autograd (HIP backward) == float64
+    autograd of the reference's formulas (resamplers.py:28-56) on the kernel's indices."""
+    from resamplers.resamplers import soft_resampler
+    g = torch.Generator().manual_seed(B * N)
+    x = torch.randn(B, N, 2, generator=g) * 10
+    logits = torch.randn(B, N, generator=g) * (6.0 if kind == "peaked" else 1.0)
+    p = torch.softmax(logits, -1)
+    gx_out, gw_out = torch.randn(B, N, 2, generator=g), torch.randn(B, N, generator=g)
+    xd, pd = x.to(DEV).requires_grad_(True), p.to(DEV).requires_grad_(True)
+    xo, wo, idx = soft_resampler(xd, pd, alpha, N)
+    ((xo * gx_out.to(DEV)).sum() + (wo * gw_out.to(DEV)).sum()).backward()
+    xr, pr = x.double().requires_grad_(True), p.double().requires_grad_(True)
+    xo_r, wo_r = _soft_ref(xr, pr, idx.cpu(), alpha)
+    ((xo_r * gx_out.double()).sum() + (wo_r * gw_out.double()).sum()).backward()
+    _soft_check(xo.detach(), xo_r.detach(), "x'")
+    _soft_check(wo.detach(), wo_r.detach(), "w'")
+    _soft_check(xd.grad, xr.grad, "dL/dx")
+    if pr.grad is None:  # hard resampling (alpha = 1): w = 1/N, no path to p
+        assert pd.grad is None or bool((pd.grad == 0).all())
+    else:
+        _soft_check(pd.grad, pr.grad, "dL/dp")
+
+
+def test_soft_resample_backward_edges():
+    """Hand-made sorted indices with long runs, unreferenced sources and the out-of-range
+    edge (into the next row, and past the last row)."""
+    from nfdpf import ops
+    B, N = 3, 6
+    idx = torch.tensor([[0, 0, 0, 0, 3, 6],        # row 0: a run of 4, a skip, the edge into row 1
+                        [6, 6, 9, 10, 11, 11],
+                        [12, 12, 12, 12, 12, 18]])  # row 2: past the batch -> own particle 5
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, N, 2, generator=g)
+    p = torch.softmax(torch.randn(B, N, generator=g), -1)
+    gx_out, gw_out = torch.randn(B, N, 2, generator=g), torch.randn(B, N, generator=g)
+    xr, pr = x.double().requires_grad_(True), p.double().requires_grad_(True)
+    xo_r, wo_r = _soft_ref(xr, pr, idx, 0.5)
+    ((xo_r * gx_out.double()).sum() + (wo_r * gw_out.double()).sum()).backward()
+    gx, gp = ops.soft_resample_backward(p.to(DEV), idx.to(DEV), wo_r.detach().float().to(DEV), gx_out.to(DEV),
+                                        gw_out.to(DEV), 0.5, 2)
+    _soft_check(gx, xr.grad, "dL/dx")
+    _soft_check(gp, pr.grad, "dL/dp")
