@@ -942,6 +942,10 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
     if (role == 0) lr = S.hp[i];
     if (defer_here) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
   }
+  // slot t-1's row normaliser (softmax partials of the previous launch): read now, so its
+  // global latency hides under the prologue instead of the epilogue
+  const RowNorm rn_prev = defer_here && valid ? row_norm(prev_sm(d, b, tiles), tiles, shifted_meas(d.measurement))
+                                              : RowNorm{0.f, 1.f, 0.f};
   measure_row_setup<NFDPF_MEAS_COS>(S.enc, d.meas_params, L);
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
   const int ncb = d.n_flows * 4 * kH;
@@ -986,10 +990,9 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
     double sf[4] = {0, 0, 0, 0};
     if (defer_here && valid) {
       const bool shifted = shifted_meas(d.measurement);
-      const RowNorm rn = row_norm(prev_sm(d, b, tiles), tiles, shifted);
       const RowSlot Sp = row_slot(d, b, d.t - 1);
       float lw, lk;
-      const float p = prev_p_of(pv, rn, shifted, lw, lk);
+      const float p = prev_p_of(pv, rn_prev, shifted, lw, lk);
       if (shifted) Sp.hlik[i] = lk;
       Sp.hp[i] = p;
       sf[0] = (double)p * p;
