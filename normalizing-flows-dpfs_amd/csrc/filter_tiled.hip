@@ -543,11 +543,22 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
       if (threadIdx.x == 0) fire_sh = (s / (float)d.B_global) < 0.5f * (float)N;
     }
   } else if (spec) {
-    for (int j = threadIdx.x - 64; j < N; j += blockDim.x - 64) {
-      if (defer)
-        acc(j, Sp.hx[2 * j], Sp.hx[2 * j + 1]);
-      else
-        acc(j, xprev[2 * j], xprev[2 * j + 1]);
+    // every source load of this thread first (one memory latency instead of one per
+    // particle), then the draws and sums; N <= kMergedMaxN = 4096 -> <= 10 per thread
+    constexpr int kPer = 10;
+    const float *src = defer ? Sp.hx : xprev;
+    const int j0 = threadIdx.x - 64, js = blockDim.x - 64;
+    float xs0[kPer], xs1[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int j = j0 + k * js;
+      xs0[k] = j < N ? src[2 * j] : 0.f;
+      xs1[k] = j < N ? src[2 * j + 1] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int j = j0 + k * js;
+      if (j < N) acc(j, xs0[k], xs1[k]);
     }
   }
   __syncthreads();
