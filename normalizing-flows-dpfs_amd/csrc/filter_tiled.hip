@@ -509,6 +509,24 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   const float *pprev = d.p_prev + b * d.p_prev_rs;
   const RowSlot Sp = defer ? row_slot(d, b, d.t - 1) : S;
   const float v0 = d.vel[2 * b], v1 = d.vel[2 * b + 1];
+  // fold operands that depend on nothing computed in this launch, loaded now so their latency
+  // hides under the gate / speculative motion: the nf_dyn fold's bias and context weights
+  // (threads < n_flows*4*H) and, in tile 0, the proposal fold over the encoding columns
+  const bool dyn_fold_lane = threadIdx.x < d.n_flows * 4 * kH;
+  float fw[1 + kOctxDyn] = {};
+  if (dyn_fold_lane) {
+    const FoldRef r = fold_ref(d.dyn_params, kNsDyn, threadIdx.x);
+    fw[0] = fold_bias0(r, kOctxDyn);
+#pragma unroll
+    for (int c = 0; c < kOctxDyn; ++c) fw[1 + c] = r.w1c[2 * (r.j * kOctxDyn + c) + r.w];
+  }
+  const bool enc_fold_lane =
+      d.nf_cond && tile == 0 && threadIdx.x >= kTile && threadIdx.x - kTile < d.n_flows * 4 * kH;
+  float enc_fold = 0.f;
+  if (enc_fold_lane) {  // proposal fold over the encoding columns (model/models.py:338-346); K3 adds mean/std
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), threadIdx.x - kTile);
+    enc_fold = fold_acc(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
+  }
   // the row's sums over x_phys = (x_src + vel) + eps (motion_apply_eps's arithmetic)
   double a0 = 0, a1 = 0, c0 = 0, c1 = 0;
   auto acc = [&](int j, float xs0, float xs1) {
@@ -662,18 +680,15 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
     }
   }
   const Ctx4 c = ctx_from_sums(a0, a1, c0, c1, N);
-  if (threadIdx.x < d.n_flows * 4 * kH) {
+  if (dyn_fold_lane) {  // fold_one's fma sequence on the prefetched weights
     const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
-    const float v = fold_one(d.dyn_params, kNsDyn, kOctxDyn, threadIdx.x, cv);
+    float v = fw[0];
+#pragma unroll
+    for (int q = 0; q < kOctxDyn; ++q) v = fmaf(fw[1 + q], cv[q], v);
     reinterpret_cast<float *>(cb)[threadIdx.x] = v;
     reinterpret_cast<float *>(cbs)[split_cb_index(threadIdx.x)] = v;
   }
-  if (d.nf_cond && tile == 0 && threadIdx.x >= kTile && threadIdx.x - kTile < d.n_flows * 4 * kH) {
-    // proposal fold over the encoding columns (model/models.py:338-346); K3 adds mean/std
-    const int k = threadIdx.x - kTile;
-    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), k);
-    ws.cb_cond[b * kCb + k] = fold_acc(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
-  }
+  if (enc_fold_lane) ws.cb_cond[b * kCb + threadIdx.x - kTile] = enc_fold;
   __syncthreads();
   if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
     ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
