@@ -512,6 +512,18 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   // fold operands that depend on nothing computed in this launch, loaded now so their latency
   // hides under the gate / speculative motion: the nf_dyn fold's bias and context weights
   // (threads < n_flows*4*H) and, in tile 0, the proposal fold over the encoding columns
+  // this thread's own particle of slot t-1 (the no-resample source), loaded up front too
+  PrevIn pv{};
+  float xp0 = 0.f, xp1 = 0.f, pp = 1.f;
+  if (valid) {
+    if (defer) {
+      pv = load_prev_in(Sp, i);
+    } else {
+      xp0 = xprev[2 * i];
+      xp1 = xprev[2 * i + 1];
+      pp = pprev[i];
+    }
+  }
   const bool dyn_fold_lane = threadIdx.x < d.n_flows * 4 * kH;
   float fw[1 + kOctxDyn] = {};
   if (dyn_fold_lane) {
@@ -650,13 +662,14 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
         x1 = d.ot_x[((int64_t)b * N + i) * 2 + 1];
         lr = logf(1.0f / (float)N);
       } else if (defer) {
-        x0 = Sp.hx[2 * i];
-        x1 = Sp.hx[2 * i + 1];
-        lr = logf(prev_p(i));
+        float lw, lk;
+        x0 = pv.x0;
+        x1 = pv.x1;
+        lr = logf(prev_p_of(pv, rn, shifted, lw, lk));
       } else {
-        x0 = xprev[2 * i];
-        x1 = xprev[2 * i + 1];
-        lr = logf(pprev[i]);
+        x0 = xp0;
+        x1 = xp1;
+        lr = logf(pp);
       }
     }
   }
