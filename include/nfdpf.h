@@ -197,6 +197,19 @@ NFDPF_API int nfdpf_measurement(int kind, const float *pe_params, const float *m
                       const float *enc, const float *x, int B, int N, int E, float prior_std,
                       float *lik, void *stream);
 
+/* Backward of the cosine-distance measurement (kind NFDPF_MEAS_COS of nfdpf_measurement;
+ * training): the autograd gradient of model/models.py:206-219 (particle
+ * encoder :130-139, et_distance utils.py:8-15).
+ *   pe_params: the same packed encoder blob; enc [B, E] frame encodings; x [B, N, 2];
+ *   g_lik [B, N] = dL/dlik
+ *   g_enc [B, E], g_x [B, N, 2]; g_params [1648]: the encoder's gradient in the plain
+ *   nn.Linear layout W1 b1 W2 b2 W3 b3 (= the module's parameter order)
+ *   workspace: nfdpf_cos_measurement_backward_workspace(B, N) bytes (fixed-order partials) */
+NFDPF_API int64_t nfdpf_cos_measurement_backward_workspace(int B, int N);
+NFDPF_API int nfdpf_cos_measurement_backward(const float *pe_params, const float *enc, const float *x,
+                                             const float *g_lik, int B, int N, int E, float *g_enc,
+                                             float *g_x, float *g_params, void *workspace, void *stream);
+
 /* Conditional-GLOW measurement (model/models.py:280-303; nf/cglow/CGlowModel.py with the
  * default flow_depth K = 1, L = 1, x_size = y_size = (3,8,8)): particle (b,i) at
  * x + b*x_rs + 2i, frame encoding of row b at enc + b*enc_rs (192 floats) -> the RAW

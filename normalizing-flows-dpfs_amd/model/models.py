@@ -149,6 +149,23 @@ class _MeasRunner:
             meas = blob(m, "meas", m.likelihood_estimator, lambda: paired_mlp_tensors(m.likelihood_estimator), x.device)
         return (_ops.measurement(self.kind, pe, meas, nfl, enc, x, pstd),)
 
+    def hip_backward(self, enc, x, gouts):
+        """Cosine measurement: d/d(enc, x, encoder parameters) by nfdpf_cos_measurement_backward
+        (csrc/measure_bwd.hip); None for the other models (autograd then differentiates
+        ``torch``)."""
+        m = self.model
+        if self.kind != "cos" or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 or x.shape[-1] != 2:
+            return None
+        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
+        g = gouts[0] if gouts[0] is not None else torch.zeros(x.shape[:2], device=x.device)
+        g_enc, gx, gp = _ops.cos_measurement_backward(pe, enc.float(), x.float(), g.float())
+        params = list(m.parameters())
+        out, off = [], 0
+        for p in params:  # the module's parameters are the encoder's W1 b1 W2 b2 W3 b3
+            out.append(gp[off:off + p.numel()].view_as(p).to(p.dtype) if p.requires_grad else None)
+            off += p.numel()
+        return (g_enc.to(enc.dtype), gx.to(x.dtype)), out
+
     def torch(self, enc, x):
         return (self.model.torch_forward(enc, x),)
 

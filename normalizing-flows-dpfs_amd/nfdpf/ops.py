@@ -124,6 +124,24 @@ def soft_resample_backward(p, idx, w_out, g_x_out, g_w_out, alpha, D, row_base=0
     return gx, gp
 
 
+def cos_measurement_backward(pe_blob, enc, x, g_lik):
+    """Backward of the cosine measurement -> (g_enc [B, E], g_x [B, N, 2], g_params [1648] in
+    nn.Linear order W1 b1 W2 b2 W3 b3) (include/nfdpf.h nfdpf_cos_measurement_backward)."""
+    require_device(x, "cos_measurement_backward")
+    B, N, _ = x.shape
+    enc, x, g_lik = _c(enc), _c(x), _c(g_lik)
+    E = enc.shape[-1]
+    g_enc = torch.empty_like(enc)
+    gx = torch.empty_like(x)
+    gp = torch.empty(1648, device=x.device, dtype=f32)
+    nb = int(lib().nfdpf_cos_measurement_backward_workspace(B, N))
+    ws = torch.empty(max(1, nb // 4), device=x.device, dtype=f32)
+    check(lib().nfdpf_cos_measurement_backward(ptr(pe_blob), ptr(enc), ptr(x), ptr(g_lik), B, N, E, ptr(g_enc),
+                                               ptr(gx), ptr(gp), ptr(ws), stream_ptr(x.device)),
+          "nfdpf_cos_measurement_backward")
+    return g_enc, gx, gp
+
+
 _ws = {}
 
 

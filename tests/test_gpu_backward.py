@@ -328,3 +328,39 @@ def test_soft_resample_backward_edges():
                                         gw_out.to(DEV), 0.5, 2)
     _soft_check(gx, xr.grad, "dL/dx")
     _soft_check(gp, pr.grad, "dL/dp")
+
+
+@pytest.mark.parametrize("B,N,scale", [(4, 1000, 1.0), (3, 77, 20.0), (2, 1, 1.0)])
+def test_cos_measurement_backward_vs_autograd(B, N, scale, monkeypatch):
+    """measurement_model_cosine_distance under autograd (HIP backward) == float64 autograd of
+    model/models.py:206-219 + et_distance utils.py:8-15 (d/d encodings, particles, encoder)."""
+    import torch.nn as nn
+    from model.models import measurement_model_cosine_distance
+    from nfdpf import ops
+    calls = []
+    real = ops.cos_measurement_backward
+    monkeypatch.setattr(ops, "cos_measurement_backward", lambda *a, **k: calls.append(1) or real(*a, **k))
+    torch.manual_seed(B * 100 + N)
+    pe = nn.Sequential(nn.Linear(2, 16), nn.ReLU(), nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 32))
+    ref_pe = copy.deepcopy(pe).double()
+    m = measurement_model_cosine_distance(pe.to(DEV))
+    g = torch.Generator().manual_seed(N)
+    enc = torch.randn(B, 32, generator=g)
+    x = torch.randn(B, N, 2, generator=g) * scale
+    gl = torch.randn(B, N, generator=g)
+    encd, xd = enc.to(DEV).requires_grad_(True), x.to(DEV).requires_grad_(True)
+    lik = m(encd, xd)
+    (lik * gl.to(DEV)).sum().backward()
+    assert len(calls) == 1, "the backward did not run through nfdpf_cos_measurement_backward"
+    er, xr = enc.double().requires_grad_(True), x.double().requires_grad_(True)
+    es = ref_pe(xr)
+    eo = er[:, None, :].repeat(1, N, 1)
+    cosd = 1.0 - (torch.nn.functional.normalize(eo, p=2, dim=-1, eps=1e-12) *
+                  torch.nn.functional.normalize(es, p=2, dim=-1, eps=1e-12)).sum(-1)
+    lr = (1 / (1e-7 + cosd)).log()
+    (lr * gl.double()).sum().backward()
+    _soft_check(lik.detach(), lr.detach(), "lik")
+    _soft_check(xd.grad, xr.grad, "dL/dx")
+    _soft_check(encd.grad, er.grad, "dL/denc")
+    for (name, p), pr in zip(m.named_parameters(), ref_pe.parameters()):
+        _soft_check(p.grad, pr.grad, f"dL/d{name}")
