@@ -205,6 +205,13 @@ NFDPF_API int nfdpf_measurement(int kind, const float *pe_params, const float *m
  *   g_enc [B, E], g_x [B, N, 2]; g_params [1648]: the encoder's gradient in the plain
  *   nn.Linear layout W1 b1 W2 b2 W3 b3 (= the module's parameter order)
  *   workspace: nfdpf_cos_measurement_backward_workspace(B, N) bytes (fixed-order partials) */
+/* The particle encoder alone (model/models.py:130-139), for models that feed its output on
+ * (CRNVP: the flow's condition, model/models.py:256-278): mode 0 e_out [B*N, 32] = PE(x);
+ * mode 1 the backward for a given g_e [B*N, 32] -> g_x [B, N, 2], g_params [1648] (nn.Linear
+ * order), workspace nfdpf_cos_measurement_backward_workspace(B, N) bytes. */
+NFDPF_API int nfdpf_particle_encoder(int mode, const float *pe_params, const float *x, int B, int N,
+                                     const float *g_e, float *e_out, float *g_x, float *g_params,
+                                     void *workspace, void *stream);
 NFDPF_API int64_t nfdpf_cos_measurement_backward_workspace(int B, int N);
 NFDPF_API int nfdpf_cos_measurement_backward(const float *pe_params, const float *enc, const float *x,
                                              const float *g_lik, int B, int N, int E, float *g_enc,

@@ -46,6 +46,12 @@ __device__ __forceinline__ void normalize_bwd(const float (&a)[n], float norm, c
   }
 }
 
+// MODE: kPeCos (the cosine measurement: g = dL/dlik), kPeGrad (dL/de given per particle in
+// g_e [B*N, 32]: the particle encoder inside another model, e.g. the CRNVP condition),
+// kPeFwd (forward only: write e to e_out -- the recompute those models' backward needs)
+constexpr int kPeCos = 0, kPeGrad = 1, kPeFwd = 2;
+
+template <int MODE>
 __global__ __launch_bounds__(kMbRows) void cos_meas_bwd_kernel(const float *__restrict__ pe_params,
                                                                const float *__restrict__ enc,
                                                                const float *__restrict__ x,
@@ -60,16 +66,18 @@ __global__ __launch_bounds__(kMbRows) void cos_meas_bwd_kernel(const float *__re
   const int i = blk * kMbRows + lane;
   const bool valid = i < N;
   const int64_t o = (int64_t)b * N + i;
-  // the row's frame encoding, normalised (F.normalize, eps 1e-12)
-  float vv = lane < kE ? enc[(int64_t)b * kE + lane] : 0.f;
-  float ss = vv * vv;
+  if (MODE == kPeCos) {
+    // the row's frame encoding, normalised (F.normalize, eps 1e-12)
+    float vv = lane < kE ? enc[(int64_t)b * kE + lane] : 0.f;
+    float ss = vv * vv;
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) ss += __shfl_xor(ss, m);
-  const float vn = fmaxf(sqrtf(ss), 1e-12f);
-  if (lane < kE) vh[lane] = vv / vn;
-  __syncthreads();
+    for (int m = 1; m < 64; m <<= 1) ss += __shfl_xor(ss, m);
+    const float vn = fmaxf(sqrtf(ss), 1e-12f);
+    if (lane < kE) vh[lane] = vv / vn;
+    __syncthreads();
+  }
   const float x0 = valid ? x[2 * o] : 0.f, x1 = valid ? x[2 * o + 1] : 0.f;
-  const float g = valid ? g_lik[o] : 0.f;
+  const float g = (MODE == kPeCos && valid) ? g_lik[o] : 0.f;
   // ---- forward recompute ----
   float h1[kPe1], h2[kPe2], e[kE];
 #pragma unroll
@@ -91,26 +99,38 @@ __global__ __launch_bounds__(kMbRows) void cos_meas_bwd_kernel(const float *__re
     e[q] = a;
     es = fmaf(a, a, es);
   }
-  const float en = fmaxf(sqrtf(es), 1e-12f);
-  float dot = 0.f;
+  if (MODE == kPeFwd) {
+    if (valid)
 #pragma unroll
-  for (int q = 0; q < kE; ++q) dot = fmaf(e[q] / en, vh[q], dot);
-  const float cosd = 1.f - dot;
-  // dlik/dcosd = -1 / (1e-7 + cosd); dcosd/d e^ = -v^  ->  g_e^ = g r v^, g_v^ = g r e^
-  const float gr = g / (1e-7f + cosd);
-  float ge_hat[kE], ge[kE];
+      for (int q = 0; q < kE; ++q) g_x[o * kE + q] = e[q];  // e_out
+    return;
+  }
+  float ge[kE];
+  if (MODE == kPeCos) {
+    const float en = fmaxf(sqrtf(es), 1e-12f);
+    float dot = 0.f;
 #pragma unroll
-  for (int q = 0; q < kE; ++q) ge_hat[q] = gr * vh[q];
-  normalize_bwd<kE>(e, sqrtf(es), ge_hat, ge);
-  // this particle's share of the frame-encoding gradient, before the row's normalisation
-  // Jacobian: g r e^ summed over the workgroup (wave reduction per component)
-  float *vp = g_vpart + ((int64_t)b * gridDim.x + blk) * kE;
+    for (int q = 0; q < kE; ++q) dot = fmaf(e[q] / en, vh[q], dot);
+    const float cosd = 1.f - dot;
+    // dlik/dcosd = -1 / (1e-7 + cosd); dcosd/d e^ = -v^  ->  g_e^ = g r v^, g_v^ = g r e^
+    const float gr = g / (1e-7f + cosd);
+    float ge_hat[kE];
 #pragma unroll
-  for (int q = 0; q < kE; ++q) {
-    float s = gr * (e[q] / en);
+    for (int q = 0; q < kE; ++q) ge_hat[q] = gr * vh[q];
+    normalize_bwd<kE>(e, sqrtf(es), ge_hat, ge);
+    // this particle's share of the frame-encoding gradient, before the row's normalisation
+    // Jacobian: g r e^ summed over the workgroup (wave reduction per component)
+    float *vp = g_vpart + ((int64_t)b * gridDim.x + blk) * kE;
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
-    if (lane == 0) vp[q] = s;
+    for (int q = 0; q < kE; ++q) {
+      float s = gr * (e[q] / en);
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
+      if (lane == 0) vp[q] = s;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kE; ++q) ge[q] = valid ? g_lik[o * kE + q] : 0.f;  // dL/de given
   }
   // ---- back-propagation through the encoder ----
   float gh2[kPe2], gh1[kPe1];
@@ -248,8 +268,36 @@ extern "C" int nfdpf_cos_measurement_backward(const float *pe_params, const floa
   const int nblk = (N + kMbRows - 1) / kMbRows;
   float *partial = (float *)workspace;
   float *vpart = partial + (int64_t)B * nblk * kPeParams;
-  cos_meas_bwd_kernel<<<dim3(nblk, B), kMbRows, 0, st>>>(pe_params, enc, x, g_lik, N, g_x, vpart, partial);
+  cos_meas_bwd_kernel<kPeCos><<<dim3(nblk, B), kMbRows, 0, st>>>(pe_params, enc, x, g_lik, N, g_x, vpart, partial);
   cos_meas_finish_kernel<<<B, 64, 0, st>>>(enc, vpart, nblk, g_enc);
   meas_param_reduce_kernel<<<(kPeParams + 63) / 64, 256, 0, st>>>(partial, (int64_t)B * nblk, g_params);
   return launch_status("nfdpf_cos_measurement_backward");
+}
+
+// The particle encoder alone (model/models.py:130-139), for the measurement models that feed
+// its output into a further model (CRNVP: the flow's condition): mode 0 forward (e_out
+// [B*N, 32] = PE(x)), mode 1 backward (g_e [B*N, 32] given -> g_x, g_params in nn.Linear
+// order, fixed-order partials in the workspace of nfdpf_cos_measurement_backward_workspace).
+extern "C" int nfdpf_particle_encoder(int mode, const float *pe_params, const float *x, int B, int N,
+                                      const float *g_e, float *e_out, float *g_x, float *g_params,
+                                      void *workspace, void *stream) {
+  NFDPF_REQUIRE(B >= 0 && N >= 1 && (mode == 0 || mode == 1), "nfdpf_particle_encoder: bad arguments");
+  hipStream_t st = as_stream(stream);
+  if (B == 0) {
+    if (mode == 1 && g_params) (void)hipMemsetAsync(g_params, 0, sizeof(float) * kPeParams, st);
+    return launch_status("nfdpf_particle_encoder");
+  }
+  const int nblk = (N + kMbRows - 1) / kMbRows;
+  if (mode == 0) {
+    NFDPF_REQUIRE(pe_params && x && e_out, "nfdpf_particle_encoder: null pointer");
+    cos_meas_bwd_kernel<kPeFwd><<<dim3(nblk, B), kMbRows, 0, st>>>(pe_params, nullptr, x, nullptr, N, e_out,
+                                                                   nullptr, nullptr);
+  } else {
+    NFDPF_REQUIRE(pe_params && x && g_e && g_x && g_params && workspace, "nfdpf_particle_encoder: null pointer");
+    float *partial = (float *)workspace;
+    cos_meas_bwd_kernel<kPeGrad><<<dim3(nblk, B), kMbRows, 0, st>>>(pe_params, nullptr, x, g_e, N, g_x, nullptr,
+                                                                    partial);
+    meas_param_reduce_kernel<<<(kPeParams + 63) / 64, 256, 0, st>>>(partial, (int64_t)B * nblk, g_params);
+  }
+  return launch_status("nfdpf_particle_encoder");
 }

@@ -15,7 +15,7 @@ from nf.flows import FCNN, RealNVP, RealNVP_cond, MAF  # noqa: F401  (reference 
 from nf.models import NormalizingFlowModel, NormalizingFlowModel_cond
 from nfdpf import autograd as _ag
 from nfdpf import ops as _ops
-from nfdpf.pack import blob, encoder_tensors, flows_tensors, paired_mlp_tensors
+from nfdpf.pack import blob, blob_grad_to_params, encoder_tensors, flows_tensors, paired_mlp_tensors
 from utils import et_distance
 
 device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
@@ -154,17 +154,56 @@ class _MeasRunner:
         (csrc/measure_bwd.hip); None for the other models (autograd then differentiates
         ``torch``)."""
         m = self.model
-        if self.kind != "cos" or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 or x.shape[-1] != 2:
+        if self.kind not in ("cos", "CRNVP") or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 \
+                or x.shape[-1] != 2:
             return None
         pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
         g = gouts[0] if gouts[0] is not None else torch.zeros(x.shape[:2], device=x.device)
-        g_enc, gx, gp = _ops.cos_measurement_backward(pe, enc.float(), x.float(), g.float())
-        params = list(m.parameters())
-        out, off = [], 0
-        for p in params:  # the module's parameters are the encoder's W1 b1 W2 b2 W3 b3
-            out.append(gp[off:off + p.numel()].view_as(p).to(p.dtype) if p.requires_grad else None)
+        g = g.float()
+        pe_params = list(m.particle_encoder.parameters())
+        if self.kind == "cos":
+            g_enc, gx, gp = _ops.cos_measurement_backward(pe, enc.float(), x.float(), g)
+            extra = []
+        else:
+            out = self._crnvp_backward(pe, enc.float(), x.float(), g)
+            if out is None:
+                return None
+            g_enc, gx, gp, extra = out
+        res, off = [], 0
+        for p in pe_params:  # the encoder's W1 b1 W2 b2 W3 b3, nn.Linear layout
+            res.append(gp[off:off + p.numel()].view_as(p).to(p.dtype) if p.requires_grad else None)
             off += p.numel()
-        return (g_enc.to(enc.dtype), gx.to(x.dtype)), out
+        res += extra  # CRNVP: the flow's parameters (m.parameters() lists the encoder first)
+        return (g_enc.to(enc.dtype), gx.to(x.dtype)), res
+
+    def _crnvp_backward(self, pe, enc, x, g):
+        """measurement_model_cnf (model/models.py:256-278): lik = u - max_n u with u = log N(z) +
+        log-det of the CNF stack on the frame encoding conditioned on the particle encoding.
+        The max routes -sum_n g to the row's argmax; then the stack backward (HIP) gives d/d the
+        condition (-> encoder backward, HIP) and d/d the repeated frame encoding (summed per row)."""
+        from nf.models import _isotropic
+        m = self.model
+        fl = list(m.CNF.flows)
+        iso = _isotropic(m.CNF.prior)
+        if iso is None or fl[0].dim != 32 or fl[0].hidden_dim != 8 or not 1 <= len(fl) <= 4:
+            return None
+        pm, ps = iso
+        B, N, _ = x.shape
+        cb = blob(m, "meas", m.CNF.flows, lambda: flows_tensors(m.CNF.flows), x.device)
+        es = _ops.particle_encoder_forward(pe, x)
+        eo = enc[:, None, :].expand(B, N, 32).reshape(B * N, 32).contiguous()
+        _, ld, lp = _ops.cond_stack(cb, len(fl), 32, 32, 8, eo, es, 1, False, pm, ps, want_prior=True)
+        am = (lp + ld).view(B, N).argmax(-1)
+        g_u = g.clone()
+        g_u[torch.arange(B, device=g.device), am] -= g.sum(-1)
+        g_u = g_u.reshape(-1)
+        g_eo, g_es, g_cb = _ops.cond_stack_backward(cb, len(fl), 32, 32, 8, eo, es, False, torch.zeros_like(eo),
+                                                    g_u, g_u, pm, ps)
+        gx, gp = _ops.particle_encoder_backward(pe, x, g_es)
+        cnf_params = [p for f in fl for p in f.parameters()]
+        gf = blob_grad_to_params(m, "meas", cnf_params, lambda get: flows_tensors(fl, get), g_cb)
+        gf = [gi if p.requires_grad else None for gi, p in zip(gf, cnf_params)]
+        return g_eo.view(B, N, 32).sum(1), gx, gp, gf
 
     def torch(self, enc, x):
         return (self.model.torch_forward(enc, x),)

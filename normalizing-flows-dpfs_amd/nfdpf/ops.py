@@ -142,6 +142,31 @@ def cos_measurement_backward(pe_blob, enc, x, g_lik):
     return g_enc, gx, gp
 
 
+def particle_encoder_forward(pe_blob, x):
+    """PE(x) -> [B*N, 32] (nfdpf_particle_encoder mode 0)."""
+    require_device(x, "particle_encoder_forward")
+    B, N, _ = x.shape
+    x = _c(x)
+    e = torch.empty((B * N, 32), device=x.device, dtype=f32)
+    check(lib().nfdpf_particle_encoder(0, ptr(pe_blob), ptr(x), B, N, None, ptr(e), None, None, None,
+                                       stream_ptr(x.device)), "nfdpf_particle_encoder")
+    return e
+
+
+def particle_encoder_backward(pe_blob, x, g_e):
+    """-> (g_x [B, N, 2], g_params [1648] nn.Linear order) (nfdpf_particle_encoder mode 1)."""
+    require_device(x, "particle_encoder_backward")
+    B, N, _ = x.shape
+    x, g_e = _c(x), _c(g_e)
+    gx = torch.empty_like(x)
+    gp = torch.empty(1648, device=x.device, dtype=f32)
+    nb = int(lib().nfdpf_cos_measurement_backward_workspace(B, N))
+    ws = torch.empty(max(1, nb // 4), device=x.device, dtype=f32)
+    check(lib().nfdpf_particle_encoder(1, ptr(pe_blob), ptr(x), B, N, ptr(g_e), None, ptr(gx), ptr(gp), ptr(ws),
+                                       stream_ptr(x.device)), "nfdpf_particle_encoder")
+    return gx, gp
+
+
 _ws = {}
 
 
