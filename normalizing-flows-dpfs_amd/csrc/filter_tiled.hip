@@ -960,6 +960,7 @@ template <bool MERGED>
 __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;  // cb_dyn / cb_cond in split order
   __shared__ float xbuf[4 * kTile];
+  __shared__ float hbuf[2 * kPeH2 / 2 * kTile];  // the encoder's hidden halves (encode_dot_pair)
   __shared__ int xflag[16];
   __shared__ float smf[16];
   __shared__ double smd[48];
@@ -1009,7 +1010,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
     stage_prior_split(d, S, i, in, L.cb_dyn, q0x, q1x, jp, x, kTile, propose, prior);
     // cosine measurement (model/models.py:206-219): outputs [16 role, 16 role + 16) here
     float ss, dot;
-    encode_dot<kE, kE / 4>(wptr(d.pe_params), q0x, q1x, L.encv, ss, dot, role * (kE / 4));
+    encode_dot_pair<kE>(wptr(d.pe_params), q0x, q1x, L.encv, ss, dot, x, hbuf, kTile);
     const float ss_o = pair_swap(x, ss, kTile), dot_o = pair_swap(x, dot, kTile);
     ss = role ? ss_o + ss : ss + ss_o;
     dot = role ? dot_o + dot : dot + dot_o;

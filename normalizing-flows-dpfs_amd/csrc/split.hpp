@@ -92,6 +92,70 @@ __device__ __forceinline__ float pair_swap(PairX &x, float v, int tile_len) {
   return b[(1 - x.role) * tile_len + x.slot];
 }
 
+// Cosine pieces (|e|^2, <e, v> over this role's output pairs) with the particle encoder's
+// second layer split over the wave pair as well (model/models.py:130-139): role r computes
+// hidden pairs [8 r, 8 r + 8) of Linear(16, 32), the pair exchanges them through `hbuf`
+// ([2 roles][16 floats][tile_len], used once per launch), and each role then computes its 8
+// output pairs from all 32 hidden units -- the fma sequence of pe_hidden / pe_out per output.
+template <int E>
+__device__ __forceinline__ void encode_dot_pair(cfloat *pe, float x0, float x1, const float *v, float &ss,
+                                                float &dot, PairX &x, float *hbuf, int tile_len) {
+  constexpr int M = kPeH2 / 2, MH = M / 2;  // 16 hidden pairs, 8 per role
+  cf2 *w1 = (cf2 *)pe, *b1 = (cf2 *)(pe + kPeB1);
+  f2 h1[kPeH1 / 2];
+#pragma unroll
+  for (int m = 0; m < kPeH1 / 2; ++m)
+    h1[m] = relu2(pfma(w1[2 * m + 1], splat(x1), pfma(w1[2 * m], splat(x0), b1[m])));
+  const int m0 = x.role * MH;
+  cf2 *w2 = (cf2 *)(pe + kPeW2) + m0, *b2 = (cf2 *)(pe + kPeB2) + m0;
+  f2 mine[MH];
+#pragma unroll
+  for (int m = 0; m < MH; ++m) mine[m] = b2[m];
+#pragma unroll
+  for (int k = 0; k < kPeH1; ++k) {
+    const float hk = pick(h1, k);
+#pragma unroll
+    for (int m = 0; m < MH; ++m) mine[m] = pfma(w2[k * M + m], splat(hk), mine[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < MH; ++m) mine[m] = relu2(mine[m]);
+  // exchange the halves (the pair_swap protocol: values, then the counter, then spin)
+  lds_float *hb = (lds_float *)hbuf;
+#pragma unroll
+  for (int m = 0; m < MH; ++m) {
+    hb[(x.role * 2 * MH + 2 * m) * tile_len + x.slot] = mine[m].x;
+    hb[(x.role * 2 * MH + 2 * m + 1) * tile_len + x.slot] = mine[m].y;
+  }
+  const int k = ++x.k;
+#ifndef NFDPF_EXP_NOWAIT
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  *x.mine = k;
+  for (int it = 0; __builtin_amdgcn_readfirstlane(*x.theirs) < k && it < kSpinCap; ++it)
+    __builtin_amdgcn_s_sleep(1);
+#endif
+  asm volatile("" ::: "memory");
+  f2 h2[M];
+  const int other = 1 - x.role;
+#pragma unroll
+  for (int m = 0; m < MH; ++m) {
+    const f2 o{hb[(other * 2 * MH + 2 * m) * tile_len + x.slot], hb[(other * 2 * MH + 2 * m + 1) * tile_len + x.slot]};
+    h2[x.role ? m : MH + m] = o;
+    h2[x.role ? MH + m : m] = mine[m];
+  }
+  f2 a[E / 4];
+  pe_out<E, E / 4>(pe, h2, x.role * (E / 4), a);
+  ss = 0.f;
+  dot = 0.f;
+  const int o0 = x.role * (E / 4);
+#pragma unroll
+  for (int m = 0; m < E / 4; ++m) {
+    ss = fmaf(a[m].x, a[m].x, ss);
+    dot = fmaf(a[m].x, v[2 * (o0 + m)], dot);
+    ss = fmaf(a[m].y, a[m].y, ss);
+    dot = fmaf(a[m].y, v[2 * (o0 + m) + 1], dot);
+  }
+}
+
 // One net (t or s) of a coupling half on input u; cb = this net's 4 folded bias pairs.
 __device__ __forceinline__ float net_split(cf2 *w, float u, const f2 *cb) {
   constexpr int P = kH / 2;
