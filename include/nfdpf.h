@@ -283,9 +283,11 @@ typedef struct nfdpf_filter_desc {
   float *scratch;           /* [2][B,N,4] per-particle hand-off between stages (x_dyn, propose, prior),
                                indexed by step parity: step t's values must not overwrite step t-1's,
                                which the deferred normalisation of slot t-1 reads during step t */
-  void *prof_events;        /* optional hipEvent_t[2]: recorded around the dominant launch
-                               (the whole step for nfdpf_filter_step, the proposal+measurement
-                               launch for nfdpf_filter_step_tiled) -- live kernel timing */
+  void *prof_events;        /* optional hipEvent_t[2]: live kernel timing of the dominant launch
+                               -- recorded around the whole step for nfdpf_filter_step; carried
+                               by the proposal+measurement launch's own dispatch
+                               (hipExtLaunchKernel: its begin / end timestamps) for
+                               nfdpf_filter_step_tiled */
   int32_t ess_local;        /* tiled: 1 = ess_all holds this shard's B rows only (row b at b), the
                                gate coming from `gate` -- the speculative-gate mode of a sharded
                                batch (nfdpf_ess_gate_tiled_batch verifies it after the pass) */

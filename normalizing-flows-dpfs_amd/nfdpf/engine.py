@@ -353,8 +353,11 @@ class FilterEngine:
                     d.ot_x = xin.data_ptr()  # not read: the motion stage keeps the previous particles
             d.prof_events = None
             ev = None
-            if self.step_events is not None and t == T // 2:
-                # one sampled step per pass: an event pair costs ~6 us of stream time
+            # the tiled step carries the events in the timed launch's own dispatch (no stream
+            # cost): every step; elsewhere an event pair costs ~6 us of stream time: one sampled
+            # step per pass
+            every = c.kernel == "tiled" and not external
+            if self.step_events is not None and (every or t == T // 2):
                 from .prof import EventPair
                 ev = EventPair()
                 self.step_events.append(ev)
