@@ -346,7 +346,10 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q) {
 
 // x: particle (b, i) at x + b * x_rs + 2 i;  enc: row b at enc + b * enc_rs (192 floats);
 // lik: (b, i) at lik + b * lik_rs + i.  Raw likelihood (no row-max shift).
-__global__ __launch_bounds__(kThreads, 2) void cglow_kernel(const float *__restrict__ pe,
+// Occupancy is set by the LDS (80 KB per workgroup: 2 per CU) whatever the bound says; a
+// minimum of 1 block per CU lets the compiler keep 128 more uniform values in SGPRs/VGPRs
+// (SGPR spills 182 -> 54): C5 launch 5.24 -> 5.09 ms (A/B, 3 runs each).
+__global__ __launch_bounds__(kThreads, 1) void cglow_kernel(const float *__restrict__ pe,
                                                             const float *__restrict__ glow,
                                                             const float *__restrict__ enc,
                                                             int64_t enc_rs, const float *__restrict__ x,
