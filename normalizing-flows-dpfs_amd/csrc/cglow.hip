@@ -59,22 +59,34 @@ constexpr int kOffA = 0, kOffI = CondA::size, kOffF = kOffI + CondI::size;
 constexpr int kStep = kOffF + Aff::size;
 
 // ---- workgroup LDS ----
+// Stage-local buffers share storage (anonymous union): the encoder's hidden layers, the
+// conditioning nets' activations and the y / coupling stage's grids are never live together
+// (every hand-over is separated by a SYNC, the tile loop ends with one), which brings the
+// workgroup from 80 KB to 50 KB of LDS: 3 workgroups per CU instead of 2.
 struct Lds {
   float pxy[kTileP][2];
-  float h1[kTileP][kPeH1 + 1];
-  float h2[kTileP][kPeH2 + 1];
   float xs[kTileP][kE + 1];            // particle encoding, [c][8][8]
-  float cv1[kTileP][16][2 * kXH + 1];  // cond conv1 (A | I) at the 4x4 positions
-  float cv2[kTileP][4][2 * kXH + 1];   // cond conv2 at 2x2
-  float cv3[kTileP][2 * kXH + 1];
-  float v0[kTileP][2 * kXS + 1];
-  float v1[kTileP][2 * kXS + 1];
   float an[kTileP][2 * kC + 1];        // actnorm (logs | bias)
   float wm[kTileP][kC * kC + 1];       // 1x1 conv weight, row-major [out][in]
-  float ex[kTileP][16][kC + 1];        // 4x4-grid exchange
-  float yv[kTileP][16][kC + 1];        // y after actnorm + 1x1 conv, per position
   float ld[kTileP];                    // per-particle log-det of actnorm + 1x1 conv
   int row[kTileP];
+  union {
+    struct {  // particle encoder
+      float h1[kTileP][kPeH1 + 1];
+      float h2[kTileP][kPeH2 + 1];
+    };
+    struct {  // conditioning nets (actnorm A | 1x1 conv I)
+      float cv1[kTileP][16][2 * kXH + 1];  // cond conv1 (A | I) at the 4x4 positions
+      float cv2[kTileP][4][2 * kXH + 1];   // cond conv2 at 2x2
+      float cv3[kTileP][2 * kXH + 1];
+      float v0[kTileP][2 * kXS + 1];
+      float v1[kTileP][2 * kXS + 1];
+    };
+    struct {  // y after actnorm + 1x1 conv, the coupling's convolutions
+      float ex[kTileP][16][kC + 1];  // 4x4-grid exchange
+      float yv[kTileP][16][kC + 1];  // y after actnorm + 1x1 conv, per position
+    };
+  };
 };
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -346,10 +358,10 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q) {
 
 // x: particle (b, i) at x + b * x_rs + 2 i;  enc: row b at enc + b * enc_rs (192 floats);
 // lik: (b, i) at lik + b * lik_rs + i.  Raw likelihood (no row-max shift).
-// Occupancy is set by the LDS (80 KB per workgroup: 2 per CU) whatever the bound says; a
-// minimum of 1 block per CU lets the compiler keep 128 more uniform values in SGPRs/VGPRs
-// (SGPR spills 182 -> 54): C5 launch 5.24 -> 5.09 ms (A/B, 3 runs each).
-__global__ __launch_bounds__(kThreads, 1) void cglow_kernel(const float *__restrict__ pe,
+// 3 workgroups per CU: 50 KB of LDS each (the stage union of Lds) and <= 168 VGPRs (162) for
+// 3 waves per SIMD.  (r01f: min-blocks 2 with 80 KB of LDS spilled 182 SGPRs and ran 5.24 ms
+// at C5; min-blocks 1, same occupancy, 5.09 ms; the union + min-blocks 3 4.72 ms -- A/B, 3 runs.)
+__global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restrict__ pe,
                                                             const float *__restrict__ glow,
                                                             const float *__restrict__ enc,
                                                             int64_t enc_rs, const float *__restrict__ x,
