@@ -557,7 +557,7 @@ extern "C" int nfdpf_cglow_measurement(const float *pe_params, const float *glow
     hipDeviceProp_t pr;
     if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
   }
-  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 4);
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 3);  // the resident count: 3 per CU
   cglow_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(pe_params, glow_params, enc, enc_rs, x, x_rs, B, N,
                                                         lik, lik_rs);
   return launch_status("nfdpf_cglow_measurement");
