@@ -554,10 +554,12 @@ extern "C" int nfdpf_cglow_measurement(const float *pe_params, const float *glow
   const int64_t tiles = ((int64_t)B * N + kTileP - 1) / kTileP;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t pr;
-    if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
   }
-  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 3);  // the resident count: 3 per CU
+  // a persistent grid of exactly the resident workgroups (3 per CU: LDS 50 KB, 162 VGPRs):
+  // more would start a second, late round of workgroups and leave the tail unbalanced
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 3);
   cglow_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(pe_params, glow_params, enc, enc_rs, x, x_rs, B, N,
                                                         lik, lik_rs);
   return launch_status("nfdpf_cglow_measurement");
