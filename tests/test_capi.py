@@ -68,3 +68,17 @@ def test_argument_validation_without_device():
     assert lib.nfdpf_filter_step(ctypes.byref(d), None) == _lib.NFDPF_EINVAL
     assert b"N >= 2" in lib.nfdpf_last_error()
     assert lib.nfdpf_ot_workspace_bytes(64, 1000) > 64 * 1000 * 4 * 8
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes binding (nfdpf/_lib.py SIGNATURES) passes as many arguments as the header
+    prototype declares -- a drift here would shift every later argument at the C ABI."""
+    import re
+    from nfdpf import _lib
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    protos = dict(re.findall(r"NFDPF_API\s+[\w\s\*]+?\b(nfdpf_\w+)\s*\(([^)]*)\)", txt))
+    assert set(_lib.SIGNATURES) <= set(protos), sorted(set(_lib.SIGNATURES) - set(protos))
+    for name, (_, argtypes) in _lib.SIGNATURES.items():
+        params = protos[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert len(argtypes) == n, f"{name}: ctypes passes {len(argtypes)} arguments, the header declares {n}"
