@@ -69,3 +69,19 @@ def test_blob_grad_scatter_matches_autograd_of_pack():
         ref = torch.autograd.grad(flat, params, g)
         ours = blob_grad_to_params(fl[0], "t", params, lambda get: flows_tensors(fl, get), g)
         assert all(torch.equal(a, b) for a, b in zip(ref, ours))
+
+
+def test_hip_backward_declines_unsupported_stacks():
+    """CouplingStack.hip_backward returns None (autograd then differentiates the PyTorch
+    restatement) for what nfdpf_cond_stack_backward is not built for -- before any device call."""
+    import torch
+    from nf.flows import CouplingStack, RealNVP_cond
+    wide = [RealNVP_cond(2, 16, obser_dim=4)]             # hidden 16
+    many = [RealNVP_cond(2, 8, obser_dim=4) for _ in range(5)]  # 5 flows
+    x, c = torch.zeros(3, 2), torch.zeros(3, 4)
+    g = (torch.zeros(3, 2), torch.zeros(3))
+    assert CouplingStack(wide[0], wide, 2, 4, 16, False).hip_backward(x, c, g) is None
+    assert CouplingStack(many[0], many, 2, 4, 8, True).hip_backward(x, c, g) is None
+    # a broadcast (per-batch) condition is not the per-row layout the kernel takes
+    one = [RealNVP_cond(2, 8, obser_dim=4)]
+    assert CouplingStack(one[0], one, 2, 4, 8, False).hip_backward(x, torch.zeros(1, 4), g) is None
