@@ -181,6 +181,12 @@ NFDPF_API int nfdpf_ot_transport_backward(const float *g_out, int B, int N, floa
  *   softmin evaluations that left the shifted fast path and were recomputed exactly. */
 NFDPF_API int nfdpf_ot_stats(const void *workspace, int32_t *host_out);
 
+/* Health of the wave-pair hand-offs of the tiled step (csrc/split.hpp): the number of
+ * exchanges that gave up waiting for their partner wave since the last reset (a correct run
+ * never does; the launch's outputs are then invalid).  Synchronous device read; reset != 0
+ * clears the count.  Returns -1 if the read failed. */
+NFDPF_API int nfdpf_split_fault(int reset);
+
 /* ESS gate of DPFs.py:163-165: gate = mean_b(inv_ess[b]) < 0.5 N (or force) -> int32 [1] */
 NFDPF_API int nfdpf_ess_gate(const float *inv_ess, int B, int N, int force, int32_t *gate,
                    void *stream);

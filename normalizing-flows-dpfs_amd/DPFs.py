@@ -1,13 +1,15 @@
 """DPF -- the reference's DPFs.py class, same constructor / attributes / methods / returns,
 with the particle-update hot path on MI355X.
 
-``filtering_pos`` (DPFs.py:144-216) runs one fused HIP kernel per time step
-(nfdpf.engine.FilterEngine, csrc/filter_step.hip) whenever autograd is not recording --
-evaluation, testing, benchmarking.  With autograd active (``e2e_train``) it runs the
-reference's loop over this package's modules: each flow / measurement / resampler call is
-a HIP forward whose backward is recomputed with PyTorch ops (nfdpf.autograd; HIP backward
-kernels are SURVEY.md §8f1 "next").  Epoch loops, logging and checkpoint IO around the hot
-path keep the reference's behaviour (DPFs.py:218-451).
+``filtering_pos`` (DPFs.py:144-216) runs on nfdpf.engine.FilterEngine whenever autograd is not
+recording -- evaluation, testing, benchmarking: the tiled multi-CU step pipeline of
+csrc/filter_tiled.hip (two launches per time step at C2), plus the Sinkhorn launches when the
+OT gate fires.  With autograd active (``e2e_train``) it runs the reference's loop over this
+package's modules: every flow / measurement / resampler call is a HIP forward, and the
+backward is a HIP kernel for the coupling-flow stacks, the soft and OT resamplers and the
+cosine / CRNVP measurements (the other models differentiate a PyTorch recompute of their
+forward, nfdpf/autograd.py).  Epoch loops, logging and checkpoint IO around the hot path keep
+the reference's behaviour (DPFs.py:218-451).
 """
 import os
 import time
@@ -25,7 +27,7 @@ from model.models import (build_conditional_glow, build_conditional_nf, build_de
                           measurement_model_Gaussian, measurement_model_NN, motion_update, nf_dynamic_model,
                           proposal_likelihood)
 from nfdpf.engine import FilterConfig, FilterEngine, ShardInfo
-from nfdpf.gradsync import GradBucket, global_mean, world_size
+from nfdpf.gradsync import GradBucket, global_mean, sharded_supervised_loss, world_size
 from resamplers.resamplers import resampler
 from utils import (checkpoint_state, compute_normal_density, load_model, normalize_log_probs,
                    particle_initialization)
@@ -125,7 +127,10 @@ class DPF(nn.Module):
         (particle_list, particle_weight_list, noise_list, likelihood_list, init_weights_log, index_list, jac_list,
          prior_list, obs_likelihood) = self.filtering_pos(image, start_state, vel)
         mask = self.get_mask() if train else 1.0
-        loss_sup, predictions = supervised_loss(particle_list, particle_weight_list, state, mask, train)
+        if world_size() > 1:  # batch-sharded: the full-batch RMSE and its exact gradient (nfdpf.gradsync)
+            loss_sup, predictions = sharded_supervised_loss(particle_list, particle_weight_list, state, mask, train)
+        else:
+            loss_sup, predictions = supervised_loss(particle_list, particle_weight_list, state, mask, train)
         loss_ae = autoencoder_loss(image, train, self.encoder, self.decoder)
         if self.param.trainType == "DPF":
             loss_pseud_lik = None
@@ -180,7 +185,13 @@ class DPF(nn.Module):
             shard = ShardInfo.from_env(enc.shape[0])
             res = eng.run(enc, start_state_vs, vel_input[:, :self.seq_len], shard=shard)
         self.last_filter_result = res
-        return res.as_tuple()
+        out = list(res.as_tuple())
+        if shard.row_base:
+            # the engine keeps GLOBAL flat indices (N * (row_base + b) + j, FilterResult.index);
+            # the reference's tuple holds them flat into THIS batch's B * N (DPFs.py:162,166),
+            # which the pseudo-likelihood losses index with (losses.py:33-69)
+            out[5] = res.index - self.num_particle * shard.row_base
+        return tuple(out)
 
     def _filtering_modules(self, obs, start_state_vs, vel_input):
         """The reference loop over this package's HIP-backed modules (autograd path)."""

@@ -870,7 +870,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   __shared__ StepShared L;
   __shared__ float qx[kTile][2];
   __shared__ float lx[kTile];
-  __shared__ float ssx[ROLES][kTile], dotx[ROLES][kTile];
+  __shared__ double ssx[ROLES][kTile], dotx[ROLES][kTile];
   __shared__ float smf[16];   // per-wave softmax partials (up to 12 waves)
   __shared__ double smd[48];
   TRACE(2, 0)
@@ -921,7 +921,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
       // cosine measurement, half of the encoder outputs per role (model/models.py:206-219)
       static_assert(ROLES != 3 || MEAS == NFDPF_MEAS_COS, "three roles: cosine measurement only");
       constexpr int HP = kE / 4;  // output pairs per role
-      float ss, dot;
+      double ss, dot;
       encode_dot<kE, HP>(wptr(d.pe_params), qx[pl][0], qx[pl][1], L.encv, ss, dot, (role - 1) * HP);
       ssx[role][pl] = ss;
       dotx[role][pl] = dot;
@@ -935,9 +935,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   if (flows && valid) {
     float lik;
     if (ROLES == 3) {
-      const float ss = ssx[1][pl] + ssx[2][pl], dot = dotx[1][pl] + dotx[2][pl];
-      const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
-      lik = logf(1.0f / (1e-7f + cosd));
+      lik = cos_lik(ssx[1][pl] + ssx[2][pl], dotx[1][pl] + dotx[2][pl], L.vinv);
       S.hlik[i] = lik;
     } else {
       lik = lx[pl];
@@ -963,6 +961,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
   __shared__ StepShared L;  // cb_dyn / cb_cond in split order
   __shared__ float xbuf[4 * kTile];
   __shared__ float hbuf[2 * kPeH2 / 2 * kTile];  // the encoder's hidden halves (encode_dot_pair)
+  __shared__ float dbuf[2 * 4 * kTile];          // the fp64 cosine partials (pair_swap_once2)
   __shared__ int xflag[16];
   __shared__ float smf[16];
   __shared__ double smd[48];
@@ -1011,13 +1010,13 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
     const float jp = stage_propose_inverse_split(d, in, L.cb_cond, x, kTile, q0x, q1x);
     stage_prior_split(d, S, i, in, L.cb_dyn, q0x, q1x, jp, x, kTile, propose, prior);
     // cosine measurement (model/models.py:206-219): outputs [16 role, 16 role + 16) here
-    float ss, dot;
+    double ss, dot;
     encode_dot_pair<kE>(wptr(d.pe_params), q0x, q1x, L.encv, ss, dot, x, hbuf, kTile);
-    const float ss_o = pair_swap(x, ss, kTile), dot_o = pair_swap(x, dot, kTile);
+    double ss_o, dot_o;
+    pair_swap_once2(x, ss, dot, dbuf, kTile, ss_o, dot_o);
     ss = role ? ss_o + ss : ss + ss_o;
     dot = role ? dot_o + dot : dot + dot_o;
-    const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
-    const float lk = logf(1.0f / (1e-7f + cosd));
+    const float lk = cos_lik(ss, dot, L.vinv);
     if (role == 0) {
       S.hlik[i] = lk;
       u = logw(lr, lk, prior, propose);
@@ -1247,6 +1246,19 @@ extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *es
   if (B == 0) return NFDPF_OK;
   tiled_ess_init_kernel<<<dim3(n_tiles(N), B), kTile, 0, as_stream(stream)>>>(p0, N, ess_parts);
   return launch_status("nfdpf_filter_tiled_init");
+}
+
+extern "C" int nfdpf_split_fault(int reset) {
+  int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_split_fault), sizeof(int)) != hipSuccess) {
+    set_error("nfdpf_split_fault: hipMemcpyFromSymbol failed");
+    return -1;
+  }
+  if (reset && v != 0) {
+    const int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_fault), &z, sizeof(int)) != hipSuccess) return -1;
+  }
+  return v;
 }
 
 #ifdef NFDPF_EXP_TRACE

@@ -322,23 +322,36 @@ __device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, 
 
 // Cosine-distance pieces for the particle encoder output (|e|^2, <e, v>) over output pairs
 // [m0, m0 + MP) (model/models.py:130-139 then utils.py:8-15); a caller may split the E
-// outputs over several waves.
+// outputs over several waves.  v is the RAW frame encoding; both sums accumulate in fp64 (the
+// cosine distance 1 - cos ~ 1e-2 at a likely particle cancels two digits of them, and
+// -log(1e-7 + 1 - cos) amplifies what is left by 1 / (1 - cos): fp32 sums made the likelihood
+// ~1.3x less accurate than the reference's own fp32 F.normalize-then-dot, fp64 sums make it
+// ~10x more accurate -- tests/test_gpu_parity_full.py).
 template <int E, int MP = E / 2>
-__device__ __forceinline__ void encode_dot(cfloat *pe, float x0, float x1, const float *v, float &ss,
-                                           float &dot, int m0 = 0) {
+__device__ __forceinline__ void encode_dot(cfloat *pe, float x0, float x1, const float *v, double &ss,
+                                           double &dot, int m0 = 0) {
   f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
   f2 a[MP];
   pe_out<E, MP>(pe, h2, m0, a);
-  ss = 0.f;
-  dot = 0.f;
+  ss = 0.0;
+  dot = 0.0;
 #pragma unroll
   for (int m = 0; m < MP; ++m) {
-    ss = fmaf(a[m].x, a[m].x, ss);
-    dot = fmaf(a[m].x, v[2 * (m0 + m)], dot);
-    ss = fmaf(a[m].y, a[m].y, ss);
-    dot = fmaf(a[m].y, v[2 * (m0 + m) + 1], dot);
+    const double ax = a[m].x, ay = a[m].y;
+    ss = fma(ax, ax, ss);
+    dot = fma(ax, (double)v[2 * (m0 + m)], dot);
+    ss = fma(ay, ay, ss);
+    dot = fma(ay, (double)v[2 * (m0 + m) + 1], dot);
   }
+}
+
+// log(1 / (1e-7 + cosd)), cosd = 1 - <e / max(|e|, 1e-12), v / max(|v|, 1e-12)>
+// (measurement_model_cosine_distance + et_distance, model/models.py:206-219, utils.py:8-15),
+// from fp64 |e|^2, <e, v> and the row's 1 / max(|v|, 1e-12) (fp64).
+__device__ __forceinline__ float cos_lik(double ss, double dot, double vinv) {
+  const double cosd = 1.0 - dot * vinv / fmax(sqrt(ss), 1e-12);
+  return -logf((float)(1e-7 + cosd));
 }
 
 }  // namespace nfdpf

@@ -17,7 +17,8 @@ struct StepShared {
   f2 cb_dyn[kMaxFlows * 2 * kH];   // folded bias pairs [flow][coupling half][j] of nf_dyn
   f2 cb_cond[kMaxFlows * 2 * kH];  // ... of the proposal flow
   float ctx[kMaxCtx];
-  float encv[kE];       // this row's frame encoding (normalised for cos)
+  float encv[kE];       // this row's frame encoding (raw)
+  double vinv;          // cos: 1 / max(|encv|, 1e-12), fp64
   float nnrow[kNnH];    // NN: folded first layer of the obs half
   float f[16];
   double d[16];
@@ -41,11 +42,10 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
                                          float x1) {
   if constexpr (MEAS == NFDPF_MEAS_COS) {
     // measurement_model_cosine_distance + et_distance (model/models.py:206-219, utils.py:8-15)
-    // <e/|e|, v> computed as <e, v>/|e| (same value to ~1 ulp, no E-wide register array)
-    float ss, dot;
+    // <e/|e|, v/|v|> computed as <e, v>/(|e| |v|) in fp64 (flows.hpp cos_lik)
+    double ss, dot;
     encode_dot<kE>(wptr(d.pe_params), x0, x1, L.encv, ss, dot);
-    const float cosd = 1.0f - dot / fmaxf(sqrtf(ss), 1e-12f);
-    return logf(1.0f / (1e-7f + cosd));
+    return cos_lik(ss, dot, L.vinv);
   } else if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
     // measurement_model_cnf (model/models.py:256-278): flow input = frame encoding,
     // condition = particle encoding; N(0, prior_std^2 I) prior + log-det
@@ -69,15 +69,17 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
         for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_pair_c<HALF, kH, kE>(fw + n * ns, j, e);
       ld += coupling_forward<HALF, kH>(fw, kE, lo, up, cb);
     }
-    const float is = 1.0f / d.meas_prior_std;
-    float m = 0.f;
+    // the prior's quadratic form in fp64 (32 terms of ~10 each: fp32 lost ~1e-4 absolute)
+    const double is = 1.0 / (double)d.meas_prior_std;
+    double m = 0.0;
 #pragma unroll
     for (int k = 0; k < HALF; ++k) {
-      m = fmaf(lo[k] * is, lo[k] * is, m);
-      m = fmaf(up[k] * is, up[k] * is, m);
+      const double a = lo[k] * is, c = up[k] * is;
+      m = fma(a, a, m);
+      m = fma(c, c, m);
     }
-    const float lp = -0.5f * (kE * 1.8378770664093453f + m) - kE * logf(d.meas_prior_std);
-    return lp + ld;
+    const double lp = -0.5 * (kE * 1.8378770664093453 + m) - kE * log((double)d.meas_prior_std);
+    return (float)(lp + (double)ld);
   } else if constexpr (MEAS == NFDPF_MEAS_GAUSSIAN) {
     // measurement_model_Gaussian with N(1, 100 I) (DPFs.py:84-86, model/models.py:237-254)
     float e[kE];
@@ -129,8 +131,9 @@ __device__ __forceinline__ void measure_row_setup(const float *enc, const float 
   if (tid < 64) {
     const float v = tid < kE ? enc[tid] : 0.f;
     if (MEAS == NFDPF_MEAS_COS) {
-      const float nrm = sqrtf(wave_sum(v * v));
-      if (tid < kE) L.encv[tid] = v / fmaxf(nrm, 1e-12f);
+      const double nrm = sqrt(wave_sum((double)v * v));
+      if (tid < kE) L.encv[tid] = v;
+      if (tid == 0) L.vinv = 1.0 / fmax(nrm, 1e-12);
     } else if (tid < kE) {
       L.encv[tid] = v;
     }

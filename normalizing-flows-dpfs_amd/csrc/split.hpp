@@ -78,17 +78,29 @@ __device__ __forceinline__ PairX pair_of(float *buf, int *flags, int role, int s
 
 constexpr int kSpinCap = 1 << 22;  // ~0.1 s of s_sleep: a safety exit, never reached in a correct run
 
-__device__ __forceinline__ float pair_swap(PairX &x, float v, int tile_len) {
+// Count of hand-offs that gave up at kSpinCap (the partner never arrived: a broken pairing).
+// The kernel then proceeds on stale data, so the host must treat any count as a failed
+// launch: nfdpf_split_fault (filter_tiled.hip) reads and clears it, FilterEngine.run raises.
+static __device__ int g_split_fault = 0;
+
+// publish this wave's exchange counter (after its values have landed) and wait for the
+// partner's; both waves of a pair execute the same sequence of exchanges
+__device__ __forceinline__ void pair_wait(PairX &x) {
   const int k = ++x.k;
-  lds_float *b = x.buf + (k & 1) * 2 * tile_len;
-  b[x.role * tile_len + x.slot] = v;
 #ifndef NFDPF_EXP_NOWAIT
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the value lands before the counter
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the values land before the counter
   *x.mine = k;
-  for (int it = 0; __builtin_amdgcn_readfirstlane(*x.theirs) < k && it < kSpinCap; ++it)
-    __builtin_amdgcn_s_sleep(1);
+  int it = 0;
+  for (; __builtin_amdgcn_readfirstlane(*x.theirs) < k && it < kSpinCap; ++it) __builtin_amdgcn_s_sleep(1);
+  if (it == kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
 #endif
   asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ float pair_swap(PairX &x, float v, int tile_len) {
+  lds_float *b = x.buf + ((x.k + 1) & 1) * 2 * tile_len;
+  b[x.role * tile_len + x.slot] = v;
+  pair_wait(x);
   return b[(1 - x.role) * tile_len + x.slot];
 }
 
@@ -98,8 +110,8 @@ __device__ __forceinline__ float pair_swap(PairX &x, float v, int tile_len) {
 // ([2 roles][16 floats][tile_len], used once per launch), and each role then computes its 8
 // output pairs from all 32 hidden units -- the fma sequence of pe_hidden / pe_out per output.
 template <int E>
-__device__ __forceinline__ void encode_dot_pair(cfloat *pe, float x0, float x1, const float *v, float &ss,
-                                                float &dot, PairX &x, float *hbuf, int tile_len) {
+__device__ __forceinline__ void encode_dot_pair(cfloat *pe, float x0, float x1, const float *v, double &ss,
+                                                double &dot, PairX &x, float *hbuf, int tile_len) {
   constexpr int M = kPeH2 / 2, MH = M / 2;  // 16 hidden pairs, 8 per role
   cf2 *w1 = (cf2 *)pe, *b1 = (cf2 *)(pe + kPeB1);
   f2 h1[kPeH1 / 2];
@@ -126,14 +138,7 @@ __device__ __forceinline__ void encode_dot_pair(cfloat *pe, float x0, float x1, 
     hb[(x.role * 2 * MH + 2 * m) * tile_len + x.slot] = mine[m].x;
     hb[(x.role * 2 * MH + 2 * m + 1) * tile_len + x.slot] = mine[m].y;
   }
-  const int k = ++x.k;
-#ifndef NFDPF_EXP_NOWAIT
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  *x.mine = k;
-  for (int it = 0; __builtin_amdgcn_readfirstlane(*x.theirs) < k && it < kSpinCap; ++it)
-    __builtin_amdgcn_s_sleep(1);
-#endif
-  asm volatile("" ::: "memory");
+  pair_wait(x);
   f2 h2[M];
   const int other = 1 - x.role;
 #pragma unroll
@@ -144,16 +149,34 @@ __device__ __forceinline__ void encode_dot_pair(cfloat *pe, float x0, float x1, 
   }
   f2 a[E / 4];
   pe_out<E, E / 4>(pe, h2, x.role * (E / 4), a);
-  ss = 0.f;
-  dot = 0.f;
+  ss = 0.0;  // fp64 partials: see encode_dot (flows.hpp)
+  dot = 0.0;
   const int o0 = x.role * (E / 4);
 #pragma unroll
   for (int m = 0; m < E / 4; ++m) {
-    ss = fmaf(a[m].x, a[m].x, ss);
-    dot = fmaf(a[m].x, v[2 * (o0 + m)], dot);
-    ss = fmaf(a[m].y, a[m].y, ss);
-    dot = fmaf(a[m].y, v[2 * (o0 + m) + 1], dot);
+    const double ax = a[m].x, ay = a[m].y;
+    ss = fma(ax, ax, ss);
+    dot = fma(ax, (double)v[2 * (o0 + m)], dot);
+    ss = fma(ay, ay, ss);
+    dot = fma(ay, (double)v[2 * (o0 + m) + 1], dot);
   }
+}
+
+// One exchange of two doubles between the waves of a pair through a buffer used once per
+// launch ([2 roles][4 floats][tile_len]; single use, so no parity is needed -- cf. pair_swap).
+__device__ __forceinline__ void pair_swap_once2(PairX &x, double a, double b, float *dbuf, int tile_len,
+                                                double &ao, double &bo) {
+  lds_float *db = (lds_float *)dbuf;
+  const long long ia = __double_as_longlong(a), ib = __double_as_longlong(b);
+  db[(x.role * 4 + 0) * tile_len + x.slot] = __int_as_float((int)ia);
+  db[(x.role * 4 + 1) * tile_len + x.slot] = __int_as_float((int)(ia >> 32));
+  db[(x.role * 4 + 2) * tile_len + x.slot] = __int_as_float((int)ib);
+  db[(x.role * 4 + 3) * tile_len + x.slot] = __int_as_float((int)(ib >> 32));
+  pair_wait(x);
+  const int o = 1 - x.role;
+  auto get = [&](int j) { return (unsigned int)__float_as_int(db[(o * 4 + j) * tile_len + x.slot]); };
+  ao = __longlong_as_double((long long)(((unsigned long long)get(1) << 32) | get(0)));
+  bo = __longlong_as_double((long long)(((unsigned long long)get(3) << 32) | get(2)));
 }
 
 // One net (t or s) of a coupling half on input u; cb = this net's 4 folded bias pairs.

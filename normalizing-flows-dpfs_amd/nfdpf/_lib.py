@@ -78,6 +78,7 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int, c_void_p]),
     "nfdpf_ess_gate": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_split_fault": (c_int, [c_int]),
     "nfdpf_normalize_log_probs": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "nfdpf_cglow_params_size": (c_int64, [c_int]),
     "nfdpf_cglow_measurement": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
@@ -127,6 +128,15 @@ def check(rc: int, what: str):
     if rc != NFDPF_OK:
         msg = lib().nfdpf_last_error().decode(errors="replace")
         raise NfdpfError(f"{what} failed (rc={rc}): {msg}")
+
+
+def check_split_fault(what: str = "tiled filter step"):
+    """Raise if a wave-pair hand-off of the tiled step gave up on its partner (csrc/split.hpp
+    kSpinCap) since the last check: that launch ran on stale data.  Synchronous."""
+    n = lib().nfdpf_split_fault(1)
+    if n != 0:
+        raise NfdpfError(f"{what}: {n} wave-pair hand-off(s) timed out on the device (outputs invalid)"
+                         if n > 0 else f"{what}: could not read the device fault counter")
 
 
 def require_device(t: torch.Tensor, what: str):

@@ -1,12 +1,20 @@
 """Filtering driver: DPF.filtering_pos (DPFs.py:144-216) on the HIP path.
 
-Per step one ``nfdpf_filter_step`` launch (soft / no resampling), preceded by the OT
-resampler kernels when ``resampler == 'ot'``.  Histories are preallocated (B, T, N, .)
-tensors written in place (the reference grows them with torch.cat, O(T^2) copies).  The
-ESS gate never syncs the host in device-RNG mode: each step reads the previous step's
-per-row 1/sum(p^2) from device memory.  With a process group of world size > 1 the batch
-is sharded by rows; the per-row terms are all-gathered each step so every rank takes the
-same batch-global gate decision (DPFs.py:163-165), and nothing else is exchanged.
+Per time step the tiled pipeline ``nfdpf_filter_step_tiled`` (two launches at C2: gate +
+resampling + motion + nf_dyn inverse, then proposal + nf_dyn forward + densities +
+measurement; the normalisation of step t is deferred into step t+1) or the one-workgroup-per-
+row ``nfdpf_filter_step``, preceded by the Sinkhorn launches when the OT gate fires.
+Histories are preallocated (B, T, N, .) tensors written in place (the reference grows them
+with torch.cat, O(T^2) copies).  In device-RNG mode the ESS gate never syncs the host: each
+step's launches read the previous step's per-(row, tile) softmax partials from device memory.
+
+Batch sharding (world size > 1, rows [rank B, (rank + 1) B) per rank):
+  * soft resampling: the pass runs speculatively with every gate assumed off and no exchange,
+    then ONE all-gather of all steps' partials verifies the T batch-global gates
+    (DPFs.py:163-165); a fired gate reruns the pass with a per-step all-gather;
+  * OT: a per-step all-gather of the partials feeds the gate, and each Sinkhorn call takes
+    the MIN of the stop iteration over ranks (resamplers.py:126-129) and reruns to it;
+  * one all-reduce of the obs-likelihood sums at the end.
 """
 from __future__ import annotations
 
@@ -381,6 +389,9 @@ class FilterEngine:
                 ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
             else:
                 ess_all = ess_bufs[t & 1]
+        # a wave-pair hand-off that timed out leaves stale data (csrc/split.hpp): fail loudly
+        if tiled and d.split_nets and not torch.cuda.is_current_stream_capturing():
+            L.check_split_fault("nfdpf_filter_step_tiled")
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)
         if spec:

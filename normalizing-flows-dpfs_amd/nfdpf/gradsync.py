@@ -6,8 +6,15 @@ ranks with ONE all-reduce of a single flat fp32 bucket per step (RCCL over xGMI 
 node; gloo on CPU).  The models are small (the coupling nets are ~1-5 k parameters, the frame
 encoder/decoder a few hundred k), so one bucket is latency-optimal on xGMI's point-to-point
 links -- splitting it would only add per-collective latency.  The reference trains on one
-device (DPFs.py:304-383); the averaged gradient equals the gradient of the mean loss over the
-whole batch when the shards are equal.
+device (DPFs.py:304-383).
+
+What the average reproduces: for a loss that is a MEAN over batch rows (the auto-encoder MSE,
+the pseudo-likelihood) the average of the per-shard gradients is the full-batch gradient
+when the shards are equal.  The supervised loss is an RMSE, sqrt(mean(err^2)), whose per-shard
+gradients do NOT average to the full-batch one; ``global_rmse`` therefore builds it from the
+all-reduced sum of squared errors, with a gradient scaled so that the bucket's average is
+exactly d RMSE_full / d theta.  Parameters no rank produced a gradient for keep ``.grad = None``
+(as on one device), so the optimiser state matches the reference's.
 """
 from __future__ import annotations
 
@@ -34,28 +41,35 @@ class GradBucket:
         if w == 1 or not self.params:
             return
         n = sum(p.numel() for p in self.params)
+        P = len(self.params)
         dev = self.params[0].device
-        if self._buf is None or self._buf.numel() != n or self._buf.device != dev:
-            self._buf = torch.empty(n, device=dev, dtype=torch.float32)
+        if self._buf is None or self._buf.numel() != n + P or self._buf.device != dev:
+            self._buf = torch.empty(n + P, device=dev, dtype=torch.float32)
         buf = self._buf
         off = 0
-        for p in self.params:  # a parameter with no gradient contributes zeros on this rank
+        for j, p in enumerate(self.params):  # a parameter with no gradient contributes zeros
             k = p.numel()
             if p.grad is None:
                 buf[off:off + k].zero_()
             else:
                 buf[off:off + k].copy_(p.grad.reshape(-1))
+            buf[n + j] = 0.0 if p.grad is None else 1.0  # presence flag, reduced in the same bucket
             off += k
         dist.all_reduce(buf, group=self.group)
+        present = buf[n:].cpu()
+        buf = buf[:n]
         buf.mul_(1.0 / w)
         off = 0
-        for p in self.params:
+        for j, p in enumerate(self.params):
             k = p.numel()
-            g = buf[off:off + k].view_as(p).to(p.dtype)
-            if p.grad is None:
-                p.grad = g.clone()
+            if float(present[j]) == 0.0:  # no rank touched it: leave it as one device would
+                p.grad = None
             else:
-                p.grad.copy_(g)
+                g = buf[off:off + k].view_as(p).to(p.dtype)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
             off += k
 
 
@@ -68,3 +82,32 @@ def global_mean(local_sum: torch.Tensor, local_count: int, group=None) -> torch.
                      torch.tensor(float(local_count), dtype=torch.float64, device=local_sum.device)])
     dist.all_reduce(t, group=group)
     return (t[0] / t[1]).to(local_sum.dtype)
+
+
+def global_rmse(err2_sum: torch.Tensor, count: float, group=None) -> torch.Tensor:
+    """sqrt(sum over ALL ranks of err2_sum / sum of count) -- the full-batch RMSE of a
+    batch-sharded run (losses.py:18-31) -- with a gradient that GradBucket's average over the
+    ranks turns into exactly d RMSE_full / d theta: the value is built from the all-reduced
+    sum, the local term carries w times its gradient (the bucket divides by w)."""
+    w = world_size(group)
+    if w == 1:
+        return torch.sqrt(err2_sum / count)
+    t = torch.stack([err2_sum.detach().double().reshape(()),
+                     torch.tensor(float(count), dtype=torch.float64, device=err2_sum.device)])
+    dist.all_reduce(t, group=group)
+    s_glob = t[0].to(err2_sum.dtype)
+    s_eff = s_glob + w * (err2_sum - err2_sum.detach())
+    return torch.sqrt(s_eff / t[1].to(err2_sum.dtype))
+
+
+def sharded_supervised_loss(particle_list, particle_weight_list, true_state, mask, train, labeledRatio=1.0,
+                            group=None):
+    """losses.supervised_loss over the whole sharded batch (value and gradient of the
+    single-device loss); returns (loss, this rank's predictions)."""
+    prediction = torch.sum(particle_list * particle_weight_list[:, :, :, None], dim=2)
+    err2 = (prediction - true_state[:, :, :2]) ** 2
+    if not train:
+        return global_rmse(err2.sum(), err2.numel(), group), prediction
+    if labeledRatio > 0:
+        return global_rmse((mask[:, :, None] * err2).sum(), err2.numel() * labeledRatio, group), prediction
+    return 0

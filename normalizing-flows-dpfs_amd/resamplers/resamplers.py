@@ -10,9 +10,11 @@
   autograd.grad result is discarded, :241-245) -- nfdpf_ot_transport_backward.
 """
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from nfdpf import ops as _ops
+from nfdpf.gradsync import world_size
 
 device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
 
@@ -68,6 +70,20 @@ def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, 
     return (xo, wo, idx) if index else (xo, wo)
 
 
+def _ot_call(particles, weights, eps, scaling, threshold, max_iter, keep=None):
+    """One Sinkhorn resampling with the reference's batch-coupled stop rule (the loop ends
+    when ANY row converges, resamplers.py:126-129).  Batch-sharded (world > 1): each rank
+    runs its rows with the local rule, the ranks take the MIN of the stop iteration (the
+    first row to converge anywhere) and rerun to exactly that count -- the unsharded loop's
+    result (nfdpf.engine._ot_global_stop does the same in the no-grad engine)."""
+    xo, wo, idx, it = _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=keep)
+    if world_size() > 1:
+        dist.all_reduce(it, op=dist.ReduceOp.MIN)
+        xo, wo, idx, _ = _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=keep,
+                                          stop_at=it)
+    return xo, wo, idx, it
+
+
 class _OtTransport(torch.autograd.Function):
     """x' = T x with the Sinkhorn plan T held constant in backward (resamplers.py:234-264):
     dL/dx = T^T g by nfdpf_ot_transport_backward from this call's own workspace; no gradient
@@ -77,7 +93,7 @@ class _OtTransport(torch.autograd.Function):
     def forward(ctx, particles, weights, eps, scaling, threshold, max_iter):
         B, N, _ = particles.shape
         ws = _ops.ot_workspace(B, N, particles.device)
-        xo, wo, idx, _ = _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=ws)
+        xo, wo, idx, _ = _ot_call(particles, weights, eps, scaling, threshold, max_iter, keep=ws)
         ctx.ws, ctx.eps = ws, eps
         ctx.mark_non_differentiable(wo, idx)
         return xo, wo, idx
@@ -93,7 +109,7 @@ def resampler_ot(particles, weights, eps=0.1, scaling=0.75, threshold=1e-3, max_
     """OT resampling -> (x', uniform weights, identity flat index) (resamplers.py:62-70)."""
     if torch.is_grad_enabled() and particles.requires_grad:
         return _OtTransport.apply(particles, weights.detach(), eps, scaling, threshold, max_iter)
-    xo, wo, idx, _ = _ops.ot_resample(particles.detach(), weights.detach(), eps, scaling, threshold, max_iter)
+    xo, wo, idx, _ = _ot_call(particles.detach(), weights.detach(), eps, scaling, threshold, max_iter)
     return xo, wo, idx
 
 

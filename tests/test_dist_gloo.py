@@ -145,3 +145,117 @@ def test_grad_bucket_world2():
         for a, b in zip(gs, ref):
             np.testing.assert_allclose(a, b.numpy(), rtol=1e-6, atol=1e-7)
         assert abs(ess - (0 + 1 + 2 + 10 + 11 + 12) / 6) < 1e-6
+
+
+def _rmse_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf.gradsync import GradBucket, sharded_supervised_loss
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Tanh(), torch.nn.Linear(4, 2))
+        unused = torch.nn.Linear(2, 2)  # touched by no rank: its .grad must stay None
+        holder = torch.nn.ModuleDict({"m": m, "unused": unused})
+        B, T, N = 3, 4, 5
+        g = torch.Generator().manual_seed(100 + rank)
+        x = torch.randn(B, T, N, 3, generator=g)
+        w = torch.softmax(torch.randn(B, T, N, generator=g), -1)
+        state = torch.randn(B, T, 4, generator=g)
+        mask = (torch.rand(B, T, generator=g) > 0.3).float()
+        loss, _ = sharded_supervised_loss(m(x), w, state, mask, True, 0.7)
+        loss.backward()
+        GradBucket(holder).sync()
+        ev, _ = sharded_supervised_loss(m(x).detach(), w, state, mask, False)
+        q.put((rank, float(loss), [p.grad.clone().numpy() for p in m.parameters()],
+               [p.grad is None for p in unused.parameters()], float(ev)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_rmse_gradient_world2():
+    """The batch-sharded supervised RMSE (nfdpf.gradsync.sharded_supervised_loss + GradBucket)
+    has the value AND the gradient of the single-device full-batch RMSE (losses.py:18-31) --
+    not the average of per-shard RMSE gradients; a parameter no rank used keeps .grad None."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rmse_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    from losses import supervised_loss
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Tanh(), torch.nn.Linear(4, 2))
+    B, T, N = 3, 4, 5
+    xs, ws, ss, ms = [], [], [], []
+    for r in range(world):
+        g = torch.Generator().manual_seed(100 + r)
+        xs.append(torch.randn(B, T, N, 3, generator=g))
+        ws.append(torch.softmax(torch.randn(B, T, N, generator=g), -1))
+        ss.append(torch.randn(B, T, 4, generator=g))
+        ms.append((torch.rand(B, T, generator=g) > 0.3).float())
+    x, w, s, mk = (torch.cat(v) for v in (xs, ws, ss, ms))
+    loss, _ = supervised_loss(m(x), w, s, mk, True, 0.7)
+    loss.backward()
+    ev, _ = supervised_loss(m(x).detach(), w, s, mk, False)
+    for rank, l, gs, unused_none, e in res:
+        assert abs(l - loss.item()) < 1e-5 * loss.item()
+        assert abs(e - float(ev)) < 1e-5 * float(ev)
+        for a, p in zip(gs, m.parameters()):
+            np.testing.assert_allclose(a, p.grad.numpy(), rtol=1e-5, atol=1e-7)
+        assert all(unused_none)
+
+
+def _ot_stop_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import resamplers.resamplers as R
+        calls = []
+
+        def fake_ot(x, w, eps, scaling, threshold, max_iter, row_base=0, gate=None, stop_at=None, poll=None,
+                    keep=None):
+            # local stop rule: rank r's rows converge after 20 + 9 r iterations
+            it = stop_at.clone() if stop_at is not None else torch.tensor([20 + 9 * rank], dtype=torch.int32)
+            calls.append(None if stop_at is None else int(stop_at.item()))
+            return x + int(it.item()), w, torch.zeros(w.shape, dtype=torch.int64), it
+
+        R._ops.ot_resample = fake_ot
+        x = torch.zeros(2, 5, 2)
+        w = torch.full((2, 5), 0.2)
+        xo, _, _ = R.resampler_ot(x, w)
+        q.put((rank, calls, float(xo[0, 0, 0])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ot_stop_exchange_in_autograd_loop_world2():
+    """resampler_ot under batch sharding (the e2e_train loop, resamplers.py:126-129): each rank
+    runs its local stop rule, the ranks take the MIN iteration, and every rank reruns to it."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ot_stop_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, calls, x0 in res:
+        assert calls == [None, 20], calls
+        assert x0 == 20.0
