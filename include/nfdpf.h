@@ -235,6 +235,13 @@ NFDPF_API int nfdpf_cglow_measurement(const float *pe_params, const float *glow_
                             const float *enc, int64_t enc_rs, const float *x, int64_t x_rs,
                             int B, int N, float *lik, int64_t lik_rs, void *stream);
 
+/* CondGlowModel.forward(x, y) (nf/cglow/CGlowModel.py:167-176) with the reference's default
+ * configuration (K = 1, L = 1, learn_top off, 256 bins): x [M,3,8,8] the condition, y [M,3,8,8]
+ * the flow input, both per sample -> z [M,12,4,4] (NULL: not written) and nll [M]
+ * (= -(log-det + Gaussian log-prob) / (192 log 2)).  glow_params as nfdpf_cglow_measurement. */
+NFDPF_API int nfdpf_cglow_flow(const float *glow_params, int K, const float *x, const float *y, int64_t M,
+                               float *z, float *nll, void *stream);
+
 /* particle_initialization (utils.py:46-62) in DEVICE rng mode:
  * uniform on [-width/2, width/2)^2 (or start + N(0,1) when true_state)        */
 NFDPF_API int nfdpf_particle_init(const float *start_xy, int B, int N, float width, int true_state,

@@ -274,7 +274,7 @@ __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int 
 
 // resize conv3, the coupling net f, the affine update of z2 and the Gaussian log-prob;
 // returns this particle's sum (over its 16 positions) of log scale + logp
-__device__ __noinline__ float phase_f(const float *glow_, int p, int q) {
+__device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *zrow) {
   const float *glow = sgpr_ptr(glow_);
   cfloat *F = wptr(glow + kOffF);
   float fin[kC];  // cat(resize_x(x), z1)
@@ -340,6 +340,10 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q) {
     const float sc = sigmoidf_(hc + 2.0f);
     const float z1 = S.yv[p][q][c];
     const float z2 = (S.yv[p][q][kCh + c] + hs) * sc;
+    if (zrow) {  // z = cat(z1, z2) as (12, 4, 4) (CondAffineCoupling.forward, modules.py:288-303)
+      zrow[c * 16 + q] = z1;
+      zrow[(kCh + c) * 16 + q] = z2;
+    }
     lsum += logf(sc);
     lp += z2 * z2;
     lp += z1 * z1;
@@ -366,7 +370,9 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
                                                             const float *__restrict__ enc,
                                                             int64_t enc_rs, const float *__restrict__ x,
                                                             int64_t x_rs, int B, int N,
-                                                            float *__restrict__ lik, int64_t lik_rs) {
+                                                            float *__restrict__ lik, int64_t lik_rs,
+                                                            const float *__restrict__ xin,
+                                                            float *__restrict__ zout, float out_sign) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int64_t total = (int64_t)B * N;
   const int64_t ntiles = (total + kTileP - 1) / kTileP;
@@ -384,49 +390,60 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
     // W2 / W3 in col_pairs order (nfdpf.pack.encoder_tensors): {W[2m, k], W[2m+1, k]} at [k][m]
     auto W3 = [&](int n, int k) { return pw3[(k * (kE / 2) + (n >> 1)) * 2 + (n & 1)]; };
     const int64_t g0 = tile * kTileP;
-    // ---- particles of the tile
-    if (tid < kTileP) {
-      const int64_t gi = g0 + tid;
-      float a = 0.f, c = 0.f;
-      int rb = 0;
-      if (gi < total) {
-        rb = (int)(gi / N);
-        const int i = (int)(gi - (int64_t)rb * N);
-        a = x[rb * x_rs + 2 * i];
-        c = x[rb * x_rs + 2 * i + 1];
+    if (xin) {
+      // CondGlowModel.forward(x, y): the condition x (3 x 8 x 8) is given per sample and y is
+      // per sample too (N = 1: row = sample), no particle encoder
+      for (int k = tid; k < kTileP * kE; k += kThreads) {
+        const int p = k / kE, c = k - p * kE;
+        const int64_t gi = g0 + p;
+        S.xs[p][c] = gi < total ? xin[gi * kE + c] : 0.f;
       }
-      S.pxy[tid][0] = a;
-      S.pxy[tid][1] = c;
-      S.row[tid] = rb;
-    }
-    SYNC();
-    // ---- particle encoder (model/models.py:141-150): 2 -> 16 -> 32 (ReLU), then 32 -> 192
-    {
-      const int p = tid >> 4, j = tid & 15;
-      const float h = fmaf(PW(pw1, j, 1, 2), S.pxy[p][1], fmaf(PW(pw1, j, 0, 2), S.pxy[p][0], pb1[j]));
-      S.h1[p][j] = relu(h);
-    }
-    SYNC();
-    {
-      const int p = tid >> 4, j = tid & 15;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int o = j + 16 * hh;
-        float a = pb2[o];
-#pragma unroll
-        for (int k = 0; k < kPeH1; ++k) a = fmaf(pw2[(k * (kPeH2 / 2) + (o >> 1)) * 2 + (o & 1)], S.h1[p][k], a);
-        S.h2[p][o] = relu(a);
+      if (tid < kTileP) S.row[tid] = (int)(g0 + tid < total ? g0 + tid : 0);
+      SYNC();
+    } else {
+      // ---- particles of the tile
+      if (tid < kTileP) {
+        const int64_t gi = g0 + tid;
+        float a = 0.f, c = 0.f;
+        int rb = 0;
+        if (gi < total) {
+          rb = (int)(gi / N);
+          const int i = (int)(gi - (int64_t)rb * N);
+          a = x[rb * x_rs + 2 * i];
+          c = x[rb * x_rs + 2 * i + 1];
+        }
+        S.pxy[tid][0] = a;
+        S.pxy[tid][1] = c;
+        S.row[tid] = rb;
       }
+      SYNC();
+      // ---- particle encoder (model/models.py:141-150): 2 -> 16 -> 32 (ReLU), then 32 -> 192
+      {
+        const int p = tid >> 4, j = tid & 15;
+        const float h = fmaf(PW(pw1, j, 1, 2), S.pxy[p][1], fmaf(PW(pw1, j, 0, 2), S.pxy[p][0], pb1[j]));
+        S.h1[p][j] = relu(h);
+      }
+      SYNC();
+      {
+        const int p = tid >> 4, j = tid & 15;
+  #pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int o = j + 16 * hh;
+          float a = pb2[o];
+  #pragma unroll
+          for (int k = 0; k < kPeH1; ++k) a = fmaf(pw2[(k * (kPeH2 / 2) + (o >> 1)) * 2 + (o & 1)], S.h1[p][k], a);
+          S.h2[p][o] = relu(a);
+        }
+      }
+      SYNC();
+      for (int nt = w; nt < kE / 16; nt += 4) {
+        const int n0 = nt * 16;
+        const f4 acc = mfma_tile<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; },
+                                            [&](int k, int c) { return W3(n0 + c, k); });
+        mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + pb3[n0 + c]; });
+      }
+      SYNC();
     }
-    SYNC();
-    for (int nt = w; nt < kE / 16; nt += 4) {
-      const int n0 = nt * 16;
-      const f4 acc = mfma_tile<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; },
-                                          [&](int k, int c) { return W3(n0 + c, k); });
-      mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + pb3[n0 + c]; });
-    }
-    SYNC();
-
     // ---- conditioning nets, conv1 (3 -> 8, 2x2 stride 2, 8x8 -> 4x4) for actnorm (A) and
     //      1x1-conv (I) nets: VALU, lane = (particle, 4x4 position)
     const int p = w * 4 + (l >> 4), q = l & 15, qi = q >> 2, qj = q & 3;
@@ -525,14 +542,14 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
     SYNC();
     phase_resize(gw, p, q);
     SYNC();
-    const float part = phase_f(gw, p, q);
     const int64_t gi = g0 + p;
+    const float part = phase_f(gw, p, q, zout && gi < total ? zout + gi * kE : nullptr);
     if (q == 0 && gi < total) {
       // logdet0 = -log(256) * 192, plus actnorm / 1x1-conv log-dets, plus this particle's sum
       const float obj = (-5.545177444479562f * (float)kE + S.ld[p]) + part;
       const int rb = S.row[p];
       const int i = (int)(gi - (int64_t)rb * N);
-      lik[rb * lik_rs + i] = obj / (0.6931471805599453f * (float)kE);
+      lik[rb * lik_rs + i] = out_sign * (obj / (0.6931471805599453f * (float)kE));
     }
     SYNC();
   }
@@ -561,6 +578,27 @@ extern "C" int nfdpf_cglow_measurement(const float *pe_params, const float *glow
   // more would start a second, late round of workgroups and leave the tail unbalanced
   const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 3);
   cglow_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(pe_params, glow_params, enc, enc_rs, x, x_rs, B, N,
-                                                        lik, lik_rs);
+                                                        lik, lik_rs, nullptr, nullptr, 1.0f);
   return launch_status("nfdpf_cglow_measurement");
+}
+
+static int cglow_grid(int64_t tiles) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+  }
+  return (int)std::min<int64_t>(tiles, (int64_t)cus * 3);
+}
+
+extern "C" int nfdpf_cglow_flow(const float *glow_params, int K, const float *x, const float *y, int64_t M,
+                                float *z, float *nll, void *stream) {
+  NFDPF_REQUIRE(glow_params && x && y && nll, "nfdpf_cglow_flow: null pointer");
+  NFDPF_REQUIRE(K == 1, "nfdpf_cglow_flow: built for flow_depth K = 1 (got %d)", K);
+  NFDPF_REQUIRE(M >= 0 && M <= (int64_t)INT32_MAX, "nfdpf_cglow_flow: bad size");
+  if (M == 0) return NFDPF_OK;
+  // B = M rows of N = 1 (y row m is sample m), the condition x given, out_sign -1: nll
+  cglow_kernel<<<cglow_grid((M + kTileP - 1) / kTileP), kThreads, 0, as_stream(stream)>>>(
+      glow_params, glow_params, y, kE, nullptr, 0, (int)M, 1, nll, 1, x, z, -1.0f);
+  return launch_status("nfdpf_cglow_flow");
 }

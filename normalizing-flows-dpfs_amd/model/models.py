@@ -15,6 +15,7 @@ from nf.flows import FCNN, RealNVP, RealNVP_cond, MAF  # noqa: F401  (reference 
 from nf.models import NormalizingFlowModel, NormalizingFlowModel_cond
 from nfdpf import autograd as _ag
 from nfdpf import ops as _ops
+from nfdpf._lib import NfdpfError
 from nfdpf.pack import blob, blob_grad_to_params, encoder_tensors, flows_tensors, paired_mlp_tensors
 from utils import et_distance
 
@@ -292,6 +293,25 @@ class measurement_model_cnf(nn.Module):
         return lik - lik.max(dim=-1, keepdim=True)[0]
 
 
+class _CglowRunner:
+    """measurement_model_cglow's raw likelihood -nll: the fused HIP kernel forward (particle
+    encoder + CGLOW, csrc/cglow.hip); backward differentiates the PyTorch restatement (the
+    particle encoder, then CondGlowModel.torch_forward) on the saved inputs (nfdpf.autograd)."""
+
+    def __init__(self, model):
+        self.model = model
+
+    def hip(self, enc, x):
+        from nfdpf.pack import cglow_tensors
+        m = self.model
+        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
+        glow = blob(m, "glow", m.CGLOW, lambda: cglow_tensors(m.CGLOW), x.device)
+        return (_ops.cglow_measurement(pe, glow, enc.float(), x.float()),)
+
+    def torch(self, enc, x):
+        return (self.model.torch_forward_raw(enc, x),)
+
+
 class measurement_model_cglow(nn.Module):
     """Conditional-GLOW likelihood (model/models.py:280-303)."""
 
@@ -301,15 +321,23 @@ class measurement_model_cglow(nn.Module):
         self.CGLOW = CGLOW
 
     def forward(self, encodings, update_particles):
-        """One HIP kernel (csrc/cglow.hip: encoder, conditioning nets, actnorm, 1x1 conv with
-        its 12x12 log-determinant, affine coupling, Gaussian log-prob), then the row-max shift.
-        Forward only: gradients through CGLOW are SURVEY §8(f1) work."""
-        from nfdpf.pack import cglow_tensors
-        m = self
-        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), update_particles.device)
-        glow = blob(m, "glow", m.CGLOW, lambda: cglow_tensors(m.CGLOW), update_particles.device)
-        lik = _ops.cglow_measurement(pe, glow, encodings.float(), update_particles.float())
+        """One HIP kernel (csrc/cglow.hip: particle encoder, conditioning nets, actnorm, 1x1 conv
+        with its 12x12 log-determinant, affine coupling, Gaussian log-prob), then the row-max
+        shift.  Under autograd the particle encoder and every CGLOW parameter get their
+        gradients through the recompute backward of _CglowRunner."""
+        if not self.CGLOW.kernel_supported():
+            raise NfdpfError("measurement_model_cglow: the HIP kernel is built for the reference's default CGLOW "
+                             "(K = 1, L = 1, 3x8x8, learn_top off, 256 bins)")
+        lik = _ag.apply(_CglowRunner(self), (encodings, update_particles), list(self.parameters()))[0]
         return lik - lik.max(dim=-1, keepdim=True)[0]
+
+    def torch_forward_raw(self, encodings, particles):
+        """-nll before the row-max shift (model/models.py:285-300), PyTorch."""
+        B, N, D = particles.shape
+        es = self.particle_encoder(particles.reshape(-1, D).float()).reshape(B * N, 3, 8, 8)
+        eo = encodings[:, None, :].repeat(1, N, 1).reshape(B * N, 3, 8, 8)
+        _, nll = self.CGLOW.torch_forward(es, eo)
+        return -nll.reshape(B, N)
 
 
 # ------------------------------------------------------------------------------------------

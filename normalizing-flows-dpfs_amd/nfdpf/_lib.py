@@ -83,6 +83,7 @@ SIGNATURES = {
     "nfdpf_cglow_params_size": (c_int64, [c_int]),
     "nfdpf_cglow_measurement": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
                                         c_int, c_void_p, c_int64, c_void_p]),
+    "nfdpf_cglow_flow": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "nfdpf_measurement": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                   c_float, c_void_p, c_void_p]),
     "nfdpf_particle_init": (c_int, [c_void_p, c_int, c_int, c_float, c_int, c_uint64, c_int64, c_void_p, c_void_p,

@@ -185,6 +185,11 @@ class FilterEngine:
         B, T, E = enc.shape
         N = c.N
         shard = shard or ShardInfo(1, 0, B, 0, None)
+        if shard.world == 1 and shard.B_global != B:
+            # without a process group nothing gathers the other rows' gate partials: the kernels
+            # would index a B_global-row table that holds B rows
+            raise L.NfdpfError(f"FilterEngine.run: a ShardInfo without a process group needs B_global == B "
+                               f"(got B_global={shard.B_global}, B={B})")
         host_mode = c.rng_mode == "host"
         if host_mode and host is None:
             host = HostDraws()

@@ -300,6 +300,21 @@ def cglow_measurement(pe_blob, glow_blob, enc, x, K=1, out=None):
     return lik
 
 
+def cglow_flow(glow_blob, x, y, K=1):
+    """CondGlowModel.forward(x, y) (nf/cglow/CGlowModel.py:167-176) -> (z [M,12,4,4], nll [M]);
+    x, y [M,3,8,8] (the condition and the flow input, per sample)."""
+    require_device(x, "cglow_flow")
+    M = x.shape[0]
+    if tuple(x.shape[1:]) != (3, 8, 8) or tuple(y.shape) != tuple(x.shape):
+        raise L.NfdpfError(f"cglow_flow: x and y must both be [M, 3, 8, 8] (got {tuple(x.shape)}, {tuple(y.shape)})")
+    x, y = _c(x), _c(y)
+    z = torch.empty((M, 12, 4, 4), device=x.device, dtype=f32)
+    nll = torch.empty((M,), device=x.device, dtype=f32)
+    check(lib().nfdpf_cglow_flow(ptr(_c(glow_blob)), int(K), ptr(x), ptr(y), int(M), ptr(z), ptr(nll),
+                                 stream_ptr(x.device)), "nfdpf_cglow_flow")
+    return z, nll
+
+
 def particle_init(start_xy, B, N, width, true_state, seed, row_base=0, device=None):
     """particle_initialization (utils.py:46-62), device RNG -> (x [B,N,2], logw [B,N])."""
     device = device if device is not None else start_xy.device

@@ -20,6 +20,16 @@ Fixtures:
   G6 e2e_*.npz        DPF.filtering_pos end to end (encoder = identity on precomputed
                       encodings), with the CPU-generator draws recorded
   G7                  RMSE (losses.supervised_loss) stored inside each e2e file
+  G8 fwd_*.npz        DPF.forward(inputs, train=False) end to end -- 128x128 frames, the
+                      frame encoder / decoder swapped for tests/_tiny.py in the reference's
+                      DPF (its CNNs are 1.6 M parameters), global CPU generator seeded
+  G9 state_dict_keys.json  DPF(args).state_dict() key -> shape for every measurement model
+  G11 cglow_flow.npz  CondGlowModel.forward(x, y) -> (z, nll)
+  G10 grads.npz       the reference's AUTOGRAD gradients (training): flow stacks
+                      (forward and inverse), MAF, soft and OT resamplers, all five measurement
+                      models, each for a random linear functional of its outputs; and one
+                      DPF.forward(train=True) + total_loss.backward() (tiny frame encoder /
+                      decoder) with every parameter's gradient
 """
 import argparse
 import os
@@ -351,6 +361,269 @@ def gen_e2e(mods, name):
     print(name, "resample fired at steps", [t for t, f in enumerate(fired) if f])
 
 
+FWD = {
+    # name: (flag overrides, B, N, T)
+    "fwd_c2_sdpf": (dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="soft", trainType="SDPF",
+                         block_length=2), 3, 64, 4),
+    "fwd_c1_sdpf": (dict(NF_dyn=False, NF_cond=False, measurement="cos", resampler_type="soft", trainType="SDPF",
+                         block_length=2), 3, 64, 4),
+    "fwd_c3": (dict(NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler_type="ot", trainType="DPF"), 2, 48,
+               3),
+}
+
+
+def gen_forward(mods, name):
+    """DPF.forward(inputs, train=False) (DPFs.py:96-142) of the reference, all 13 outputs."""
+    import torch
+    sys.path.insert(0, os.path.dirname(OUT))
+    from _tiny import TinyDecoder, TinyEncoder
+    from DPFs import DPF
+    flags, B, N, T = FWD[name]
+    g = torch.Generator().manual_seed(21)
+    torch.manual_seed(700)
+    a = make_args(num_particles=N, batchsize=B, sequence_length=T, **flags)
+    dpf = DPF(a)
+    dpf.encoder, dpf.decoder = TinyEncoder(a.hiddensize), TinyDecoder(a.hiddensize)
+    perturb(dpf.encoder, 0.3, g)
+    perturb(dpf.decoder, 0.3, g)
+    perturb(dpf.particle_encoder, 0.5, g)
+    for m in (dpf.nf_dyn.flows, dpf.cond_model.flows):
+        perturb(m, 0.05, g)
+    if flags["measurement"] == "CRNVP":
+        perturb(dpf.cnf_measurement.flows, 0.1, g)
+    dpf.eval()
+    start = torch.cat([torch.rand(B, 2, generator=g) * 100 - 50, torch.randn(B, 2, generator=g) * 3], -1)
+    vel = torch.randn(B, T, 2, generator=g) * 3
+    pos = start[:, None, :2] + torch.cumsum(vel, 1)
+    state = torch.cat([pos + torch.randn(B, T, 2, generator=g) * 2, vel], -1)
+    # frames: 16x16 random blocks of 8x8 pixels (stored small; fwd_frames() expands them)
+    img = torch.randint(0, 256, (B, T, 16, 16, 3), generator=g, dtype=torch.uint8)
+    start_img = torch.randint(0, 256, (B, 16, 16, 3), generator=g, dtype=torch.uint8)
+    up = lambda t: t.float().div(255).repeat_interleave(8, -3).repeat_interleave(8, -2)  # noqa: E731
+    inputs = (up(start_img), start, up(img), state, torch.zeros(B, T), torch.ones(B, T))
+    seed = 800
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        out = dpf.forward(inputs, train=False)
+    (total, sup, pseud, ae, pred, pl, pwl, st, ss, image, ll, nl, obs) = out
+    res = {"B": np.int32(B), "N": np.int32(N), "T": np.int32(T), "seed": np.int32(seed), "H": np.int32(a.hiddensize)}
+    for k, v in flags.items():
+        res[f"flag/{k}"] = np.array(v)
+    for k, v in sd_np(dpf).items():
+        if k.split(".")[0] in ("encoder", "decoder", "nf_dyn", "cond_model", "particle_encoder", "cnf_measurement"):
+            res[f"w/{k}"] = v
+    res.update(start=start.numpy(), state=state.numpy(), img=img.numpy(), start_img=start_img.numpy(),
+               total=np.float32(total), sup=np.float32(sup), ae=np.float32(ae), pred=pred.numpy(), x=pl.numpy(),
+               p=pwl.numpy(), lik=ll.numpy(), noise=nl.numpy(), obs_lik=np.float32(obs))
+    if pseud is not None:
+        res["pseud"] = np.float32(pseud)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    print(name, "total", float(total), "sup", float(sup))
+
+
+def gen_keys(mods):
+    """state_dict key -> shape of the reference's DPF for every measurement model (checkpoint
+    compatibility of the drop-in, SURVEY.md §5 checkpoint row)."""
+    import json
+    import torch
+    from DPFs import DPF
+    out = {}
+    for meas, H in (("cos", 32), ("CRNVP", 32), ("NN", 32), ("gaussian", 32), ("CGLOW", 192)):
+        torch.manual_seed(0)
+        dpf = DPF(make_args(measurement=meas, hiddensize=H, NF_dyn=True, NF_cond=meas != "CGLOW"))
+        out[meas] = {k: list(v.shape) for k, v in dpf.state_dict().items()}
+    with open(os.path.join(OUT, "state_dict_keys.json"), "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+
+
+def _grad_pack(out, key, named):
+    for k, v in named:
+        out[f"{key}/g/{k}"] = (v.grad if v.grad is not None else torch_zeros_like(v)).detach().numpy().copy()
+
+
+def torch_zeros_like(v):
+    import torch
+    return torch.zeros_like(v)
+
+
+def gen_grads(mods):
+    """Reference autograd gradients of L = sum(out * g_out) for random g_out."""
+    import torch
+    import resamplers.resamplers as R
+    from DPFs import DPF
+    from model.models import build_conditional_nf
+    from nf.flows import MAF
+    from nf.models import NormalizingFlowModel
+    from torch.distributions import MultivariateNormal
+    out = {}
+    g = torch.Generator().manual_seed(31)
+    # -- conditional RealNVP stacks (nf/models.py:37-66), forward and inverse
+    for D, O, pstd in ((2, 4, 1.0), (2, 36, 1.0), (32, 32, 2.5)):
+        for inv in (False, True):
+            torch.manual_seed(900 + D + O)
+            m = build_conditional_nf(2, O, D, init_var=0.01, prior_std=pstd)
+            perturb(m.flows, 0.2, g)
+            M = 64
+            x = (torch.randn(M, D, generator=g) * 3).requires_grad_(True)
+            c = torch.randn(M, O, generator=g).requires_grad_(True)
+            gz, gl, gp = torch.randn(M, D, generator=g), torch.randn(M, generator=g), torch.randn(M, generator=g)
+            if inv:
+                z, ld = m.inverse(x, c)
+                loss = (z * gz).sum() + (ld * gl).sum()
+            else:
+                z, lp, ld = m.forward(x, c)
+                loss = (z * gz).sum() + (ld * gl).sum() + (lp * gp).sum()
+            loss.backward()
+            k = f"cond_D{D}_O{O}_{'inv' if inv else 'fwd'}"
+            for kk, v in sd_np(m.flows, "flows.").items():
+                out[f"{k}/w/{kk}"] = v
+            out[f"{k}/prior_std"] = np.float32(pstd)
+            for name, v in (("x", x), ("c", c), ("gz", gz), ("gl", gl), ("gp", gp)):
+                out[f"{k}/{name}"] = v.detach().numpy()
+            out[f"{k}/dx"], out[f"{k}/dc"] = x.grad.numpy(), c.grad.numpy()
+            _grad_pack(out, k, [("flows." + n, q) for n, q in m.flows.named_parameters()])
+    # -- MAF stack (nf/flows.py:241-284), D = 2: forward only -- the reference's MAF.inverse
+    # writes x in place while reading it (:279-283), so its autograd raises ("modified by an
+    # inplace operation"); there is no reference gradient to pin for the inverse
+    for inv in (False,):
+        torch.manual_seed(950)
+        flows = [MAF(dim=2) for _ in range(2)]
+        perturb(torch.nn.ModuleList(flows), 0.3, g)
+        m = NormalizingFlowModel(MultivariateNormal(torch.zeros(2), torch.eye(2)), flows, device="cpu")
+        x = (torch.randn(64, 2, generator=g) * 2).requires_grad_(True)
+        gz, gl = torch.randn(64, 2, generator=g), torch.randn(64, generator=g)
+        z, ld = m.inverse(x) if inv else m.forward(x)[::2]
+        ((z * gz).sum() + (ld * gl).sum()).backward()
+        k = f"maf_{'inv' if inv else 'fwd'}"
+        for kk, v in sd_np(m.flows, "flows.").items():
+            out[f"{k}/w/{kk}"] = v
+        for name, v in (("x", x), ("gz", gz), ("gl", gl)):
+            out[f"{k}/{name}"] = v.detach().numpy()
+        out[f"{k}/dx"] = x.grad.numpy()
+        _grad_pack(out, k, [("flows." + n, q) for n, q in m.flows.named_parameters()])
+    # -- soft resampler (resamplers.py:20-60): d/dx through the gather, d/dp through p / q
+    B, N = 4, 200
+    x = (torch.randn(B, N, 2, generator=g) * 30).requires_grad_(True)
+    lw = torch.randn(B, N, generator=g) * 2
+    p = (torch.softmax(lw, -1) + 1e-12).requires_grad_(True)
+    gx, gw = torch.randn(B, N, 2, generator=g), torch.randn(B, N, generator=g)
+    torch.manual_seed(77)
+    xo, wo, idx = R.soft_resampler(x, p, 0.5, N, index=True, device="cpu")
+    torch.manual_seed(77)
+    off = torch.FloatTensor(B).uniform_(0.0, 1.0 / N)
+    ((xo * gx).sum() + (wo * gw).sum()).backward()
+    out.update({"soft/x": x.detach().numpy(), "soft/p": p.detach().numpy(), "soft/offsets": off.numpy(),
+                "soft/gx": gx.numpy(), "soft/gw": gw.numpy(), "soft/dx": x.grad.numpy(), "soft/dp": p.grad.numpy(),
+                "soft/idx": idx.numpy().astype(np.int32)})
+    # -- OT resampler (resamplers.py:234-264): T held constant, no gradient to the weights
+    B, N = 3, 96
+    x = (torch.randn(B, N, 2, generator=g) * 30).requires_grad_(True)
+    p = torch.softmax(torch.randn(B, N, generator=g) * 2, -1) + 1e-12
+    gx = torch.randn(B, N, 2, generator=g)
+    xo, wo, idx = R.resampler_ot(x, p, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, device="cpu")
+    (xo * gx).sum().backward()
+    out.update({"ot/x": x.detach().numpy(), "ot/p": p.numpy(), "ot/gx": gx.numpy(), "ot/dx": x.grad.numpy()})
+    # -- measurement models (model/models.py:206-303): d/d(encodings, particles, parameters)
+    for meas, H in (("cos", 32), ("CRNVP", 32), ("NN", 32), ("gaussian", 32), ("CGLOW", 192)):
+        torch.manual_seed(960)
+        dpf = DPF(make_args(measurement=meas, hiddensize=H, num_particles=40, batchsize=3))
+        perturb(dpf.particle_encoder, 0.3, g)
+        if meas == "CRNVP":
+            perturb(dpf.cnf_measurement.flows, 0.1, g)
+        if meas == "CGLOW":
+            perturb(dpf.cglow_measurement, 0.1, g)
+        if meas == "NN":
+            perturb(dpf.likelihood_est, 0.2, g)
+        mm = dpf.measurement_model
+        enc = torch.randn(3, 192 if meas == "CGLOW" else H, generator=g).requires_grad_(True)
+        x = (torch.randn(3, 40, 2, generator=g) * 30).requires_grad_(True)
+        gl = torch.randn(3, 40, generator=g)
+        (mm(enc, x) * gl).sum().backward()
+        k = f"meas_{meas}"
+        for kk, v in sd_np(dpf).items():
+            if kk.split(".")[0] in ("particle_encoder", "cnf_measurement", "cglow_measurement", "likelihood_est"):
+                out[f"{k}/w/{kk}"] = v
+        out.update({f"{k}/enc": enc.detach().numpy(), f"{k}/x": x.detach().numpy(), f"{k}/gl": gl.numpy(),
+                    f"{k}/denc": enc.grad.numpy(), f"{k}/dx": x.grad.numpy()})
+        _grad_pack(out, k, [n_q for n_q in mm.named_parameters()])
+    np.savez_compressed(os.path.join(OUT, "grads.npz"), **out)
+
+
+def gen_train_step(mods, name="train_c2"):
+    """One training forward + backward of the reference (DPFs.py:318-331): DPF.forward(inputs,
+    train=True) -> total_loss.backward(), every parameter's gradient recorded."""
+    import torch
+    sys.path.insert(0, os.path.dirname(OUT))
+    from _tiny import TinyDecoder, TinyEncoder
+    from DPFs import DPF
+    flags = dict(NF_dyn=True, NF_cond=True, measurement="cos", resampler_type="soft", trainType="SDPF",
+                 block_length=2)
+    B, N, T = 3, 48, 4
+    g = torch.Generator().manual_seed(41)
+    torch.manual_seed(710)
+    a = make_args(num_particles=N, batchsize=B, sequence_length=T, **flags)
+    dpf = DPF(a)
+    dpf.encoder, dpf.decoder = TinyEncoder(a.hiddensize), TinyDecoder(a.hiddensize)
+    perturb(dpf.encoder, 0.3, g)
+    perturb(dpf.decoder, 0.3, g)
+    perturb(dpf.particle_encoder, 0.5, g)
+    for m in (dpf.nf_dyn.flows, dpf.cond_model.flows):
+        perturb(m, 0.05, g)
+    dpf.train()
+    start = torch.cat([torch.rand(B, 2, generator=g) * 100 - 50, torch.randn(B, 2, generator=g) * 3], -1)
+    vel = torch.randn(B, T, 2, generator=g) * 3
+    pos = start[:, None, :2] + torch.cumsum(vel, 1)
+    state = torch.cat([pos + torch.randn(B, T, 2, generator=g) * 2, vel], -1)
+    img = torch.randint(0, 256, (B, T, 16, 16, 3), generator=g, dtype=torch.uint8)
+    start_img = torch.randint(0, 256, (B, 16, 16, 3), generator=g, dtype=torch.uint8)
+    up = lambda t: t.float().div(255).repeat_interleave(8, -3).repeat_interleave(8, -2)  # noqa: E731
+    inputs = (up(start_img), start, up(img), state, torch.zeros(B, T), torch.ones(B, T))
+    seed = 810
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    outp = dpf.forward(inputs, train=True)
+    dpf.zero_grad()
+    outp[0].backward()
+    res = {"B": np.int32(B), "N": np.int32(N), "T": np.int32(T), "seed": np.int32(seed), "H": np.int32(a.hiddensize)}
+    for k, v in flags.items():
+        res[f"flag/{k}"] = np.array(v)
+    for k, v in sd_np(dpf).items():
+        if k.split(".")[0] in ("encoder", "decoder", "nf_dyn", "cond_model", "particle_encoder"):
+            res[f"w/{k}"] = v
+    res.update(start=start.numpy(), state=state.numpy(), img=img.numpy(), start_img=start_img.numpy(),
+               total=np.float32(outp[0].detach()), sup=np.float32(outp[1].detach()),
+               pseud=np.float32(outp[2].detach()), ae=np.float32(outp[3].detach()),
+               x=outp[5].detach().numpy(), p=outp[6].detach().numpy())
+    for n, q in dpf.named_parameters():
+        if q.grad is not None:
+            res[f"g/{n}"] = q.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    print(name, "total", float(outp[0]), "grads", sum(1 for k in res if k.startswith("g/")))
+
+
+def gen_cglow_flow(mods):
+    """CondGlowModel.forward(x, y) (nf/cglow/CGlowModel.py:167-176) -> (z, nll), reference
+    defaults (K = 1, L = 1).  (Its reverse, :178-184, raises in the reference: Cond1x1Conv
+    .view()s the non-contiguous inverse weight, modules.py:195 -- nothing to record.)"""
+    import torch
+    from nf.cglow.CGlowModel import CondGlowModel
+    g = torch.Generator().manual_seed(51)
+    torch.manual_seed(52)
+    m = CondGlowModel(make_args())
+    perturb(m, 0.1, g)
+    with torch.no_grad():
+        m.new_mean.zero_()
+        m.new_logs.zero_()
+    M = 40
+    x = torch.randn(M, 3, 8, 8, generator=g)
+    y = torch.randn(M, 3, 8, 8, generator=g)
+    with torch.no_grad():
+        z, nll = m(x, y)
+    out = {f"w/{k}": v for k, v in sd_np(m).items()}
+    out.update(x=x.numpy(), y=y.numpy(), z=z.numpy(), nll=nll.numpy())
+    np.savez_compressed(os.path.join(OUT, "cglow_flow.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -364,6 +637,17 @@ def main():
     for name in E2E:
         if not args.only or args.only == name:
             gen_e2e(mods, name)
+    for name in FWD:
+        if not args.only or args.only == name:
+            gen_forward(mods, name)
+    if not args.only or args.only == "keys":
+        gen_keys(mods)
+    if not args.only or args.only == "cglow_flow":
+        gen_cglow_flow(mods)
+    if not args.only or args.only == "grads":
+        gen_grads(mods)
+    if not args.only or args.only == "train_c2":
+        gen_train_step(mods)
 
 
 if __name__ == "__main__":
