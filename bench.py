@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 CONFIGS = {
     # name: (flags, B, N, T, algorithmic FLOP per particle-step,
     #        of which in the proposal+measurement launch of the tiled pipeline)
+    # (EXECUTED FLOP of that launch, where it differs, are in F_EXEC below)
     # C2 matmul FLOP per particle: nf_dyn inverse 1,792 + proposal 5,888 +
     # nf_dyn forward 1,792 + cos measurement 3,136 = 12,608, x 13.1/12.608 elementwise.
     "c1": (dict(NF_dyn=False, NF_cond=False, measurement="cos", resampler_type="soft"), 16, 100, 24, 3.3e3, 3.3e3),
@@ -46,7 +47,16 @@ CONFIGS = {
     "c5": (dict(NF_dyn=True, NF_cond=True, measurement="CGLOW", resampler_type="soft", hiddensize=192), 64,
            10000, 100, 201e3, 13376 + 158080),
 }
+# FLOP per particle the proposal launch actually executes: the per-row context columns of the
+# coupling nets' first layers (36 of 37 inputs of the proposal's, 4 of 5 of nf_dyn's) are
+# folded into per-row biases once per row, so a coupling net runs 1->8->8->1:
+# (8 + 64 + 8) MAC x 2 FLOP x 2 nets x 2 halves x 2 flows = 1,280 per stack.
+# C2: proposal inverse 1,280 + nf_dyn forward 1,280 + cosine encoder 3,136 = 5,696.
+# C4: proposal 1,280 + MAF forward 2 x 176 + cosine encoder 3,136 = 4,768.
+F_EXEC = {"c2": 5696.0, "c4": 4768.0}
 B_ALG = 52.0            # algorithmic HBM bytes per particle-step
+B_SOFT = 36.0           # soft resampling, HBM bytes per particle: read x 8 + p 4,
+#                         write x' 8 + w' 4 + index 8, + 4 for the row's CDF pass
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
 PEAK_HBM_GBS = 8000.0
 
@@ -81,7 +91,7 @@ def synthetic_disk(B, T, seed, E):
             torch.from_numpy(enc))
 
 
-def cpu_baseline(cfg_name, seconds_budget=25.0):
+def cpu_baseline(cfg_name, seconds_budget=25.0, force=False):
     """The oracle (PyTorch-CPU restatement, timing-faithful: O(N^2) marker matching, FP64
     Sinkhorn, torch.cat history) on the host cores, on a bounded sample of the workload."""
     from oracle import dpf_oracle as O
@@ -97,6 +107,8 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
     Bs, Ts = B, T
     if flags["resampler_type"] == "ot":
         Bs, Ts = max(1, B // 16), min(T, 10)   # one FP64 OT call is tens of seconds at B=64
+        if force:
+            Bs, Ts = max(1, B // 16), 4        # every step calls the FP64 Sinkhorn
     if N >= 4000:
         Bs, Ts = 4, 8                          # C5: 4 rows x 8 steps (dense N^2 resampler work)
         if flags["resampler_type"] == "ot":
@@ -115,7 +127,8 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
         return ot_orig(*a, **k)
 
     O.ot_resample = ot_counted
-    run = lambda: O.filtering(cfg, params, enc[:Bs, :Ts], start[:Bs], vel[:Bs, :Ts], rng=O.HostRNG())
+    run = lambda: O.filtering(cfg, params, enc[:Bs, :Ts], start[:Bs], vel[:Bs, :Ts], rng=O.HostRNG(),  # noqa: E731
+                              force_resample=force)
     with torch.no_grad():
         t0 = time.perf_counter()
         run()  # warm-up
@@ -132,7 +145,8 @@ def cpu_baseline(cfg_name, seconds_budget=25.0):
     if flags["resampler_type"] == "ot":
         ot_note = f", OT resampling in {len(ot_calls) // (reps + 1)} of {Ts} steps"
     return {"value": Bs * N * Ts / med, "unit": "particle-steps/s", "cores": cores, "kind": "port",
-            "sample": f"oracle filtering B={Bs} N={N} T={Ts} (ESS-gated{ot_note}), median of {reps} after 1 "
+            "sample": f"oracle filtering B={Bs} N={N} T={Ts} ({'forced' if force else 'ESS-gated'} resampling"
+                      f"{ot_note}), median of {reps} after 1 "
                       f"warm-up; host {platform.processor() or platform.machine()}"}
 
 
@@ -162,6 +176,41 @@ def ot_iteration_ms(res, T):
             best = a.elapsed_time(b) if best is None else min(best, a.elapsed_time(b))
         out[k] = best
     return (out[20] - out[10]) / 10.0
+
+
+def soft_resample_ms(res, T, reps=20):
+    """Average duration of the standalone soft resampler (nfdpf_soft_resample ->
+    soft_resample_kernel, resamplers.py:20-60) on this workload's particles (history slot T/2):
+    one event pair around ``reps`` back-to-back calls after a warm-up."""
+    from nfdpf import ops
+    x = res.particles[:, T // 2].contiguous()
+    p = res.probs[:, T // 2].contiguous()
+    off = torch.rand(p.shape[0], device=p.device) / p.shape[1]
+    ops.soft_resample(x, p, 0.5, off)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        ops.soft_resample(x, p, 0.5, off)
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def ot_call_ms(res, T, iters=10):
+    """Whole OT resampler call (all launches) forced to ``iters`` iterations, best of 3."""
+    from nfdpf import ops
+    x = res.particles[:, T // 2].contiguous()
+    w = res.probs[:, T // 2].contiguous()
+    stop = torch.full((1,), iters + 2, dtype=torch.int32, device=x.device)
+    best = None
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ops.ot_resample(x, w, stop_at=stop, poll=False)
+        b.record()
+        torch.cuda.synchronize()
+        best = a.elapsed_time(b) if best is None else min(best, a.elapsed_time(b))
+    return best
 
 
 def pmc_traffic(cfg_name, kname):
@@ -294,6 +343,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kernel_ms = float(np.mean([e.ms() for e in evs]))
+    front = [e.ms(1) for e in evs if e.n == 4]
+    front_ms = float(np.mean(front)) if front else None
     for e in evs:
         e.close()
     kname = "filter_step_kernel"
@@ -307,12 +358,14 @@ def main():
             kname = "tiled_prop_kernel"
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
+    F_EX = F_EXEC.get(args.config, F_ALG) if kname.startswith("tiled_prop") else F_ALG
     ot_iter_ms = None
     if flags["resampler_type"] == "ot" and eng.last_ot_calls:
         ot_iter_ms = ot_iteration_ms(res, T)
         if ot_iter_ms * eng.last_ot_calls * 10 > kernel_ms * T:  # the Sinkhorn loop dominates
             kname, kernel_ms = "ot_iter_kernel", ot_iter_ms
             F_ALG, launch_units = F_OT_PAIR, B * N * N
+            F_EX = F_ALG
             # per particle: x~ (8 B) + logw (4) + both potentials read and written (fp64, 32)
             launch_bytes = 44.0 * B * N
     traffic, traffic_src = pmc_traffic(args.config, kname)
@@ -330,6 +383,26 @@ def main():
     else:
         ident = (torch.arange(N, device=dev) + N * (shard.row_base + torch.arange(B, device=dev))[:, None])
         resampled = int((res.index != ident[:, None, :]).flatten(2).any(-1).any(0).sum())
+
+    # the resampler on its own (timed with --force-resample as well as gated)
+    if flags["resampler_type"] == "soft":
+        rs_ms = soft_resample_ms(res, T)
+        rs_gbs = B_SOFT * B * N / (rs_ms * 1e-3) / 1e9
+        resample = {"kernel": "soft_resample_kernel (standalone nfdpf_soft_resample on slot T/2)",
+                    "avg_ms": rs_ms, "bound": "hbm", "bytes_per_particle": B_SOFT, "achieved_GBs": rs_gbs,
+                    "peak_GBs": PEAK_HBM_GBS, "frac": rs_gbs / PEAK_HBM_GBS,
+                    "particles_per_s": B * N / (rs_ms * 1e-3)}
+    else:
+        it_ms = ot_iter_ms if ot_iter_ms is not None else ot_iteration_ms(res, T)
+        call10 = ot_call_ms(res, T, 10)
+        tf = F_OT_PAIR * B * N * N / (it_ms * 1e-3) / 1e12
+        resample = {"kernel": "ot_iter_kernel (one Sinkhorn iteration)", "avg_ms": it_ms, "bound": "valu",
+                    "flop_per_pair": F_OT_PAIR, "pairs_per_launch": B * N * N, "achieved_TFLOPs": tf,
+                    "peak_TFLOPs": PEAK_FP32_TFLOPS, "frac": tf / PEAK_FP32_TFLOPS,
+                    "call_ms_at_10_iterations": call10, "fixed_ms_per_call": call10 - 10 * it_ms,
+                    "calls_in_last_pass": eng.last_ot_calls}
+    if front_ms is not None:
+        resample["front_launch_ms"] = front_ms  # the step's gate + resampling + motion launch, live
 
     if rank == 0:
         units = B * world * N * T * args.steps
@@ -351,15 +424,21 @@ def main():
                        "parallelism": f"batch-sharded x{world}"},
             "rmse": rmse,
             "resampled_steps": resampled,
-            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            # bound: the FP32 issue rate of the CU -- VALU for the coupling nets / Sinkhorn
+            # (v_pk_fma_f32, v_exp_f32), f32 MFMA + VALU for CGLOW; same 157.3 TFLOP/s peak
+            "roofline": {"bound": "mfma" if kname == "cglow_kernel" else "valu", "achieved": achieved_tf,
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": kname, "kernel_avg_ms": kernel_ms,
                          "flop_per_unit": F_ALG, "units_per_launch": per_launch_units,
+                         "flop_per_unit_executed": F_EX,
+                         "frac_executed": F_EX * per_launch_units / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
                          "hbm_achieved_GBs": hbm_gbs, "hbm_frac": hbm_gbs / PEAK_HBM_GBS},
+            "resample": resample,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.config)
+            out["cpu_baseline"] = cpu_baseline(args.config, force=args.force_resample)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

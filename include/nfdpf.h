@@ -304,6 +304,9 @@ typedef struct nfdpf_filter_desc {
   int32_t ess_local;        /* tiled: 1 = ess_all holds this shard's B rows only (row b at b), the
                                gate coming from `gate` -- the speculative-gate mode of a sharded
                                batch (nfdpf_ess_gate_tiled_batch verifies it after the pass) */
+  int32_t prof_front;       /* tiled, with prof_events: 1 = prof_events is hipEvent_t[4] and events
+                               [2], [3] ride in the front launch's dispatch (ESS gate + resampling +
+                               motion [+ nf_dyn]: the resampler's launch) */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);

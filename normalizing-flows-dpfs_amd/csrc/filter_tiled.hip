@@ -1011,9 +1011,13 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
     stage_prior_split(d, S, i, in, L.cb_dyn, q0x, q1x, jp, x, kTile, propose, prior);
     // cosine measurement (model/models.py:206-219): outputs [16 role, 16 role + 16) here
     double ss, dot;
-    encode_dot_pair<kE>(wptr(d.pe_params), q0x, q1x, L.encv, ss, dot, x, hbuf, kTile);
     double ss_o, dot_o;
+#ifdef NFDPF_EXP_NOENC  // experiment builds only: the cosine encoder left out (prices it)
+    ss = 1.0 + q0x * 1e-9, dot = 0.5 + q1x * 1e-9, ss_o = 1.0, dot_o = 0.25;
+#else
+    encode_dot_pair<kE>(wptr(d.pe_params), q0x, q1x, L.encv, ss, dot, x, hbuf, kTile);
     pair_swap_once2(x, ss, dot, dbuf, kTile, ss_o, dot_o);
+#endif
     ss = role ? ss_o + ss : ss + ss_o;
     dot = role ? dot_o + dot : dot + dot_o;
     const float lk = cos_lik(ss, dot, L.vinv);
@@ -1314,9 +1318,16 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
     // C / gate staging [max(N, B_global)], gathered weights [N], deferred p_{t-1} [N]
     const size_t lds = d.resampler == NFDPF_RESAMPLE_SOFT ? (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4
                                                          : (size_t)d.B_global * 4;
+    // live timing of the front launch (the resampler's) in its own dispatch, as launch_prop
+    hipEvent_t *fev = d.prof_events && d.prof_front ? (hipEvent_t *)d.prof_events + 2 : nullptr;
     if (use_merged(d)) {
       const size_t mlds = (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4;
-      tiled_fdyn_kernel<<<g, 2 * kTile, mlds, st>>>(d, ws);
+      if (fev)
+        hipExtLaunchKernelGGL(tiled_fdyn_kernel, g, dim3(2 * kTile), mlds, st, fev[0], fev[1], 0, d, ws);
+      else
+        tiled_fdyn_kernel<<<g, 2 * kTile, mlds, st>>>(d, ws);
+    } else if (fev) {
+      hipExtLaunchKernelGGL(tiled_front_kernel, g, dim3(kTile), lds, st, fev[0], fev[1], 0, d, ws);
     } else {
       tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
     }

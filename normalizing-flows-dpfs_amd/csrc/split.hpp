@@ -204,15 +204,24 @@ __device__ __forceinline__ float net_split(cf2 *w, float u, const f2 *cb) {
 // RealNVP_cond flow, forward (nf/flows.py:215-226) / inverse (:228-239), split over a wave
 // pair.  fw = the flow's split block (kSplitFlow floats, wave-uniform), cbs = its folded
 // biases in split order (16 pairs).  Both waves end with identical lo, up and log-det.
+// NFDPF_EXP_SAMEW (experiment builds only, scripts/exp_build.sh; wrong results): every net of
+// a stack reads the first net's weights -- the scalar-cache footprint of the coupling nets
+// shrinks from 16 nets to 2, which prices their weight misses.
+#ifdef NFDPF_EXP_SAMEW
+#define EXP_NET(k) 0
+#else
+#define EXP_NET(k) (k)
+#endif
+
 __device__ __forceinline__ float coupling_forward_split(const float *fw, float &lo, float &up, const f2 *cbs,
                                                         PairX &x, int tile_len) {
   const int r = x.role;
-  float v = net_split(wptr2(fw + r * kSplitNet), lo, cbs + r * 4);
+  float v = net_split(wptr2(fw + EXP_NET(r) * kSplitNet), lo, cbs + r * 4);
   float o = pair_swap(x, v, tile_len);
   float t = r ? o : v, s = r ? v : o;
   up = t + up * expf(s);
   const float l1 = s;
-  v = net_split(wptr2(fw + (2 + r) * kSplitNet), up, cbs + (2 + r) * 4);
+  v = net_split(wptr2(fw + EXP_NET(2 + r) * kSplitNet), up, cbs + (2 + r) * 4);
   o = pair_swap(x, v, tile_len);
   t = r ? o : v;
   s = r ? v : o;
@@ -223,12 +232,12 @@ __device__ __forceinline__ float coupling_forward_split(const float *fw, float &
 __device__ __forceinline__ float coupling_inverse_split(const float *fw, float &lo, float &up, const f2 *cbs,
                                                         PairX &x, int tile_len) {
   const int r = x.role;
-  float v = net_split(wptr2(fw + (2 + r) * kSplitNet), up, cbs + (2 + r) * 4);
+  float v = net_split(wptr2(fw + EXP_NET(2 + r) * kSplitNet), up, cbs + (2 + r) * 4);
   float o = pair_swap(x, v, tile_len);
   float t = r ? o : v, s = r ? v : o;
   lo = (lo - t) * expf(-s);
   const float l2 = -s;
-  v = net_split(wptr2(fw + r * kSplitNet), lo, cbs + r * 4);
+  v = net_split(wptr2(fw + EXP_NET(r) * kSplitNet), lo, cbs + r * 4);
   o = pair_swap(x, v, tile_len);
   t = r ? o : v;
   s = r ? v : o;
@@ -245,7 +254,7 @@ __device__ __forceinline__ void stage_dyn_inverse_split(const nfdpf_filter_desc 
   const float *base = d.dyn_params + split_suffix_offset(d.n_flows, kOctxDyn);
   float lo = x0, up = x1, ld = 0.f;
   for (int f = d.n_flows - 1; f >= 0; --f)
-    ld += coupling_inverse_split(base + f * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
+    ld += coupling_inverse_split(base + EXP_NET(f) * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
   if (x.role == 0) {
     S.scr[4 * i] = lo;
     S.scr[4 * i + 1] = up;
@@ -262,7 +271,7 @@ __device__ __forceinline__ float stage_propose_inverse_split(const nfdpf_filter_
   const float *base = d.cond_params + split_suffix_offset(d.n_flows, d.E + 4);
   float lo = in.xd0, up = in.xd1, ld = 0.f;
   for (int f = d.n_flows - 1; f >= 0; --f)
-    ld += coupling_inverse_split(base + f * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
+    ld += coupling_inverse_split(base + EXP_NET(f) * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
   q0x = lo;
   q1x = up;
   return -ld;
@@ -280,7 +289,8 @@ __device__ __forceinline__ void stage_prior_split(const nfdpf_filter_desc &d, co
   const float r0 = in.p0 - in.e0, r1 = in.p1 - in.e1;
   const float *base = d.dyn_params + split_suffix_offset(d.n_flows, kOctxDyn);
   float lo = q0x, up = q1x, ld2 = 0.f;
-  for (int f = 0; f < d.n_flows; ++f) ld2 += coupling_forward_split(base + f * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
+  for (int f = 0; f < d.n_flows; ++f)
+    ld2 += coupling_forward_split(base + EXP_NET(f) * kSplitFlow, lo, up, cbs + f * 16, x, tile_len);
   prior = density(lo - r0, up - r1, K, two_var) - (-ld2);
   propose = (de + in.jac) + jac_prop;
   if (x.role == 0) {

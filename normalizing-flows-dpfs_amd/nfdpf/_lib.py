@@ -45,6 +45,7 @@ class FilterDesc(Structure):
         ("ess_out", c_void_p), ("lw_sum", c_void_p), ("pred", c_void_p), ("scratch", c_void_p),
         ("prof_events", c_void_p),
         ("ess_local", c_int32),
+        ("prof_front", c_int32),
     ]
 
 

@@ -365,6 +365,7 @@ class FilterEngine:
                 else:
                     d.ot_x = xin.data_ptr()  # not read: the motion stage keeps the previous particles
             d.prof_events = None
+            d.prof_front = 0
             ev = None
             # the tiled step carries the events in the timed launch's own dispatch (no stream
             # cost): every step; elsewhere an event pair costs ~6 us of stream time: one sampled
@@ -372,10 +373,11 @@ class FilterEngine:
             every = c.kernel == "tiled" and not external
             if self.step_events is not None and (every or t == T // 2):
                 from .prof import EventPair
-                ev = EventPair()
+                ev = EventPair(4 if every else 2)
                 self.step_events.append(ev)
                 if not external:
                     d.prof_events = ev.ptr  # around the step's dominant launch, inside the library
+                    d.prof_front = int(every)  # and, tiled, around its front (resampling) launch
             if external:
                 d.phase = 1
                 step()

@@ -24,11 +24,13 @@ def hip():
 
 
 class EventPair:
-    """Two hipEvents in a C array (the ABI's prof_events)."""
+    """hipEvents in a C array (the ABI's prof_events): one pair, or two with ``n=4`` (the
+    tiled step's proposal launch, then its front launch -- nfdpf_filter_desc.prof_front)."""
 
-    def __init__(self):
-        self.arr = (ctypes.c_void_p * 2)()
-        for k in range(2):
+    def __init__(self, n: int = 2):
+        self.n = n
+        self.arr = (ctypes.c_void_p * n)()
+        for k in range(n):
             e = ctypes.c_void_p()
             rc = hip().hipEventCreate(ctypes.byref(e))
             if rc != 0:
@@ -52,16 +54,17 @@ class EventPair:
     def record_end(self, device):
         self._record(1, device)
 
-    def ms(self) -> float:
-        hip().hipEventSynchronize(self.arr[1])
+    def ms(self, pair: int = 0) -> float:
+        a, b = self.arr[2 * pair], self.arr[2 * pair + 1]
+        hip().hipEventSynchronize(b)
         out = ctypes.c_float()
-        rc = hip().hipEventElapsedTime(ctypes.byref(out), self.arr[0], self.arr[1])
+        rc = hip().hipEventElapsedTime(ctypes.byref(out), a, b)
         if rc != 0:
             raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
         return float(out.value)
 
     def close(self):
-        for k in range(2):
+        for k in range(self.n):
             if self.arr[k]:
                 hip().hipEventDestroy(self.arr[k])
                 self.arr[k] = None

@@ -301,7 +301,7 @@ def test_cglow_module_matches_kernel():
     pe = build_particle_encoder_cglow(192, 2)
     pe.load_state_dict({k[len("particle_encoder."):]: v for k, v in w.items() if k.startswith("particle_encoder.")})
     m = measurement_model_cglow(pe, _glow_module(w)).to(DEV)
-    lik = m(t(fx["enc"]).to(DEV), t(fx["x"]).to(DEV)).cpu()
+    lik = m(t(fx["enc"]).to(DEV), t(fx["x"]).to(DEV)).detach().cpu()
     assert_close(lik, fx["lik"], 1e-5, 5e-5, "CGLOW module")
 
 

@@ -158,6 +158,16 @@ def test_fullsize_teacher_forced(name):
         # against the reference's fp64 loop (x' within ~2e-5 relative, test_fullsize_ot_direct),
         # an error the reference's float32 run does not have, so rows where the reference's
         # own error happens to be tiny carry no per-row bound there.
+        if ot and what == "particles":
+            # x' of an OT step carries the fp32 pair work of our Sinkhorn (the reference
+            # iterates in fp64): bounded, as in test_fullsize_ot_direct, relative to the scale
+            # of the row's cloud rather than by the reference's float32 envelope
+            o64, r = o.numpy().astype(np.float64), r64[k]
+            scale = np.maximum(np.abs(r).max(axis=(2, 3), keepdims=True), 1.0)
+            rel = (np.abs(o64 - r) / scale).max()
+            print(f"  particles: max error / row scale {rel:.2e} (bound 5e-5)")
+            assert rel <= 5e-5, rel
+            continue
         _check_envelope(o, ref[i], r64[k], 1e-5, atol, what, k_row=np.inf if ot else 16.0)
     dump = os.environ.get("NFDPF_PARITY_DUMP")
     if dump:  # diagnostics: per-(row, step) miss counts and the rows where ours misses most
