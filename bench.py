@@ -351,7 +351,7 @@ def main():
     if args.kernel == "tiled":  # the proposal launch (csrc/filter_tiled.hip launch_prop)
         if fcfg.split_nets and flags["NF_dyn"] and flags["NF_cond"] and flags["measurement"] == "cos" \
                 and flags.get("NF_dyn_flow", "RealNVP") == "RealNVP":
-            kname = "tiled_prop_split_kernel"  # coupling nets on wave pairs
+            kname = "tiled_prop_quad_kernel"  # coupling nets on wave pairs beside the encoder pair
         elif flags["NF_cond"] and flags["measurement"] != "CGLOW":
             kname = "tiled_prop2_kernel"       # two roles: flow chain, measurement
         else:

@@ -242,6 +242,17 @@ NFDPF_API int nfdpf_cglow_measurement(const float *pe_params, const float *glow_
 NFDPF_API int nfdpf_cglow_flow(const float *glow_params, int K, const float *x, const float *y, int64_t M,
                                float *z, float *nll, void *stream);
 
+/* The rational-quadratic spline of the neural spline flows NSF_AR / NSF_CL (nf/flows.py:343-458)
+ * on M elements with K bins each: RQS (nf/utils.py:55-147) on [left, right] x [bottom, top],
+ * or, with tails = 1, unconstrained_RQS (:23-53): inputs outside [left, right] pass through
+ * with log-det 0.  W, H: [M, K] unnormalised widths / heights; D: [M, K + 1] unnormalised
+ * derivatives (full_derivatives = 1) or [M, K - 1] inner ones with the reference's constant at
+ * both ends (0).  Out: y [M], logdet [M] (inverse = 1: the inverse map and its log-det).      */
+NFDPF_API int nfdpf_rqs(const float *x, const float *W, const float *H, const float *D, int64_t M, int K,
+                        int full_derivatives, int inverse, float left, float right, float bottom, float top,
+                        int tails, float min_bin_width, float min_bin_height, float min_derivative, float *y,
+                        float *logdet, void *stream);
+
 /* particle_initialization (utils.py:46-62) in DEVICE rng mode:
  * uniform on [-width/2, width/2)^2 (or start + N(0,1) when true_state)        */
 NFDPF_API int nfdpf_particle_init(const float *start_xy, int B, int N, float width, int true_state,

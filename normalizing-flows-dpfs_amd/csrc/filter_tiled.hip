@@ -35,6 +35,15 @@ __device__ unsigned long long g_trace[4][2048][8];
 #else
 #define TRACE(K, P)
 #endif
+#ifdef NFDPF_EXP_QTRACE
+// experiment-only: per-WAVE phase timestamps of the quad proposal launch (last step run)
+__device__ unsigned long long g_qtrace[1024][16][8];
+#define QTRACE(P)                                                                           \
+  if ((threadIdx.x & 63) == 0 && blockIdx.y * gridDim.x + blockIdx.x < 1024)                \
+    g_qtrace[blockIdx.y * gridDim.x + blockIdx.x][threadIdx.x >> 6][P] = __builtin_amdgcn_s_memrealtime();
+#else
+#define QTRACE(P)
+#endif
 
 struct TiledWs {
   double *st_phys;  // [B][tiles][4] sum x0, x1, x0^2, x1^2 of x_phys
@@ -1053,6 +1062,196 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
   TRACE(2, 3)
 }
 
+// store_softmax_fin for the 16-wave quad launch: u rides on the flow t-waves 0, 2, 4, 6, the
+// deferred-normalisation sums on the encoder waves 8, 10, 12, 14 -- the same lanes, values and
+// summation order as the split launch's (waves 0, 2, 4, 6 and 1, 3, 5, 7).  shd >= 96 doubles.
+__device__ __forceinline__ void store_softmax_fin_quad(float u, bool valid, double *sm, const double (&sf)[4],
+                                                       double *fin, float *shf, double *shd) {
+  const float mw = wave_max_dpp(valid ? u : -INFINITY);
+  const float ev = valid ? expf(u - mw) : 0.f;
+  const double ew = wave_sum_dpp((double)ev);
+  const double qw = wave_sum_dpp((double)ev * ev);
+  double f4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) f4[k] = wave_sum_dpp(sf[k]);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    shf[w] = mw;
+    shd[2 * w] = ew;
+    shd[2 * w + 1] = qw;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) shd[32 + 4 * w + k] = f4[k];
+  }
+  QTRACE(6)
+  __syncthreads();
+  QTRACE(7)
+  if (threadIdx.x == 0) {
+    float m = shf[0];
+    for (int k = 1; k < 16; ++k) m = fmaxf(m, shf[k]);
+    double sum = 0.0, sq = 0.0;
+    for (int k = 0; k < 16; ++k)
+      if (shf[k] > -INFINITY) {
+        const double f = (double)expf(shf[k] - m);
+        sum += shd[2 * k] * f;
+        sq += shd[2 * k + 1] * f * f;
+      }
+    sm[0] = m;
+    sm[1] = sum;
+    sm[2] = sq;
+  } else if (fin && threadIdx.x >= 64 && threadIdx.x < 68) {  // encoder waves 8, 10, 12, 14 in order
+    const int k = threadIdx.x - 64;
+    double a = shd[32 + 4 * 8 + k];
+    for (int q = 1; q < 4; ++q) a += shd[32 + 4 * (8 + 2 * q) + k];
+    fin[k] = a;
+  }
+}
+
+// ---- K3 on wave quads (--NF-dyn RealNVP, --NF-cond, cosine measurement): per particle group
+// of 64, a flow pair (waves 2g, 2g + 1: the t- and s-nets of the proposal inverse, then of the
+// nf_dyn forward, split.hpp) and an encoder pair (waves 8 + 2g, 9 + 2g: the particle encoder
+// split over two waves, encode_dot_pair).  The measurement needs only the proposal
+// (model/models.py:358-377), so the encoder pair takes it from the flow t-wave through LDS and
+// runs BESIDE the nf_dyn forward: the launch costs proposal + max(nf_dyn forward, encoder)
+// instead of their sum, at four waves per SIMD.  While it waits for the proposal the encoder
+// t-wave normalises slot t-1's particles (the deferred normalisation).  1024 threads per tile.
+template <bool MERGED>
+__global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ StepShared L;
+  __shared__ float xbuf[4 * kTile];              // flow-pair hand-offs (pair_swap)
+  __shared__ float hbuf[2 * kPeH2 / 2 * kTile];  // encoder hidden halves (encode_dot_pair)
+  __shared__ float dbuf[2 * 4 * kTile];          // fp64 cosine partials (pair_swap_once2)
+  __shared__ float qbuf[2 * kTile];              // the proposal, flow t-wave -> encoder pair
+  __shared__ float rbuf[3 * kTile];              // likelihood | prior | propose per particle
+  __shared__ float encq[8][kE];                  // each encoder wave's copy of the frame encoding
+  __shared__ int xflag[16];
+  __shared__ int qflag[4];
+  __shared__ float smf[16];
+  __shared__ double smd[96];
+  TRACE(2, 0)
+  QTRACE(0)
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool enc = w >= 8;
+  const int role = w & 1, g = (w >> 1) & 3;
+  const int slot = g * 64 + (threadIdx.x & 63);
+  const int i = tile * kTile + slot;
+  const RowSlot S = row_slot(d, b);
+  const bool valid = i < d.N;
+  PropIn in{};
+  float lr = 0.f;
+  // with the merged front + dyn launch, slot t-1's deferred normalisation runs here (encoder t-wave)
+  const bool defer_here = MERGED && d.defer_norm && d.t > 0 && enc && role == 0;
+  PrevIn pv{};
+  if (valid) {  // issued before the row prologue so they overlap it
+    if (!enc) in = load_prop_in<true>(S, i);
+    if (!enc && role == 0) lr = S.hp[i];
+    if (defer_here) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
+  }
+  // the encoder waves' row constants (the frame encoding, slot t-1's normaliser) are read after
+  // the prologue barrier: they are needed only once the proposal has arrived
+  if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+  if (threadIdx.x < 4) qflag[threadIdx.x] = 0;
+  const int ncb = d.n_flows * 4 * kH;
+  if (threadIdx.x < ncb)
+    reinterpret_cast<float *>(L.cb_dyn)[split_cb_index(threadIdx.x)] = ws.cb_dyn[b * kCb + threadIdx.x];
+  if (threadIdx.x >= kTile && threadIdx.x - kTile < ncb) {
+    // finish the proposal fold: the encoding columns came from K1, add [mean, std] of x_dyn
+    const int k = threadIdx.x - kTile;
+    const Ctx4 cp = tiled_ctx(ws.st_dyn, b, tiles, d.N);
+    const float c4[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), k);
+    reinterpret_cast<float *>(L.cb_cond)[split_cb_index(k)] =
+        fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + k], c4, d.E, d.E + 4);
+  }
+  __syncthreads();
+  TRACE(2, 1)
+  QTRACE(1)
+  double sf[4] = {0, 0, 0, 0};
+  lds_vint *qf = (lds_vint *)(qflag + g);
+  if (!enc) {
+    PairX x = pair_of(xbuf, xflag, role, slot);
+    float q0x = 0.f, q1x = 0.f, jp = 0.f;
+    if (valid) {
+      jp = stage_propose_inverse_split(d, in, L.cb_cond, x, kTile, q0x, q1x);
+      if (role == 0) {
+        qbuf[slot] = q0x;
+        qbuf[kTile + slot] = q1x;
+      }
+    }
+    if (role == 0) {  // publish the proposal to the encoder pair (values land first)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      *qf = 1;
+    }
+    QTRACE(2)
+    if (valid) {
+      float propose, prior;
+      stage_prior_split(d, S, i, in, L.cb_dyn, q0x, q1x, jp, x, kTile, propose, prior);
+      if (role == 0) {
+        rbuf[kTile + slot] = prior;
+        rbuf[2 * kTile + slot] = propose;
+      }
+    }
+    QTRACE(3)
+  } else {
+    // measure_row_setup (cosine), per encoder wave into its own LDS copy (no barrier needed)
+    const int lane = threadIdx.x & 63;
+    float *encv = encq[w - 8];
+    const float ve = lane < kE ? S.enc[lane] : 0.f;
+    const double vinv = 1.0 / fmax(sqrt(wave_sum((double)ve * ve)), 1e-12);
+    if (lane < kE) encv[lane] = ve;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const RowNorm rn_prev = defer_here && valid ? row_norm(prev_sm(d, b, tiles), tiles, shifted_meas(d.measurement))
+                                                : RowNorm{0.f, 1.f, 0.f};
+    if (defer_here && valid) {  // finish_prev's arithmetic for slot t-1 while the proposal runs
+      const bool shifted = shifted_meas(d.measurement);
+      const RowSlot Sp = row_slot(d, b, d.t - 1);
+      float lw, lk;
+      const float p = prev_p_of(pv, rn_prev, shifted, lw, lk);
+      if (shifted) Sp.hlik[i] = lk;
+      Sp.hp[i] = p;
+      sf[0] = (double)p * p;
+      sf[1] = (double)p * pv.x0;
+      sf[2] = (double)p * pv.x1;
+      sf[3] = lw;
+    }
+    if (valid) {
+      int it = 0;
+      for (; __builtin_amdgcn_readfirstlane(*qf) == 0 && it < kSpinCap; ++it) __builtin_amdgcn_s_sleep(1);
+      if (it == kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
+      asm volatile("" ::: "memory");
+      QTRACE(2)
+      const float q0x = qbuf[slot], q1x = qbuf[kTile + slot];
+      PairX xe = pair_of(xbuf, xflag, role, slot);  // flags 8..15: the encoder pairs' own
+      // cosine measurement (model/models.py:206-219): outputs [16 role, 16 role + 16) here
+      double ss, dot, ss_o, dot_o;
+      encode_dot_pair<kE>(wptr(d.pe_params), q0x, q1x, encv, ss, dot, xe, hbuf, kTile);
+      pair_swap_once2(xe, ss, dot, dbuf, kTile, ss_o, dot_o);
+      ss = role ? ss_o + ss : ss + ss_o;
+      dot = role ? dot_o + dot : dot + dot_o;
+      const float lk = cos_lik(ss, dot, vinv);
+      if (role == 0) {
+        S.hlik[i] = lk;
+        rbuf[slot] = lk;
+      }
+    }
+    QTRACE(3)
+  }
+  __syncthreads();
+  TRACE(2, 2)
+  QTRACE(4)
+  const bool carry = !enc && role == 0 && valid;
+  const float u = carry ? logw(lr, rbuf[slot], rbuf[kTile + slot], rbuf[2 * kTile + slot]) : 0.f;
+  double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
+  if (threadIdx.x == 0) sm[3] = 0.f;
+  const bool fin = MERGED && d.defer_norm && d.t > 0;
+  store_softmax_fin_quad(u, carry, sm, sf, fin ? ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4 : nullptr,
+                         smf, smd);
+  TRACE(2, 3)
+  QTRACE(5)
+}
+
 // ---- K3b (phase 2 of an EXTERNAL measurement): raw likelihood from lik_ext
 __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ double shd2[32];
@@ -1178,10 +1377,17 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
   // 11.4 us for the compute phase at C2 -- the extra waves duplicate the encoder's first layers)
   if constexpr (NFD && NFC && MEAS == NFDPF_MEAS_COS) {
     if (use_merged(d)) {
+#ifndef NFDPF_PROP_SPLIT  // the quad launch (flow pair beside encoder pair); -DNFDPF_PROP_SPLIT: the pair launch
+      if (ev)
+        hipExtLaunchKernelGGL(tiled_prop_quad_kernel<true>, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
+      else
+        tiled_prop_quad_kernel<true><<<g, 4 * kTile, 0, st>>>(d, ws);
+#else
       if (ev)
         hipExtLaunchKernelGGL(tiled_prop_split_kernel<true>, g, dim3(2 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
       else
         tiled_prop_split_kernel<true><<<g, 2 * kTile, 0, st>>>(d, ws);
+#endif
       return;
     }
     if (use_split(d)) {
@@ -1265,6 +1471,11 @@ extern "C" int nfdpf_split_fault(int reset) {
   return v;
 }
 
+#ifdef NFDPF_EXP_QTRACE
+extern "C" NFDPF_API int nfdpf_exp_qtrace_read(void *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_qtrace), sizeof(g_qtrace)) == hipSuccess ? 0 : 1;
+}
+#endif
 #ifdef NFDPF_EXP_TRACE
 extern "C" NFDPF_API int nfdpf_exp_trace_read(void *host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), sizeof(g_trace)) == hipSuccess ? 0 : 1;

@@ -231,3 +231,224 @@ class MAF(nn.Module):
 
     def inverse(self, z):
         return _ag.apply(MafStack(self, [self], self.dim, self.hidden_dim, True), (z,), _params([self]))
+
+
+# ------------------------------------------------------------------------------------------
+# The reference's other flows (nf/flows.py:11-98, 287-458), not on the DPF path (SURVEY.md
+# §8(f4)): same classes, constructor arguments, parameter names and returns.  The neural
+# spline flows' rational-quadratic spline is the HIP kernel nfdpf_rqs (nf.utils); Planar,
+# Radial, ActNorm and OneByOneConv are a few elementwise / (dim x dim) ops each and run as
+# PyTorch ops on the tensors' device.
+# ------------------------------------------------------------------------------------------
+import numpy as np  # noqa: E402
+import scipy as sp  # noqa: E402
+import scipy.linalg  # noqa: E402,F401
+import torch.nn.functional as F  # noqa: E402
+
+from nf.utils import unconstrained_RQS  # noqa: E402
+
+# supported non-linearities and their derivatives (nf/flows.py:11-18); evaluated on the
+# input's own device
+functional_derivatives = {
+    torch.tanh: lambda x: 1 - torch.pow(torch.tanh(x), 2),
+    F.leaky_relu: lambda x: (x > 0).to(x.dtype) + (x < 0).to(x.dtype) * -0.01,
+    F.elu: lambda x: (x > 0).to(x.dtype) + (x < 0).to(x.dtype) * torch.exp(x),
+}
+
+
+class Planar(nn.Module):
+    """Planar flow z = x + u h(w^T x + b) (nf/flows.py:22-64) [Rezende and Mohamed 2015]."""
+
+    def __init__(self, dim, nonlinearity=torch.tanh):
+        super().__init__()
+        self.h = nonlinearity
+        self.w = nn.Parameter(torch.Tensor(dim))
+        self.u = nn.Parameter(torch.Tensor(dim))
+        self.b = nn.Parameter(torch.Tensor(1))
+        self.reset_parameters(dim)
+
+    def reset_parameters(self, dim):
+        bound = math.sqrt(1 / dim)
+        for p in (self.w, self.u, self.b):
+            init.uniform_(p, -bound, bound)
+
+    def forward(self, x):
+        if self.h in (F.elu, F.leaky_relu):
+            u = self.u
+        elif self.h == torch.tanh:
+            # u constrained so that w^T u >= -1 (invertibility)
+            wu = self.w @ self.u
+            u = self.u + (torch.log(1 + torch.exp(wu)) - wu - 1) * self.w / torch.norm(self.w) ** 2
+        else:
+            raise NotImplementedError("Non-linearity is not supported.")
+        lin = torch.unsqueeze(x @ self.w, 1) + self.b
+        z = x + u * self.h(lin)
+        phi = functional_derivatives[self.h](lin) * self.w
+        return z, torch.log(torch.abs(1 + phi @ u) + 1e-4)
+
+    def inverse(self, z):
+        raise NotImplementedError("Planar flow has no algebraic inverse.")
+
+
+class Radial(nn.Module):
+    """Radial flow z = x + beta h(alpha, r) (x - x0) (nf/flows.py:67-98) [Rezende and Mohamed
+    2015].  As in the reference, __init__ leaves the parameters uninitialised (reset_parameters
+    is not called) and r is the norm over the whole input matrix."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.x0 = nn.Parameter(torch.Tensor(dim))
+        self.log_alpha = nn.Parameter(torch.Tensor(1))
+        self.beta = nn.Parameter(torch.Tensor(1))
+
+    def reset_parameters(self, dim):
+        bound = math.sqrt(1 / dim)
+        for p in (self.x0, self.log_alpha, self.beta):
+            init.uniform_(p, -bound, bound)
+
+    def forward(self, x):
+        m, n = x.shape
+        alpha = torch.exp(self.log_alpha)
+        r = torch.norm(x - self.x0)
+        h = 1 / (alpha + r)
+        beta = -alpha + torch.log(1 + torch.exp(self.beta))
+        z = x + beta * h * (x - self.x0)
+        log_det = (n - 1) * torch.log(1 + beta * h) + torch.log(1 + beta * h - beta * r / (alpha + r) ** 2)
+        return z, log_det
+
+
+class ActNorm(nn.Module):
+    """Per-dimension affine map with a scalar log-det (nf/flows.py:287-306) [Kingma and
+    Dhariwal 2018]."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.mu = nn.Parameter(torch.zeros(dim, dtype=torch.float))
+        self.log_sigma = nn.Parameter(torch.zeros(dim, dtype=torch.float))
+
+    def forward(self, x):
+        return x * torch.exp(self.log_sigma) + self.mu, torch.sum(self.log_sigma)
+
+    def inverse(self, z):
+        return (z - self.mu) / torch.exp(self.log_sigma), -torch.sum(self.log_sigma)
+
+
+class OneByOneConv(nn.Module):
+    """Invertible 1x1 convolution, W = P L (U + diag S) from the LU of a random orthogonal
+    matrix drawn with numpy's global generator (nf/flows.py:309-340) [Kingma and Dhariwal 2018].
+    As in the reference, L, S and U are registered parameters only when ``device`` is the CPU
+    (``nn.Parameter(...).to(device)`` returns a plain tensor on the GPU).  The inverse matrix is
+    cached after the first ``inverse`` (the reference's ``if not self.W_inv`` raises on the
+    second call for dim > 1; this build tests ``is None``)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        W, _ = sp.linalg.qr(np.random.randn(dim, dim))
+        P, L, U = sp.linalg.lu(W)
+        self.P = torch.tensor(P, dtype=torch.float).to(device)
+        self.L = nn.Parameter(torch.tensor(L, dtype=torch.float)).to(device)
+        self.S = nn.Parameter(torch.tensor(np.diag(U), dtype=torch.float)).to(device)
+        self.U = nn.Parameter(torch.triu(torch.tensor(U, dtype=torch.float), diagonal=1)).to(device)
+        self.W_inv = None
+
+    def _w(self):
+        eye = torch.diag(torch.ones(self.dim).to(device))
+        L = torch.tril(self.L, diagonal=-1) + eye
+        return self.P @ L @ (torch.triu(self.U, diagonal=1) + torch.diag(self.S))
+
+    def forward(self, x):
+        return x @ self._w(), torch.sum(torch.log(torch.abs(self.S)))
+
+    def inverse(self, z):
+        if self.W_inv is None:
+            self.W_inv = torch.inverse(self._w())
+        return z.float() @ self.W_inv, -torch.sum(torch.log(torch.abs(self.S)))
+
+
+def _spline_params(out, K, B, dim):
+    """(W, H, D) of a spline from a net output split K / K / K-1 along ``dim``: softmax'ed and
+    scaled by 2B, softplus'ed -- the reference then hands these to unconstrained_RQS as its
+    UNNORMALISED inputs (a second softmax inside; nf/flows.py:378-381)."""
+    W, H, D = torch.split(out, K, dim=dim)
+    W, H = 2 * B * torch.softmax(W, dim=dim), 2 * B * torch.softmax(H, dim=dim)
+    return W, H, F.softplus(D)
+
+
+class NSF_AR(nn.Module):
+    """Neural spline flow, autoregressive (nf/flows.py:343-398) [Durkan et al. 2019]: dimension
+    i's spline comes from FCNN(x[:, :i]) (the first from ``init_param``)."""
+
+    def __init__(self, dim, K=5, B=3, hidden_dim=8, base_network=FCNN):
+        super().__init__()
+        self.dim = dim
+        self.K = K
+        self.B = B
+        self.layers = nn.ModuleList()
+        self.init_param = nn.Parameter(torch.Tensor(3 * K - 1))
+        for i in range(1, dim):
+            self.layers += [base_network(i, 3 * K - 1, hidden_dim)]
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        init.uniform_(self.init_param, -1 / 2, 1 / 2)
+
+    def _params_of(self, i, x):
+        if i == 0:
+            out = self.init_param.expand(x.shape[0], 3 * self.K - 1)
+        else:
+            out = self.layers[i - 1](x[:, :i])
+        return _spline_params(out, self.K, self.B, 1)
+
+    def _run(self, v, inverse):
+        out = torch.zeros_like(v).to(device)
+        log_det = torch.zeros(out.shape[0]).to(device)
+        src = out if inverse else v  # the inverse conditions on the dimensions already inverted
+        for i in range(self.dim):
+            W, H, D = self._params_of(i, src)
+            out[:, i], ld = unconstrained_RQS(v[:, i], W, H, D, inverse=inverse, tail_bound=self.B)
+            log_det += ld
+        return out, log_det
+
+    def forward(self, x):
+        return self._run(x, False)
+
+    def inverse(self, z):
+        return self._run(z, True)
+
+
+class NSF_CL(nn.Module):
+    """Neural spline flow, coupling layer (nf/flows.py:401-458) [Durkan et al. 2019]."""
+
+    def __init__(self, dim, K=5, B=3, hidden_dim=8, base_network=FCNN):
+        super().__init__()
+        self.dim = dim
+        self.K = K
+        self.B = B
+        self.f1 = base_network(dim // 2, (3 * K - 1) * dim // 2, hidden_dim)
+        self.f2 = base_network(dim // 2, (3 * K - 1) * dim // 2, hidden_dim)
+
+    def _half(self, net, cond, v, inverse):
+        out = net(cond).reshape(-1, self.dim // 2, 3 * self.K - 1)
+        W, H, D = _spline_params(out, self.K, self.B, 2)
+        y, ld = unconstrained_RQS(v, W, H, D, inverse=inverse, tail_bound=self.B)
+        return y, torch.sum(ld, dim=1)
+
+    def forward(self, x):
+        log_det = torch.zeros(x.shape[0]).to(device)
+        lower, upper = x[:, :self.dim // 2], x[:, self.dim // 2:]
+        upper, ld = self._half(self.f1, lower, upper, False)
+        log_det += ld
+        lower, ld = self._half(self.f2, upper, lower, False)
+        log_det += ld
+        return torch.cat([lower, upper], dim=1), log_det
+
+    def inverse(self, z):
+        log_det = torch.zeros(z.shape[0]).to(device)
+        lower, upper = z[:, :self.dim // 2], z[:, self.dim // 2:]
+        lower, ld = self._half(self.f2, upper, lower, True)
+        log_det += ld
+        upper, ld = self._half(self.f1, lower, upper, True)
+        log_det += ld
+        return torch.cat([lower, upper], dim=1), log_det

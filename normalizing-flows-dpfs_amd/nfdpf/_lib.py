@@ -79,6 +79,8 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int, c_void_p]),
     "nfdpf_ess_gate": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_rqs": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_float, c_float,
+                          c_float, c_float, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "nfdpf_split_fault": (c_int, [c_int]),
     "nfdpf_normalize_log_probs": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "nfdpf_cglow_params_size": (c_int64, [c_int]),

@@ -326,6 +326,29 @@ def particle_init(start_xy, B, N, width, true_state, seed, row_base=0, device=No
     return x, lw
 
 
+def rqs(x, W, H, D, inverse=False, left=-1.0, right=1.0, bottom=-1.0, top=1.0, tails=True, min_bin_width=1e-3,
+        min_bin_height=1e-3, min_derivative=1e-3):
+    """The rational-quadratic spline (include/nfdpf.h nfdpf_rqs) -> (y, logdet), shapes of
+    ``x``.  W, H: x.shape + (K,); D: x.shape + (K - 1,) (unconstrained_RQS, nf/utils.py:23-53,
+    tails pass through) or x.shape + (K + 1,) (RQS, :55-147)."""
+    require_device(x, "rqs")
+    shape = x.shape
+    K = W.shape[-1]
+    x, W, H, D = _c(x), _c(W), _c(H), _c(D)
+    M = x.numel()
+    full = D.shape[-1] == K + 1
+    if W.numel() != M * K or H.numel() != M * K or D.numel() != M * (K + 1 if full else K - 1):
+        raise ValueError(f"rqs: parameter shapes {tuple(W.shape)}, {tuple(H.shape)}, {tuple(D.shape)} do not match "
+                         f"{M} inputs x {K} bins")
+    y = torch.empty_like(x)
+    ld = torch.empty_like(x)
+    check(lib().nfdpf_rqs(ptr(x), ptr(W), ptr(H), ptr(D), M, K, int(full), int(bool(inverse)), float(left),
+                          float(right), float(bottom), float(top), int(bool(tails)), float(min_bin_width),
+                          float(min_bin_height), float(min_derivative), ptr(y), ptr(ld), stream_ptr(x.device)),
+          "nfdpf_rqs")
+    return y.reshape(shape), ld.reshape(shape)
+
+
 def filter_step(desc: L.FilterDesc, device):
     check(lib().nfdpf_filter_step(desc, stream_ptr(device)), "nfdpf_filter_step")
 

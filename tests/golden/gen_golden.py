@@ -25,6 +25,9 @@ Fixtures:
                       DPF (its CNNs are 1.6 M parameters), global CPU generator seeded
   G9 state_dict_keys.json  DPF(args).state_dict() key -> shape for every measurement model
   G11 cglow_flow.npz  CondGlowModel.forward(x, y) -> (z, nll)
+  G12 flows_extra.npz the flows off the DPF path (Planar, Radial, ActNorm, OneByOneConv,
+                      NSF_AR, NSF_CL -- forward / inverse, spline-flow gradients) and the
+                      rational-quadratic spline (unconstrained_RQS, RQS)
   G10 grads.npz       the reference's AUTOGRAD gradients (training): flow stacks
                       (forward and inverse), MAF, soft and OT resamplers, all five measurement
                       models, each for a random linear functional of its outputs; and one
@@ -624,6 +627,94 @@ def gen_cglow_flow(mods):
     np.savez_compressed(os.path.join(OUT, "cglow_flow.npz"), **out)
 
 
+def gen_flows_extra(mods):
+    """The flows the DPF never instantiates (nf/flows.py:22-98, 287-458) and
+    the rational-quadratic spline (nf/utils.py:23-147): forward / inverse outputs, and for the
+    spline flows the autograd gradients of a random linear functional of (z, log_det)."""
+    import torch
+    import torch.nn.functional as F
+    from nf import flows as fl
+    from nf.utils import RQS, unconstrained_RQS
+    out = {}
+    g = torch.Generator().manual_seed(61)
+    # splines: K bins, inputs partly outside the tail bound
+    for K, B in ((5, 3.0), (8, 2.0)):
+        M = 300
+        x = (torch.rand(M, generator=g) * 2 - 1) * (B * 1.3)
+        W, H, D = (torch.randn(M, K, generator=g) * 1.5, torch.randn(M, K, generator=g) * 1.5,
+                   torch.randn(M, K - 1, generator=g))
+        y, ld = unconstrained_RQS(x, W.clone(), H.clone(), D.clone(), inverse=False, tail_bound=B)
+        xi, ldi = unconstrained_RQS(y, W.clone(), H.clone(), D.clone(), inverse=True, tail_bound=B)
+        k = f"urqs_K{K}/"
+        out.update({k + "x": x.numpy(), k + "W": W.numpy(), k + "H": H.numpy(), k + "D": D.numpy(),
+                    k + "B": np.float32(B), k + "y": y.numpy(), k + "ld": ld.numpy(), k + "xi": xi.numpy(),
+                    k + "ldi": ldi.numpy()})
+        xb = torch.rand(M, generator=g) * 0.98 + 0.01
+        Df = torch.randn(M, K + 1, generator=g)
+        yb, ldb = RQS(xb, W.clone(), H.clone(), Df.clone())
+        xbi, ldbi = RQS(yb, W.clone(), H.clone(), Df.clone(), inverse=True)
+        k = f"rqs_K{K}/"
+        out.update({k + "x": xb.numpy(), k + "D": Df.numpy(), k + "y": yb.numpy(), k + "ld": ldb.numpy(),
+                    k + "xi": xbi.numpy(), k + "ldi": ldbi.numpy()})
+    # neural spline flows (forward, inverse of the forward output, gradients)
+    for name, ctor, D in (("nsf_ar_D2", lambda: fl.NSF_AR(2), 2), ("nsf_ar_D4", lambda: fl.NSF_AR(4), 4),
+                          ("nsf_cl_D4", lambda: fl.NSF_CL(4), 4), ("nsf_cl_D6", lambda: fl.NSF_CL(6, K=6, B=2), 6)):
+        torch.manual_seed(70 + D)
+        m = ctor()
+        M = 64
+        x = torch.randn(M, D, generator=g) * 1.5
+        z, ld = m(x)
+        xi, ldi = m.inverse(z.detach())
+        k = name + "/"
+        out.update({k + "w/" + n: v for n, v in sd_np(m).items()})
+        out.update({k + "x": x.numpy(), k + "z": z.detach().numpy(), k + "ld": ld.detach().numpy(),
+                    k + "xi": xi.detach().numpy(), k + "ldi": ldi.detach().numpy()})
+        xg = x.clone().requires_grad_(True)
+        z, ld = m(xg)
+        cz, cl = torch.randn(M, D, generator=g), torch.randn(M, generator=g)
+        ((z * cz).sum() + (ld * cl).sum()).backward()
+        out.update({k + "cz": cz.numpy(), k + "cl": cl.numpy(), k + "gx": xg.grad.numpy()})
+        for n, p_ in m.named_parameters():
+            out[k + "g/" + n] = p_.grad.numpy().copy()
+    # planar (three non-linearities), radial, actnorm, 1x1 convolution
+    for nl, tag in ((torch.tanh, "tanh"), (F.leaky_relu, "leaky_relu"), (F.elu, "elu")):
+        torch.manual_seed(80)
+        m = fl.Planar(3, nonlinearity=nl)
+        x = torch.randn(50, 3, generator=g) * 2
+        with torch.no_grad():
+            z, ld = m(x)
+        k = f"planar_{tag}/"
+        out.update({k + "w/" + n: v for n, v in sd_np(m).items()})
+        out.update({k + "x": x.numpy(), k + "z": z.numpy(), k + "ld": ld.numpy()})
+    torch.manual_seed(81)
+    m = fl.Radial(3)
+    m.reset_parameters(3)
+    x = torch.randn(50, 3, generator=g)
+    with torch.no_grad():
+        z, ld = m(x)
+    out.update({"radial/w/" + n: v for n, v in sd_np(m).items()})
+    out.update({"radial/x": x.numpy(), "radial/z": z.numpy(), "radial/ld": ld.numpy()})
+    m = fl.ActNorm(3)
+    perturb(m, 0.5, g)
+    x = torch.randn(50, 3, generator=g)
+    with torch.no_grad():
+        z, ld = m(x)
+        xi, ldi = m.inverse(z)
+    out.update({"actnorm/w/" + n: v for n, v in sd_np(m).items()})
+    out.update({"actnorm/x": x.numpy(), "actnorm/z": z.numpy(), "actnorm/ld": np.float32(ld),
+                "actnorm/xi": xi.numpy(), "actnorm/ldi": np.float32(ldi)})
+    np.random.seed(82)
+    m = fl.OneByOneConv(3)
+    x = torch.randn(50, 3, generator=g)
+    with torch.no_grad():
+        z, ld = m(x)
+        xi, ldi = m.inverse(z)
+    out.update({"conv1x1/P": m.P.numpy(), "conv1x1/L": m.L.detach().numpy(), "conv1x1/S": m.S.detach().numpy(),
+                "conv1x1/U": m.U.detach().numpy(), "conv1x1/x": x.numpy(), "conv1x1/z": z.numpy(),
+                "conv1x1/ld": np.float32(ld), "conv1x1/xi": xi.numpy(), "conv1x1/ldi": np.float32(ldi)})
+    np.savez_compressed(os.path.join(OUT, "flows_extra.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -644,6 +735,8 @@ def main():
         gen_keys(mods)
     if not args.only or args.only == "cglow_flow":
         gen_cglow_flow(mods)
+    if not args.only or args.only == "flows_extra":
+        gen_flows_extra(mods)
     if not args.only or args.only == "grads":
         gen_grads(mods)
     if not args.only or args.only == "train_c2":
