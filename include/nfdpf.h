@@ -242,6 +242,15 @@ NFDPF_API int nfdpf_cglow_measurement(const float *pe_params, const float *glow_
 NFDPF_API int nfdpf_cglow_flow(const float *glow_params, int K, const float *x, const float *y, int64_t M,
                                float *z, float *nll, void *stream);
 
+/* Backward of nfdpf_maf_stack (training): g_out [rows, dim] = dL/d(output), g_logdet [rows]
+ * (either may be NULL = 0) -> g_x [rows, dim] = dL/dx and g_params = dL/d(blob), the blob's
+ * layout.  dim 2 or 4, hidden 8, n_flows <= 4 (dim 4: <= 2).  workspace: caller-owned,
+ * nfdpf_maf_stack_backward_workspace bytes (-1 = unsupported sizes).  Deterministic.      */
+NFDPF_API int64_t nfdpf_maf_stack_backward_workspace(int n_flows, int dim, int hidden, int64_t rows);
+NFDPF_API int nfdpf_maf_stack_backward(const float *params, int n_flows, int dim, int hidden, const float *x,
+                                       int64_t rows, int inverse, const float *g_out, const float *g_logdet,
+                                       float *g_x, float *g_params, void *workspace, void *stream);
+
 /* The rational-quadratic spline of the neural spline flows NSF_AR / NSF_CL (nf/flows.py:343-458)
  * on M elements with K bins each: RQS (nf/utils.py:55-147) on [left, right] x [bottom, top],
  * or, with tails = 1, unconstrained_RQS (:23-53): inputs outside [left, right] pass through

@@ -139,6 +139,22 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_d<kDppMirror>(v);
   return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
+// wave_sum_dpp of K values at once, step by step across the values: the K butterfly chains
+// are independent, so their DPP / fp64-add latencies overlap (same arithmetic per value).
+template <int K>
+__device__ __forceinline__ void wave_sum_dpp_n(double (&v)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppXor1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppXor2>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppHalfMirror>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppMirror>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    v[k] = (readlane_d(v[k], 0) + readlane_d(v[k], 16)) + (readlane_d(v[k], 32) + readlane_d(v[k], 48));
+}
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_f<kDppXor1>(v));
   v = fmaxf(v, dpp_f<kDppXor2>(v));

@@ -20,6 +20,16 @@
 #include "soft.hpp"
 #include <hip/hip_ext.h>
 
+#ifdef NFDPF_EXP_QTRACE
+// experiment-only: per-WAVE phase timestamps of the quad proposal launch (last step run)
+__device__ unsigned long long g_qtrace[1024][16][16];
+#define QTRACE(P)                                                                           \
+  if ((threadIdx.x & 63) == 0 && blockIdx.y * gridDim.x + blockIdx.x < 1024)                \
+    g_qtrace[blockIdx.y * gridDim.x + blockIdx.x][threadIdx.x >> 6][P] = __builtin_amdgcn_s_memrealtime();
+#else
+#define QTRACE(P)
+#endif
+
 #include "split.hpp"
 
 namespace nfdpf {
@@ -34,15 +44,6 @@ __device__ unsigned long long g_trace[4][2048][8];
     g_trace[K][blockIdx.y * gridDim.x + blockIdx.x][P] = __builtin_amdgcn_s_memrealtime();
 #else
 #define TRACE(K, P)
-#endif
-#ifdef NFDPF_EXP_QTRACE
-// experiment-only: per-WAVE phase timestamps of the quad proposal launch (last step run)
-__device__ unsigned long long g_qtrace[1024][16][8];
-#define QTRACE(P)                                                                           \
-  if ((threadIdx.x & 63) == 0 && blockIdx.y * gridDim.x + blockIdx.x < 1024)                \
-    g_qtrace[blockIdx.y * gridDim.x + blockIdx.x][threadIdx.x >> 6][P] = __builtin_amdgcn_s_memrealtime();
-#else
-#define QTRACE(P)
 #endif
 
 struct TiledWs {
@@ -376,13 +377,16 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
 // over the same particles.
 __device__ __forceinline__ void block_sum_roles_store(const double (&v)[4], double *dst0, double *dst1,
                                                       double *sh) {
-  double w4[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) w4[k] = wave_sum_dpp(v[k]);
   const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0)
+  // a role whose destination is null skips its reductions (wave-uniform; fp64 DPP sums of 8
+  // waves are a visible share of a short launch's epilogue)
+  if ((w & 1 ? dst1 : dst0) != nullptr) {
+    double w4[4] = {v[0], v[1], v[2], v[3]};
+    wave_sum_dpp_n(w4);
+    if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) sh[4 * w + k] = w4[k];
+      for (int k = 0; k < 4; ++k) sh[4 * w + k] = w4[k];
+  }
   __syncthreads();
   if (threadIdx.x < 8) {
     const int r = threadIdx.x >> 2, k = threadIdx.x & 3;
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kTile : kTile) void tiled_dyn_kernel(co
   __shared__ double shd[64];
   __shared__ f2 cb[kMaxFlows * 2 * kH];
   __shared__ f2 cbs[SPLIT ? kMaxFlows * 2 * kH : 1];  // split order (split_cb_index)
-  __shared__ float xbuf[SPLIT ? 4 * kTile : 1];
+  __shared__ __attribute__((aligned(8))) float xbuf[SPLIT ? 8 * kTile : 1];
   __shared__ int xflag[16];
   TRACE(1, 0)
   const int tiles = n_tiles(d.N);
@@ -423,6 +427,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kTile : kTile) void tiled_dyn_kernel(co
   const RowNorm rn = defer_here ? row_norm(prev_sm(d, b, tiles), tiles, shifted) : RowNorm{0.f, 1.f, 0.f};
   if (SPLIT) {
     if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+    pair_clear(xbuf, kTile);
     if (threadIdx.x < d.n_flows * 4 * kH) {
       const Ctx4 c = tiled_ctx(ws.st_phys, b, tiles, d.N);
       const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   __shared__ float w_sh[kTile];
   __shared__ f2 cb[kMaxFlows * 2 * kH];
   __shared__ f2 cbs[kMaxFlows * 2 * kH];
-  __shared__ float xbuf[4 * kTile];
+  __shared__ __attribute__((aligned(8))) float xbuf[8 * kTile];
   __shared__ int xflag[16];
   TRACE(0, 0)
   const int tiles = n_tiles(d.N), N = d.N;
@@ -512,6 +517,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   const bool shifted = shifted_meas(d.measurement);
   float *Cbuf = dyn_lds;
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+  pair_clear(xbuf, kTile);
   float e0 = 0.f, e1 = 0.f;
   if (valid) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: under its latency
   const int64_t my_row = ess_row(d, b);
@@ -686,7 +692,8 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   }
   // the row context: wave sums (DPP), then the 8 wave partials in wave order, in every thread
   {
-    const double w4[4] = {wave_sum_dpp(a0), wave_sum_dpp(a1), wave_sum_dpp(c0), wave_sum_dpp(c1)};
+    double w4[4] = {a0, a1, c0, c1};
+    wave_sum_dpp_n(w4);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
@@ -968,7 +975,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
 template <bool MERGED>
 __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;  // cb_dyn / cb_cond in split order
-  __shared__ float xbuf[4 * kTile];
+  __shared__ __attribute__((aligned(8))) float xbuf[8 * kTile];
   __shared__ float hbuf[2 * kPeH2 / 2 * kTile];  // the encoder's hidden halves (encode_dot_pair)
   __shared__ float dbuf[2 * 4 * kTile];          // the fp64 cosine partials (pair_swap_once2)
   __shared__ int xflag[16];
@@ -998,6 +1005,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
                                               : RowNorm{0.f, 1.f, 0.f};
   measure_row_setup<NFDPF_MEAS_COS>(S.enc, d.meas_params, L);
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+  pair_clear(xbuf, kTile);
   const int ncb = d.n_flows * 4 * kH;
   if (threadIdx.x < ncb)
     reinterpret_cast<float *>(L.cb_dyn)[split_cb_index(threadIdx.x)] = ws.cb_dyn[b * kCb + threadIdx.x];
@@ -1062,29 +1070,33 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
   TRACE(2, 3)
 }
 
-// store_softmax_fin for the 16-wave quad launch: u rides on the flow t-waves 0, 2, 4, 6, the
-// deferred-normalisation sums on the encoder waves 8, 10, 12, 14 -- the same lanes, values and
-// summation order as the split launch's (waves 0, 2, 4, 6 and 1, 3, 5, 7).  shd >= 96 doubles.
-__device__ __forceinline__ void store_softmax_fin_quad(float u, bool valid, double *sm, const double (&sf)[4],
-                                                       double *fin, float *shf, double *shd) {
+// The quad launch's softmax / deferred-normalisation partials: the encoder t-waves 8, 10, 12,
+// 14 (groups 0-3) carry u and the slot t-1 sums and leave their wave partials in LDS before
+// the launch's one closing barrier (wave_partials_quad); after it thread 0 merges the tile's
+// {max, sum e, sum e^2} and threads 64-67 the four sums -- the same lanes, values and
+// summation order as the split launch's (u on waves 0, 2, 4, 6, sums on 1, 3, 5, 7).
+// shf >= 16 floats, shd >= 96 doubles.
+__device__ __forceinline__ void wave_partials_quad(float u, bool valid, bool carry, const double (&sf)[4],
+                                                   float *shf, double *shd) {
+  const int w = threadIdx.x >> 6;
+  if (!carry) {  // wave-uniform: this wave holds no partials
+    if ((threadIdx.x & 63) == 0) shf[w] = -INFINITY;
+    return;
+  }
   const float mw = wave_max_dpp(valid ? u : -INFINITY);
   const float ev = valid ? expf(u - mw) : 0.f;
-  const double ew = wave_sum_dpp((double)ev);
-  const double qw = wave_sum_dpp((double)ev * ev);
-  double f4[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) f4[k] = wave_sum_dpp(sf[k]);
-  const int w = threadIdx.x >> 6;
+  double r[6] = {(double)ev, (double)ev * ev, sf[0], sf[1], sf[2], sf[3]};
+  wave_sum_dpp_n(r);
   if ((threadIdx.x & 63) == 0) {
     shf[w] = mw;
-    shd[2 * w] = ew;
-    shd[2 * w + 1] = qw;
+    shd[2 * w] = r[0];
+    shd[2 * w + 1] = r[1];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) shd[32 + 4 * w + k] = f4[k];
+    for (int k = 0; k < 4; ++k) shd[32 + 4 * w + k] = r[2 + k];
   }
-  QTRACE(6)
-  __syncthreads();
-  QTRACE(7)
+}
+// after the barrier
+__device__ __forceinline__ void merge_partials_quad(double *sm, double *fin, const float *shf, const double *shd) {
   if (threadIdx.x == 0) {
     float m = shf[0];
     for (int k = 1; k < 16; ++k) m = fmaxf(m, shf[k]);
@@ -1098,7 +1110,8 @@ __device__ __forceinline__ void store_softmax_fin_quad(float u, bool valid, doub
     sm[0] = m;
     sm[1] = sum;
     sm[2] = sq;
-  } else if (fin && threadIdx.x >= 64 && threadIdx.x < 68) {  // encoder waves 8, 10, 12, 14 in order
+    sm[3] = 0.0;
+  } else if (fin && threadIdx.x >= 64 && threadIdx.x < 68) {  // encoder t-waves 8, 10, 12, 14 in order
     const int k = threadIdx.x - 64;
     double a = shd[32 + 4 * 8 + k];
     for (int q = 1; q < 4; ++q) a += shd[32 + 4 * (8 + 2 * q) + k];
@@ -1117,14 +1130,19 @@ __device__ __forceinline__ void store_softmax_fin_quad(float u, bool valid, doub
 template <bool MERGED>
 __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;
-  __shared__ float xbuf[4 * kTile];              // flow-pair hand-offs (pair_swap)
+  __shared__ __attribute__((aligned(8))) float xbuf[8 * kTile];              // flow-pair hand-offs (pair_swap)
+#ifdef NFDPF_ENC_VALU
   __shared__ float hbuf[2 * kPeH2 / 2 * kTile];  // encoder hidden halves (encode_dot_pair)
   __shared__ float dbuf[2 * 4 * kTile];          // fp64 cosine partials (pair_swap_once2)
+#else
+  __shared__ float Hws[8][32 * kHPitch];         // each encoder wave's layer-2 / layer-3 outputs
+#endif
   __shared__ float qbuf[2 * kTile];              // the proposal, flow t-wave -> encoder pair
   __shared__ float rbuf[3 * kTile];              // likelihood | prior | propose per particle
   __shared__ float encq[8][kE];                  // each encoder wave's copy of the frame encoding
   __shared__ int xflag[16];
   __shared__ int qflag[4];
+  __shared__ int rflag[4];
   __shared__ float smf[16];
   __shared__ double smd[96];
   TRACE(2, 0)
@@ -1143,15 +1161,27 @@ __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_
   // with the merged front + dyn launch, slot t-1's deferred normalisation runs here (encoder t-wave)
   const bool defer_here = MERGED && d.defer_norm && d.t > 0 && enc && role == 0;
   PrevIn pv{};
+#ifndef NFDPF_ENC_VALU
+  EncFrag2 ef{};
+  if (enc) ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
+  // an encoder wave's measured particles: lanes 0-31 <- particles [32 role, 32 role + 32) of the group
+  const int slot_e = g * 64 + 32 * role + (threadIdx.x & 31), i_e = tile * kTile + slot_e;
+  const bool valid_e = enc && (threadIdx.x & 63) < 32 && i_e < d.N;
+#else
+  const int slot_e = slot, i_e = i;
+  const bool valid_e = enc && role == 0 && valid;
+#endif
   if (valid) {  // issued before the row prologue so they overlap it
     if (!enc) in = load_prop_in<true>(S, i);
-    if (!enc && role == 0) lr = S.hp[i];
     if (defer_here) pv = load_prev_in(row_slot(d, b, d.t - 1), i);
   }
+  if (valid_e) lr = S.hp[i_e];
   // the encoder waves' row constants (the frame encoding, slot t-1's normaliser) are read after
   // the prologue barrier: they are needed only once the proposal has arrived
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
+  pair_clear(xbuf, kTile);
   if (threadIdx.x < 4) qflag[threadIdx.x] = 0;
+  if (threadIdx.x >= 4 && threadIdx.x < 8) rflag[threadIdx.x - 4] = 0;
   const int ncb = d.n_flows * 4 * kH;
   if (threadIdx.x < ncb)
     reinterpret_cast<float *>(L.cb_dyn)[split_cb_index(threadIdx.x)] = ws.cb_dyn[b * kCb + threadIdx.x];
@@ -1168,7 +1198,8 @@ __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_
   TRACE(2, 1)
   QTRACE(1)
   double sf[4] = {0, 0, 0, 0};
-  lds_vint *qf = (lds_vint *)(qflag + g);
+  float u = 0.f;
+  lds_vint *qf = (lds_vint *)(qflag + g), *rf = (lds_vint *)(rflag + g);
   if (!enc) {
     PairX x = pair_of(xbuf, xflag, role, slot);
     float q0x = 0.f, q1x = 0.f, jp = 0.f;
@@ -1191,6 +1222,10 @@ __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_
         rbuf[kTile + slot] = prior;
         rbuf[2 * kTile + slot] = propose;
       }
+    }
+    if (role == 0) {  // publish prior / propose to the encoder t-wave
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      *rf = 1;
     }
     QTRACE(3)
   } else {
@@ -1216,38 +1251,51 @@ __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_
       sf[2] = (double)p * pv.x1;
       sf[3] = lw;
     }
-    if (valid) {
+    // valid lanes are a prefix of the wave: it has work iff its first lane has
+    if (tile * kTile + g * 64 < d.N) {
       int it = 0;
       for (; __builtin_amdgcn_readfirstlane(*qf) == 0 && it < kSpinCap; ++it) __builtin_amdgcn_s_sleep(1);
       if (it == kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
       asm volatile("" ::: "memory");
       QTRACE(2)
-      const float q0x = qbuf[slot], q1x = qbuf[kTile + slot];
+      // cosine measurement (model/models.py:206-219)
+      double ss, dot;
+#ifdef NFDPF_ENC_VALU  // the pair splits the outputs: [16 role, 16 role + 16) here, then exchanges
       PairX xe = pair_of(xbuf, xflag, role, slot);  // flags 8..15: the encoder pairs' own
-      // cosine measurement (model/models.py:206-219): outputs [16 role, 16 role + 16) here
-      double ss, dot, ss_o, dot_o;
-      encode_dot_pair<kE>(wptr(d.pe_params), q0x, q1x, encv, ss, dot, xe, hbuf, kTile);
+      double ss_o, dot_o;
+      encode_dot_pair<kE>(wptr(d.pe_params), qbuf[slot], qbuf[kTile + slot], encv, ss, dot, xe, hbuf, kTile);
       pair_swap_once2(xe, ss, dot, dbuf, kTile, ss_o, dot_o);
       ss = role ? ss_o + ss : ss + ss_o;
       dot = role ? dot_o + dot : dot + dot_o;
+#else  // the pair splits the particles: no hand-off
+      encode_dot_mfma_half<kE>(ef, role, qbuf + g * 64, qbuf + kTile + g * 64, encv, ss, dot, Hws[w - 8]);
+#endif
+      QTRACE(11)
       const float lk = cos_lik(ss, dot, vinv);
-      if (role == 0) {
-        S.hlik[i] = lk;
-        rbuf[slot] = lk;
+      if (valid_e) {
+        S.hlik[i_e] = lk;
+        // the log-weight (DPFs.py:187) once the flow t-wave has left prior / propose
+        int it2 = 0;
+        for (; __builtin_amdgcn_readfirstlane(*rf) == 0 && it2 < kSpinCap; ++it2) __builtin_amdgcn_s_sleep(1);
+        if (it2 == kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
+        asm volatile("" ::: "memory");
+        u = logw(lr, lk, rbuf[kTile + slot_e], rbuf[2 * kTile + slot_e]);
       }
     }
     QTRACE(3)
   }
+  // the encoder waves' softmax and slot t-1 partials, then the launch's one closing barrier
+#ifdef NFDPF_ENC_VALU
+  wave_partials_quad(u, valid_e, enc && role == 0, sf, smf, smd);
+#else
+  wave_partials_quad(u, valid_e, enc, sf, smf, smd);
+#endif
   __syncthreads();
   TRACE(2, 2)
   QTRACE(4)
-  const bool carry = !enc && role == 0 && valid;
-  const float u = carry ? logw(lr, rbuf[slot], rbuf[kTile + slot], rbuf[2 * kTile + slot]) : 0.f;
   double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
-  if (threadIdx.x == 0) sm[3] = 0.f;
   const bool fin = MERGED && d.defer_norm && d.t > 0;
-  store_softmax_fin_quad(u, carry, sm, sf, fin ? ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4 : nullptr,
-                         smf, smd);
+  merge_partials_quad(sm, fin ? ws.fin + (((int64_t)b * d.T + d.t - 1) * tiles + tile) * 4 : nullptr, smf, smd);
   TRACE(2, 3)
   QTRACE(5)
 }

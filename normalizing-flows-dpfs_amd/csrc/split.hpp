@@ -52,7 +52,7 @@ typedef __attribute__((address_space(3))) float lds_float;
 typedef volatile __attribute__((address_space(3))) int lds_vint;
 
 struct PairX {
-  lds_float *buf;  // [2 parities][2 nets][kTile]
+  lds_float *buf;  // pair_swap: [2 parities][2 nets][kTile] x {value, tag} (2 floats each)
   lds_vint *mine;  // this wave's counter
   lds_vint *theirs;
   int role, slot, k;
@@ -97,11 +97,31 @@ __device__ __forceinline__ void pair_wait(PairX &x) {
   asm volatile("" ::: "memory");
 }
 
+// One value each way, tagged: every lane writes {value, exchange number} with ONE 64-bit LDS
+// store and polls its partner lane's {value, tag} until the tag is this exchange's -- one LDS
+// round trip per side instead of value store, counter store, counter poll and value load.
+// Buffers alternate by exchange parity (a side cannot be two exchanges ahead: it needs the
+// partner's value of the previous one first).  buf = [2 parities][2 roles][tile_len] x 2 words.
+typedef volatile __attribute__((address_space(3))) unsigned long long lds_vu64;
+// LDS is not cleared between workgroups: a previous workgroup's tags would satisfy a poll, so
+// every kernel zeroes its pair_swap buffer (4 tile_len words) before its first barrier
+__device__ __forceinline__ void pair_clear(float *buf, int tile_len) {
+  for (int j = threadIdx.x; j < 4 * tile_len; j += blockDim.x) ((lds_vu64 *)buf)[j] = 0ull;
+}
 __device__ __forceinline__ float pair_swap(PairX &x, float v, int tile_len) {
-  lds_float *b = x.buf + ((x.k + 1) & 1) * 2 * tile_len;
-  b[x.role * tile_len + x.slot] = v;
-  pair_wait(x);
-  return b[(1 - x.role) * tile_len + x.slot];
+  const int k = ++x.k;
+  lds_vu64 *tb = (lds_vu64 *)x.buf + (k & 1) * 2 * tile_len;
+  tb[x.role * tile_len + x.slot] = ((unsigned long long)(unsigned)k << 32) | (unsigned)__float_as_uint(v);
+  unsigned long long r;
+  int it = 0;
+  for (;;) {
+    r = tb[(1 - x.role) * tile_len + x.slot];
+    if (__all((int)(r >> 32) == k) || ++it >= kSpinCap) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (it >= kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
+  asm volatile("" ::: "memory");
+  return __uint_as_float((unsigned)r);
 }
 
 // Cosine pieces (|e|^2, <e, v> over this role's output pairs) with the particle encoder's
@@ -159,6 +179,111 @@ __device__ __forceinline__ void encode_dot_pair(cfloat *pe, float x0, float x1, 
     dot = fma(ax, (double)v[2 * (o0 + m)], dot);
     ss = fma(ay, ay, ss);
     dot = fma(ay, (double)v[2 * (o0 + m) + 1], dot);
+  }
+}
+
+// ---- the cosine encoder's dense layers on f32 MFMA (v_mfma_f32_16x16x4_f32) ----------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// The cosine measurement's encoder on MFMA with the pair split by PARTICLES instead of outputs:
+// wave r of the pair takes particle blocks {2r, 2r + 1} (particles [32 r, 32 r + 32) of the
+// group) through all three layers, so the pair never hands off (no layer-3 operand exchange,
+// no partial-sum exchange).  Layer 1 as encode_dot_pair_mfma; layers 2 / 3 per block as two
+// 16-column output tiles (bias-initialised exact k-ordered MFMA chains); the 32 outputs of a
+// particle come back to lane (particle - 32 r) through Eo, which accumulates |e|^2 and <e, v>
+// in fp64 in output order (particle_encode + encode_dot's arithmetic).  Lanes >= 32 return 0.
+struct EncFrag2 {
+  float w10[4], w11[4], b1[4];  // layer 1 for k = 4 s + (lane >> 4)
+  float b2[2][4], b3[2][8];     // B fragments of output tiles n = 0, 1 (columns 16 n + (lane & 15))
+  float bias2[2], bias3[2];
+};
+__device__ __forceinline__ EncFrag2 enc_frag2_load(const float *pe) {
+  EncFrag2 f;
+  const int l = threadIdx.x & 63, kk = l >> 4;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int k = 4 * st + kk;
+    f.w10[st] = pe[4 * (k >> 1) + (k & 1)];
+    f.w11[st] = pe[4 * (k >> 1) + 2 + (k & 1)];
+    f.b1[st] = pe[kPeB1 + k];
+  }
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int c = 16 * n + (l & 15);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) f.b2[n][st] = pe[kPeW2 + kPeH2 * (4 * st + kk) + c];
+#pragma unroll
+    for (int st = 0; st < 8; ++st) f.b3[n][st] = pe[kPeW3 + kE * (4 * st + kk) + c];
+    f.bias2[n] = pe[kPeB2 + c];
+    f.bias3[n] = pe[kPeW3 + kE * kPeH2 + c];
+  }
+  return f;
+}
+constexpr int kHPitch = 36;  // [32 particles][32 units] LDS rows (bank spread of the A reads)
+
+// q0 / q1: the group's proposals (64 each); Hw: [32][kHPitch] this wave's own (layer-2 outputs,
+// then layer-3 outputs).  Every lane takes part (MFMA operands).
+template <int E>
+__device__ __forceinline__ void encode_dot_mfma_half(const EncFrag2 &f, int role, const float *q0, const float *q1,
+                                                     const float *v, double &ss, double &dot, float *Hw) {
+  static_assert(E == kE && kPeH1 == 16 && kPeH2 == 32, "MFMA encoder: 2 -> 16 -> 32 -> 32");
+  const int l = threadIdx.x & 63, r16 = l & 15, kk = l >> 4;
+  lds_float *hw = (lds_float *)Hw;
+  f4v acc[2][2];
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {  // layer 1 in A order, layer 2
+    const int p = 32 * role + 16 * bb + r16;
+    const float x0 = q0[p], x1 = q1[p];
+    float h[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) h[st] = relu(fmaf(f.w11[st], x1, fmaf(f.w10[st], x0, f.b1[st])));
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      acc[bb][n] = f4v{f.bias2[n], f.bias2[n], f.bias2[n], f.bias2[n]};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) acc[bb][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(h[st], f.b2[n][st], acc[bb][n], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hw[(16 * bb + 4 * kk + i) * kHPitch + 16 * n + r16] = relu(acc[bb][n][i]);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  QTRACE(8)
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {  // layer 3
+    float a[8];
+#pragma unroll
+    for (int st = 0; st < 8; ++st) a[st] = hw[(16 * bb + r16) * kHPitch + 4 * st + kk];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      acc[bb][n] = f4v{f.bias3[n], f.bias3[n], f.bias3[n], f.bias3[n]};
+#pragma unroll
+      for (int st = 0; st < 8; ++st) acc[bb][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], f.b3[n][st], acc[bb][n], 0, 0, 0);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // every lane's layer-3 A reads are done before Hw is reused
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hw[(16 * bb + 4 * kk + i) * kHPitch + 16 * n + r16] = acc[bb][n][i];
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  QTRACE(9)
+  ss = 0.0;
+  dot = 0.0;
+  if (l < 32) {
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      const double a = hw[l * kHPitch + c];
+      ss = fma(a, a, ss);
+      dot = fma(a, (double)v[c], dot);
+    }
   }
 }
 

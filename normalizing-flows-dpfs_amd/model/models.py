@@ -155,7 +155,7 @@ class _MeasRunner:
         (csrc/measure_bwd.hip); None for the other models (autograd then differentiates
         ``torch``)."""
         m = self.model
-        if self.kind not in ("cos", "CRNVP") or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 \
+        if self.kind not in ("cos", "CRNVP", "gaussian") or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 \
                 or x.shape[-1] != 2:
             return None
         pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
@@ -164,6 +164,12 @@ class _MeasRunner:
         pe_params = list(m.particle_encoder.parameters())
         if self.kind == "cos":
             g_enc, gx, gp = _ops.cos_measurement_backward(pe, enc.float(), x.float(), g)
+            extra = []
+        elif self.kind == "gaussian":
+            out = self._gaussian_backward(pe, enc.float(), x.float(), g)
+            if out is None:
+                return None
+            g_enc, gx, gp = out
             extra = []
         else:
             out = self._crnvp_backward(pe, enc.float(), x.float(), g)
@@ -176,6 +182,27 @@ class _MeasRunner:
             off += p.numel()
         res += extra  # CRNVP: the flow's parameters (m.parameters() lists the encoder first)
         return (g_enc.to(enc.dtype), gx.to(x.dtype)), res
+
+    def _gaussian_backward(self, pe, enc, x, g):
+        """measurement_model_Gaussian (model/models.py:237-254): lik = log N(o - e; mu, s^2 I) minus
+        the row max.  The max routes -sum_n g to the row's argmax; dlik/de = (o - e - mu) / s^2
+        (elementwise on the (B, N, 32) encodings); the particle encoder forward and backward are
+        the HIP kernels (nfdpf_particle_encoder modes 0 / 1)."""
+        dist = self.model.gaussian_distribution
+        cov = dist.covariance_matrix
+        var = float(cov[0, 0])
+        if not torch.equal(cov, torch.eye(cov.shape[0], device=cov.device, dtype=cov.dtype) * var):
+            return None  # a non-isotropic covariance: differentiate the PyTorch restatement
+        B, N, _ = x.shape
+        es = _ops.particle_encoder_forward(pe, x).view(B, N, 32)
+        d = enc[:, None, :] - es - dist.loc.to(es.dtype)
+        u = -0.5 * (d * d).sum(-1)  # the log-density up to a constant: only its argmax is used
+        am = u.argmax(-1)
+        g_u = g.clone()
+        g_u[torch.arange(B, device=g.device), am] -= g.sum(-1)
+        r = g_u[..., None] * d / var        # = dL/de (lik rises as e approaches o - mu)
+        gx, gp = _ops.particle_encoder_backward(pe, x, r.reshape(B * N, 32).contiguous())
+        return -r.sum(1), gx, gp
 
     def _crnvp_backward(self, pe, enc, x, g):
         """measurement_model_cnf (model/models.py:256-278): lik = u - max_n u with u = log N(z) +

@@ -157,6 +157,20 @@ class MafStack:
         b = blob(self.owner, "maf", self.flows, lambda: flows_tensors(self.flows), x.device)
         return _ops.maf_stack(b, len(self.flows), self.dim, self.hidden, x, self.inverse)
 
+    def hip_backward(self, x, gouts):
+        """d/d(x, parameters) by nfdpf_maf_stack_backward (csrc/maf_bwd.hip); None when the
+        kernel does not cover the case (autograd then differentiates ``torch``)."""
+        b = blob(self.owner, "maf", self.flows, lambda: flows_tensors(self.flows), x.device)
+        got = _ops.maf_stack_backward(b, len(self.flows), self.dim, self.hidden, x.float(), self.inverse,
+                                      None if gouts[0] is None else gouts[0].float(),
+                                      None if gouts[1] is None else gouts[1].float())
+        if got is None:
+            return None
+        gx, gb = got
+        params = _params(self.flows)
+        gp = blob_grad_to_params(self.owner, "maf", params, lambda get: flows_tensors(self.flows, get), gb)
+        return (gx.to(x.dtype),), [g if p.requires_grad else None for g, p in zip(gp, params)]
+
     def torch(self, x):
         ld = torch.zeros(x.shape[0], device=x.device)
         for f in (self.flows[::-1] if self.inverse else self.flows):

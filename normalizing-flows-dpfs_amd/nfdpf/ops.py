@@ -73,6 +73,26 @@ def maf_stack(blob, n_flows, dim, hidden, x, inverse=False):
     return out, ld
 
 
+def maf_stack_backward(blob, n_flows, dim, hidden, x, inverse, g_out, g_logdet):
+    """Backward of maf_stack -> (g_x, g_blob), or None when the kernel does not cover the sizes
+    (include/nfdpf.h nfdpf_maf_stack_backward)."""
+    require_device(x, "maf_stack_backward")
+    x = _c(x)
+    rows = x.shape[0]
+    nbytes = int(lib().nfdpf_maf_stack_backward_workspace(n_flows, dim, hidden, rows))
+    if nbytes < 0 or (dim == 4 and n_flows > 2):
+        return None
+    gx = torch.empty_like(x)
+    gb = torch.empty_like(blob)
+    ws = torch.empty(max(1, nbytes // 4), device=x.device, dtype=f32)
+    go = _c(g_out) if g_out is not None else None
+    gl = _c(g_logdet) if g_logdet is not None else None
+    check(lib().nfdpf_maf_stack_backward(ptr(blob), n_flows, dim, hidden, ptr(x), rows, int(bool(inverse)), ptr(go),
+                                         ptr(gl), ptr(gx), ptr(gb), ptr(ws), stream_ptr(x.device)),
+          "nfdpf_maf_stack_backward")
+    return gx, gb
+
+
 @functools.lru_cache(maxsize=64)
 def _lin_cpu(N: int) -> torch.Tensor:
     # the reference's marker base, torch.linspace on CPU (resamplers.py:42); a per-N constant

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ -n "$TESTS" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-500} python -u -m pytest -x -v -rP --timeout 300 --timeout-method thread \
+  timeout -k 10 ${TEST_TIMEOUT:-500} python -u -m pytest -x -v -rP --tb=short --timeout 300 --timeout-method thread \
     -p no:cacheprovider $TESTS ${KEXPR:+-k "$KEXPR"} > gpurun_out/quick_tests.log 2>&1
   rc=$?; echo "pytest rc=$rc" >> gpurun_out/quick_tests.log; tail -4 gpurun_out/quick_tests.log
   [ $rc -eq 0 ] || exit $rc

@@ -25,6 +25,9 @@ Fixtures:
                       DPF (its CNNs are 1.6 M parameters), global CPU generator seeded
   G9 state_dict_keys.json  DPF(args).state_dict() key -> shape for every measurement model
   G11 cglow_flow.npz  CondGlowModel.forward(x, y) -> (z, nll)
+  G14 autoencoder.npz frame encoder / decoder CNNs + autoencoder_loss (seeded init checksums,
+                      features, reconstruction sample, loss; train and eval mode)
+  G13 dataset.npz     the disk generator's trajectories (start state, states, q)
   G12 flows_extra.npz the flows off the DPF path (Planar, Radial, ActNorm, OneByOneConv,
                       NSF_AR, NSF_CL -- forward / inverse, spline-flow gradients) and the
                       rational-quadratic spline (unconstrained_RQS, RQS)
@@ -715,6 +718,74 @@ def gen_flows_extra(mods):
     np.savez_compressed(os.path.join(OUT, "flows_extra.npz"), **out)
 
 
+def gen_autoencoder(mods):
+    """The frame encoder / decoder CNNs and autoencoder_loss (model/models.py:10-117,
+    losses.py:5-16).  The networks are 1.6 M parameters: instead of storing
+    them, each is built right after torch.manual_seed(s) -- the same layers in the same order
+    draw the same default init -- and the fixture holds a checksum of every parameter, the
+    input frames' seed, the features, a fixed subsample of the reconstruction and the loss,
+    in train (batch statistics) and eval mode."""
+    import torch
+    from model.models import build_decoder, build_decoder_cglow, build_encoder, build_encoder_cglow
+    from losses import autoencoder_loss
+    out = {}
+    for tag, benc, bdec, H in (("h32", build_encoder, build_decoder, 32),
+                               ("cglow", build_encoder_cglow, build_decoder_cglow, 192)):
+        torch.manual_seed(301)
+        enc = benc(H)
+        torch.manual_seed(302)
+        dec = bdec(H)
+        for name, m in (("enc", enc), ("dec", dec)):
+            for k, v in m.state_dict().items():
+                out[f"{tag}/{name}/sum/{k}"] = np.float64(v.double().sum())
+                out[f"{tag}/{name}/abs/{k}"] = np.float64(v.double().abs().sum())
+        g = torch.Generator().manual_seed(303)
+        img = torch.rand(2, 2, 3, 128, 128, generator=g)
+        idx = torch.randint(0, 4 * 3 * 128 * 128, (512,), generator=g)
+        out[f"{tag}/idx"] = idx.numpy()
+        for mode in ("train", "eval"):
+            enc.train(mode == "train")
+            dec.train(mode == "train")
+            with torch.no_grad():
+                x = img.reshape(4, 3, 128, 128)
+                f = enc(x)
+                r = dec(f)
+                loss = autoencoder_loss(img, mode == "train", enc, dec)
+            out[f"{tag}/{mode}/feature"] = f.numpy()
+            out[f"{tag}/{mode}/recon_sample"] = r.reshape(-1)[idx].numpy()
+            out[f"{tag}/{mode}/recon_mean"] = r.mean(dim=(0, 2, 3)).numpy()
+            out[f"{tag}/{mode}/loss"] = np.float32(loss)
+    np.savez_compressed(os.path.join(OUT, "autoencoder.npz"), **out)
+
+
+def gen_dataset(mods):
+    """The disk generator's trajectories (data/disk/create_dataset.py:120-216): start state,
+    states and q of a few sequences drawn from numpy's global generator.  The reference draws
+    its frames with cv2.circle; cv2 is not installed, so for THIS fixture its placeholder
+    module gets a no-op ``circle`` -- circle draws no random numbers, so the recorded
+    trajectories are the reference's own; its frames / visibility are not recorded."""
+    import importlib.util
+    sys.modules["cv2"].circle = lambda *a, **k: None
+    spec = importlib.util.spec_from_file_location("ref_create_dataset", os.path.join(REF, "data/disk/create_dataset.py"))
+    cd = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cd)
+    import tempfile
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        param = types.SimpleNamespace(width=128, out_dir=tmp, name="fixture", num_examples=4, sequence_length=6,
+                                      file_size=500)
+        ex = cd.ToyExample(param)
+        for case, (nd, pn, seed) in enumerate(((0, 2.0, 91), (3, 2.0, 92), (25, 5.0, 93))):
+            np.random.seed(seed)
+            for n in range(2):
+                v = ex._get_data(nd, pn)
+                for k in ("start_state", "state", "q"):
+                    out[f"c{case}/s{n}/{k}"] = np.asarray(v[k])
+            out[f"c{case}/cfg"] = np.array([nd, pn, seed], dtype=np.float64)
+            out[f"c{case}/next_uniform"] = np.float64(np.random.uniform())  # the RNG state after
+    np.savez_compressed(os.path.join(OUT, "dataset.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -737,6 +808,10 @@ def main():
         gen_cglow_flow(mods)
     if not args.only or args.only == "flows_extra":
         gen_flows_extra(mods)
+    if not args.only or args.only == "dataset":
+        gen_dataset(mods)
+    if not args.only or args.only == "autoencoder":
+        gen_autoencoder(mods)
     if not args.only or args.only == "grads":
         gen_grads(mods)
     if not args.only or args.only == "train_c2":
