@@ -251,6 +251,20 @@ NFDPF_API int nfdpf_maf_stack_backward(const float *params, int n_flows, int dim
                                        int64_t rows, int inverse, const float *g_out, const float *g_logdet,
                                        float *g_x, float *g_params, void *workspace, void *stream);
 
+/* Block pseudo-likelihood of the semi-supervised objective (compute_block_density_nf,
+ * losses.py:37-68) on the filter histories w, lik, prior [B,T,N] and the ancestor index
+ * [B,T,N] (int64, flat into B*N): Q [B] (fp64) = the reference's Q / number of blocks.
+ * Backward: g_Q [B] -> g_w, g_lik, g_prior [B,T,N]; the ancestor maps must be non-decreasing
+ * over the flattened batch (the filter's always are: nfdpf_pseudo_lik_check sets *ok = 0
+ * otherwise; *ok must be 1 on entry).  workspace: nfdpf_pseudo_lik_workspace bytes.        */
+NFDPF_API int nfdpf_pseudo_lik_forward(const float *w, const float *lik, const float *prior, const int64_t *index,
+                                       int B, int T, int N, int block_len, double *Q, void *stream);
+NFDPF_API int64_t nfdpf_pseudo_lik_workspace(int B, int T, int N, int block_len);
+NFDPF_API int nfdpf_pseudo_lik_check(const int64_t *index, int B, int T, int N, int32_t *ok, void *stream);
+NFDPF_API int nfdpf_pseudo_lik_backward(const float *w, const float *lik, const float *prior, const int64_t *index,
+                                        int B, int T, int N, int block_len, const float *g_Q, float *g_w,
+                                        float *g_lik, float *g_prior, void *workspace, void *stream);
+
 /* The rational-quadratic spline of the neural spline flows NSF_AR / NSF_CL (nf/flows.py:343-458)
  * on M elements with K bins each: RQS (nf/utils.py:55-147) on [left, right] x [bottom, top],
  * or, with tails = 1, unconstrained_RQS (:23-53): inputs outside [left, right] pass through

@@ -24,7 +24,7 @@
 //   * the two softmins of an iteration share c_ij, so a slice is summed as
 //       2^(M_s - m_i) sum_j alpha_j 2^(-c_ij),   alpha_j = 2^(h_j - M_s)   (stored per j),
 //     ONE v_exp_f32 per pair for both softmins -- unless, for some lane of the wave,
-//     M_s - m_i > 60 (a heavy particle of the slice far from i: the near terms would underflow
+//     M_s - m_i > 96 (a heavy particle of the slice far from i: the near terms would underflow
 //     in alpha_j K_ij before the factor lifts them); the wave then takes the two-exp form;
 //   * the per-j operands form a per-row TABLE of planes written by the launch that produced
 //     them (workgroup s writes j in [256 s, 256 s + 256) and its slice maximum: no
@@ -52,7 +52,11 @@ constexpr int kOtThreads = 256;  // i (or j) per workgroup = the table slice len
 constexpr double kLog2ed = 1.4426950408889634;
 constexpr double kLn2d = 0.6931471805599453;
 constexpr float kLo = 0x1.0p-60f, kHi = 0x1.0p60f;  // outside: the lane recomputes exactly
-constexpr float kRisky = 60.f;                      // M_s - m_i above: two-exp form
+// M_s - m_i above: two-exp form.  A term matters when alpha_j K_ij 2^(M_s - m_i) >= 2^-24 (the
+// lane's sum is ~1), i.e. c_ij <= 24 + (M_s - m_i): up to 96 every such K_ij = 2^-c_ij and
+// alpha_j K_ij stay >= 2^-120, normal fp32 (2^-126); only terms below 2^-24 of the sum can
+// underflow.  (60 in r01: late, small-epsilon iterations took the two-exp form on most slices.)
+constexpr float kRisky = 96.f;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 sp2(float v) { return f2{v, v}; }

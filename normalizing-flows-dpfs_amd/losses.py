@@ -45,14 +45,50 @@ def _block_density(weights, lik, index, prior_terms, block_len):
     return Q / nb
 
 
-def compute_block_density_nf(particle_weight_list, noise_list, likelihood_list, index_list, jac_list, prior_list,
-                             block_len=10):
+def _block_density_nf_torch(particle_weight_list, likelihood_list, index_list, prior_list, block_len):
     B, T, N = particle_weight_list.shape
 
     def prior_terms(j, idx):
         p = prior_list[:, j, :]
         return p if idx is None else p.reshape(B * N)[idx]
     return _block_density(particle_weight_list, likelihood_list, index_list, prior_terms, block_len)
+
+
+class _PseudoLikNf(torch.autograd.Function):
+    """compute_block_density_nf on the HIP kernels (csrc/pseudo_lik.hip): the ancestry walks
+    and the row sums forward, the chain scatter backward; a non-monotone ancestor map (never
+    produced by the filter) is differentiated through the PyTorch restatement instead."""
+
+    @staticmethod
+    def forward(ctx, w, lik, prior, index, block_len):
+        from nfdpf import ops
+        ctx.save_for_backward(w, lik, prior, index)
+        ctx.block_len = block_len
+        return ops.pseudo_lik_forward(w, lik, prior, index, block_len).to(w.dtype)
+
+    @staticmethod
+    def backward(ctx, gQ):
+        from nfdpf import ops
+        w, lik, prior, index = ctx.saved_tensors
+        if ops.pseudo_lik_monotone(index):
+            gw, gl, gp = ops.pseudo_lik_backward(w, lik, prior, index, ctx.block_len, gQ.float())
+        else:
+            with torch.enable_grad():
+                leaves = [t.detach().requires_grad_(True) for t in (w, lik, prior)]
+                Q = _block_density_nf_torch(leaves[0], leaves[1], index, leaves[2], ctx.block_len)
+                gw, gl, gp = torch.autograd.grad(Q, leaves, gQ)
+        need = ctx.needs_input_grad
+        return (gw if need[0] else None, gl if need[1] else None, gp if need[2] else None, None, None)
+
+
+def compute_block_density_nf(particle_weight_list, noise_list, likelihood_list, index_list, jac_list, prior_list,
+                             block_len=10):
+    """losses.py:37-68 (the reference's positional accumulation of eta across blocks kept).  On
+    the HIP device: the pseudo_lik kernels; elsewhere the PyTorch restatement."""
+    w = particle_weight_list
+    if w.is_cuda and w.shape[1] // block_len > 0 and w.shape[2] <= 12288:
+        return _PseudoLikNf.apply(w, likelihood_list, prior_list, index_list, block_len)
+    return _block_density_nf_torch(w, likelihood_list, index_list, prior_list, block_len)
 
 
 def pseudolikelihood_loss_nf(particle_weight_list, noise_list, likelihood_list, index_list, jac_list, prior_list,

@@ -82,6 +82,12 @@ SIGNATURES = {
     "nfdpf_maf_stack_backward_workspace": (c_int64, [c_int, c_int, c_int, c_int64]),
     "nfdpf_maf_stack_backward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_pseudo_lik_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                         c_void_p, c_void_p]),
+    "nfdpf_pseudo_lik_workspace": (c_int64, [c_int, c_int, c_int, c_int]),
+    "nfdpf_pseudo_lik_check": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_pseudo_lik_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_rqs": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_float, c_float,
                           c_float, c_float, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "nfdpf_split_fault": (c_int, [c_int]),

@@ -93,6 +93,43 @@ def maf_stack_backward(blob, n_flows, dim, hidden, x, inverse, g_out, g_logdet):
     return gx, gb
 
 
+def pseudo_lik_forward(w, lik, prior, index, block_len):
+    """compute_block_density_nf (losses.py:37-68) -> Q [B] fp64 (nfdpf_pseudo_lik_forward)."""
+    require_device(w, "pseudo_lik_forward")
+    B, T, N = w.shape
+    w, lik, prior = _c(w), _c(lik), _c(prior)
+    index = index.to(torch.int64).contiguous()
+    Q = torch.empty(B, device=w.device, dtype=torch.float64)
+    check(lib().nfdpf_pseudo_lik_forward(ptr(w), ptr(lik), ptr(prior), ptr(index), B, T, N, int(block_len), ptr(Q),
+                                         stream_ptr(w.device)), "nfdpf_pseudo_lik_forward")
+    return Q
+
+
+def pseudo_lik_monotone(index) -> bool:
+    """True when every step's ancestor map is non-decreasing over the flattened batch (one
+    device flag read: a host sync)."""
+    B, T, N = index.shape
+    ok = torch.ones(1, device=index.device, dtype=torch.int32)
+    check(lib().nfdpf_pseudo_lik_check(ptr(index), B, T, N, ptr(ok), stream_ptr(index.device)),
+          "nfdpf_pseudo_lik_check")
+    return bool(ok.item())
+
+
+def pseudo_lik_backward(w, lik, prior, index, block_len, g_Q):
+    """-> (g_w, g_lik, g_prior) [B, T, N] (nfdpf_pseudo_lik_backward)."""
+    require_device(w, "pseudo_lik_backward")
+    B, T, N = w.shape
+    w, lik, prior, g_Q = _c(w), _c(lik), _c(prior), _c(g_Q)
+    index = index.to(torch.int64).contiguous()
+    gw, gl, gp = torch.empty_like(w), torch.empty_like(lik), torch.empty_like(prior)
+    nbytes = int(lib().nfdpf_pseudo_lik_workspace(B, T, N, int(block_len)))
+    ws = torch.empty(max(1, nbytes // 4), device=w.device, dtype=f32)
+    check(lib().nfdpf_pseudo_lik_backward(ptr(w), ptr(lik), ptr(prior), ptr(index), B, T, N, int(block_len),
+                                          ptr(g_Q), ptr(gw), ptr(gl), ptr(gp), ptr(ws), stream_ptr(w.device)),
+          "nfdpf_pseudo_lik_backward")
+    return gw, gl, gp
+
+
 @functools.lru_cache(maxsize=64)
 def _lin_cpu(N: int) -> torch.Tensor:
     # the reference's marker base, torch.linspace on CPU (resamplers.py:42); a per-N constant
