@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 ARGS=${BENCH_ARGS:---steps 20 --warmup 3 --no-cpu-baseline}
 for round in 1 2; do
   for v in ${VARIANTS:-BASE}; do
-    NFDPF_LIB=$PWD/exp/lib_$v.so timeout -k 10 120 python bench.py $ARGS > gpurun_out/exp_${v}_$round.log 2>&1 || exit 1
+    NFDPF_LIB_PARTIAL=1 NFDPF_LIB=$PWD/exp/lib_$v.so timeout -k 10 120 python bench.py $ARGS > gpurun_out/exp_${v}_$round.log 2>&1 || exit 1
     echo $v $(python3 -c "
 import json,sys
 d=json.loads(open('gpurun_out/exp_${v}_$round.log').read().strip().splitlines()[-1])
