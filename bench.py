@@ -248,6 +248,10 @@ def main():
                          "-1 auto (on when sharded), 0 off (per-step exchange), 1 on (also at one GPU)")
     ap.add_argument("--kernel", default="tiled", choices=["tiled", "fused"],
                     help="tiled: multi-CU pipeline per step; fused: one workgroup per batch row")
+    ap.add_argument("--enc-from-state", action="store_true",
+                    help="frame encodings = the particle encoder applied to the true positions (what a "
+                         "trained frame encoder approximates): the likelihood peaks near the truth, the "
+                         "weights degenerate and the ESS gate fires (cos / CRNVP measurements, 32-wide)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -276,6 +280,9 @@ def main():
     start, state, vel_in, enc = synthetic_disk(B * world, T, 2, a.hiddensize)
     sl = slice(rank * B, (rank + 1) * B)
     start, state, vel_in, enc = (t[sl].to(dev) for t in (start, state, vel_in, enc))
+    if args.enc_from_state:
+        with torch.no_grad():
+            enc = dpf.particle_encoder(state[:, :, :2].float()).contiguous()
     shard = ShardInfo.from_env(B)
     fcfg = dpf.filter_config()
     fcfg.kernel = args.kernel
@@ -419,7 +426,8 @@ def main():
                        + f", N={N}, batch={B} per GPU, seq_len={T}, state_dim=4 (2-D particles), "
                          f"{'forced' if args.force_resample else 'ESS-gated'} resampling, device RNG, "
                          f"{'hipGraph replay of the pass' if graph is not None else 'Python launches'}"
-                         + (", speculative ESS gate verified once per pass" if spec else ""),
+                         + (", speculative ESS gate verified once per pass" if spec else "")
+                         + (", frame encodings = particle encoder(true positions)" if args.enc_from_state else ""),
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
                        "parallelism": f"batch-sharded x{world}"},
             "rmse": rmse,

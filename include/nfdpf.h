@@ -223,6 +223,20 @@ NFDPF_API int nfdpf_cos_measurement_backward(const float *pe_params, const float
                                              const float *g_lik, int B, int N, int E, float *g_enc,
                                              float *g_x, float *g_params, void *workspace, void *stream);
 
+/* Backward of the NN measurement's likelihood head (kind NFDPF_MEAS_NN; training, SURVEY.md
+ * §8(f1)): lik = log sigmoid(likelihood_est([enc, PE(x)])) (model/models.py:221-235, the MLP of
+ * :119-128).  Gradients stop at the particle encodings; the caller chains g_e through
+ * nfdpf_particle_encoder mode 1.
+ *   meas_params: the likelihood_est blob of nfdpf_measurement (NN); enc [B, E] frame encodings;
+ *   e_particles [B*N, E] = PE(x) (nfdpf_particle_encoder mode 0); g_lik [B, N]
+ *   g_e [B*N, E], g_enc [B, E]; g_params [8385]: likelihood_est's gradient in the plain
+ *   nn.Linear layout W1 b1 W2 b2 W3 b3
+ *   workspace: nfdpf_nn_measurement_backward_workspace(B, N) bytes (fixed-order partials) */
+NFDPF_API int64_t nfdpf_nn_measurement_backward_workspace(int B, int N);
+NFDPF_API int nfdpf_nn_measurement_backward(const float *meas_params, const float *enc, const float *e_particles,
+                                            const float *g_lik, int B, int N, int E, float *g_e, float *g_enc,
+                                            float *g_params, void *workspace, void *stream);
+
 /* Conditional-GLOW measurement (model/models.py:280-303; nf/cglow/CGlowModel.py with the
  * default flow_depth K = 1, L = 1, x_size = y_size = (3,8,8)): particle (b,i) at
  * x + b*x_rs + 2i, frame encoding of row b at enc + b*enc_rs (192 floats) -> the RAW

@@ -151,11 +151,12 @@ class _MeasRunner:
         return (_ops.measurement(self.kind, pe, meas, nfl, enc, x, pstd),)
 
     def hip_backward(self, enc, x, gouts):
-        """Cosine measurement: d/d(enc, x, encoder parameters) by nfdpf_cos_measurement_backward
-        (csrc/measure_bwd.hip); None for the other models (autograd then differentiates
-        ``torch``)."""
+        """d/d(enc, x, encoder and model parameters) on the HIP kernels: cosine by
+        nfdpf_cos_measurement_backward (csrc/measure_bwd.hip), gaussian / CRNVP / NN through the
+        particle encoder's kernels and the model's own backward; None where a model falls outside
+        the kernels (autograd then differentiates ``torch``)."""
         m = self.model
-        if self.kind not in ("cos", "CRNVP", "gaussian") or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 \
+        if self.kind not in ("cos", "CRNVP", "gaussian", "NN") or enc.dim() != 2 or enc.shape[-1] != 32 or x.dim() != 3 \
                 or x.shape[-1] != 2:
             return None
         pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
@@ -171,6 +172,8 @@ class _MeasRunner:
                 return None
             g_enc, gx, gp = out
             extra = []
+        elif self.kind == "NN":
+            g_enc, gx, gp, extra = self._nn_backward(pe, enc.float(), x.float(), g)
         else:
             out = self._crnvp_backward(pe, enc.float(), x.float(), g)
             if out is None:
@@ -203,6 +206,23 @@ class _MeasRunner:
         r = g_u[..., None] * d / var        # = dL/de (lik rises as e approaches o - mu)
         gx, gp = _ops.particle_encoder_backward(pe, x, r.reshape(B * N, 32).contiguous())
         return -r.sum(1), gx, gp
+
+    def _nn_backward(self, pe, enc, x, g):
+        """measurement_model_NN (model/models.py:221-235): the head's backward
+        (nfdpf_nn_measurement_backward, csrc/nn_bwd.hip) gives d/d the particle encodings, the
+        frame encoding and likelihood_est's parameters; the encoder backward (HIP) takes g_e on
+        to x and the encoder's parameters."""
+        m = self.model
+        B, N, _ = x.shape
+        mb = blob(m, "meas", m.likelihood_estimator, lambda: paired_mlp_tensors(m.likelihood_estimator), x.device)
+        es = _ops.particle_encoder_forward(pe, x)
+        g_es, g_enc, g_mp = _ops.nn_measurement_backward(mb, enc, es, g)
+        gx, gp = _ops.particle_encoder_backward(pe, x, g_es)
+        extra, off = [], 0
+        for p in m.likelihood_estimator.parameters():
+            extra.append(g_mp[off:off + p.numel()].view_as(p).to(p.dtype) if p.requires_grad else None)
+            off += p.numel()
+        return g_enc, gx, gp, extra
 
     def _crnvp_backward(self, pe, enc, x, g):
         """measurement_model_cnf (model/models.py:256-278): lik = u - max_n u with u = log N(z) +

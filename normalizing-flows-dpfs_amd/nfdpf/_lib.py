@@ -67,6 +67,9 @@ SIGNATURES = {
     "nfdpf_cos_measurement_backward_workspace": (c_int64, [c_int, c_int]),
     "nfdpf_cos_measurement_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                                c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_nn_measurement_backward_workspace": (c_int64, [c_int, c_int]),
+    "nfdpf_nn_measurement_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                              c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_particle_encoder": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p]),
     "nfdpf_maf_stack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,

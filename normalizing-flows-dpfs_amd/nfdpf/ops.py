@@ -224,6 +224,23 @@ def particle_encoder_backward(pe_blob, x, g_e):
     return gx, gp
 
 
+def nn_measurement_backward(meas_blob, enc, es, g_lik):
+    """Backward of the NN likelihood head -> (g_e [B*N, 32], g_enc [B, 32], g_params [8385] in
+    nn.Linear order) for encodings es = PE(x) [B*N, 32] (nfdpf_nn_measurement_backward)."""
+    require_device(es, "nn_measurement_backward")
+    B, N = g_lik.shape
+    enc, es, g_lik = _c(enc), _c(es), _c(g_lik)
+    g_e = torch.empty_like(es)
+    g_enc = torch.empty_like(enc)
+    gp = torch.empty(8385, device=es.device, dtype=f32)
+    nb = int(lib().nfdpf_nn_measurement_backward_workspace(B, N))
+    ws = torch.empty(max(1, nb // 4), device=es.device, dtype=f32)
+    check(lib().nfdpf_nn_measurement_backward(ptr(meas_blob), ptr(enc), ptr(es), ptr(g_lik), B, N, enc.shape[-1],
+                                              ptr(g_e), ptr(g_enc), ptr(gp), ptr(ws), stream_ptr(es.device)),
+          "nfdpf_nn_measurement_backward")
+    return g_e, g_enc, gp
+
+
 _ws = {}
 
 

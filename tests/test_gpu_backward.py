@@ -381,6 +381,42 @@ def test_cos_measurement_backward_vs_autograd(B, N, scale, monkeypatch):
         _soft_check(p.grad, pr.grad, f"dL/d{name}")
 
 
+@pytest.mark.parametrize("B,N,scale", [(3, 500, 1.0), (2, 77, 10.0), (1, 1, 1.0)])
+def test_nn_measurement_backward_vs_autograd(B, N, scale, monkeypatch):
+    """measurement_model_NN under autograd (HIP: nfdpf_nn_measurement_backward + the encoder
+    backward) == float64 autograd of model/models.py:221-235 with likelihood_est of :119-128
+    (d/d encodings, particles and every parameter of both nets)."""
+    import torch.nn as nn
+    from model.models import measurement_model_NN
+    from nfdpf import ops
+    calls = []
+    real = ops.nn_measurement_backward
+    monkeypatch.setattr(ops, "nn_measurement_backward", lambda *a, **k: calls.append(1) or real(*a, **k))
+    torch.manual_seed(B * 31 + N)
+    pe = nn.Sequential(nn.Linear(2, 16), nn.ReLU(), nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 32))
+    le = nn.Sequential(nn.Linear(64, 64), nn.ReLU(), nn.Linear(64, 64), nn.ReLU(), nn.Linear(64, 1), nn.Sigmoid())
+    ref_pe, ref_le = copy.deepcopy(pe).double(), copy.deepcopy(le).double()
+    m = measurement_model_NN(pe.to(DEV), le.to(DEV))
+    g = torch.Generator().manual_seed(N + 1)
+    enc = torch.randn(B, 32, generator=g)
+    x = torch.randn(B, N, 2, generator=g) * scale
+    gl = torch.randn(B, N, generator=g)
+    encd, xd = enc.to(DEV).requires_grad_(True), x.to(DEV).requires_grad_(True)
+    lik = m(encd, xd)
+    (lik * gl.to(DEV)).sum().backward()
+    assert len(calls) == 1, "the backward did not run through nfdpf_nn_measurement_backward"
+    er, xr = enc.double().requires_grad_(True), x.double().requires_grad_(True)
+    h = torch.cat([er[:, None, :].repeat(1, N, 1), ref_pe(xr)], dim=-1)
+    lr = ref_le(h)[..., 0].log()
+    (lr * gl.double()).sum().backward()
+    _soft_check(lik.detach(), lr.detach(), "lik")
+    _soft_check(xd.grad, xr.grad, "dL/dx")
+    _soft_check(encd.grad, er.grad, "dL/denc")
+    refs = list(ref_pe.parameters()) + list(ref_le.parameters())
+    for (name, p), pr in zip(m.named_parameters(), refs):
+        _soft_check(p.grad, pr.grad, f"dL/d{name}")
+
+
 @pytest.mark.parametrize("B,N,std", [(3, 500, 0.3), (2, 70, 0.01)])
 def test_crnvp_measurement_backward_vs_autograd(B, N, std, monkeypatch):
     """measurement_model_cnf under autograd (HIP: encoder forward/backward + stack backward)

@@ -43,14 +43,24 @@ def test_pseudo_lik_forward_backward(B, T, N, L, edge):
         return
     ref = [x.double().requires_grad_(True) for x in (w, lik, prior)]
     Qr = _block_density_nf_torch(ref[0], ref[1], idx, ref[2], L)
-    gQ = torch.randn(B, dtype=torch.float64)
+    gQ = torch.randn(B, dtype=torch.float64, generator=torch.Generator().manual_seed(N))
     Qr.backward(gQ)
     dev = [x.to(DEV).requires_grad_(True) for x in (w, lik, prior)]
     Q = compute_block_density_nf(dev[0], None, dev[1], idx.to(DEV), None, dev[2], L)
     torch.testing.assert_close(Q.double().cpu(), Qr.detach(), rtol=2e-6, atol=1e-5)
     Q.backward(gQ.float().to(DEV))
     for name, a, r in zip(("w", "lik", "prior"), dev, ref):
-        torch.testing.assert_close(a.grad.double().cpu(), r.grad, rtol=1e-5, atol=1e-6, msg=name)
+        _close_scaled(a.grad, r.grad, name)
+
+
+def _close_scaled(ours, ref, name):
+    """Within 1e-5 relative + 2e-6 of the tensor's largest |gradient|: eta is an fp32 running sum
+    over up to T steps of prior + likelihood (losses.py:65), so where it cancels towards zero its
+    rounding (~1e-6 of the summands) is all that is left of dw = gQ eta."""
+    o = ours.double().cpu()
+    d = (o - ref).abs()
+    tol = 1e-5 * ref.abs() + 2e-6 * float(ref.abs().max())
+    assert bool((d <= tol).all()), f"{name}: max |d| {float(d.max()):.3g}, worst excess {float((d - tol).max()):.3g}"
 
 
 def test_pseudo_lik_non_monotone_falls_back():
@@ -61,5 +71,5 @@ def test_pseudo_lik_non_monotone_falls_back():
     _block_density_nf_torch(ref[0], ref[1], idx, ref[2], 10).sum().backward()
     dev = [x.to(DEV).requires_grad_(True) for x in (w, lik, prior)]
     compute_block_density_nf(dev[0], None, dev[1], idx.to(DEV), None, dev[2], 10).sum().backward()
-    for a, r in zip(dev, ref):
-        torch.testing.assert_close(a.grad.double().cpu(), r.grad, rtol=1e-5, atol=1e-6)
+    for name, a, r in zip(("w", "lik", "prior"), dev, ref):
+        _close_scaled(a.grad, r.grad, name)
