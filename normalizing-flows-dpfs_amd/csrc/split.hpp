@@ -190,8 +190,8 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // group) through all three layers, so the pair never hands off (no layer-3 operand exchange,
 // no partial-sum exchange).  Layer 1 as encode_dot_pair_mfma; layers 2 / 3 per block as two
 // 16-column output tiles (bias-initialised exact k-ordered MFMA chains); the 32 outputs of a
-// particle come back through Hw: lane l < 32 accumulates |e|^2 and lane l + 32 <e, v> of
-// particle 32 r + l in fp64 (four interleaved chains); both lanes return both sums.
+// particle come back through Hw to lane l = particle - 32 r, which accumulates |e|^2 and <e, v>
+// in fp64 in output order (particle_encode + encode_dot's arithmetic).  Lanes >= 32 return 0.
 struct EncFrag2 {
   float w10[4], w11[4], b1[4];  // layer 1 for k = 4 s + (lane >> 4)
   float b2[2][4], b3[2][8];     // B fragments of output tiles n = 0, 1 (columns 16 n + (lane & 15))
@@ -275,19 +275,19 @@ __device__ __forceinline__ void encode_dot_mfma_half(const EncFrag2 &f, int role
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   QTRACE(9)
-  // lanes 0-31: |e|^2 of particle l, lanes 32-63: <e, v> of particle l - 32; each as four
-  // interleaved fp64 chains over the outputs (c = 4 q + r), combined (r0 + r1) + (r2 + r3)
-  const int pl = l & 31;
-  double acc4[4] = {0.0, 0.0, 0.0, 0.0};
+  // lane l < 32: |e|^2 and <e, v> of particle 32 r + l, in output order.  (Splitting the two
+  // sums over the lane halves in interleaved chains measured 3.8 us SLOWER per launch --
+  // profiles/r02_experiments.md, QUAD8.)
+  ss = 0.0;
+  dot = 0.0;
+  if (l < 32) {
 #pragma unroll
-  for (int c = 0; c < 32; ++c) {
-    const double a = hw[pl * kHPitch + c];
-    acc4[c & 3] = fma(a, l < 32 ? a : (double)v[c], acc4[c & 3]);
+    for (int c = 0; c < 32; ++c) {
+      const double a = hw[l * kHPitch + c];
+      ss = fma(a, a, ss);
+      dot = fma(a, (double)v[c], dot);
+    }
   }
-  const double part = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
-  const double other = __shfl_xor(part, 32);
-  ss = l < 32 ? part : other;
-  dot = l < 32 ? other : part;
 }
 
 // One exchange of two doubles between the waves of a pair through a buffer used once per
