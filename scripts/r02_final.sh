@@ -34,6 +34,9 @@ case "$PART" in
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof_$tag -o run -- \
       python3 bench.py $A > gpurun_out/fprof_$tag.log 2>&1
     rc=$?; echo "prof $tag rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    # keep only the summaries (the raw traces exceed gpurun's 64 MiB copy-back)
+    find gpurun_out/fprof_$tag -name "*kernel_stats.csv" -exec cp {} gpurun_out/kstats_$tag.csv \;
+    rm -rf gpurun_out/fprof_$tag
     for pass in "sq:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SMEM" \
                 "mfma:SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
                 "fetch:FETCH_SIZE" "write:WRITE_SIZE"; do
@@ -42,6 +45,7 @@ case "$PART" in
         python3 bench.py $A --graph 0 > gpurun_out/fpmc_${tag}_$name.log 2>&1
       rc=$?; echo "pmc $tag $name rc=$rc"; [ $rc -eq 0 ] || exit $rc
     done
+    python3 scripts/pmc_summary.py gpurun_out/fpmc_${tag}_* > gpurun_out/pmc_$tag.csv && rm -rf gpurun_out/fpmc_${tag}_*/
   done
   ;;
 esac
