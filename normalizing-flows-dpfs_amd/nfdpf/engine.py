@@ -139,6 +139,8 @@ class FilterEngine:
         self.cfg = cfg
         self.m = models
         self.step_events = None  # list -> nfdpf.prof.EventPair around the dominant launch of step T//2 of every pass
+        self._spec_backoff = 0  # auto speculative gate: passes to run per-step after the next miss / 2
+        self._spec_skip = 0     # per-step passes left before speculating again
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -208,8 +210,14 @@ class FilterEngine:
                                           c.seed, shard.row_base, dev)
         p0, ie0 = ops.normalize_log_probs(logw0)
         tiled = c.kernel == "tiled"
+        auto = speculate is None and c.speculate_gate is None
         if speculate is None:
             speculate = c.speculate_gate if c.speculate_gate is not None else shard.world > 1
+        if auto and speculate and self._spec_skip > 0:
+            # auto mode after a fired gate: the per-step exchange for the next passes (a miss
+            # costs a whole second pass -- profiles/r02_dist_*.json), retried with backoff
+            self._spec_skip -= 1
+            speculate = False
         spec = bool(speculate and tiled and c.resampler == "soft" and not host_mode and teacher is None
                     and not c.force_resample and not external)
 
@@ -243,7 +251,7 @@ class FilterEngine:
             ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
             ess0 = ie0
             gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
-        ess_all = ess0 if spec else self._gather(ess0, shard)
+        ess_all = ess0 if spec else self._gather(ess0, shard, gather_buf)
         gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
         spec_gate = torch.zeros(1, device=dev, dtype=torch.int32) if spec else None
         # velocity used by each step's motion: start velocity, then vel_input[:, t-1] (DPFs.py:158,173)
@@ -407,8 +415,12 @@ class FilterEngine:
             if not finish:
                 return res
             if self.finish_pending():
+                self._spec_backoff = 0
                 return res
             # a gate fired: the pass again, with the per-step exchange
+            if auto:
+                self._spec_backoff = min(2 * self._spec_backoff or 1, 64)
+                self._spec_skip = self._spec_backoff
             return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, speculate=False)
         if shard.world > 1:
             dist.all_reduce(tot, group=shard.group)
