@@ -207,39 +207,51 @@ __device__ __noinline__ void phase_y(const float *__restrict__ enc, int64_t enc_
 __device__ __noinline__ void phase_resize(const float *glow_, int p, int q) {
   const float *glow = sgpr_ptr(glow_);
   const int qi = q >> 2, qj = q & 3;
-  float xp[3][4][4];  // rows 2qi-1 .. 2qi+2, cols 2qj-1 .. 2qj+2 of x, zero outside
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        const int rr = 2 * qi - 1 + r, ss = 2 * qj - 1 + s2;
-        xp[c][r][s2] = (rr >= 0 && rr < 8 && ss >= 0 && ss < 8) ? S.xs[p][c * 64 + rr * 8 + ss] : 0.f;
-      }
+  // The 4x4 window (rows 2qi-1 .. 2qi+2, cols 2qj-1 .. 2qj+2, zero outside) is read from LDS per
+  // tap, and the tap loop is OUTERMOST: each tap's 16 weights (one s_load_dwordx16) feed the
+  // four 8x8 outputs of this position's 2x2 block -- 32 independent v_pk_fma per tap.  (r01: a
+  // 48-value register window indexed by the partly unrolled tap loop lived in scratch, and the
+  // weights were loaded once per block.)  Out-of-window reads stay inside the LDS struct and
+  // are discarded by the select.
+  const float *xrow = &S.xs[p][(2 * qi - 1) * 8 + 2 * qj - 1];
+  const bool r0 = qi > 0, r3 = qi < 3, c0 = qj > 0, c3 = qj < 3;
   cf2 *F2 = (cf2 *)wptr(glow + kOffF);
+  f2 hb[4][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const f2 bias = F2[Aff::r0b / 2 + m];
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) hb[ab][m] = bias;
+  }
+#pragma unroll 1
+  for (int t = 0; t < 27; ++t) {  // taps (dr, ds, c) of the 3x3x3 window
+    F2 = (cf2 *)wptr(glow + kOffF);
+    const int dr = t / 9, ds = (t / 3) % 3, c = t % 3;
+    float v[4];
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) {
+      const int r = (ab >> 1) + dr, s2 = (ab & 1) + ds;
+      const bool in = (r > 0 || r0) && (r < 3 || r3) && (s2 > 0 || c0) && (s2 < 3 || c3);
+      const float x = xrow[c * 64 + r * 8 + s2];
+      v[ab] = in ? x : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const f2 wgt = F2[(Aff::r0w + t * 16) / 2 + m];
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) hb[ab][m] = pfma(wgt, splat(v[ab]), hb[ab][m]);
+    }
+  }
   f2 h62[kCh / 2];
+  F2 = (cf2 *)wptr(glow + kOffF);
 #pragma unroll
   for (int m = 0; m < kCh / 2; ++m) h62[m] = F2[Aff::r2b / 2 + m];
 #pragma unroll
   for (int ab = 0; ab < 4; ++ab) {
-    const int a = ab >> 1, b2 = ab & 1;
-    f2 hb[8];
-    F2 = (cf2 *)wptr(glow + kOffF);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) hb[m] = F2[Aff::r0b / 2 + m];
-#pragma unroll 3
-    for (int t = 0; t < 27; ++t) {  // taps (dr, ds, c) of the 3x3x3 window
-      F2 = (cf2 *)wptr(glow + kOffF);
-      const int dr = t / 9, ds = (t / 3) % 3, c = t % 3;
-      const float v = xp[c][a + dr][b2 + ds];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) hb[m] = pfma(F2[(Aff::r0w + t * 16) / 2 + m], splat(v), hb[m]);
-    }
     F2 = (cf2 *)wptr(glow + kOffF);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      const f2 hv = relu2(hb[m]);
+      const f2 hv = relu2(hb[ab][m]);
 #pragma unroll
       for (int n = 0; n < kCh / 2; ++n) {
         h62[n] = pfma(F2[(Aff::r2w + (ab * 16 + 2 * m) * kCh) / 2 + n], splat(hv.x), h62[n]);

@@ -190,11 +190,21 @@ struct TBlock {  // 8 consecutive j of NP planes
 };
 
 // load block j of the planes pl[0..NP) of a row table
+// The words are wave-uniform.  -DNFDPF_OT_SLOAD reads them through the constant address space
+// (scalar loads into SGPRs, one block at a time) instead of the pipelined vector loads that
+// return the same 16 B to all 64 lanes: measured SLOWER (C4 iteration 124 vs 118 us, C3 22 vs
+// 17 us; the compiler keeps half of the words as vector loads and the scalar waits are not
+// overlapped -- profiles/r02_experiments.md).
+typedef const float4 __attribute__((address_space(4))) cfloat4;
 template <int NP>
 __device__ __forceinline__ void tload(TBlock<NP> &B, const float *tab, int64_t Np, int j, const int (&pl)[NP]) {
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
+#if !defined(NFDPF_OT_SLOAD) || !defined(__HIP_DEVICE_COMPILE__)
     const float4 *X = reinterpret_cast<const float4 *>(tab + pl[p] * Np + j);
+#else
+    cfloat4 *X = (cfloat4 *)(tab + pl[p] * Np + j);
+#endif
     B.v[p][0] = X[0];
     B.v[p][1] = X[1];
   }
@@ -215,6 +225,16 @@ __device__ __forceinline__ f2 tpair(const TBlock<NP> &B, int p, int q) {
 template <int NP, class Body>
 __device__ __forceinline__ void pipelined(const float *tab, int64_t Np, int j0, int j1, const int (&pl)[NP],
                                           const Body &body) {
+#ifdef NFDPF_OT_SLOAD
+  // scalar loads: one block at a time (a scalar wait is lgkmcnt(0), so a prefetched block would
+  // be waited for with the current one); the other waves of the SIMD cover the latency
+  for (int j = j0; j < j1; j += 8) {
+    TBlock<NP> A;
+    tload(A, tab, Np, j, pl);
+    body(A);
+  }
+  return;
+#endif
   TBlock<NP> A, Bk;
   tload(A, tab, Np, j0, pl);
   for (int j = j0; j < j1; j += 16) {
@@ -340,7 +360,7 @@ __device__ __forceinline__ void wg_table_sums(const float *tab, const double *ms
 #pragma unroll
     for (int v = 0; v < NV; ++v) accv[r][v] = sp2(0.f);
   }
-  for (int s = threadIdx.x >> 6; s < splits; s += kWaves) {
+  for (int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); s < splits; s += kWaves) {
     f2 o[kR][NH];
 #pragma unroll
     for (int r = 0; r < kR; ++r)
@@ -383,7 +403,7 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
     Sk[r][0] = Sk[r][1] = 0.f;
     hacc[r][0] = hacc[r][1] = sp2(0.f);
   }
-  for (int s = threadIdx.x >> 6; s < splits; s += kWaves) {
+  for (int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); s < splits; s += kWaves) {
     const double Ma = msh[2 * s], Mb = msh[2 * s + 1];
     float oa[kR], ob[kR];
     bool risky = false;
