@@ -267,10 +267,14 @@ __device__ __noinline__ void phase_resize(const float *glow_, int p, int q) {
 }
 
 // 3x3 'same' conv on the 4x4 grid from the neighbours' channel vectors in S.ex; weights
-// [tap][c][o] with o fastest; acc holds NP output pairs
+// [tap][c][o] with o fastest; acc holds NP output pairs.  Per tap the neighbour's CIN channels
+// are read together and the tap's weights in chunks of 4 channels (one scalar-load batch per
+// chunk), so a tap is 3-12 x NP independent v_pk_fma instead of NP per loop trip.  Same
+// (tap, channel) order of the fma chain as the per-(tap, channel) loop it replaces.
 template <int CIN, int NP>
 __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int q, f2 (&acc)[NP]) {
   const int qi = q >> 2, qj = q & 3;
+#ifdef NFDPF_CG_CONV_TC
 #pragma unroll 2
   for (int tc = 0; tc < 9 * CIN; ++tc) {  // (tap, input channel), tap-major
     const int t9 = tc / CIN, c = tc - CIN * (tc / CIN);
@@ -282,6 +286,28 @@ __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int 
 #pragma unroll
     for (int n = 0; n < NP; ++n) acc[n] = pfma(F2[(wofs + tc * (2 * NP)) / 2 + n], splat(v), acc[n]);
   }
+#else
+  constexpr int kChunk = CIN % 4 == 0 ? 4 : (CIN % 3 == 0 ? 3 : 2);
+#pragma unroll 1
+  for (int t9 = 0; t9 < 9; ++t9) {
+    const int dr = t9 / 3, ds = t9 - 3 * (t9 / 3);
+    const int rr = qi + dr - 1, ss = qj + ds - 1;
+    const bool in = rr >= 0 && rr < 4 && ss >= 0 && ss < 4;
+    const float *src = S.ex[p][in ? rr * 4 + ss : q];  // a valid row either way
+    float v[CIN];
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) v[c] = in ? src[c] : 0.f;
+#pragma unroll
+    for (int c0 = 0; c0 < CIN; c0 += kChunk) {
+      cf2 *F2 = (cf2 *)wptr(glow + kOffF);
+#pragma unroll
+      for (int c = c0; c < c0 + kChunk; ++c)
+#pragma unroll
+        for (int n = 0; n < NP; ++n)
+          acc[n] = pfma(F2[(wofs + (t9 * CIN + c) * (2 * NP)) / 2 + n], splat(v[c]), acc[n]);
+    }
+  }
+#endif
 }
 
 // resize conv3, the coupling net f, the affine update of z2 and the Gaussian log-prob;
