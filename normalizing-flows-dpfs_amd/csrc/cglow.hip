@@ -67,7 +67,7 @@ struct Lds {
   float pxy[kTileP][2];
   float xs[kTileP][kE + 1];            // particle encoding, [c][8][8]
   float an[kTileP][2 * kC + 1];        // actnorm (logs | bias)
-  float wm[kTileP][kC * kC + 1];       // 1x1 conv weight, row-major [out][in]
+  float wm[kTileP][kC * kC + 4];       // 1x1 conv weight, row-major [out][in] (rows 16-B aligned)
   float ld[kTileP];                    // per-particle log-det of actnorm + 1x1 conv
   int row[kTileP];
   union {
@@ -92,6 +92,15 @@ struct Lds {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 __shared__ Lds S;  // one instance per workgroup, shared by the phase functions below
+
+#ifdef NFDPF_EXP_CGTRACE  // experiment: per-phase timestamps of one tile per workgroup
+__device__ uint64_t g_cgtrace[1024][16];
+#define CGTRACE(k)                                                                  \
+  if (trace_it && threadIdx.x == 0 && blockIdx.x < 1024)                           \
+    g_cgtrace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define CGTRACE(k)
+#endif
 
 // One 16x16 output tile of C = A B over K (zero-padded to 4*KSTEPS): lane l feeds A[l&15][k]
 // and B[k][l&15] for k = 4s + (l>>4), and gets C rows 4(l>>4)+i, column l&15.
@@ -122,14 +131,16 @@ __device__ __forceinline__ const float *sgpr_ptr(const float *p) {
 }
 
 // log|det W| of the 12x12 matrix held one row per lane (lanes g*16 + r, r < 12), partial
-// pivoting by |value|; every lane of the group returns the same value.
-__device__ float logabsdet12(float (&a)[kC], int q) {
+// pivoting by |value|; every lane of the group returns the same value.  The pivot search is a
+// 16-lane (|v|, lane) max on DPP (ties to the lowest lane); the pivot row goes through LDS
+// (the pivot lane writes it to prow_lds, the group reads it back: same wave, in order).
+#ifdef NFDPF_CG_SHFL_LU
+__device__ float logabsdet12(float (&a)[kC], int q, float *) {
   const int base = (threadIdx.x & 63) & ~15;  // first lane of this particle's group
   float ld = 0.f;
   bool done = q >= kC;                        // lanes 12..15 hold no row
 #pragma unroll
   for (int k = 0; k < kC; ++k) {
-    // pivot: the undone row with the largest |a[r][k]|, ties to the lowest lane
     float v = done ? -1.f : fabsf(a[k]);
     int who = q;
 #pragma unroll
@@ -141,7 +152,6 @@ __device__ float logabsdet12(float (&a)[kC], int q) {
         who = w2;
       }
     }
-    // pivot row to everyone
     float prow[kC];
 #pragma unroll
     for (int j = 0; j < kC; ++j) prow[j] = __shfl(a[j], base + who, 64);
@@ -157,6 +167,49 @@ __device__ float logabsdet12(float (&a)[kC], int q) {
   }
   return ld;
 }
+#else
+template <int CTRL>
+__device__ __forceinline__ void argmax_step(float &v, int &who) {
+  const float v2 = dpp_f<CTRL>(v);
+  const int w2 = __builtin_amdgcn_update_dpp(who, who, CTRL, 0xf, 0xf, false);
+  if (v2 > v || (v2 == v && w2 < who)) {
+    v = v2;
+    who = w2;
+  }
+}
+__device__ __forceinline__ float logabsdet12(float (&a)[kC], int q, float *prow_lds) {
+  float ld = 0.f;
+  bool done = q >= kC;  // lanes 12..15 hold no row
+#pragma unroll
+  for (int k = 0; k < kC; ++k) {
+    float v = done ? -1.f : fabsf(a[k]);
+    int who = q;
+    argmax_step<kDppXor1>(v, who);
+    argmax_step<kDppXor2>(v, who);
+    argmax_step<kDppHalfMirror>(v, who);
+    argmax_step<kDppMirror>(v, who);
+    if (q == who)
+#pragma unroll
+      for (int j = k; j < kC; ++j) prow_lds[j] = a[j];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float prow[kC];
+#pragma unroll
+    for (int j = k; j < kC; ++j) prow[j] = prow_lds[j];
+    const float piv = prow[k];
+    ld += logf(fabsf(piv));
+    if (q == who) done = true;
+    if (!done) {
+      const float f = a[k] / piv;
+#pragma unroll
+      for (int j = k + 1; j < kC; ++j) a[j] = fmaf(-f, prow[j], a[j]);
+    }
+    __builtin_amdgcn_wave_barrier();  // every lane has read the row before the next is written
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  return ld;
+}
+#endif
 
 }  // namespace cg
 
@@ -170,15 +223,18 @@ using namespace cg;
     __builtin_amdgcn_sched_barrier(0);    \
   } while (0)
 
-// squeeze(y) at position q, cond-actnorm, cond-1x1 conv (-> S.yv), their log-dets (-> S.ld)
-__device__ __noinline__ void phase_y(const float *__restrict__ enc, int64_t enc_rs, int p, int q) {
+// squeeze(y) at position q (y prefetched at the tile's start: yq = y_fetch(...)),
+// cond-actnorm, cond-1x1 conv (-> S.yv), their log-dets (-> S.ld)
+__device__ __forceinline__ void y_fetch(const float *__restrict__ enc, int64_t enc_rs, int row, int q,
+                                        float (&y)[kC]) {
   const int qi = q >> 2, qj = q & 3;
-  const float *er = enc + (int64_t)S.row[p] * enc_rs;
-  float y[kC];
+  const float *er = enc + (int64_t)row * enc_rs;
 #pragma unroll
   for (int c = 0; c < 3; ++c)
 #pragma unroll
     for (int f = 0; f < 4; ++f) y[c * 4 + f] = er[c * 64 + (2 * qi + (f >> 1)) * 8 + 2 * qj + (f & 1)];
+}
+__device__ __forceinline__ void phase_y(float (&y)[kC], int p, int q) {
   float sl = 0.f;
 #pragma unroll
   for (int c = 0; c < kC; ++c) {
@@ -186,17 +242,28 @@ __device__ __noinline__ void phase_y(const float *__restrict__ enc, int64_t enc_
     y[c] = (y[c] + S.an[p][kC + c]) * expf(ls);
     sl += ls;
   }
+  const f4 *wrow = reinterpret_cast<const f4 *>(&S.wm[p][0]);
 #pragma unroll
   for (int o = 0; o < kC; ++o) {
     float a = 0.f;
 #pragma unroll
-    for (int c = 0; c < kC; ++c) a = fmaf(S.wm[p][o * kC + c], y[c], a);
+    for (int c4 = 0; c4 < kC / 4; ++c4) {
+      const f4 w4 = wrow[o * (kC / 4) + c4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a = fmaf(w4[e], y[4 * c4 + e], a);
+    }
     S.yv[p][q][o] = a;
   }
   float wr[kC];
+  const int qr = q < kC ? q : 0;
 #pragma unroll
-  for (int j = 0; j < kC; ++j) wr[j] = q < kC ? S.wm[p][q * kC + j] : 0.f;
-  const float ldw = logabsdet12(wr, q);
+  for (int c4 = 0; c4 < kC / 4; ++c4) {
+    const f4 w4 = wrow[qr * (kC / 4) + c4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[4 * c4 + e] = q < kC ? w4[e] : 0.f;
+  }
+  // the pivot rows go through this particle's S.ex[p][0] (free until phase_resize writes it)
+  const float ldw = logabsdet12(wr, q, &S.ex[p][0][0]);
   if (q == 0) S.ld[p] = 16.0f * sl + 16.0f * ldw;  // dimensions (4x4) x (sum logs, log|det W|)
 }
 
@@ -417,6 +484,18 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
   auto PW = [](const float *w, int o, int i, int K) { return w[((o >> 1) * K + i) * 2 + (o & 1)]; };
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+#ifdef NFDPF_EXP_CGTRACE
+    const bool trace_it = tile == blockIdx.x + 2 * (int64_t)gridDim.x;
+#endif
+    CGTRACE(0)
+    // this lane's squeezed y (phase_y), fetched now so its latency hides behind the encoder
+    // and the conditioning nets (lane = (particle w * 4 + l / 16, position l % 16))
+    float yq[kC];
+    {
+      const int64_t gy = tile * kTileP + (tid >> 4);
+      const int rowy = gy < total ? (int)(gy / N) : 0;
+      y_fetch(enc, enc_rs, xin ? (int)(gy < total ? gy : 0) : rowy, tid & 15, yq);
+    }
     // weight pointers re-derived per tile behind an asm barrier, so the compiler re-reads
     // weights from the caches instead of hoisting every one of them out of the tile loop
     const float *gw = glow, *pe_ = pe;
@@ -482,6 +561,7 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       }
       SYNC();
     }
+    CGTRACE(1)
     // ---- conditioning nets, conv1 (3 -> 8, 2x2 stride 2, 8x8 -> 4x4) for actnorm (A) and
     //      1x1-conv (I) nets: VALU, lane = (particle, 4x4 position)
     const int p = w * 4 + (l >> 4), q = l & 15, qi = q >> 2, qj = q & 3;
@@ -506,6 +586,7 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       }
     }
     SYNC();
+    CGTRACE(2)
     // conv2 (8 -> 8, 2x2 stride 2, 4x4 -> 2x2): GEMM, rows (particle, 2x2 pos), k (ci, a, b)
     for (int job = w; job < 8; job += 4) {
       const int net = job >> 2, mt = job & 3;  // 4 row tiles of 16 = 64 rows
@@ -525,6 +606,7 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       });
     }
     SYNC();
+    CGTRACE(3)
     // conv3 (8 -> 8, 2x2 stride 2, 2x2 -> 1x1): rows = particles, k = (ci, a, b)
     if (w < 2) {
       const int net = w;
@@ -537,6 +619,7 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       });
     }
     SYNC();
+    CGTRACE(4)
     // x_Linear: 8 -> 16 -> 16 (ReLU)
     if (w < 2) {
       const int net = w;
@@ -554,6 +637,7 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       mfma_store(acc, [&](int r, int c, float v) { S.v1[r][net * kXS + c] = relu(v + G[CondA::l2b + c]); });
     }
     SYNC();
+    CGTRACE(5)
     // last layer + tanh: actnorm (24 = 2 tiles) and 1x1 conv (144 = 9 tiles)
     for (int job = w; job < 11; job += 4) {
       const bool isI = job >= 2;
@@ -574,12 +658,15 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       });
     }
     SYNC();
+    CGTRACE(6)
 
     // ---- squeeze(y) at position q, cond-actnorm, cond-1x1 conv, log|det W|
-    phase_y(enc, enc_rs, p, q);
+    phase_y(yq, p, q);
     SYNC();
+    CGTRACE(7)
     phase_resize(gw, p, q);
     SYNC();
+    CGTRACE(8)
     const int64_t gi = g0 + p;
     const float part = phase_f(gw, p, q, zout && gi < total ? zout + gi * kE : nullptr);
     if (q == 0 && gi < total) {
@@ -590,12 +677,19 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       lik[rb * lik_rs + i] = out_sign * (obj / (0.6931471805599453f * (float)kE));
     }
     SYNC();
+    CGTRACE(9)
   }
 }
 
 }  // namespace nfdpf
 
 using namespace nfdpf;
+
+#ifdef NFDPF_EXP_CGTRACE
+extern "C" NFDPF_API int nfdpf_exp_cgtrace_read(void *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cgtrace), sizeof(g_cgtrace)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int64_t nfdpf_cglow_params_size(int K) { return K == 1 ? (int64_t)kStep : -1; }
 
