@@ -222,6 +222,22 @@ using namespace cg;
     __syncthreads();                      \
     __builtin_amdgcn_sched_barrier(0);    \
   } while (0)
+// From phase_y to the tile's end every LDS hand-off stays inside one particle's 16 lanes (lane
+// = (particle tid / 16, position tid % 16): the 3x3 neighbourhoods, S.yv, S.ex, S.ld), i.e.
+// inside one wave, whose LDS accesses execute in order: a compiler fence suffices, and the
+// waves run those phases without waiting for each other.  (-DNFDPF_CG_BARRIERS: workgroup
+// barriers there, as in r01.)
+#ifdef NFDPF_CG_BARRIERS
+#define WSYNC() SYNC()
+#else
+#define WSYNC()                                          \
+  do {                                                   \
+    __builtin_amdgcn_sched_barrier(0);                   \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+    __builtin_amdgcn_wave_barrier();                     \
+    __builtin_amdgcn_sched_barrier(0);                   \
+  } while (0)
+#endif
 
 // squeeze(y) at position q (y prefetched at the tile's start: yq = y_fetch(...)),
 // cond-actnorm, cond-1x1 conv (-> S.yv), their log-dets (-> S.ld)
@@ -396,10 +412,10 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *z
   }
 #pragma unroll
   for (int c = 0; c < kCh; ++c) fin[kCh + c] = S.yv[p][q][c];
-  SYNC();
+  WSYNC();
 #pragma unroll
   for (int c = 0; c < kC; ++c) S.ex[p][q][c] = fin[c];
-  SYNC();
+  WSYNC();
   // f: Conv2dNormy(12->8, 3x3) ReLU, Conv2dNormy(8->8, 1x1) ReLU, Conv2dZerosy(8->12) Tanh
   float g8b[kYH];
   {
@@ -427,10 +443,10 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *z
       g8b[2 * m + 1] = relu((a1[m].y + F[Aff::f2ab + 2 * m + 1]) * expf(F[Aff::f2al + 2 * m + 1]));
     }
   }
-  SYNC();
+  WSYNC();
 #pragma unroll
   for (int c = 0; c < kYH; ++c) S.ex[p][q][c] = g8b[c];
-  SYNC();
+  WSYNC();
   f2 a4[kC / 2];  // pair m = (shift_m, scale_m): channels 2m, 2m+1 (split_feature "cross")
 #pragma unroll
   for (int m = 0; m < kC / 2; ++m) a4[m] = splat(0.f);
@@ -662,10 +678,10 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
 
     // ---- squeeze(y) at position q, cond-actnorm, cond-1x1 conv, log|det W|
     phase_y(yq, p, q);
-    SYNC();
+    WSYNC();
     CGTRACE(7)
     phase_resize(gw, p, q);
-    SYNC();
+    WSYNC();
     CGTRACE(8)
     const int64_t gi = g0 + p;
     const float part = phase_f(gw, p, q, zout && gi < total ? zout + gi * kE : nullptr);
