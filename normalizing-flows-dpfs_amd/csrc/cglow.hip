@@ -70,6 +70,7 @@ struct Lds {
   float wm[kTileP][kC * kC + 4];       // 1x1 conv weight, row-major [out][in] (rows 16-B aligned)
   float ld[kTileP];                    // per-particle log-det of actnorm + 1x1 conv
   int row[kTileP];
+  float escale[2 * kYH + kC];          // exp of the coupling net's log-scales (once per launch)
   union {
     struct {  // particle encoder
       float h1[kTileP][kPeH1 + 1];
@@ -120,6 +121,17 @@ __device__ __forceinline__ void mfma_store(const f4 &acc, const FE &epi) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+// tanh of the conditioning nets' outputs and of the coupling's shift / scale: libm tanhf.
+// (-DNFDPF_CG_FAST_TANH: tanh_fast, common.hpp -- 2 % faster per launch, but the golden
+// error grows from 1.8e-6 to 5.5e-6 against the reference's own 2.1e-6: not shipped.)
+__device__ __forceinline__ float cg_tanh(float x) {
+#ifdef NFDPF_CG_FAST_TANH
+  return tanh_fast(x);
+#else
+  return tanhf(x);
+#endif
+}
 
 // A pointer argument of a non-inlined function arrives in VGPRs; it is wave-uniform, so move
 // it to SGPRs (readfirstlane) before making it a scalar-load weight pointer.
@@ -427,8 +439,8 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *z
     float g8[kYH];
 #pragma unroll
     for (int m = 0; m < kYH / 2; ++m) {
-      g8[2 * m] = relu((a0[m].x + F[Aff::f0ab + 2 * m]) * expf(F[Aff::f0al + 2 * m]));
-      g8[2 * m + 1] = relu((a0[m].y + F[Aff::f0ab + 2 * m + 1]) * expf(F[Aff::f0al + 2 * m + 1]));
+      g8[2 * m] = relu((a0[m].x + F[Aff::f0ab + 2 * m]) * S.escale[2 * m]);
+      g8[2 * m + 1] = relu((a0[m].y + F[Aff::f0ab + 2 * m + 1]) * S.escale[2 * m + 1]);
     }
     f2 a1[kYH / 2];
 #pragma unroll
@@ -439,8 +451,8 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *z
       for (int m = 0; m < kYH / 2; ++m) a1[m] = pfma(((cf2 *)F)[(Aff::f2w + c * kYH) / 2 + m], splat(g8[c]), a1[m]);
 #pragma unroll
     for (int m = 0; m < kYH / 2; ++m) {
-      g8b[2 * m] = relu((a1[m].x + F[Aff::f2ab + 2 * m]) * expf(F[Aff::f2al + 2 * m]));
-      g8b[2 * m + 1] = relu((a1[m].y + F[Aff::f2ab + 2 * m + 1]) * expf(F[Aff::f2al + 2 * m + 1]));
+      g8b[2 * m] = relu((a1[m].x + F[Aff::f2ab + 2 * m]) * S.escale[kYH + 2 * m]);
+      g8b[2 * m + 1] = relu((a1[m].y + F[Aff::f2ab + 2 * m + 1]) * S.escale[kYH + 2 * m + 1]);
     }
   }
   WSYNC();
@@ -455,9 +467,9 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *z
   float lsum = 0.f, lp = 0.f;
 #pragma unroll
   for (int c = 0; c < kCh; ++c) {
-    const float hs = tanhf((a4[c].x + F[Aff::f4b + 2 * c] + F[Aff::f4nb + 2 * c]) * expf(F[Aff::f4l + 2 * c] * 3.0f));
+    const float hs = cg_tanh((a4[c].x + F[Aff::f4b + 2 * c] + F[Aff::f4nb + 2 * c]) * S.escale[2 * kYH + 2 * c]);
     const float hc =
-        tanhf((a4[c].y + F[Aff::f4b + 2 * c + 1] + F[Aff::f4nb + 2 * c + 1]) * expf(F[Aff::f4l + 2 * c + 1] * 3.0f));
+        cg_tanh((a4[c].y + F[Aff::f4b + 2 * c + 1] + F[Aff::f4nb + 2 * c + 1]) * S.escale[2 * kYH + 2 * c + 1]);
     const float sc = sigmoidf_(hc + 2.0f);
     const float z1 = S.yv[p][q][c];
     const float z2 = (S.yv[p][q][kCh + c] + hs) * sc;
@@ -498,6 +510,14 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
   const int64_t total = (int64_t)B * N;
   const int64_t ntiles = (total + kTileP - 1) / kTileP;
   auto PW = [](const float *w, int o, int i, int K) { return w[((o >> 1) * K + i) * 2 + (o & 1)]; };
+  // the coupling net's per-channel scales exp(logs) (Conv2dNormy, nf/cglow/modules.py:214) and exp(3 logs)
+  // (Conv2dZerosy, :233), once per launch (ordered before use by the tile's first SYNC)
+  if (tid < 2 * kYH + kC) {
+    const float *F = glow + kOffF;
+    S.escale[tid] = tid < kYH ? expf(F[Aff::f0al + tid])
+                    : tid < 2 * kYH ? expf(F[Aff::f2al + tid - kYH])
+                                    : expf(F[Aff::f4l + tid - 2 * kYH] * 3.0f);
+  }
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
 #ifdef NFDPF_EXP_CGTRACE
@@ -665,7 +685,7 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
       mfma_store(acc, [&](int r, int c, float v) {
         const int n = n0 + c;
         if (n < nout) {
-          const float t = tanhf(v + G[lb + n]);
+          const float t = cg_tanh(v + G[lb + n]);
           if (isI)
             S.wm[r][n] = t;
           else
