@@ -194,7 +194,8 @@ struct TBlock {  // 8 consecutive j of NP planes
 // (scalar loads into SGPRs, one block at a time) instead of the pipelined vector loads that
 // return the same 16 B to all 64 lanes: measured SLOWER (C4 iteration 124 vs 118 us, C3 22 vs
 // 17 us; the compiler keeps half of the words as vector loads and the scalar waits are not
-// overlapped -- profiles/r02_experiments.md).
+// overlapped -- profiles/r02_experiments.md).  So was one coalesced load per block handed out by
+// v_readlane as SGPR operands (C4 iteration 129-141 vs 117 us).
 typedef const float4 __attribute__((address_space(4))) cfloat4;
 template <int NP>
 __device__ __forceinline__ void tload(TBlock<NP> &B, const float *tab, int64_t Np, int j, const int (&pl)[NP]) {
