@@ -48,7 +48,17 @@
 
 namespace nfdpf {
 
-constexpr int kOtThreads = 256;  // i (or j) per workgroup = the table slice length
+// i (or j) per workgroup = the table slice length: 256, each lane carrying kR = 4 of the
+// workgroup's i.  -DNFDPF_OT_SL=128 builds a layout with twice the waves per launch (kR = 2,
+// the 4 waves split the slices four ways; 4 waves per SIMD at C4 instead of 2): measured
+// slower on one box (C4 90.4 vs 83.1 ms per pass, C3 forced 27.1 vs 25.5) -- the per-workgroup
+// prologue / epilogue doubles with the workgroup count.
+#ifndef NFDPF_OT_SL
+#define NFDPF_OT_SL 256
+#endif
+constexpr int kOtThreads = NFDPF_OT_SL;
+constexpr int kOtBlock = 256;  // threads per workgroup; threads >= kOtThreads own no i
+static_assert(kOtThreads == 128 || kOtThreads == 256, "slice length");
 constexpr double kLog2ed = 1.4426950408889634;
 constexpr double kLn2d = 0.6931471805599453;
 constexpr float kLo = 0x1.0p-60f, kHi = 0x1.0p60f;  // outside: the lane recomputes exactly
@@ -86,9 +96,13 @@ struct OtWs {  // carve of the caller's workspace
   double *mC;    // [B][splits]
   float *tabA;   // [B][5][Np] apply pass: X, Y, r_j - M, x_j, y_j (x = the input particles)
   double *mA;    // [B][splits]
+  double *epsk;  // [B][kEpsTab] running epsilon of iteration k (ot_setup_kernel)
 };
 
 static inline int64_t align256(int64_t v) { return (v + 255) / 256 * 256; }
+// the running-epsilon table: iterations 0 .. kEpsTab-1 (annealing is over long before: eps0 is
+// the squared diameter of the scaled cloud, a few dozen steps of s^2 = 0.5625 above eps)
+constexpr int kEpsTab = 128;
 
 static inline int ot_splits(int N) { return (N + kOtThreads - 1) / kOtThreads; }
 
@@ -124,6 +138,7 @@ static OtWs carve(void *ws, int B, int N, int64_t *bytes = nullptr) {
   w.mC = c.take<double>((int64_t)B * S);
   w.tabA = c.take<float>(B * 5 * Np + 64);
   w.mA = c.take<double>((int64_t)B * S);
+  w.epsk = c.take<double>((int64_t)B * kEpsTab);
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -170,6 +185,12 @@ __device__ __forceinline__ double run_eps(double eps0, int k, double sf, double 
   return e;
 }
 
+// run_eps of row b from the table (the same fp64 recurrence, evaluated once per call)
+__device__ __forceinline__ double eps_at(const OtWs &ws, const OtParams &P, int b, int k) {
+  const double *t = ws.epsk + (int64_t)b * kEpsTab;
+  return k < kEpsTab ? t[k] : run_eps(t[kEpsTab - 1], k - (kEpsTab - 1), P.sf, P.eps);
+}
+
 // sc with sc |dx|^2 = |dx|^2 / (2 e) * log2(e): C_ij / e in base 2
 __device__ __forceinline__ float cost_scale(double inv_e) { return (float)(0.5 * inv_e * kLog2ed); }
 
@@ -180,8 +201,8 @@ __device__ __forceinline__ float cost_scale(double inv_e) { return (float)(0.5 *
 // are wave-uniform; a vector load returns them to every lane, and at one i per lane the L1
 // return path, not the VALU, bounds the loop.)  Partial sums meet in LDS in wave order.
 // ------------------------------------------------------------------------------------------
-constexpr int kR = 4;
-constexpr int kWaves = kOtThreads / 64;
+constexpr int kR = kOtThreads / 64;  // i per lane
+constexpr int kWaves = kOtBlock / 64;
 constexpr int kLdsPart = kWaves * 3 * kOtThreads;  // floats: wave partials of <= 3 sums per i
 
 template <int NP>
@@ -244,6 +265,74 @@ __device__ __forceinline__ void pipelined(const float *tab, int64_t Np, int j0, 
     body(A);
     __builtin_amdgcn_sched_barrier(0);
     tload(A, tab, Np, j + 16, pl);
+    __builtin_amdgcn_sched_barrier(0);
+    body(Bk);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// LDS-staged slices (default; -DNFDPF_OT_L1 keeps the wave-uniform vector loads above).  A
+// wave copies a whole slice (256 j of up to kSlicePl planes) with coalesced loads -- lane l
+// holds j0 + 4l .. j0 + 4l + 3 of every plane, 1 KB per plane and load instruction, all of it
+// used -- into its own LDS region, and the pair loop reads the wave-uniform words from there
+// (ds_read_b128, one address for all lanes).  It replaces wave-uniform 16-B vector loads that
+// each returned their 16 B to all 64 lanes through the L1.  Measured (C4 iteration, one box):
+// 120 -> 116.5 us -- the L1 return path was not the bound the r01 notes assumed; a register
+// prefetch of the next slice was kept in scratch by the compiler and is not used.
+constexpr int kSlicePl = 6;                                  // planes of the widest table (iteration)
+constexpr int kSliceFloats = kSlicePl * kOtThreads + 16;     // + padding: the loop reads one block ahead
+constexpr int kLdsAll = kLdsPart + kWaves * kSliceFloats;    // combine() area + the waves' slices
+
+// one slice (planes 0 .. NPL-1, kOtThreads j each) into the wave's LDS region: float4 f of
+// the slice (f = lane + 64 q) is plane f / (kOtThreads / 4), j0 + 4 (f % (kOtThreads / 4))
+template <int Q, int NPL>
+__device__ __forceinline__ void slice_copy_q(const float *tab, int64_t Np, int j0, float *sl) {
+  constexpr int kPer = kOtThreads / 4;  // float4 per plane
+  if constexpr (Q * 64 < NPL * kPer) {
+    const int f = (threadIdx.x & 63) + 64 * Q;
+    const int p = f / kPer, o = 4 * (f % kPer);
+    const bool in = p < NPL;  // the last instruction may hold a part plane (NPL odd, 128 j)
+    float4 v{};
+    if (in) v = *reinterpret_cast<const float4 *>(tab + p * Np + j0 + o);
+    slice_copy_q<Q + 1, NPL>(tab, Np, j0, sl);
+    if (in) *reinterpret_cast<float4 *>(sl + p * kOtThreads + o) = v;
+  }
+}
+template <int NPL>
+__device__ __forceinline__ void slice_copy(const float *tab, int64_t Np, int j0, float *sl) {
+  asm volatile("" ::: "memory");
+  slice_copy_q<0, NPL>(tab, Np, j0, sl);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+template <int NP>
+__device__ __forceinline__ void lds_tblock(TBlock<NP> &B, const float *sl, int j, const int (&pl)[NP]) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const float4 *X = reinterpret_cast<const float4 *>(sl + pl[p] * kOtThreads + j);
+    B.v[p][0] = X[0];
+    B.v[p][1] = X[1];
+  }
+}
+// the 32 blocks of 8 j of a staged slice, one block read ahead
+template <int NP, class Body>
+__device__ __forceinline__ void slice_blocks(const float *sl, const int (&pl)[NP], const Body &body) {
+#ifdef NFDPF_OT_LDS1  // one block at a time (32 fewer VGPRs; the SIMD's other waves cover the LDS latency)
+  for (int j = 0; j < kOtThreads; j += 8) {
+    TBlock<NP> A;
+    lds_tblock(A, sl, j, pl);
+    body(A);
+  }
+  return;
+#endif
+  TBlock<NP> A, Bk;
+  lds_tblock(A, sl, 0, pl);
+  for (int j = 0; j < kOtThreads; j += 16) {
+    lds_tblock(Bk, sl, j + 8, pl);
+    __builtin_amdgcn_sched_barrier(0);
+    body(A);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_tblock(A, sl, j + 16, pl);  // past the end: the padding / the next plane, discarded
     __builtin_amdgcn_sched_barrier(0);
     body(Bk);
     __builtin_amdgcn_sched_barrier(0);
@@ -331,10 +420,11 @@ __device__ __forceinline__ void combine(float *lds, const float (&mine)[kR][NK],
 #pragma unroll
     for (int k = 0; k < NK; ++k) lds[(w * NK + k) * kOtThreads + lane + 64 * r] = mine[r][k];
   __syncthreads();
+  const int t = threadIdx.x % kOtThreads;  // threads >= kOtThreads get a copy (unused)
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    float a = lds[k * kOtThreads + threadIdx.x];
-    for (int u = 1; u < kWaves; ++u) a += lds[(u * NK + k) * kOtThreads + threadIdx.x];
+    float a = lds[k * kOtThreads + t];
+    for (int u = 1; u < kWaves; ++u) a += lds[(u * NK + k) * kOtThreads + t];
     out[k] = a;
   }
 }
@@ -361,14 +451,23 @@ __device__ __forceinline__ void wg_table_sums(const float *tab, const double *ms
 #pragma unroll
     for (int v = 0; v < NV; ++v) accv[r][v] = sp2(0.f);
   }
-  for (int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); s < splits; s += kWaves) {
+  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifndef NFDPF_OT_L1
+  float *sl = lds + kLdsPart + w0 * kSliceFloats;
+#endif
+  for (int s = w0; s < splits; s += kWaves) {
     f2 o[kR][NH];
 #pragma unroll
     for (int r = 0; r < kR; ++r)
 #pragma unroll
       for (int w = 0; w < NH; ++w) o[r][w] = sp2(slice_off(msh[s * MS + w], m[r][w]));
+#ifndef NFDPF_OT_L1
+    slice_copy<NP>(tab, Np, s * kOtThreads, sl);
+    slice_blocks<NP>(sl, pl, [&](const TBlock<NP> &B) { hblock<NH, NV>(B, L, nsc2, o, acc, accv); });
+#else
     pipelined<NP>(tab, Np, s * kOtThreads, (s + 1) * kOtThreads, pl,
                   [&](const TBlock<NP> &B) { hblock<NH, NV>(B, L, nsc2, o, acc, accv); });
+#endif
   }
   float mine[kR][NH + NV], out[NH + NV];
 #pragma unroll
@@ -404,7 +503,11 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
     Sk[r][0] = Sk[r][1] = 0.f;
     hacc[r][0] = hacc[r][1] = sp2(0.f);
   }
-  for (int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); s < splits; s += kWaves) {
+  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifndef NFDPF_OT_L1
+  float *sl = lds + kLdsPart + w0 * kSliceFloats;
+#endif
+  for (int s = w0; s < splits; s += kWaves) {
     const double Ma = msh[2 * s], Mb = msh[2 * s + 1];
     float oa[kR], ob[kR];
     bool risky = false;
@@ -415,11 +518,18 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
       risky |= (oa[r] > kRisky) || (ob[r] > kRisky);
     }
     const int j0 = s * kOtThreads, j1 = j0 + kOtThreads;
+#ifndef NFDPF_OT_L1
+    slice_copy<6>(tab, Np, s * kOtThreads, sl);
+    (void)j1;
+#define OT_SLICE_LOOP(PL, ...) slice_blocks<4>(sl, PL, __VA_ARGS__)
+#else
+#define OT_SLICE_LOOP(PL, ...) pipelined<4>(tab, Np, j0, j1, PL, __VA_ARGS__)
+#endif
     if (__builtin_amdgcn_ballot_w64(risky) == 0) {
       f2 acc[kR][2];
 #pragma unroll
       for (int r = 0; r < kR; ++r) acc[r][0] = acc[r][1] = sp2(0.f);
-      pipelined<4>(tab, Np, j0, j1, plk, [&](const TBlock<4> &B) { kblock(B, L, nsc2, acc); });
+      OT_SLICE_LOOP(plk, [&](const TBlock<4> &B) { kblock(B, L, nsc2, acc); });
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         Sk[r][0] = fmaf(exp2f(oa[r]), hsum2(acc[r][0]), Sk[r][0]);
@@ -432,8 +542,9 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
         o[r][0] = sp2(oa[r]);
         o[r][1] = sp2(ob[r]);
       }
-      pipelined<4>(tab, Np, j0, j1, plh, [&](const TBlock<4> &B) { hblock<2, 0>(B, L, nsc2, o, hacc, none); });
+      OT_SLICE_LOOP(plh, [&](const TBlock<4> &B) { hblock<2, 0>(B, L, nsc2, o, hacc, none); });
     }
+#undef OT_SLICE_LOOP
   }
   float mine[kR][2], out[2];
 #pragma unroll
@@ -475,26 +586,31 @@ __device__ __forceinline__ double lse2_from(float S, double m, const float *xs, 
   return lse2_exact(xs, N, xi, yi, sc, h);
 }
 
-// Thread's column of a table (j = 256 blockIdx.x + threadIdx.x): planes X, Y, then NE exponent
+// Thread's column of a table (j = kOtThreads blockIdx.x + threadIdx.x, threads < kOtThreads): planes X, Y, then NE exponent
 // planes stored as h - M_s (slice maxima to msh[blockIdx.x * NE + e]), then NV value planes.
 // With ALPHA, planes 2 + NE + e hold 2^(h_e - M_s) (the iteration table's alpha / beta).
 template <int NE, int NV, bool ALPHA>
 __device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, bool valid, float X, float Y,
                                           const double (&h)[NE], const float *vals, double *shd) {
   const int64_t j = (int64_t)blockIdx.x * kOtThreads + threadIdx.x;
-  tab[j] = valid ? X : 0.f;
-  tab[Np + j] = valid ? Y : 0.f;
+  const bool own = threadIdx.x < kOtThreads;  // the slice's columns; other threads only reduce
+  valid = valid && own;
+  if (own) {
+    tab[j] = valid ? X : 0.f;
+    tab[Np + j] = valid ? Y : 0.f;
+  }
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
     const double he = valid ? h[e] : -INFINITY;
     const double M = block_max(he, shd);
     const float E = (he > -INFINITY) ? (float)(he - M) : -INFINITY;
-    tab[(2 + e) * Np + j] = E;
-    if (ALPHA) tab[(2 + NE + e) * Np + j] = E > -INFINITY ? __builtin_amdgcn_exp2f(E) : 0.f;
+    if (own) tab[(2 + e) * Np + j] = E;
+    if (ALPHA && own) tab[(2 + NE + e) * Np + j] = E > -INFINITY ? __builtin_amdgcn_exp2f(E) : 0.f;
     if (threadIdx.x == 0) msh[blockIdx.x * NE + e] = M;
   }
 #pragma unroll
-  for (int v = 0; v < NV; ++v) tab[(2 + NE + (ALPHA ? NE : 0) + v) * Np + j] = valid ? vals[v] : 0.f;
+  for (int v = 0; v < NV; ++v)
+    if (own) tab[(2 + NE + (ALPHA ? NE : 0) + v) * Np + j] = valid ? vals[v] : 0.f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -502,7 +618,8 @@ __device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, b
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict__ x,
                                                         const float *__restrict__ w, int N,
-                                                        OtWs ws, const int32_t *gate) {
+                                                        OtWs ws, const int32_t *gate, double sf,
+                                                        double eps) {
   if (gate && *gate == 0) return;
   __shared__ double shd[16];
   __shared__ float shf[16];
@@ -549,6 +666,11 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
     ws.rowc[b * 4 + 0] = mm * mm;                        // epsilon_0 = diameter^2 (:117)
     ws.rowc[b * 4 + 1] = -(double)logf((float)N);       // uniform log weight (:214-215)
     ws.rowc[b * 4 + 2] = (double)lwmax;                 // shift of the first a-softmin
+    double e = mm * mm;                                 // eps_k, k = 0 .. kEpsTab-1 (:158)
+    for (int k = 0; k < kEpsTab; ++k) {
+      ws.epsk[(int64_t)b * kEpsTab + k] = e;
+      e = fmax(e * sf, eps);
+    }
     if (b == 0) {
       ws.st->stopped = 0;
       ws.st->K = 0;
@@ -558,11 +680,11 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
 }
 
 // table of the initial softmins at eps0 (:120-121): h_a = logw, h_b = logu (base 2)
-__global__ __launch_bounds__(kOtThreads) void ot_prep_kernel(OtParams P, OtWs ws) {
+__global__ __launch_bounds__(kOtBlock) void ot_prep_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
   __shared__ double shd[16];
   const int b = blockIdx.y, N = P.N, i = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = i < N;
+  const bool v = i < N && threadIdx.x < kOtThreads;
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const double h[2] = {v ? (double)ws.logw[(int64_t)b * N + i] * kLog2ed : 0.0, ws.rowc[b * 4 + 1] * kLog2ed};
   write_col<2, 0, true>(tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), np_of(P), v, v ? xs[2 * i] : 0.f,
@@ -576,7 +698,7 @@ __device__ __forceinline__ void emit_state_tables(const OtParams &P, const OtWs 
                                                   float xi, float yi, float lw, double logu, double ay,
                                                   double bx, double *shd) {
   const int64_t Np = np_of(P);
-  const double e = run_eps(ws.rowc[b * 4], ks, P.sf, P.eps);
+  const double e = eps_at(ws, P, b, ks);
   {
     const double inv = 1.0 / e;
     const double h[2] = {((double)lw + bx * inv) * kLog2ed, (logu + ay * inv) * kLog2ed};
@@ -608,13 +730,13 @@ __device__ __forceinline__ void softmin_pair(const OtParams &P, const float *tab
 }
 
 // initial potentials at eps0 (:120-121): a_y = softmin(eps0, C, logw), b_x = softmin(eps0, C, logu)
-__global__ __launch_bounds__(kOtThreads) void ot_init_kernel(OtParams P, OtWs ws) {
+__global__ __launch_bounds__(kOtBlock) void ot_init_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
   __shared__ double shd[16];
-  __shared__ float lds[kLdsPart];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = i < N;
+  const bool v = i < N && threadIdx.x < kOtThreads;
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
   const double e = ws.rowc[b * 4], logu = ws.rowc[b * 4 + 1];
@@ -639,33 +761,38 @@ __global__ __launch_bounds__(kOtThreads) void ot_init_kernel(OtParams P, OtWs ws
 }
 
 // does the loop stop before iteration k?  (stop_condition :126-129) -- every workgroup
-// evaluates the same residuals of iteration k-1 in the same order
+// evaluates the same residuals of iteration k-1 (wave 0, lanes over rows; every load of a
+// lane independent, one memory latency).  r01 ran this on one lane, row after row with the
+// epsilon recurrence re-run per row: a serial chain at the start of every iteration launch.
 __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws, int k) {
   if (k == 0) return false;
   if (P.stop_at) return k >= *P.stop_at - 2;  // the batch-global decision, taken by the caller
   const double *res = ws.res + (int64_t)((k - 1) & 1) * P.B * P.splits;
-  for (int b = 0; b < P.B; ++b) {
-    const double e0 = ws.rowc[b * 4];
-    const double re = run_eps(e0, k - 1, P.sf, P.eps);
+  bool conv = false;
+  for (int b = threadIdx.x & 63; b < P.B; b += 64) {
+    const double re = eps_at(ws, P, b, k - 1);
     const double ne = fmax(re * P.sf, P.eps);
-    bool cont = ne < re;
-    for (int s = 0; s < P.splits && !cont; ++s) cont = res[b * P.splits + s] > P.thr;
-    if (!cont) return true;  // some row converged -> torch.all(continue_) is False
+    double mx = 0.0;
+    for (int s = 0; s < P.splits; ++s) mx = fmax(mx, res[b * P.splits + s]);
+    conv |= !(ne < re || mx > P.thr);  // this row converged -> torch.all(continue_) is False
   }
-  return false;
+  return __builtin_amdgcn_ballot_w64(conv) != 0;
 }
 
 // iteration k: state k (buffer k&1) -> state k+1 (buffer (k+1)&1)  (apply_one :131-153)
-__global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
+#ifndef NFDPF_OT_ITER_WPS
+#define NFDPF_OT_ITER_WPS 1
+#endif
+__global__ __launch_bounds__(kOtBlock, NFDPF_OT_ITER_WPS) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
   if (ot_off(P)) {
     if (lead && P.host) host_flag(P.host, 0, P.seq);  // nothing to iterate: stop enqueueing
     return;
   }
   __shared__ double shd[16];
-  __shared__ float lds[kLdsPart];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   __shared__ int s_stop;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // wave 0 (ot_stop_before is a wave-level decision)
     int st = ws.st->stopped;
     if (!st && ot_stop_before(P, ws, k)) {
       st = 1;
@@ -674,7 +801,7 @@ __global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws
         ws.st->K = k;
       }
     }
-    s_stop = st;
+    if (threadIdx.x == 0) s_stop = st;
     if (lead && P.host) {
       host_flag(P.host, 1, P.seq * 4096 + k);
       if (st) host_flag(P.host, 0, P.seq);
@@ -684,8 +811,8 @@ __global__ __launch_bounds__(kOtThreads) void ot_iter_kernel(OtParams P, OtWs ws
   if (s_stop) return;
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = i < N;
-  const double re = run_eps(ws.rowc[b * 4], k, P.sf, P.eps), inv = 1.0 / re;
+  const bool v = i < N && threadIdx.x < kOtThreads;
+  const double re = eps_at(ws, P, b, k), inv = 1.0 / re;
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
   const double logu = ws.rowc[b * 4 + 1];
@@ -726,13 +853,13 @@ __device__ __forceinline__ int ot_total_iter(const OtParams &P, const OtWs &ws) 
 // final potential at eps (:173-176): f = softmin(eps, C, logw + b_x/eps).  (g = softmin(eps,
 // C, logu + a_y/eps) cancels in the column normalisation of the transport matrix: not formed.)
 // Writes the column table: X, Y, f_i / eps (base 2).
-__global__ __launch_bounds__(kOtThreads) void ot_final_kernel(OtParams P, OtWs ws) {
+__global__ __launch_bounds__(kOtBlock) void ot_final_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
   __shared__ double shd[16];
-  __shared__ float lds[kLdsPart];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = i < N;
+  const bool v = i < N && threadIdx.x < kOtThreads;
   const int64_t Np = np_of(P);
   const int K = ot_total_iter(P, ws);
   const double e = P.eps, inv = 1.0 / P.eps;
@@ -741,7 +868,7 @@ __global__ __launch_bounds__(kOtThreads) void ot_final_kernel(OtParams P, OtWs w
   const float *lw = ws.logw + (int64_t)b * N;
   const double *ay = pot_ptr(ws, P, K & 1, 0, b), *bx = pot_ptr(ws, P, K & 1, 1, b);
   // the state's iteration table is at eps unless the row was still annealing at the stop
-  const bool annealing = run_eps(ws.rowc[b * 4], K, P.sf, P.eps) != P.eps;
+  const bool annealing = eps_at(ws, P, b, K) != P.eps;
   const float *tab = annealing ? ws.tabF + (int64_t)b * 4 * Np : tabI_row(ws, P, K & 1, b);
   const double *msh = annealing ? ws.mF + (int64_t)b * P.splits * 2 : mI_row(ws, P, K & 1, b);
   const float xi = v ? xs[2 * i] : 0.f, yi = v ? xs[2 * i + 1] : 0.f;
@@ -769,13 +896,13 @@ __global__ __launch_bounds__(kOtThreads) void ot_final_kernel(OtParams P, OtWs w
 
 // r_j = log N + logw_j - LSE_i(f_i/eps - C_ij/eps)   (transport_from_potentials :200-207,
 // with the column log-normaliser; g_j cancels).  Writes the apply table: X, Y, r_j, x_j, y_j.
-__global__ __launch_bounds__(kOtThreads) void ot_col_kernel(OtParams P, OtWs ws, const float *__restrict__ x) {
+__global__ __launch_bounds__(kOtBlock) void ot_col_kernel(OtParams P, OtWs ws, const float *__restrict__ x) {
   if (ot_off(P)) return;
   __shared__ double shd[16];
-  __shared__ float lds[kLdsPart];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int j = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = j < N;
+  const bool v = j < N && threadIdx.x < kOtThreads;
   const int64_t Np = np_of(P);
   const int K = ot_total_iter(P, ws);
   const double inv = 1.0 / P.eps;
@@ -808,17 +935,17 @@ __global__ __launch_bounds__(kOtThreads) void ot_col_kernel(OtParams P, OtWs ws,
 
 // x'_i = sum_j T_ij x_j with T_ij = exp(f_i/eps - C_ij/eps + r_j)  (apply_transport_matrix
 // :254-264): the terms are the matrix entries themselves (shift -f_i/eps, sum ~ 1)
-__global__ __launch_bounds__(kOtThreads) void ot_apply_kernel(OtParams P, OtWs ws,
+__global__ __launch_bounds__(kOtBlock) void ot_apply_kernel(OtParams P, OtWs ws,
                                                              const float *__restrict__ x,
                                                              int64_t row_base,
                                                              float *__restrict__ x_out,
                                                              float *__restrict__ w_out,
                                                              int64_t *__restrict__ idx_out) {
   if (ot_off(P)) return;
-  __shared__ float lds[kLdsPart];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = i < N;
+  const bool v = i < N && threadIdx.x < kOtThreads;
   const int64_t Np = np_of(P);
   const double inv = 1.0 / P.eps;
   const float sc = cost_scale(inv);
@@ -873,13 +1000,13 @@ __global__ __launch_bounds__(kOtThreads) void ot_apply_kernel(OtParams P, OtWs w
 // L_j = log2 N + log2 w_j - R_j the shifted sum over i is 1 and dL/dx_j = N w_j * SV_j.
 // The forward's workspace must be untouched since its call; the iteration tables (free after
 // the loop) hold the backward's table: X, Y, F_i - M, g_x, g_y.
-__global__ __launch_bounds__(kOtThreads) void ot_bwd_table_kernel(OtParams P, OtWs ws,
+__global__ __launch_bounds__(kOtBlock) void ot_bwd_table_kernel(OtParams P, OtWs ws,
                                                                  const float *__restrict__ g) {
   if (ot_off(P)) return;
   __shared__ double shd[16];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = i < N;
+  const bool v = i < N && threadIdx.x < kOtThreads;
   const int64_t Np = np_of(P);
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const double fsh = (1.0 / P.eps) * kLog2ed;
@@ -889,12 +1016,12 @@ __global__ __launch_bounds__(kOtThreads) void ot_bwd_table_kernel(OtParams P, Ot
                          v ? xs[2 * i + 1] : 0.f, h, vals, shd);
 }
 
-__global__ __launch_bounds__(kOtThreads) void ot_bwd_apply_kernel(OtParams P, OtWs ws,
+__global__ __launch_bounds__(kOtBlock) void ot_bwd_apply_kernel(OtParams P, OtWs ws,
                                                                  const float *__restrict__ g,
                                                                  float *__restrict__ g_x) {
   const int b = blockIdx.y, N = P.N;
   const int j = blockIdx.x * kOtThreads + threadIdx.x;
-  const bool v = j < N;
+  const bool v = j < N && threadIdx.x < kOtThreads;
   const int64_t o = (int64_t)b * N + j;
   if (ot_off(P)) {  // no resampling happened: x' = x
     if (v) {
@@ -903,7 +1030,7 @@ __global__ __launch_bounds__(kOtThreads) void ot_bwd_apply_kernel(OtParams P, Ot
     }
     return;
   }
-  __shared__ float lds[kLdsPart];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int64_t Np = np_of(P);
   const float sc = cost_scale(1.0 / P.eps);
   const float *xs = ws.xs + (int64_t)b * N * 2;
@@ -1023,12 +1150,12 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
     if (!poll_flags(&hf, &P.host)) return launch_status("nfdpf_ot_resample (poll flags)");
     P.seq = (g_poll_seq = (g_poll_seq + 1) & 0x7ffff);
   }
-  ot_setup_kernel<<<B, row_threads(N), 0, st>>>(x, w, N, ws, gate);
+  ot_setup_kernel<<<B, row_threads(N), 0, st>>>(x, w, N, ws, gate, P.sf, P.eps);
   const dim3 g(splits, B);
-  ot_prep_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
-  ot_init_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
+  ot_prep_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
+  ot_init_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   if (!poll) {
-    for (int k = 0; k < max_iter - 1; ++k) ot_iter_kernel<<<g, kOtThreads, 0, st>>>(P, ws, k);
+    for (int k = 0; k < max_iter - 1; ++k) ot_iter_kernel<<<g, kOtBlock, 0, st>>>(P, ws, k);
   } else {
     // Keep at most kAhead iterations queued past the one the device has started, and stop
     // enqueueing once an iteration has observed the stop (or the gate is off): the loop then
@@ -1038,7 +1165,7 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
     bool blind = false;
     for (int k = 0; k < max_iter - 1; ++k) {
       if (!blind && hf[0] == P.seq) break;
-      ot_iter_kernel<<<g, kOtThreads, 0, st>>>(P, ws, k);
+      ot_iter_kernel<<<g, kOtBlock, 0, st>>>(P, ws, k);
       if (blind) continue;
       const auto t0 = std::chrono::steady_clock::now();
       for (;;) {
@@ -1053,9 +1180,9 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
       }
     }
   }
-  ot_final_kernel<<<g, kOtThreads, 0, st>>>(P, ws);
-  ot_col_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x);
-  ot_apply_kernel<<<g, kOtThreads, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);
+  ot_final_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
+  ot_col_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x);
+  ot_apply_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);
   if (iters_out) ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
   return launch_status("nfdpf_ot_resample");
 }
@@ -1072,8 +1199,8 @@ extern "C" int nfdpf_ot_transport_backward(const float *g_out, int B, int N, flo
   OtWs ws = carve(workspace, B, N);
   OtParams P{B, N, splits, 1, (double)eps, 1.0, 0.0, gate, nullptr, nullptr, 0};
   const dim3 g(splits, B);
-  ot_bwd_table_kernel<<<g, kOtThreads, 0, st>>>(P, ws, g_out);
-  ot_bwd_apply_kernel<<<g, kOtThreads, 0, st>>>(P, ws, g_out, g_x);
+  ot_bwd_table_kernel<<<g, kOtBlock, 0, st>>>(P, ws, g_out);
+  ot_bwd_apply_kernel<<<g, kOtBlock, 0, st>>>(P, ws, g_out, g_x);
   return launch_status("nfdpf_ot_transport_backward");
 }
 
