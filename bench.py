@@ -54,6 +54,10 @@ CONFIGS = {
 # C2: proposal inverse 1,280 + nf_dyn forward 1,280 + cosine encoder 3,136 = 5,696.
 # C4: proposal 1,280 + MAF forward 2 x 176 + cosine encoder 3,136 = 4,768.
 F_EXEC = {"c2": 5696.0, "c4": 4768.0}
+# ... of the whole step when it runs as one launch (tiled_step_fused_kernel): + the nf_dyn
+# inverse's executed 1,280 (4 coupling halves x 2 nets x (1 + 8x8 + 8) MAC; 4 of its 5 inputs are
+# the per-row context, folded)
+F_EXEC_STEP = {"c2": 6976.0}
 B_ALG = 52.0            # algorithmic HBM bytes per particle-step
 B_SOFT = 36.0           # soft resampling, HBM bytes per particle: read x 8 + p 4,
 #                         write x' 8 + w' 4 + index 8, + 4 for the row's CDF pass
@@ -366,6 +370,9 @@ def main():
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
     F_EX = F_EXEC.get(args.config, F_ALG) if kname.startswith("tiled_prop") else F_ALG
+    if args.kernel == "tiled" and eng.last_fused:  # the whole step in one launch: all of its FLOP
+        kname, F_ALG = "tiled_step_fused_kernel", F_STEP
+        F_EX = F_EXEC_STEP.get(args.config, F_ALG)
     ot_iter_ms = None
     if flags["resampler_type"] == "ot" and eng.last_ot_calls:
         ot_iter_ms = ot_iteration_ms(res, T)

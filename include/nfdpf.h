@@ -370,6 +370,11 @@ NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
  * the T steps of one sequence.                                                        */
 NFDPF_API int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T);
 NFDPF_API int nfdpf_filter_tiled_tiles(int N);
+/* 1 when nfdpf_filter_step_tiled runs this step as ONE launch (tiled_step_fused_kernel: the
+ * C2-shaped path -- split RealNVP nets, NF_cond, cosine measurement -- with every workgroup of
+ * the (tiles, B) grid resident on the current device; opt-in: NFDPF_FUSED_STEP=1), else 0.
+ * prof_front is then ignored (no separate front launch).  No reference counterpart: a query. */
+NFDPF_API int nfdpf_filter_tiled_fused(const nfdpf_filter_desc *d);
 /* the t = 0 gate input from p0 [B,N] -> ess_parts [B][tiles][4] */
 NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
                             void *stream);

@@ -32,6 +32,9 @@ __device__ unsigned long long g_qtrace[1024][16][16];
 
 #include "split.hpp"
 
+// front + dyn in one launch (tiled_fdyn_kernel) for rows up to this length (LDS)
+constexpr int kMergedMaxN_ = 4096;
+
 namespace nfdpf {
 
 constexpr int kTile = 256;  // particles per workgroup, one per lane
@@ -52,6 +55,7 @@ struct TiledWs {
   float *cb_dyn;    // [B][kCb] folded nf_dyn biases of the row (K2, tile 0)
   float *cb_cond;   // [B][kCb] proposal fold over the encoding columns (K1, tile 0)
   double *fin;      // [B][T][tiles][4] sum p^2, sum p x0, sum p x1, sum logw
+  uint64_t *rowx;   // [B][tiles][8] the fused step's x_dyn partials as tagged granules
 };
 // The step's softmax partials live in the caller's ess_out / ess_all (include/nfdpf.h):
 // per (row, tile) {max u, sum e^(u-max), sum e^(2(u-max)), max raw likelihood}.
@@ -64,7 +68,7 @@ __host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / 
 
 static int64_t tiled_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(bt * 32) * 2 + al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32);
+  return al256(bt * 32) * 2 + al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32) + al256(bt * 64);
 }
 
 static TiledWs tiled_carve(void *ws, int B, int N, int T) {
@@ -80,6 +84,8 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   w.cb_cond = (float *)p;
   p += al256((int64_t)B * kCb * 4);
   w.fin = (double *)p;
+  p += al256(bt * T * 32);
+  w.rowx = (uint64_t *)p;
   return w;
 }
 
@@ -368,6 +374,56 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   TRACE(0, 3)
 }
 
+// ---- the fused step (tiled_step_fused_kernel, below; opt-in, see use_fused): the merged front
+// launch and the quad proposal launch as ONE launch per step.  Their only coupling inside a step is the row's x_dyn
+// sums (the proposal's [mean, std] context): instead of a launch boundary, the four workgroups
+// of a row exchange their partials through data-tagged 8-byte granules {32 data bits, tag}
+// (agent-scope stores / loads: L2, no flag, no fence; MI355X_MICROARCH.md handoff-1to1).  The
+// tag is (pass epoch << 16) + t + 1 -- the epoch is bumped by a one-lane kernel at the start
+// of every pass (graph replays included), so granules of an earlier pass never match.  Needs
+// every workgroup of the grid resident at once (the host checks grid <= CUs, one 1024-thread
+// workgroup per CU); a poll that never sees its tag gives up at kSpinCap and counts a fault.
+__device__ uint32_t g_step_epoch = 0;
+constexpr int kFusedMaxTiles = kMergedMaxN_ / kTile;
+struct FusedLds {
+  float cb[kMaxFlows * 4 * kH];       // nf_dyn fold of the row (tiled_fdyn_kernel's cb, flat)
+  float encfold[kMaxFlows * 4 * kH];  // the proposal fold over the encoding columns
+  double rowst[kFusedMaxTiles * 4];   // the row's x_dyn partials, tile order (tiled_ctx input)
+};
+__device__ __forceinline__ void publish_granules(uint64_t *g, double v, uint32_t tag) {
+  const uint64_t bits = (uint64_t)__double_as_longlong(v);
+  __hip_atomic_store(g, ((uint64_t)tag << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, ((uint64_t)tag << 32) | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wave 0 polls the row's granules (8 per tile) until every tag matches, then leaves the
+// doubles in fx->rowst; all threads call (one barrier)
+__device__ __forceinline__ void row_sync(const nfdpf_filter_desc &d, const TiledWs &ws, FusedLds *fx, uint32_t tag) {
+  const int tiles = n_tiles(d.N);
+  const int ng = tiles * 8;
+  if (threadIdx.x < 64) {
+    const uint64_t *g = ws.rowx + (int64_t)blockIdx.y * tiles * 8;
+    for (int base = 0; base < ng; base += 64) {
+      const int q = base + (int)threadIdx.x;
+      uint64_t v = 0;
+      bool ok = q >= ng;
+      for (int it = 0;; ++it) {
+        if (!ok) {
+          v = __hip_atomic_load(g + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = (uint32_t)(v >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        if (it >= kSpinCap) {
+          if (threadIdx.x == 0) atomicAdd(&g_split_fault, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (q < ng) reinterpret_cast<uint32_t *>(fx->rowst)[q] = (uint32_t)v;
+    }
+  }
+  __syncthreads();
+}
+
 // ---- K2: nf_dyn inverse; with defer_norm also the normalisation of slot t-1 (finish_prev's
 // arithmetic, its sums reduced together with this launch's in one barrier).  SPLIT: the
 // RealNVP nets on wave pairs (split.hpp) -- role 0 = t-nets (and the stores), role 1 =
@@ -376,11 +432,11 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
 // k / 4 in particle-group order (waves k / 4, 2 + k / 4, ...) -- the order of block_sum8_store
 // over the same particles.
 __device__ __forceinline__ void block_sum_roles_store(const double (&v)[4], double *dst0, double *dst1,
-                                                      double *sh) {
+                                                      double *sh, uint64_t *gran = nullptr, uint32_t tag = 0) {
   const int w = threadIdx.x >> 6;
   // a role whose destination is null skips its reductions (wave-uniform; fp64 DPP sums of 8
   // waves are a visible share of a short launch's epilogue)
-  if ((w & 1 ? dst1 : dst0) != nullptr) {
+  if (w < 8 && (w & 1 ? dst1 : dst0) != nullptr) {  // waves >= 8 (the fused step's) hold nothing here
     double w4[4] = {v[0], v[1], v[2], v[3]};
     wave_sum_dpp_n(w4);
     if ((threadIdx.x & 63) == 0)
@@ -395,6 +451,7 @@ __device__ __forceinline__ void block_sum_roles_store(const double (&v)[4], doub
       double a = sh[4 * r + k];
       for (int q = 1; q < 4; ++q) a += sh[4 * (2 * q + r) + k];
       dst[k] = a;
+      if (gran && r == 0) publish_granules(gran + 2 * k, a, tag);  // the fused step's row exchange
     }
   }
 }
@@ -492,7 +549,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kTile : kTile) void tiled_dyn_kernel(co
 // its deferred normalisation moves to the proposal launch (the scratch row is double-
 // buffered by step parity, so step t's propose / prior do not overwrite step t-1's).
 // Dynamic LDS: C[max(N, B_global)], w'[N], p_{t-1}[N].
-__global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+template <bool FUSED>
+__device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const TiledWs &ws, FusedLds *fx,
+                                          uint32_t tag) {
   extern __shared__ float dyn_lds[];
   __shared__ double shd[64];
   __shared__ float shf[16];
@@ -511,7 +570,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   const SplitLane sl = split_lane(8);
   const int role = sl.role, slot = sl.slot;
   const int i = tile * kTile + slot;
-  const bool valid = i < N;
+  const bool valid = i < N && (!FUSED || role < 2);  // fused: waves 8-15 carry no particle here
   const int64_t grow = d.row_base + b;
   const bool defer = d.defer_norm && d.t > 0;
   const bool shifted = shifted_meas(d.measurement);
@@ -549,11 +608,13 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
 #pragma unroll
     for (int c = 0; c < kOctxDyn; ++c) fw[1 + c] = r.w1c[2 * (r.j * kOctxDyn + c) + r.w];
   }
-  const bool enc_fold_lane =
-      d.nf_cond && tile == 0 && threadIdx.x >= kTile && threadIdx.x - kTile < d.n_flows * 4 * kH;
+  // fused: every workgroup folds for itself, on the otherwise idle waves 8-15
+  const int enc_fold_t0 = FUSED ? 2 * kTile : kTile;
+  const bool enc_fold_lane = d.nf_cond && (FUSED || tile == 0) && threadIdx.x >= enc_fold_t0 &&
+                             threadIdx.x - enc_fold_t0 < d.n_flows * 4 * kH;
   float enc_fold = 0.f;
   if (enc_fold_lane) {  // proposal fold over the encoding columns (model/models.py:338-346); K3 adds mean/std
-    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), threadIdx.x - kTile);
+    const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), threadIdx.x - enc_fold_t0);
     enc_fold = fold_acc(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
   }
   // the row's sums over x_phys = (x_src + vel) + eps (motion_apply_eps's arithmetic)
@@ -589,12 +650,12 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
       const float s = cascade_row_sum([&](int r) { return Cbuf[r]; }, d.B_global);
       if (threadIdx.x == 0) fire_sh = (s / (float)d.B_global) < 0.5f * (float)N;
     }
-  } else if (spec) {
+  } else if (spec && (!FUSED || threadIdx.x < 2 * kTile)) {
     // every source load of this thread first (one memory latency instead of one per
     // particle), then the draws and sums; N <= kMergedMaxN = 4096 -> <= 10 per thread
     constexpr int kPer = 10;
     const float *src = defer ? Sp.hx : xprev;
-    const int j0 = threadIdx.x - 64, js = blockDim.x - 64;
+    const int j0 = threadIdx.x - 64, js = 2 * kTile - 64;  // waves 1-7 (fused too: the same sums)
     float xs0[kPer], xs1[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
@@ -693,8 +754,9 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
   // the row context: wave sums (DPP), then the 8 wave partials in wave order, in every thread
   {
     double w4[4] = {a0, a1, c0, c1};
-    wave_sum_dpp_n(w4);
     const int w = threadIdx.x >> 6;
+    // the fused step's waves 8-15 accumulated nothing unless they resampled: zeros, no DPP
+    if (!FUSED || w < 8 || mode != kSrcPrev || !spec) wave_sum_dpp_n(w4);
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
       for (int k = 0; k < 4; ++k) shd[4 * w + k] = w4[k];
@@ -703,7 +765,7 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
     a1 = shd[1];
     c0 = shd[2];
     c1 = shd[3];
-    for (int q = 1; q < 8; ++q) {
+    for (int q = 1; q < (int)(blockDim.x >> 6); ++q) {
       a0 += shd[4 * q];
       a1 += shd[4 * q + 1];
       c0 += shd[4 * q + 2];
@@ -718,10 +780,16 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
     for (int q = 0; q < kOctxDyn; ++q) v = fmaf(fw[1 + q], cv[q], v);
     reinterpret_cast<float *>(cb)[threadIdx.x] = v;
     reinterpret_cast<float *>(cbs)[split_cb_index(threadIdx.x)] = v;
+    if (FUSED) fx->cb[threadIdx.x] = v;
   }
-  if (enc_fold_lane) ws.cb_cond[b * kCb + threadIdx.x - kTile] = enc_fold;
+  if (enc_fold_lane) {
+    if (FUSED)
+      fx->encfold[threadIdx.x - enc_fold_t0] = enc_fold;
+    else
+      ws.cb_cond[b * kCb + threadIdx.x - kTile] = enc_fold;
+  }
   __syncthreads();
-  if (tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
+  if (!FUSED && tile == 0 && threadIdx.x < d.n_flows * 4 * kH)  // K3's nf_dyn forward uses the same fold
     ws.cb_dyn[b * kCb + threadIdx.x] = reinterpret_cast<const float *>(cb)[threadIdx.x];
   TRACE(0, 2)
   double sd[4] = {0, 0, 0, 0};
@@ -744,8 +812,13 @@ __global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filte
       sd[3] = (double)xd1 * xd1;
     }
   }
-  block_sum_roles_store(sd, ws.st_dyn + ((int64_t)b * tiles + tile) * 4, nullptr, shd);
+  block_sum_roles_store(sd, ws.st_dyn + ((int64_t)b * tiles + tile) * 4, nullptr, shd,
+                        FUSED ? ws.rowx + ((int64_t)b * tiles + tile) * 8 : nullptr, tag);
   TRACE(0, 3)
+}
+
+__global__ __launch_bounds__(2 * kTile) void tiled_fdyn_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  fdyn_part<false>(d, ws, nullptr, 0u);
 }
 
 // softmax partials of the unshifted log-weight u over this tile
@@ -1127,8 +1200,8 @@ __device__ __forceinline__ void merge_partials_quad(double *sm, double *fin, con
 // runs BESIDE the nf_dyn forward: the launch costs proposal + max(nf_dyn forward, encoder)
 // instead of their sum, at four waves per SIMD.  While it waits for the proposal the encoder
 // t-wave normalises slot t-1's particles (the deferred normalisation).  1024 threads per tile.
-template <bool MERGED>
-__global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+template <bool MERGED, bool FUSED>
+__device__ __forceinline__ void quad_part(const nfdpf_filter_desc &d, const TiledWs &ws, const FusedLds *fx) {
   __shared__ StepShared L;
   __shared__ __attribute__((aligned(8))) float xbuf[8 * kTile];              // flow-pair hand-offs (pair_swap)
 #ifdef NFDPF_ENC_VALU
@@ -1184,15 +1257,16 @@ __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_
   if (threadIdx.x >= 4 && threadIdx.x < 8) rflag[threadIdx.x - 4] = 0;
   const int ncb = d.n_flows * 4 * kH;
   if (threadIdx.x < ncb)
-    reinterpret_cast<float *>(L.cb_dyn)[split_cb_index(threadIdx.x)] = ws.cb_dyn[b * kCb + threadIdx.x];
+    reinterpret_cast<float *>(L.cb_dyn)[split_cb_index(threadIdx.x)] =
+        FUSED ? fx->cb[threadIdx.x] : ws.cb_dyn[b * kCb + threadIdx.x];
   if (threadIdx.x >= kTile && threadIdx.x - kTile < ncb) {
     // finish the proposal fold: the encoding columns came from K1, add [mean, std] of x_dyn
     const int k = threadIdx.x - kTile;
-    const Ctx4 cp = tiled_ctx(ws.st_dyn, b, tiles, d.N);
+    const Ctx4 cp = FUSED ? tiled_ctx(fx->rowst, 0, tiles, d.N) : tiled_ctx(ws.st_dyn, b, tiles, d.N);
     const float c4[4] = {cp.m0, cp.m1, cp.s0, cp.s1};
     const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), k);
     reinterpret_cast<float *>(L.cb_cond)[split_cb_index(k)] =
-        fold_acc(r, d.E + 4, ws.cb_cond[b * kCb + k], c4, d.E, d.E + 4);
+        fold_acc(r, d.E + 4, FUSED ? fx->encfold[k] : ws.cb_cond[b * kCb + k], c4, d.E, d.E + 4);
   }
   __syncthreads();
   TRACE(2, 1)
@@ -1299,6 +1373,24 @@ __global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_
   TRACE(2, 3)
   QTRACE(5)
 }
+
+template <bool MERGED>
+__global__ __launch_bounds__(4 * kTile) void tiled_prop_quad_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  quad_part<MERGED, false>(d, ws, nullptr);
+}
+
+// ---- the fused step: front + nf_dyn inverse (fdyn_part), the row's x_dyn exchange
+// (row_sync), proposal + nf_dyn forward + cosine measurement (quad_part) -- one launch
+__global__ __launch_bounds__(4 * kTile) void tiled_step_fused_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  __shared__ FusedLds fx;
+  const uint32_t tag = (g_step_epoch << 16) + (uint32_t)d.t + 1u;
+  fdyn_part<true>(d, ws, &fx, tag);
+  TRACE(1, 0)
+  row_sync(d, ws, &fx, tag);
+  TRACE(1, 3)
+  quad_part<true, true>(d, ws, &fx);
+}
+__global__ void tiled_epoch_kernel() { g_step_epoch = g_step_epoch + 1u; }
 
 // ---- K3b (phase 2 of an EXTERNAL measurement): raw likelihood from lik_ext
 __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_desc d, TiledWs ws) {
@@ -1409,10 +1501,27 @@ __global__ void tiled_gate_batch_kernel(const double *__restrict__ parts, int B,
 static bool use_split(const nfdpf_filter_desc &d) { return d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP; }
 // front + dyn in one launch (tiled_fdyn_kernel), the deferred normalisation in the proposal
 // launch: the split-net path with the cosine measurement, rows short enough for LDS
-constexpr int kMergedMaxN = 4096;
+constexpr int kMergedMaxN = kMergedMaxN_;
 static bool use_merged(const nfdpf_filter_desc &d) {
   return use_split(d) && d.nf_cond && d.measurement == NFDPF_MEAS_COS && d.N <= kMergedMaxN &&
          d.B_global <= kMergedMaxN;
+}
+
+// One launch per step (tiled_step_fused_kernel), opt-in with NFDPF_FUSED_STEP=1, when every
+// workgroup of the grid can be resident at once -- one 1024-thread workgroup per CU -- since a
+// row's four workgroups wait for each other inside it.  Measured SLOWER than the two launches
+// at C2 (1.483 vs 1.471 ms per pass, one box; profiles/r02_experiments.md): the granule
+// exchange itself costs ~0.8 us against the 1.65 us launch gap it removes, but the front half
+// runs 2.3 us longer inside the 16-wave workgroup than as its own 8-wave launch, and the
+// proposal half's prologue stays at 2 us.  Kept, bit-identical, for that record and as a base.
+static bool use_fused(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_FUSED_STEP");  // read per call: tests compare both paths
+  if (!(e && e[0] == '1') || !use_merged(d) || d.phase != 0 || n_tiles(d.N) > kFusedMaxTiles) return false;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  return (int64_t)n_tiles(d.N) * d.B <= cus;
 }
 
 // The proposal launch.  With live timing requested (prof_events) the two events ride in the
@@ -1481,6 +1590,8 @@ extern "C" int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T) {
 }
 
 extern "C" int nfdpf_filter_tiled_tiles(int N) { return N <= 0 ? 0 : n_tiles(N); }
+
+extern "C" int nfdpf_filter_tiled_fused(const nfdpf_filter_desc *d) { return d && use_fused(*d) ? 1 : 0; }
 
 extern "C" int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, int force, int32_t *gate,
                                     void *stream) {
@@ -1579,7 +1690,15 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
                                                          : (size_t)d.B_global * 4;
     // live timing of the front launch (the resampler's) in its own dispatch, as launch_prop
     hipEvent_t *fev = d.prof_events && d.prof_front ? (hipEvent_t *)d.prof_events + 2 : nullptr;
-    if (use_merged(d)) {
+    if (use_fused(d)) {  // the whole step in one launch (the live timing on it)
+      const size_t mlds = (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4;
+      if (d.t == 0) tiled_epoch_kernel<<<1, 1, 0, st>>>();  // new tags for this pass
+      hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+      if (ev)
+        hipExtLaunchKernelGGL(tiled_step_fused_kernel, g, dim3(4 * kTile), mlds, st, ev[0], ev[1], 0, d, ws);
+      else
+        tiled_step_fused_kernel<<<g, 4 * kTile, mlds, st>>>(d, ws);
+    } else if (use_merged(d)) {
       const size_t mlds = (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4;
       if (fev)
         hipExtLaunchKernelGGL(tiled_fdyn_kernel, g, dim3(2 * kTile), mlds, st, fev[0], fev[1], 0, d, ws);
@@ -1590,14 +1709,16 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
     } else {
       tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
     }
-    if (use_merged(d))
+    if (use_fused(d))
+      ;  // the whole step ran in tiled_step_fused_kernel
+    else if (use_merged(d))
       ;  // nf_dyn ran in tiled_fdyn_kernel
     else if (use_split(d))
       tiled_dyn_kernel<true><<<g, 2 * kTile, 0, st>>>(d, ws);
     else if (d.nf_dyn)
       tiled_dyn_kernel<false><<<g, kTile, 0, st>>>(d, ws);
     hipEvent_t *ev = (hipEvent_t *)d.prof_events;
-    switch (d.measurement) {
+    if (!use_fused(d)) switch (d.measurement) {
       case NFDPF_MEAS_COS: dispatch_prop<NFDPF_MEAS_COS>(d, ws, g, st, ev); break;
       case NFDPF_MEAS_CRNVP: dispatch_prop<NFDPF_MEAS_CRNVP>(d, ws, g, st, ev); break;
       case NFDPF_MEAS_NN: dispatch_prop<NFDPF_MEAS_NN>(d, ws, g, st, ev); break;

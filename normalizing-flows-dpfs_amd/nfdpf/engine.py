@@ -289,6 +289,7 @@ class FilterEngine:
 
         fired = [] if host_mode else None
         self.last_ot_calls = 0
+        self.last_fused = False  # the step ran as one launch (tiled_step_fused_kernel), set at t = 0
         keep = []  # host uploads must outlive their kernels
         # per-step pointers precomputed as integers: the loop below is the launch path of every
         # time step, so it stays free of tensor slicing and per-call lookups
@@ -372,6 +373,8 @@ class FilterEngine:
                     d.ot_x = xo.data_ptr()
                 else:
                     d.ot_x = xin.data_ptr()  # not read: the motion stage keeps the previous particles
+            if t == 0 and tiled and not external:
+                self.last_fused = bool(L.lib().nfdpf_filter_tiled_fused(d_ref))
             d.prof_events = None
             d.prof_front = 0
             ev = None
@@ -381,11 +384,12 @@ class FilterEngine:
             every = c.kernel == "tiled" and not external
             if self.step_events is not None and (every or t == T // 2):
                 from .prof import EventPair
-                ev = EventPair(4 if every else 2)
+                ev = EventPair(4 if every and not self.last_fused else 2)
                 self.step_events.append(ev)
                 if not external:
                     d.prof_events = ev.ptr  # around the step's dominant launch, inside the library
-                    d.prof_front = int(every)  # and, tiled, around its front (resampling) launch
+                    # and, tiled, around its front (resampling) launch -- none in the fused step
+                    d.prof_front = int(every and not self.last_fused)
             if external:
                 d.phase = 1
                 step()
