@@ -301,9 +301,12 @@ def main():
         res = step()
     torch.cuda.synchronize()
     graph = None
-    spec_on = (world > 1) if args.speculate < 0 else bool(args.speculate)
-    spec = spec_on and args.kernel == "tiled" and flags["resampler_type"] == "soft" and not args.force_resample
-    if args.graph and flags["resampler_type"] == "soft" and (world == 1 or spec):
+    ot = flags["resampler_type"] == "ot"
+    # auto (engine.FilterEngine.run): speculative gates when sharded, and for OT at any world size
+    # unless the previous pass resampled (then its gates are read step by step)
+    spec_on = (world > 1 or ot) if args.speculate < 0 else bool(args.speculate)
+    spec = spec_on and args.kernel == "tiled" and not args.force_resample and not (ot and eng._ot_fired)
+    if args.graph and ((flags["resampler_type"] == "soft" and world == 1) or spec):
         # the pass has no host synchronisation in this mode: capture it once, replay per step
         # (every launch of every time step runs on each replay; only the Python launch path goes).
         # Sharded: the speculative-gate pass (engine.run(finish=False): no exchange inside) is

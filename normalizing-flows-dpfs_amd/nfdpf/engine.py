@@ -141,6 +141,9 @@ class FilterEngine:
         self.step_events = None  # list -> nfdpf.prof.EventPair around the dominant launch of step T//2 of every pass
         self._spec_backoff = 0  # auto speculative gate: passes to run per-step after the next miss / 2
         self._spec_skip = 0     # per-step passes left before speculating again
+        # OT, auto mode: did the last pass resample?  Then the next one reads its gates step by
+        # step (as the reference: one host sync per step); otherwise it speculates
+        self._ot_fired = False
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -211,14 +214,21 @@ class FilterEngine:
         p0, ie0 = ops.normalize_log_probs(logw0)
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
+        ot_auto = auto and tiled and c.resampler == "ot"
         if speculate is None:
-            speculate = c.speculate_gate if c.speculate_gate is not None else shard.world > 1
-        if auto and speculate and self._spec_skip > 0:
+            # auto: sharded (one exchange per pass instead of one per step), and OT at any world
+            # size -- its gate is read on the host before every Sinkhorn call (DPFs.py:165), a
+            # device->host sync per step that keeps the pass out of a graph; speculating, a pass
+            # whose gates all stay off has no sync and no Sinkhorn launch at all
+            speculate = c.speculate_gate if c.speculate_gate is not None else (shard.world > 1 or ot_auto)
+        if ot_auto and self._ot_fired:
+            speculate = False  # the last pass resampled: per-step gates, no wasted speculative pass
+        elif auto and speculate and self._spec_skip > 0:
             # auto mode after a fired gate: the per-step exchange for the next passes (a miss
             # costs a whole second pass -- profiles/r02_dist_*.json), retried with backoff
             self._spec_skip -= 1
             speculate = False
-        spec = bool(speculate and tiled and c.resampler == "soft" and not host_mode and teacher is None
+        spec = bool(speculate and tiled and c.resampler in ("soft", "ot") and not host_mode and teacher is None
                     and not c.force_resample and not external)
 
         f32 = dict(device=dev, dtype=torch.float32)
@@ -346,13 +356,15 @@ class FilterEngine:
                 nz = nz.to(dev).contiguous()
                 keep.append(nz)
                 d.host_noise = nz.data_ptr()
-            elif c.resampler == "ot":
+            elif c.resampler == "ot" and not spec:
                 if tiled:
                     ops.ess_gate_tiled(ess_all, N, t, c.force_resample, out=gate_buf)
                 else:
                     ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
                 d.gate = gate_buf.data_ptr()
-            if c.resampler == "ot":
+            if c.resampler == "ot" and spec:
+                d.ot_x = x0.data_ptr()  # not read: every gate is taken as off (verified after the pass)
+            elif c.resampler == "ot":
                 if t == 0:
                     xin, pin = x0, p0
                 elif teacher is not None:
@@ -411,6 +423,8 @@ class FilterEngine:
         # a wave-pair hand-off that timed out leaves stale data (csrc/split.hpp): fail loudly
         if tiled and d.split_nets and not torch.cuda.is_current_stream_capturing():
             L.check_split_fault("nfdpf_filter_step_tiled")
+        if c.resampler == "ot" and not spec:
+            self._ot_fired = self.last_ot_calls > 0
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)
         if spec:
@@ -422,7 +436,9 @@ class FilterEngine:
                 self._spec_backoff = 0
                 return res
             # a gate fired: the pass again, with the per-step exchange
-            if auto:
+            if ot_auto:
+                self._ot_fired = True  # the rerun below sets it from its own OT calls
+            elif auto:
                 self._spec_backoff = min(2 * self._spec_backoff or 1, 64)
                 self._spec_skip = self._spec_backoff
             return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, speculate=False)
