@@ -163,6 +163,44 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
   return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
 }
 
+__device__ __forceinline__ double wave_max_dpp_d(double v) {
+  v = fmax(v, dpp_d<kDppXor1>(v));
+  v = fmax(v, dpp_d<kDppXor2>(v));
+  v = fmax(v, dpp_d<kDppHalfMirror>(v));
+  v = fmax(v, dpp_d<kDppMirror>(v));
+  return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+}
+// block_max of a float with the wave step on DPP (block_max: six shuffle rounds); same result
+__device__ __forceinline__ float block_max_dpp(float v, float *sh) {
+  v = wave_max_dpp(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+  float r = sh[0];
+  for (int i = 1; i < nw; ++i) r = fmaxf(r, sh[i]);
+  return r;
+}
+// K workgroup maxima with one LDS exchange (DPP inside each wave); every thread gets all K.
+// `sh` holds K doubles per wave.  (block_max below: shuffles and two barriers per value.)
+template <int K>
+__device__ __forceinline__ void block_max_n(double (&v)[K], double *sh) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_max_dpp_d(v[k]);
+  __syncthreads();  // sh may still be read by a previous reduction
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) sh[K * (threadIdx.x >> 6) + k] = v[k];
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double r = sh[k];
+    for (int i = 1; i < nw; ++i) r = fmax(r, sh[K * i + k]);
+    v[k] = r;
+  }
+}
+
 // Four workgroup sums with ONE barrier; thread q < 4 stores sum q to dst[q].  `sh` holds
 // 4 doubles per wave and must not be in use by a concurrent reduction.
 __device__ __forceinline__ void block_sum4_store(double a, double b, double c, double e, double *sh,

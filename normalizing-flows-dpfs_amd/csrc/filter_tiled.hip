@@ -940,7 +940,7 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   TRACE(2, 2)
   if (MEAS == NFDPF_MEAS_EXTERNAL) return;  // phase 1: the external likelihood comes next
   double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
-  const float lm = meas_shifted<MEAS>() ? block_max(lk, L.f) : 0.f;
+  const float lm = meas_shifted<MEAS>() ? block_max_dpp(lk, L.f) : 0.f;
   if (threadIdx.x == 0) sm[3] = lm;
   __shared__ double smd[48];
   store_softmax(u, valid, sm, L.f + 8, smd);  // L.f[0:8] held block_max
@@ -1034,7 +1034,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   TRACE(2, 2)
   double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
   // the measurement waves hold lk, the others -inf
-  const float lm = meas_shifted<MEAS>() ? block_max(lk, L.f) : 0.f;
+  const float lm = meas_shifted<MEAS>() ? block_max_dpp(lk, L.f) : 0.f;
   if (threadIdx.x == 0) sm[3] = lm;
   store_softmax(u, valid && flows, sm, smf, smd);
   TRACE(2, 3)
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_
     u = stage_logw(S, i, lk);
   }
   double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
-  const float m = block_max(lk, shf);
+  const float m = block_max_dpp(lk, shf);
   if (threadIdx.x == 0) sm[3] = m;
   store_softmax(u, valid, sm, shf + 8, shd2);  // shf[0:8] held block_max
 }

@@ -66,7 +66,21 @@ constexpr float kLo = 0x1.0p-60f, kHi = 0x1.0p60f;  // outside: the lane recompu
 // lane's sum is ~1), i.e. c_ij <= 24 + (M_s - m_i): up to 96 every such K_ij = 2^-c_ij and
 // alpha_j K_ij stay >= 2^-120, normal fp32 (2^-126); only terms below 2^-24 of the sum can
 // underflow.  (60 in r01: late, small-epsilon iterations took the two-exp form on most slices.)
-constexpr float kRisky = 96.f;
+#ifndef NFDPF_OT_RISKY
+#define NFDPF_OT_RISKY 96.f
+#endif
+constexpr float kRisky = NFDPF_OT_RISKY;
+// Prescaled coordinates (-DNFDPF_OT_PRESCALE): the iteration / final tables' X, Y planes and the
+// lanes' own points are multiplied by s = sqrt(sc) (sc = the base-2 cost scale of the table's
+// epsilon), so the pair exponent is -(dx'^2 + dy'^2) with no per-pair scaling multiply.
+// Measured (round 2d, one box): C4 +3 %, C3 forced +1 %, but the full-size C3 teacher-forced
+// likelihood error grows to 0.14 against the reference's own fp32 error of 0.0098 (the
+// difference of two prescaled coordinates rounds ~5x coarser on close pairs): not shipped.
+#ifdef NFDPF_OT_PRESCALE
+constexpr bool kPrescale = true;
+#else
+constexpr bool kPrescale = false;
+#endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 sp2(float v) { return f2{v, v}; }
@@ -339,25 +353,30 @@ __device__ __forceinline__ void slice_blocks(const float *sl, const int (&pl)[NP
   }
 }
 
-struct LaneI {  // the kR points of a lane, as packed splats
-  f2 x[kR], y[kR];
+template <int KR>
+struct LaneIK {  // the KR points of a lane, as packed splats
+  f2 x[KR], y[KR];
 };
+using LaneI = LaneIK<kR>;
 
 // Shifted-exponent block (planes X, Y, E_0..E_{NH-1}, V_0..V_{NV-1}; E = h - M_s):
 //   acc[r][w] += 2^(E_w[j] + o[r][w] - sc |p_i - p_j|^2),  accv[r][v] += (w = 0 term) V_v[j]
-template <int NH, int NV, int NP>
-__device__ __forceinline__ void hblock(const TBlock<NP> &B, const LaneI &L, f2 nsc2, const f2 (&o)[kR][NH],
-                                       f2 (&acc)[kR][NH], f2 (&accv)[kR][NV > 0 ? NV : 1]) {
+// PS: prescaled points (the lane's and the table's X, Y times sqrt(sc)): the exponent is
+// E + o - (dx^2 + dy^2), nsc2 unused.
+template <int NH, int NV, int NP, bool PS = false, int KR>
+__device__ __forceinline__ void hblock(const TBlock<NP> &B, const LaneIK<KR> &L, f2 nsc2, const f2 (&o)[KR][NH],
+                                       f2 (&acc)[KR][NH], f2 (&accv)[KR][NV > 0 ? NV : 1]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
+    for (int r = 0; r < KR; ++r) {
       const f2 dx = L.x[r] - tpair(B, 0, q);
       const f2 dy = L.y[r] - tpair(B, 1, q);
-      const f2 d2 = pfma2(dy, dy, dx * dx);
+      const f2 d2 = (PS && NH == 1) ? f2{} : pfma2(dy, dy, dx * dx);
 #pragma unroll
       for (int w = 0; w < NH; ++w) {
-        const f2 a = pfma2(nsc2, d2, tpair(B, 2 + w, q) + o[r][w]);
+        const f2 eo = tpair(B, 2 + w, q) + o[r][w];
+        const f2 a = !PS ? pfma2(nsc2, d2, eo) : NH == 1 ? pfma2(-dy, dy, pfma2(-dx, dx, eo)) : eo - d2;
         const f2 t = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
         acc[r][w] += t;
         if (w == 0)
@@ -370,14 +389,15 @@ __device__ __forceinline__ void hblock(const TBlock<NP> &B, const LaneI &L, f2 n
 
 // Shared-kernel block of the two iteration softmins (planes X, Y, alpha, beta): one
 // v_exp_f32 per pair, K = 2^(-sc |p_i - p_j|^2);  acc[r][0] += alpha_j K,  acc[r][1] += beta_j K
-__device__ __forceinline__ void kblock(const TBlock<4> &B, const LaneI &L, f2 nsc2, f2 (&acc)[kR][2]) {
+template <int KR>
+__device__ __forceinline__ void kblock(const TBlock<4> &B, const LaneIK<KR> &L, f2 nsc2, f2 (&acc)[KR][2]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
+    for (int r = 0; r < KR; ++r) {
       const f2 dx = L.x[r] - tpair(B, 0, q);
       const f2 dy = L.y[r] - tpair(B, 1, q);
-      const f2 a = pfma2(dy, dy, dx * dx) * nsc2;
+      const f2 a = kPrescale ? -pfma2(dy, dy, dx * dx) : pfma2(dy, dy, dx * dx) * nsc2;
       const f2 k = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
       acc[r][0] = pfma2(tpair(B, 2, q), k, acc[r][0]);
       acc[r][1] = pfma2(tpair(B, 3, q), k, acc[r][1]);
@@ -393,12 +413,12 @@ __device__ __forceinline__ float slice_off(double Ms, double m) {
 }
 
 // The lane's kR points and shifts: pt(i, x, y, m[NH]) for i = 256 s0 + lane + 64 r (i < N).
-template <int NH, class Pt>
-__device__ __forceinline__ void lane_points(int N, const Pt &pt, LaneI &L, double (&m)[kR][NH]) {
+template <int NH, class Pt, int KR>
+__device__ __forceinline__ void lane_points(int N, const Pt &pt, LaneIK<KR> &L, double (&m)[KR][NH], int rbase = 0) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int r = 0; r < kR; ++r) {
-    const int i = blockIdx.x * kOtThreads + lane + 64 * r;
+  for (int r = 0; r < KR; ++r) {
+    const int i = blockIdx.x * kOtThreads + lane + 64 * (rbase + r);
     float x = 0.f, y = 0.f;
     double mm[NH];
 #pragma unroll
@@ -412,13 +432,15 @@ __device__ __forceinline__ void lane_points(int N, const Pt &pt, LaneI &L, doubl
 }
 
 // Combine the waves' partials through LDS: thread t gets out[k] for its i (wave order).
-template <int NK>
-__device__ __forceinline__ void combine(float *lds, const float (&mine)[kR][NK], float (&out)[NK]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// (8-wave iteration launches: waves w and w + 4 hold the same slices for the two halves of the
+// lanes' i, rbase 0 / 2; both write slot w % 4, so the sums meet in the 4-wave order.)
+template <int NK, int KR>
+__device__ __forceinline__ void combine(float *lds, const float (&mine)[KR][NK], float (&out)[NK], int rbase = 0) {
+  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) % kWaves;
 #pragma unroll
-  for (int r = 0; r < kR; ++r)
+  for (int r = 0; r < KR; ++r)
 #pragma unroll
-    for (int k = 0; k < NK; ++k) lds[(w * NK + k) * kOtThreads + lane + 64 * r] = mine[r][k];
+    for (int k = 0; k < NK; ++k) lds[(w * NK + k) * kOtThreads + lane + 64 * (rbase + r)] = mine[r][k];
   __syncthreads();
   const int t = threadIdx.x % kOtThreads;  // threads >= kOtThreads get a copy (unused)
 #pragma unroll
@@ -429,10 +451,22 @@ __device__ __forceinline__ void combine(float *lds, const float (&mine)[kR][NK],
   }
 }
 
+// the scale of prescaled points (kPrescale): identical in the table writers and the pair loops
+__device__ __forceinline__ float pscale(float sc) { return sqrtf(sc); }
+template <int KR>
+__device__ __forceinline__ void prescale(LaneIK<KR> &L, float sc) {
+  const f2 s = sp2(pscale(sc));
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    L.x[r] *= s;
+    L.y[r] *= s;
+  }
+}
+
 // Workgroup sums over the whole row with the shifted-exponent block (table planes 0, 1,
 // 2 .. 2+NH+NV, slice maxima msh[s * MS + w]): thread t gets, for i = 256 s0 + t,
 //   S[w] = sum_j 2^(h_w[j] - sc |p_i - p_j|^2 - m_i[w]),  SV[v] = sum_j (w = 0 term) V_v[j].
-template <int NH, int NV, int MS, class Pt>
+template <int NH, int NV, int MS, bool PS = false, class Pt>
 __device__ __forceinline__ void wg_table_sums(const float *tab, const double *msh, int splits, int64_t Np, int N,
                                               float sc, const Pt &pt, float *lds, float (&S)[NH], float *SV) {
   constexpr int NP = 2 + NH + NV;
@@ -442,6 +476,7 @@ __device__ __forceinline__ void wg_table_sums(const float *tab, const double *ms
   LaneI L;
   double m[kR][NH];
   lane_points<NH>(N, pt, L, m);
+  if (PS) prescale(L, sc);
   const f2 nsc2 = sp2(-sc);
   f2 acc[kR][NH], accv[kR][NV > 0 ? NV : 1];
 #pragma unroll
@@ -463,10 +498,10 @@ __device__ __forceinline__ void wg_table_sums(const float *tab, const double *ms
       for (int w = 0; w < NH; ++w) o[r][w] = sp2(slice_off(msh[s * MS + w], m[r][w]));
 #ifndef NFDPF_OT_L1
     slice_copy<NP>(tab, Np, s * kOtThreads, sl);
-    slice_blocks<NP>(sl, pl, [&](const TBlock<NP> &B) { hblock<NH, NV>(B, L, nsc2, o, acc, accv); });
+    slice_blocks<NP>(sl, pl, [&](const TBlock<NP> &B) { hblock<NH, NV, NP, PS>(B, L, nsc2, o, acc, accv); });
 #else
     pipelined<NP>(tab, Np, s * kOtThreads, (s + 1) * kOtThreads, pl,
-                  [&](const TBlock<NP> &B) { hblock<NH, NV>(B, L, nsc2, o, acc, accv); });
+                  [&](const TBlock<NP> &B) { hblock<NH, NV, NP, PS>(B, L, nsc2, o, acc, accv); });
 #endif
   }
   float mine[kR][NH + NV], out[NH + NV];
@@ -487,35 +522,56 @@ __device__ __forceinline__ void wg_table_sums(const float *tab, const double *ms
 // The two softmins of an iteration over an iteration table (planes X, Y, h_a - M, h_b - M,
 // alpha, beta; maxima msh[2 s], msh[2 s + 1]): one exp per pair for both unless some lane of
 // the wave is "risky" for the slice (see the file header).
-template <class Pt>
+// W = 8 (iteration launches of small grids, ot_iter_waves): waves w and w + 4 take the same
+// slices, each for half of the lanes' i (KR = 2), so every (i, slice) sum and the order in
+// which they meet are those of the 4-wave launch -- bit-identical, twice the waves per SIMD.
+template <int W = kWaves, class Pt>
 __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh, int splits, int64_t Np, int N,
                                              float sc, const Pt &pt, float *lds, float (&S)[2]) {
+  static_assert(W == kWaves || W == 2 * kWaves, "iteration waves");
+  constexpr int KR = W == kWaves ? kR : kR / 2;
   const int plk[4] = {0, 1, 4, 5}, plh[4] = {0, 1, 2, 3};
-  LaneI L;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rbase = W == kWaves ? 0 : (wv / kWaves) * KR;
+  // all kR points' shifts (the two-exp decision is taken over all of them, as in the 4-wave
+  // launch); the wave's own KR points (rbase is wave-uniform: selects, no register indexing)
+  LaneI La;
   double m[kR][2];
-  lane_points<2>(N, pt, L, m);
-  const f2 nsc2 = sp2(-sc);
-  float Sk[kR][2];
-  f2 hacc[kR][2];
-  f2 none[kR][1];
+  lane_points<2>(N, pt, La, m);
+  LaneIK<KR> L;
 #pragma unroll
-  for (int r = 0; r < kR; ++r) {
+  for (int r = 0; r < KR; ++r) {
+    L.x[r] = rbase ? La.x[(kR - KR + r) % kR] : La.x[r];
+    L.y[r] = rbase ? La.y[(kR - KR + r) % kR] : La.y[r];
+  }
+  if (kPrescale) prescale(L, sc);
+  const f2 nsc2 = sp2(-sc);
+  float Sk[KR][2];
+  f2 hacc[KR][2];
+  f2 none[KR][1];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
     Sk[r][0] = Sk[r][1] = 0.f;
     hacc[r][0] = hacc[r][1] = sp2(0.f);
   }
-  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w0 = wv % kWaves;  // the wave's slice set
 #ifndef NFDPF_OT_L1
-  float *sl = lds + kLdsPart + w0 * kSliceFloats;
+  float *sl = lds + kLdsPart + wv * kSliceFloats;
 #endif
   for (int s = w0; s < splits; s += kWaves) {
     const double Ma = msh[2 * s], Mb = msh[2 * s + 1];
-    float oa[kR], ob[kR];
+    float oa4[kR], ob4[kR], oa[KR], ob[KR];
     bool risky = false;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      oa[r] = slice_off(Ma, m[r][0]);
-      ob[r] = slice_off(Mb, m[r][1]);
-      risky |= (oa[r] > kRisky) || (ob[r] > kRisky);
+      oa4[r] = slice_off(Ma, m[r][0]);
+      ob4[r] = slice_off(Mb, m[r][1]);
+      risky |= (oa4[r] > kRisky) || (ob4[r] > kRisky);
+    }
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      oa[r] = rbase ? oa4[(kR - KR + r) % kR] : oa4[r];
+      ob[r] = rbase ? ob4[(kR - KR + r) % kR] : ob4[r];
     }
     const int j0 = s * kOtThreads, j1 = j0 + kOtThreads;
 #ifndef NFDPF_OT_L1
@@ -526,33 +582,33 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
 #define OT_SLICE_LOOP(PL, ...) pipelined<4>(tab, Np, j0, j1, PL, __VA_ARGS__)
 #endif
     if (__builtin_amdgcn_ballot_w64(risky) == 0) {
-      f2 acc[kR][2];
+      f2 acc[KR][2];
 #pragma unroll
-      for (int r = 0; r < kR; ++r) acc[r][0] = acc[r][1] = sp2(0.f);
+      for (int r = 0; r < KR; ++r) acc[r][0] = acc[r][1] = sp2(0.f);
       OT_SLICE_LOOP(plk, [&](const TBlock<4> &B) { kblock(B, L, nsc2, acc); });
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
+      for (int r = 0; r < KR; ++r) {
         Sk[r][0] = fmaf(exp2f(oa[r]), hsum2(acc[r][0]), Sk[r][0]);
         Sk[r][1] = fmaf(exp2f(ob[r]), hsum2(acc[r][1]), Sk[r][1]);
       }
     } else {
-      f2 o[kR][2];
+      f2 o[KR][2];
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
+      for (int r = 0; r < KR; ++r) {
         o[r][0] = sp2(oa[r]);
         o[r][1] = sp2(ob[r]);
       }
-      OT_SLICE_LOOP(plh, [&](const TBlock<4> &B) { hblock<2, 0>(B, L, nsc2, o, hacc, none); });
+      OT_SLICE_LOOP(plh, [&](const TBlock<4> &B) { hblock<2, 0, 4, kPrescale>(B, L, nsc2, o, hacc, none); });
     }
 #undef OT_SLICE_LOOP
   }
-  float mine[kR][2], out[2];
+  float mine[KR][2], out[2];
 #pragma unroll
-  for (int r = 0; r < kR; ++r) {
+  for (int r = 0; r < KR; ++r) {
     mine[r][0] = Sk[r][0] + hsum2(hacc[r][0]);
     mine[r][1] = Sk[r][1] + hsum2(hacc[r][1]);
   }
-  combine<2>(lds, mine, out);
+  combine<2>(lds, mine, out, rbase);
   S[0] = out[0];
   S[1] = out[1];
 }
@@ -589,9 +645,10 @@ __device__ __forceinline__ double lse2_from(float S, double m, const float *xs, 
 // Thread's column of a table (j = kOtThreads blockIdx.x + threadIdx.x, threads < kOtThreads): planes X, Y, then NE exponent
 // planes stored as h - M_s (slice maxima to msh[blockIdx.x * NE + e]), then NV value planes.
 // With ALPHA, planes 2 + NE + e hold 2^(h_e - M_s) (the iteration table's alpha / beta).
+// The slice maxima M[e] come from the caller (col_max: one workgroup reduction for all of them).
 template <int NE, int NV, bool ALPHA>
-__device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, bool valid, float X, float Y,
-                                          const double (&h)[NE], const float *vals, double *shd) {
+__device__ __forceinline__ void write_col_m(float *tab, double *msh, int64_t Np, bool valid, float X, float Y,
+                                            const double (&h)[NE], const double *Ms, const float *vals) {
   const int64_t j = (int64_t)blockIdx.x * kOtThreads + threadIdx.x;
   const bool own = threadIdx.x < kOtThreads;  // the slice's columns; other threads only reduce
   valid = valid && own;
@@ -602,7 +659,7 @@ __device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, b
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
     const double he = valid ? h[e] : -INFINITY;
-    const double M = block_max(he, shd);
+    const double M = Ms[e];
     const float E = (he > -INFINITY) ? (float)(he - M) : -INFINITY;
     if (own) tab[(2 + e) * Np + j] = E;
     if (ALPHA && own) tab[(2 + NE + e) * Np + j] = E > -INFINITY ? __builtin_amdgcn_exp2f(E) : 0.f;
@@ -611,6 +668,21 @@ __device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, b
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     if (own) tab[(2 + NE + (ALPHA ? NE : 0) + v) * Np + j] = valid ? vals[v] : 0.f;
+}
+// the column's exponents as the inputs of the slice maxima (-inf outside the slice)
+template <int NE>
+__device__ __forceinline__ void col_exps(bool valid, const double (&h)[NE], double *out) {
+  valid = valid && threadIdx.x < kOtThreads;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) out[e] = valid ? h[e] : -INFINITY;
+}
+template <int NE, int NV, bool ALPHA>
+__device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, bool valid, float X, float Y,
+                                          const double (&h)[NE], const float *vals, double *shd) {
+  double M[NE];
+  col_exps<NE>(valid, h, M);
+  block_max_n<NE>(M, shd);
+  write_col_m<NE, NV, ALPHA>(tab, msh, Np, valid, X, Y, h, M, vals);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -621,7 +693,7 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
                                                         OtWs ws, const int32_t *gate, double sf,
                                                         double eps) {
   if (gate && *gate == 0) return;
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   __shared__ float shf[16];
   const int b = blockIdx.x;
   const float *xr = x + (int64_t)b * N * 2;
@@ -682,47 +754,60 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
 // table of the initial softmins at eps0 (:120-121): h_a = logw, h_b = logu (base 2)
 __global__ __launch_bounds__(kOtBlock) void ot_prep_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   const int b = blockIdx.y, N = P.N, i = blockIdx.x * kOtThreads + threadIdx.x;
   const bool v = i < N && threadIdx.x < kOtThreads;
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const double h[2] = {v ? (double)ws.logw[(int64_t)b * N + i] * kLog2ed : 0.0, ws.rowc[b * 4 + 1] * kLog2ed};
-  write_col<2, 0, true>(tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), np_of(P), v, v ? xs[2 * i] : 0.f,
-                        v ? xs[2 * i + 1] : 0.f, h, nullptr, shd);
+  const float s = kPrescale ? pscale(cost_scale(1.0 / ws.rowc[b * 4])) : 1.f;  // ot_init's epsilon
+  write_col<2, 0, true>(tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), np_of(P), v, v ? xs[2 * i] * s : 0.f,
+                        v ? xs[2 * i + 1] * s : 0.f, h, nullptr, shd);
 }
 
 // Table columns of state `ks` (the potentials a_y, b_x of thread i just produced): for the
 // iteration that consumes it (epsilon e_ks) and, for a row whose epsilon is still annealing,
 // at the final epsilon (the post-loop softmin :173-176, should the batch stop right here).
+// All slice maxima of both tables -- and the caller's residual maximum *dmax, if given -- in ONE
+// workgroup reduction (shd: 5 doubles per wave).  r02c took two barriers and a shuffle chain
+// per maximum (up to 5 per iteration launch).
 __device__ __forceinline__ void emit_state_tables(const OtParams &P, const OtWs &ws, int b, int ks, bool v,
                                                   float xi, float yi, float lw, double logu, double ay,
-                                                  double bx, double *shd) {
+                                                  double bx, double *shd, double *dmax = nullptr) {
   const int64_t Np = np_of(P);
   const double e = eps_at(ws, P, b, ks);
+  const bool fin = e != P.eps;  // the row is still annealing: also the final-epsilon table
+  const double inv = 1.0 / e, invF = 1.0 / P.eps;
+  const double hI[2] = {((double)lw + bx * inv) * kLog2ed, (logu + ay * inv) * kLog2ed};
+  const double hF[2] = {((double)lw + bx * invF) * kLog2ed, (logu + ay * invF) * kLog2ed};
+  double M[5];
+  col_exps<2>(v, hI, M);
+  col_exps<2>(v && fin, hF, M + 2);
+  M[4] = dmax ? *dmax : 0.0;
+  block_max_n<5>(M, shd);
+  if (dmax) *dmax = M[4];
   {
-    const double inv = 1.0 / e;
-    const double h[2] = {((double)lw + bx * inv) * kLog2ed, (logu + ay * inv) * kLog2ed};
-    write_col<2, 0, true>(tabI_row(ws, P, ks & 1, b), mI_row(ws, P, ks & 1, b), Np, v, xi, yi, h, nullptr, shd);
+    const float s = kPrescale ? pscale(cost_scale(inv)) : 1.f;
+    write_col_m<2, 0, true>(tabI_row(ws, P, ks & 1, b), mI_row(ws, P, ks & 1, b), Np, v, xi * s, yi * s, hI, M,
+                            nullptr);
   }
-  if (e != P.eps) {
-    const double inv = 1.0 / P.eps;
-    const double h[2] = {((double)lw + bx * inv) * kLog2ed, (logu + ay * inv) * kLog2ed};
-    write_col<2, 0, false>(ws.tabF + (int64_t)b * 4 * Np, ws.mF + (int64_t)b * P.splits * 2, Np, v, xi, yi, h,
-                           nullptr, shd);
+  if (fin) {
+    const float s = kPrescale ? pscale(cost_scale(invF)) : 1.f;
+    write_col_m<2, 0, false>(ws.tabF + (int64_t)b * 4 * Np, ws.mF + (int64_t)b * P.splits * 2, Np, v, xi * s,
+                             yi * s, hF, M + 2, nullptr);
   }
 }
 
 // the two softmins of an iteration for thread t's i (shifts ma / mb, base 2), from the
 // workgroup sums with the lanes' shifts pt(i) -> (x, y, {m_a, m_b}); exact when a sum left
 // the safe range.  Returns the softmins -e ln2 LSE2 in fp64.
-template <class Pt, class HA, class HB>
+template <int W = kWaves, class Pt, class HA, class HB>
 __device__ __forceinline__ void softmin_pair(const OtParams &P, const float *tab, const double *msh,
                                              const float *xs, bool v, float xi, float yi, double e, double ma,
                                              double mb, const Pt &pt, const HA &ha, const HB &hb, float *lds,
                                              double &A, double &Bv, int32_t *fb) {
   const float sc = cost_scale(1.0 / e);
   float S[2];
-  wg_iter_sums(tab, msh, P.splits, np_of(P), P.N, sc, pt, lds, S);
+  wg_iter_sums<W>(tab, msh, P.splits, np_of(P), P.N, sc, pt, lds, S);
   if (v) {
     A = -e * lse2_from(S[0], ma, xs, P.N, xi, yi, sc, ha, fb) * kLn2d;
     Bv = -e * lse2_from(S[1], mb, xs, P.N, xi, yi, sc, hb, fb) * kLn2d;
@@ -732,7 +817,7 @@ __device__ __forceinline__ void softmin_pair(const OtParams &P, const float *tab
 // initial potentials at eps0 (:120-121): a_y = softmin(eps0, C, logw), b_x = softmin(eps0, C, logu)
 __global__ __launch_bounds__(kOtBlock) void ot_init_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
@@ -783,14 +868,15 @@ __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws
 #ifndef NFDPF_OT_ITER_WPS
 #define NFDPF_OT_ITER_WPS 1
 #endif
-__global__ __launch_bounds__(kOtBlock, NFDPF_OT_ITER_WPS) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
+template <int W>
+__global__ __launch_bounds__(64 * W, NFDPF_OT_ITER_WPS) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
   if (ot_off(P)) {
     if (lead && P.host) host_flag(P.host, 0, P.seq);  // nothing to iterate: stop enqueueing
     return;
   }
-  __shared__ double shd[16];
-  __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
+  __shared__ double shd[64];  // block_max_n<5> over up to 8 waves
+  __shared__ __attribute__((aligned(16))) float lds[kLdsPart + W * kSliceFloats];
   __shared__ int s_stop;
   if (threadIdx.x < 64) {  // wave 0 (ot_stop_before is a wave-level decision)
     int st = ws.st->stopped;
@@ -823,7 +909,7 @@ __global__ __launch_bounds__(kOtBlock, NFDPF_OT_ITER_WPS) void ot_iter_kernel(Ot
   const double sh = -inv * kLog2ed;
   const double oa = v ? ay[i] : 0.0, ob = v ? bx[i] : 0.0;
   double A = 0.0, Bv = 0.0;
-  softmin_pair(
+  softmin_pair<W>(
       P, tabI_row(ws, P, k & 1, b), mI_row(ws, P, k & 1, b), xs, v, xi, yi, re, oa * sh, ob * sh,
       [&](int ii, float &x, float &y, double (&m)[2]) {
         x = xs[2 * ii];
@@ -841,9 +927,8 @@ __global__ __launch_bounds__(kOtBlock, NFDPF_OT_ITER_WPS) void ot_iter_kernel(Ot
     pot_ptr(ws, P, (k + 1) & 1, 1, b)[i] = nb;
     dmax = fmax(fabs(na - oa), fabs(nb - ob));
   }
-  dmax = block_max(dmax, shd);
+  emit_state_tables(P, ws, b, k + 1, v, xi, yi, v ? lw[i] : 0.f, logu, na, nb, shd, &dmax);
   if (threadIdx.x == 0) ws.res[((int64_t)(k & 1) * P.B + b) * P.splits + blockIdx.x] = dmax;
-  emit_state_tables(P, ws, b, k + 1, v, xi, yi, v ? lw[i] : 0.f, logu, na, nb, shd);
 }
 
 __device__ __forceinline__ int ot_total_iter(const OtParams &P, const OtWs &ws) {
@@ -855,7 +940,7 @@ __device__ __forceinline__ int ot_total_iter(const OtParams &P, const OtWs &ws) 
 // Writes the column table: X, Y, f_i / eps (base 2).
 __global__ __launch_bounds__(kOtBlock) void ot_final_kernel(OtParams P, OtWs ws) {
   if (ot_off(P)) return;
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
@@ -874,7 +959,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_final_kernel(OtParams P, OtWs ws)
   const float xi = v ? xs[2 * i] : 0.f, yi = v ? xs[2 * i + 1] : 0.f;
   const double sh = -inv * kLog2ed;  // f is the softmin that a_y converged to
   float S[1];
-  wg_table_sums<1, 0, 2>(tab, msh, P.splits, Np, N, sc,
+  wg_table_sums<1, 0, 2, kPrescale>(tab, msh, P.splits, Np, N, sc,
                          [&](int ii, float &x, float &y, double (&m)[1]) {
                            x = xs[2 * ii];
                            y = xs[2 * ii + 1];
@@ -898,7 +983,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_final_kernel(OtParams P, OtWs ws)
 // with the column log-normaliser; g_j cancels).  Writes the apply table: X, Y, r_j, x_j, y_j.
 __global__ __launch_bounds__(kOtBlock) void ot_col_kernel(OtParams P, OtWs ws, const float *__restrict__ x) {
   if (ot_off(P)) return;
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
   const int j = blockIdx.x * kOtThreads + threadIdx.x;
@@ -1003,7 +1088,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_apply_kernel(OtParams P, OtWs ws,
 __global__ __launch_bounds__(kOtBlock) void ot_bwd_table_kernel(OtParams P, OtWs ws,
                                                                  const float *__restrict__ g) {
   if (ot_off(P)) return;
-  __shared__ double shd[16];
+  __shared__ double shd[32];
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
   const bool v = i < N && threadIdx.x < kOtThreads;
@@ -1092,6 +1177,16 @@ __global__ void ot_iters_kernel(OtParams P, OtWs ws, int32_t *out) {
 
 using namespace nfdpf;
 
+// Waves per iteration workgroup: 4, or 8 with NFDPF_OT_ITER_WAVES=8 (the lanes' i split over
+// wave pairs, wg_iter_sums; bit-identical, tests/test_gpu_parity.py).  Measured (round 2d, one
+// box): at C3 (64 rows x 4 slices = one 4-wave workgroup per CU, one wave per SIMD) 8 waves did
+// not shorten the iteration (18.1-18.3 vs 18.4-20.8 us, pass within noise); forced at C4 they
+// cost 8 % (125 vs 117 us).  So 4 is the default at every grid size.
+static int ot_iter_waves(int /*wgs*/) {
+  const char *e = getenv("NFDPF_OT_ITER_WAVES");  // read per call (tests switch it)
+  return (e && atoi(e) == 2 * kWaves) ? 2 * kWaves : kWaves;
+}
+
 extern "C" int64_t nfdpf_ot_workspace_bytes(int B, int N) {
   return (B <= 0 || N <= 0) ? 256 : ws_bytes(B, N);
 }
@@ -1154,8 +1249,15 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
   const dim3 g(splits, B);
   ot_prep_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   ot_init_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
+  const bool w8 = ot_iter_waves(B * splits) == 2 * kWaves;
+  auto iter = [&](int k) {
+    if (w8)
+      ot_iter_kernel<2 * kWaves><<<g, 128 * kWaves, 0, st>>>(P, ws, k);
+    else
+      ot_iter_kernel<kWaves><<<g, kOtBlock, 0, st>>>(P, ws, k);
+  };
   if (!poll) {
-    for (int k = 0; k < max_iter - 1; ++k) ot_iter_kernel<<<g, kOtBlock, 0, st>>>(P, ws, k);
+    for (int k = 0; k < max_iter - 1; ++k) iter(k);
   } else {
     // Keep at most kAhead iterations queued past the one the device has started, and stop
     // enqueueing once an iteration has observed the stop (or the gate is off): the loop then
@@ -1165,7 +1267,7 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
     bool blind = false;
     for (int k = 0; k < max_iter - 1; ++k) {
       if (!blind && hf[0] == P.seq) break;
-      ot_iter_kernel<<<g, kOtBlock, 0, st>>>(P, ws, k);
+      iter(k);
       if (blind) continue;
       const auto t0 = std::chrono::steady_clock::now();
       for (;;) {

@@ -374,7 +374,8 @@ class FilterEngine:
                 # The Sinkhorn loop is max_iter launches; when the gate is off they would all be
                 # no-ops, so read the gate (one sync, as the reference's `if ESS < ...` does,
                 # DPFs.py:165) and skip the call.  The gate is batch-global: same on every rank.
-                fire = fired[-1] if host_mode else bool(gate_buf.item())
+                # (--force-resample: the gate is on by construction -- no read, no sync)
+                fire = fired[-1] if host_mode else (True if c.force_resample else bool(gate_buf.item()))
                 if fire:
                     self.last_ot_calls += 1
                     xo, _, _, it = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,

@@ -199,6 +199,28 @@ def test_ot_resampler_vs_oracle_stress(B, N, kind):
     assert torch.all(wo.cpu() == 1.0 / N)
 
 
+@pytest.mark.parametrize("B,N,kind", [(64, 1000, "peaked"), (3, 777, "outliers"), (8, 1500, "clusters")])
+def test_ot_iter_waves_bit_identical(B, N, kind, monkeypatch):
+    """The 8-wave Sinkhorn iteration launch (small grids; waves w and w + 4 split the lanes' i
+    over the same slices, csrc/resample_ot.hip wg_iter_sums) returns the 4-wave launch's result
+    bit for bit, iteration count included, on a C3-shaped batch (64 rows x N=1000) and ragged N."""
+    from nfdpf import ops
+    g = torch.Generator().manual_seed(7 * N + B)
+    x = torch.randn(B, N, 2, generator=g) * 30
+    if kind == "outliers":
+        x[:, :5] *= 40
+    if kind == "clusters":
+        x[:, : N // 2] += 400
+    s = {"peaked": 12.0, "outliers": 3.0, "clusters": 2.0}[kind]
+    p = torch.softmax(torch.randn(B, N, generator=g) * s, -1) + 1e-12
+    out = {}
+    for w in ("4", "8"):
+        monkeypatch.setenv("NFDPF_OT_ITER_WAVES", w)
+        out[w] = [u.cpu() for u in ops.ot_resample(x.to(DEV), p.to(DEV))]
+    for u, v in zip(out["4"], out["8"]):
+        assert torch.equal(u, v)
+
+
 def test_ot_poll_matches_enqueue_all():
     """poll=1 (host follows the loop and stops enqueueing) gives the bit-identical result of
     poll=0 (all max_iter - 1 launches enqueued, graph-capturable), gate on and off."""
