@@ -329,16 +329,21 @@ __device__ __forceinline__ void lds_tblock(TBlock<NP> &B, const float *sl, int j
   }
 }
 // the 32 blocks of 8 j of a staged slice, one block read ahead
-template <int NP, class Body>
-__device__ __forceinline__ void slice_blocks(const float *sl, const int (&pl)[NP], const Body &body) {
-#ifdef NFDPF_OT_LDS1  // one block at a time (32 fewer VGPRs; the SIMD's other waves cover the LDS latency)
-  for (int j = 0; j < kOtThreads; j += 8) {
-    TBlock<NP> A;
-    lds_tblock(A, sl, j, pl);
-    body(A);
-  }
-  return;
+#ifdef NFDPF_OT_LDS1
+constexpr bool kLds1 = true;
+#else
+constexpr bool kLds1 = false;
 #endif
+template <int NP, bool ONE = kLds1, class Body>
+__device__ __forceinline__ void slice_blocks(const float *sl, const int (&pl)[NP], const Body &body) {
+  if constexpr (ONE) {  // one block at a time (32 fewer VGPRs; the SIMD's other waves cover the LDS latency)
+    for (int j = 0; j < kOtThreads; j += 8) {
+      TBlock<NP> A;
+      lds_tblock(A, sl, j, pl);
+      body(A);
+    }
+    return;
+  }
   TBlock<NP> A, Bk;
   lds_tblock(A, sl, 0, pl);
   for (int j = 0; j < kOtThreads; j += 16) {
@@ -577,7 +582,7 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
 #ifndef NFDPF_OT_L1
     slice_copy<6>(tab, Np, s * kOtThreads, sl);
     (void)j1;
-#define OT_SLICE_LOOP(PL, ...) slice_blocks<4>(sl, PL, __VA_ARGS__)
+#define OT_SLICE_LOOP(PL, ...) slice_blocks<4, kLds1 || W != kWaves>(sl, PL, __VA_ARGS__)
 #else
 #define OT_SLICE_LOOP(PL, ...) pipelined<4>(tab, Np, j0, j1, PL, __VA_ARGS__)
 #endif
@@ -869,7 +874,8 @@ __device__ __forceinline__ bool ot_stop_before(const OtParams &P, const OtWs &ws
 #define NFDPF_OT_ITER_WPS 1
 #endif
 template <int W>
-__global__ __launch_bounds__(64 * W, NFDPF_OT_ITER_WPS) void ot_iter_kernel(OtParams P, OtWs ws, int k) {
+__global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) void ot_iter_kernel(
+    OtParams P, OtWs ws, int k) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
   if (ot_off(P)) {
     if (lead && P.host) host_flag(P.host, 0, P.seq);  // nothing to iterate: stop enqueueing
@@ -1181,7 +1187,9 @@ using namespace nfdpf;
 // wave pairs, wg_iter_sums; bit-identical, tests/test_gpu_parity.py).  Measured (round 2d, one
 // box): at C3 (64 rows x 4 slices = one 4-wave workgroup per CU, one wave per SIMD) 8 waves did
 // not shorten the iteration (18.1-18.3 vs 18.4-20.8 us, pass within noise); forced at C4 they
-// cost 8 % (125 vs 117 us).  So 4 is the default at every grid size.
+// cost 8 % (125 vs 117 us); with one LDS block at a time and 126 VGPRs (4 waves per SIMD at C4,
+// the build below) still 4 % slower at C4 (122-124 vs 117-120 us) and 6 % at C3 forced -- the
+// iteration is throughput-bound, not latency-bound.  So 4 is the default at every grid size.
 static int ot_iter_waves(int /*wgs*/) {
   const char *e = getenv("NFDPF_OT_ITER_WAVES");  // read per call (tests switch it)
   return (e && atoi(e) == 2 * kWaves) ? 2 * kWaves : kWaves;
