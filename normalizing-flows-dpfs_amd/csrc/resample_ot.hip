@@ -86,6 +86,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 sp2(float v) { return f2{v, v}; }
 __device__ __forceinline__ f2 pfma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
+#ifdef NFDPF_OT_RISKSTAT  // experiment builds: share of wave-slices on the two-exp path, per call
+__device__ unsigned int g_ot_risky, g_ot_wslices;
+#endif
 struct OtState {
   int32_t stopped;    // set by the iteration that observes a converged row
   int32_t K;          // total_iter of the reference
@@ -411,6 +414,7 @@ __device__ __forceinline__ void kblock(const TBlock<4> &B, const LaneIK<KR> &L, 
 }
 
 __device__ __forceinline__ float hsum2(f2 a) { return a.x + a.y; }
+__device__ __forceinline__ bool risky_any(bool r) { return __builtin_amdgcn_ballot_w64(r) != 0; }
 
 // slice offset M_s - m_i in fp32 (-inf: the slice carries no weight)
 __device__ __forceinline__ float slice_off(double Ms, double m) {
@@ -586,6 +590,12 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
 #else
 #define OT_SLICE_LOOP(PL, ...) pipelined<4>(tab, Np, j0, j1, PL, __VA_ARGS__)
 #endif
+#ifdef NFDPF_OT_RISKSTAT
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&g_ot_wslices, 1u);
+      if (risky_any(risky)) atomicAdd(&g_ot_risky, 1u);
+    }
+#endif
     if (__builtin_amdgcn_ballot_w64(risky) == 0) {
       f2 acc[KR][2];
 #pragma unroll
@@ -749,6 +759,10 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
       e = fmax(e * sf, eps);
     }
     if (b == 0) {
+#ifdef NFDPF_OT_RISKSTAT
+      g_ot_risky = 0;
+      g_ot_wslices = 0;
+#endif
       ws.st->stopped = 0;
       ws.st->K = 0;
       ws.st->fallbacks = 0;
@@ -1206,6 +1220,13 @@ extern "C" int nfdpf_ot_stats(const void *workspace, int32_t *host_out) {
     return launch_status("nfdpf_ot_stats");
   host_out[0] = st.stopped ? st.K + 2 : -1;
   host_out[1] = st.fallbacks;
+#ifdef NFDPF_OT_RISKSTAT  // per-mille of wave-slices on the two-exp path instead
+  unsigned int rk = 0, ns = 0;
+  if (hipMemcpyFromSymbol(&rk, HIP_SYMBOL(g_ot_risky), sizeof(rk)) != hipSuccess ||
+      hipMemcpyFromSymbol(&ns, HIP_SYMBOL(g_ot_wslices), sizeof(ns)) != hipSuccess)
+    return launch_status("nfdpf_ot_stats");
+  host_out[1] = ns ? (int32_t)((1000ull * rk) / ns) : -1;
+#endif
   return NFDPF_OK;
 }
 
