@@ -166,15 +166,36 @@ NFDPF_API int nfdpf_ot_transport_backward(const float *g_out, int B, int N, floa
  *   stop_at: optional device int32, in the iters_out encoding (total_iter + 2).  NULL: the
  *         reference's rule -- stop after the first iteration at which ANY of these B rows
  *         has converged (resamplers.py:126-129).  Non-NULL: run exactly that many
- *         iterations.  A batch sharded over ranks reproduces the unsharded loop by running
- *         once with NULL, taking the MIN of iters_out over ranks (the first row to converge
- *         anywhere), and running again with stop_at = that minimum.
+ *         iterations.  (A batch sharded over ranks uses the two-phase form below instead of
+ *         running once with NULL and again with stop_at = the MIN over ranks.)
  *   poll: 0 -- enqueue max_iter - 1 iteration launches (iterations after the stop exit at
  *         once; stream-ordered, graph-capturable, returns immediately).  1 -- the calling
  *         thread follows the device's progress through library-owned mapped host flags and
  *         stops enqueueing once the loop has stopped (at most 2 early-exit launches past the
  *         stop; the call returns when the last iteration has been enqueued, not capturable;
  *         the reference's own loop syncs the host every iteration, resamplers.py:126-129). */
+
+/* nfdpf_ot_resample for a batch sharded over ranks, in two phases
+ * around the caller's all-reduce, without running any Sinkhorn iteration twice:
+ *   1. nfdpf_ot_sinkhorn_local: the loop with the stop rule over THIS rank's rows, keeping
+ *      every state's potentials in `history` (nfdpf_ot_history_bytes(B, N, max_iter) bytes,
+ *      [max_iter][2][B][N] fp64); iters_out = the local count (iters_out encoding).
+ *   -- the caller: all-reduce(MIN) of iters_out over the ranks, on the stream (the first row
+ *      to converge anywhere ends the unsharded loop, resamplers.py:126-129) --
+ *   2. nfdpf_ot_sinkhorn_finish with stop_at = that minimum (<= the local count): rebuilds the
+ *      state's tables from the history, then the final potential, column normalisers and the
+ *      transport apply at that state.  iters_out (optional) = *stop_at.
+ * The outputs equal nfdpf_ot_resample of the whole batch bit for bit (tests/test_gpu_parity.py).
+ * Same workspace for both phases, untouched in between; it then serves
+ * nfdpf_ot_transport_backward as after nfdpf_ot_resample. */
+NFDPF_API int64_t nfdpf_ot_history_bytes(int B, int N, int max_iter);
+NFDPF_API int nfdpf_ot_sinkhorn_local(const float *x, const float *w, int B, int N, float eps, float scaling,
+                                      float threshold, int max_iter, int32_t *iters_out, void *workspace,
+                                      void *history, const int32_t *gate, int poll, void *stream);
+NFDPF_API int nfdpf_ot_sinkhorn_finish(const float *x, int B, int N, float eps, float scaling, float threshold,
+                                       int max_iter, int64_t row_base, float *x_out, float *w_out,
+                                       int64_t *idx_out, int32_t *iters_out, void *workspace, void *history,
+                                       const int32_t *gate, const int32_t *stop_at, void *stream);
 
 /* Diagnostics of the last nfdpf_ot_resample on `workspace` (synchronous device read):
  *   host_out[0] = iterations in the iters_out encoding (-1: ran to max_iter), host_out[1] =
@@ -183,9 +204,10 @@ NFDPF_API int nfdpf_ot_stats(const void *workspace, int32_t *host_out);
 
 /* Health of the wave-pair hand-offs of the tiled step (csrc/split.hpp): the number of
  * exchanges that gave up waiting for their partner wave since the last reset (a correct run
- * never does; the launch's outputs are then invalid).  Synchronous device read; reset != 0
- * clears the count.  Returns -1 if the read failed. */
-NFDPF_API int nfdpf_split_fault(int reset);
+ * never does; the launch's outputs are then invalid).  Read in order on `stream` (the stream
+ * the checked launches ran on), then that stream is synchronised; reset != 0 clears the count
+ * (also in stream order).  Returns -1 if the read failed. */
+NFDPF_API int nfdpf_split_fault(int reset, void *stream);
 
 /* ESS gate of DPFs.py:163-165: gate = mean_b(inv_ess[b]) < 0.5 N (or force) -> int32 [1] */
 NFDPF_API int nfdpf_ess_gate(const float *inv_ess, int B, int N, int force, int32_t *gate,

@@ -181,7 +181,12 @@ class DPF(nn.Module):
             return self._filtering_modules(obs, start_state_vs, vel_input)
         with torch.no_grad():
             enc = self._frame_encodings(obs, self.seq_len)
-            eng = FilterEngine(self.filter_config(), self)
+            # one engine per configuration, kept across calls: its speculative-gate state (the
+            # auto mode's record of a fired gate and back-off) must outlive a single pass
+            cfg = self.filter_config()
+            eng = getattr(self, "_engine", None)
+            if eng is None or eng.cfg != cfg:
+                eng = self._engine = FilterEngine(cfg, self)
             shard = ShardInfo.from_env(enc.shape[0])
             res = eng.run(enc, start_state_vs, vel_input[:, :self.seq_len], shard=shard)
         self.last_filter_result = res

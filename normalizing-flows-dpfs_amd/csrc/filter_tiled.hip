@@ -1517,11 +1517,17 @@ static bool use_merged(const nfdpf_filter_desc &d) {
 static bool use_fused(const nfdpf_filter_desc &d) {
   const char *e = getenv("NFDPF_FUSED_STEP");  // read per call: tests compare both paths
   if (!(e && e[0] == '1') || !use_merged(d) || d.phase != 0 || n_tiles(d.N) > kFusedMaxTiles) return false;
-  int dev = 0, cus = 0;
+  // a sharded pass shares the device with the collectives' kernels on other streams, which can
+  // hold CUs while the row's workgroups spin on each other: never there
+  if (d.B_global != d.B) return false;
+  int dev = 0, cus = 0, occ = 0;
+  const size_t mlds = (size_t)(std::max(d.N, d.B_global) + 2 * d.N) * 4;
   if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tiled_step_fused_kernel, 4 * kTile, mlds) != hipSuccess ||
+      occ < 1)
     return false;
-  return (int64_t)n_tiles(d.N) * d.B <= cus;
+  return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;
 }
 
 // The proposal launch.  With live timing requested (prof_events) the two events ride in the
@@ -1617,17 +1623,25 @@ extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *es
   return launch_status("nfdpf_filter_tiled_init");
 }
 
-extern "C" int nfdpf_split_fault(int reset) {
-  int v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_split_fault), sizeof(int)) != hipSuccess) {
-    set_error("nfdpf_split_fault: hipMemcpyFromSymbol failed");
+extern "C" int nfdpf_split_fault(int reset, void *stream) {
+  // stream-ordered after the launches it checks (the caller's stream, not the null stream)
+  static int v = 0;
+  static const int z = 0;
+  hipStream_t st = as_stream(stream);
+  if (hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_split_fault), sizeof(int), 0, hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    set_error("nfdpf_split_fault: reading the fault counter failed");
     return -1;
   }
-  if (reset && v != 0) {
-    const int z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_fault), &z, sizeof(int)) != hipSuccess) return -1;
+  const int n = v;
+  if (reset && n != 0) {
+    if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_split_fault), &z, sizeof(int), 0, hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return -1;
   }
-  return v;
+  return n;
 }
 
 #ifdef NFDPF_EXP_QTRACE

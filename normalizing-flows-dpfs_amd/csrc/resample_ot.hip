@@ -173,6 +173,7 @@ struct OtParams {
   const int32_t *stop_at;  // optional: total_iter + 2 to run (sharded batches), else the rule
   int32_t *host;           // optional (poll mode): mapped host flags {stop seq, seq * 4096 + k}
   int32_t seq;             // call sequence number for the host flags
+  double *hist;            // optional (sharded batches): every state's potentials [max_iter][2][B][N]
 };
 
 // progress of the Sinkhorn loop to the polling host thread (system-scope stores into
@@ -185,8 +186,11 @@ __device__ __forceinline__ bool ot_off(const OtParams &P) { return P.gate && *P.
 
 __device__ __forceinline__ int64_t np_of(const OtParams &P) { return (int64_t)P.splits * kOtThreads; }
 
-__device__ __forceinline__ double *pot_ptr(const OtWs &ws, const OtParams &P, int buf, int which, int b) {
-  return ws.pot + (((int64_t)buf * 2 + which) * P.B + b) * P.N;
+// potentials of state k: double-buffered by parity, or the state's own slot of the history
+// (a sharded call resumes its tail at the batch-global stop, which may lie behind its own)
+__device__ __forceinline__ double *pot_ptr(const OtWs &ws, const OtParams &P, int k, int which, int b) {
+  if (P.hist) return P.hist + (((int64_t)k * 2 + which) * P.B + b) * P.N;
+  return ws.pot + (((int64_t)(k & 1) * 2 + which) * P.B + b) * P.N;
 }
 __device__ __forceinline__ float *tabI_row(const OtWs &ws, const OtParams &P, int buf, int b) {
   return ws.tabI + ((int64_t)buf * P.B + b) * 6 * np_of(P);
@@ -922,7 +926,7 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
   const double logu = ws.rowc[b * 4 + 1];
-  const double *ay = pot_ptr(ws, P, k & 1, 0, b), *bx = pot_ptr(ws, P, k & 1, 1, b);
+  const double *ay = pot_ptr(ws, P, k, 0, b), *bx = pot_ptr(ws, P, k, 1, b);
   const float xi = v ? xs[2 * i] : 0.f, yi = v ? xs[2 * i + 1] : 0.f;
   // at_y = softmin(e, C, logw + b_x/e);  bt_x = softmin(e, C, logu + a_y/e); shifts from the
   // current potentials (softmin = -e ln2 LSE2)
@@ -943,8 +947,8 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
   if (v) {
     na = 0.5 * (oa + A);
     nb = 0.5 * (ob + Bv);
-    pot_ptr(ws, P, (k + 1) & 1, 0, b)[i] = na;
-    pot_ptr(ws, P, (k + 1) & 1, 1, b)[i] = nb;
+    pot_ptr(ws, P, k + 1, 0, b)[i] = na;
+    pot_ptr(ws, P, k + 1, 1, b)[i] = nb;
     dmax = fmax(fabs(na - oa), fabs(nb - ob));
   }
   emit_state_tables(P, ws, b, k + 1, v, xi, yi, v ? lw[i] : 0.f, logu, na, nb, shd, &dmax);
@@ -952,7 +956,27 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
 }
 
 __device__ __forceinline__ int ot_total_iter(const OtParams &P, const OtWs &ws) {
+  // the caller's count (a sharded batch's global stop, the MIN over ranks of their own)
+  if (P.stop_at) return min(*P.stop_at - 2, max(P.max_iter - 1, 0));
   return ws.st->stopped ? ws.st->K : max(P.max_iter - 1, 0);
+}
+
+// The tables of state K = the batch-global stop, rebuilt from the potential history: a rank
+// whose own rows converged later has since overwritten them (the iteration tables are
+// double-buffered, the final-epsilon table is rewritten every annealing iteration).  The same
+// workgroup reduction as the iteration epilogue that first wrote them: bit-identical tables.
+__global__ __launch_bounds__(kOtBlock) void ot_restore_kernel(OtParams P, OtWs ws) {
+  if (ot_off(P)) return;
+  __shared__ double shd[32];
+  const int b = blockIdx.y, N = P.N;
+  const int i = blockIdx.x * kOtThreads + threadIdx.x;
+  const bool v = i < N && threadIdx.x < kOtThreads;
+  const int K = ot_total_iter(P, ws);
+  const float *xs = ws.xs + (int64_t)b * N * 2;
+  const float *lw = ws.logw + (int64_t)b * N;
+  const double *ay = pot_ptr(ws, P, K, 0, b), *bx = pot_ptr(ws, P, K, 1, b);
+  emit_state_tables(P, ws, b, K, v, v ? xs[2 * i] : 0.f, v ? xs[2 * i + 1] : 0.f, v ? lw[i] : 0.f,
+                    ws.rowc[b * 4 + 1], v ? ay[i] : 0.0, v ? bx[i] : 0.0, shd);
 }
 
 // final potential at eps (:173-176): f = softmin(eps, C, logw + b_x/eps).  (g = softmin(eps,
@@ -971,7 +995,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_final_kernel(OtParams P, OtWs ws)
   const float sc = cost_scale(inv);
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const float *lw = ws.logw + (int64_t)b * N;
-  const double *ay = pot_ptr(ws, P, K & 1, 0, b), *bx = pot_ptr(ws, P, K & 1, 1, b);
+  const double *ay = pot_ptr(ws, P, K, 0, b), *bx = pot_ptr(ws, P, K, 1, b);
   // the state's iteration table is at eps unless the row was still annealing at the stop
   const bool annealing = eps_at(ws, P, b, K) != P.eps;
   const float *tab = annealing ? ws.tabF + (int64_t)b * 4 * Np : tabI_row(ws, P, K & 1, b);
@@ -1014,7 +1038,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_col_kernel(OtParams P, OtWs ws, c
   const float sc = cost_scale(inv);
   const float *xs = ws.xs + (int64_t)b * N * 2;
   const double *f = ws.fg + (int64_t)b * N;
-  const double *bx = pot_ptr(ws, P, K & 1, 1, b);
+  const double *bx = pot_ptr(ws, P, K, 1, b);
   const double logu = ws.rowc[b * 4 + 1];
   const float xj = v ? xs[2 * j] : 0.f, yj = v ? xs[2 * j + 1] : 0.f;
   // LSE_i(f_i/eps - C_ij/eps) = -b_x_j/eps - logu at the Sinkhorn fixed point
@@ -1250,23 +1274,11 @@ static bool poll_flags(volatile int32_t **host, int32_t **dev) {
   return true;
 }
 
-extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
-                                 float scaling, float threshold, int max_iter, int64_t row_base,
-                                 float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
-                                 void *workspace, const int32_t *gate, const int32_t *stop_at,
-                                 int poll, void *stream) {
-  NFDPF_REQUIRE(x && w && x_out && w_out && idx_out && workspace,
-                "nfdpf_ot_resample: null pointer");
-  NFDPF_REQUIRE(B >= 0 && N >= 1 && max_iter >= 1, "nfdpf_ot_resample: bad sizes");
-  NFDPF_REQUIRE(eps > 0.f && scaling > 0.f, "nfdpf_ot_resample: eps and scaling must be > 0");
-  NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_ot_resample: workspace not 256-B aligned");
-  NFDPF_REQUIRE(max_iter <= 4096, "nfdpf_ot_resample: max_iter <= 4096");
-  if (B == 0) return NFDPF_OK;
-  hipStream_t st = as_stream(stream);
-  const int splits = ot_splits(N);
-  OtWs ws = carve(workspace, B, N);
-  OtParams P{B, N, splits, max_iter, (double)eps, (double)scaling * (double)scaling,
-             (double)threshold, gate, stop_at, nullptr, 0};
+// The Sinkhorn loop (setup, the initial potentials, the iterations under the batch-coupled stop
+// rule or to *stop_at) -- the first half of nfdpf_ot_resample.
+static int ot_loop(const float *x, const float *w, OtParams &P, const OtWs &ws, int poll, hipStream_t st) {
+  const int B = P.B, N = P.N, max_iter = P.max_iter, splits = P.splits;
+  const int32_t *gate = P.gate;
   std::unique_lock<std::mutex> lock;
   volatile int32_t *hf = nullptr;
   if (poll) {
@@ -1311,11 +1323,80 @@ extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, f
       }
     }
   }
+  P.host = nullptr;
+  return NFDPF_OK;
+}
+
+// The tail: final potential, column normalisers, transport apply (at *stop_at when given).
+static void ot_tail(const float *x, const OtParams &P, const OtWs &ws, int64_t row_base, float *x_out,
+                    float *w_out, int64_t *idx_out, int32_t *iters_out, hipStream_t st) {
+  const dim3 g(P.splits, P.B);
+  if (P.hist) ot_restore_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   ot_final_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   ot_col_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x);
   ot_apply_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);
   if (iters_out) ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
+}
+
+#define NFDPF_OT_CHECK_ARGS(name)                                                          \
+  NFDPF_REQUIRE(B >= 0 && N >= 1 && max_iter >= 1, name ": bad sizes");                   \
+  NFDPF_REQUIRE(eps > 0.f && scaling > 0.f, name ": eps and scaling must be > 0");        \
+  NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, name ": workspace not 256-B aligned"); \
+  NFDPF_REQUIRE(max_iter <= 4096, name ": max_iter <= 4096")
+
+extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
+                                 float scaling, float threshold, int max_iter, int64_t row_base,
+                                 float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
+                                 void *workspace, const int32_t *gate, const int32_t *stop_at,
+                                 int poll, void *stream) {
+  NFDPF_REQUIRE(x && w && x_out && w_out && idx_out && workspace,
+                "nfdpf_ot_resample: null pointer");
+  NFDPF_OT_CHECK_ARGS("nfdpf_ot_resample");
+  if (B == 0) return NFDPF_OK;
+  hipStream_t st = as_stream(stream);
+  OtWs ws = carve(workspace, B, N);
+  OtParams P{B, N, ot_splits(N), max_iter, (double)eps, (double)scaling * (double)scaling,
+             (double)threshold, gate, stop_at, nullptr, 0, nullptr};
+  const int rc = ot_loop(x, w, P, ws, poll, st);
+  if (rc != NFDPF_OK) return rc;
+  ot_tail(x, P, ws, row_base, x_out, w_out, idx_out, iters_out, st);
   return launch_status("nfdpf_ot_resample");
+}
+
+extern "C" int64_t nfdpf_ot_history_bytes(int B, int N, int max_iter) {
+  return (B <= 0 || N <= 0 || max_iter <= 0) ? 256 : align256((int64_t)max_iter * 2 * B * N * sizeof(double));
+}
+
+extern "C" int nfdpf_ot_sinkhorn_local(const float *x, const float *w, int B, int N, float eps, float scaling,
+                                       float threshold, int max_iter, int32_t *iters_out, void *workspace,
+                                       void *history, const int32_t *gate, int poll, void *stream) {
+  NFDPF_REQUIRE(x && w && iters_out && workspace && history, "nfdpf_ot_sinkhorn_local: null pointer");
+  NFDPF_OT_CHECK_ARGS("nfdpf_ot_sinkhorn_local");
+  if (B == 0) return NFDPF_OK;
+  hipStream_t st = as_stream(stream);
+  OtWs ws = carve(workspace, B, N);
+  OtParams P{B, N, ot_splits(N), max_iter, (double)eps, (double)scaling * (double)scaling,
+             (double)threshold, gate, nullptr, nullptr, 0, (double *)history};
+  const int rc = ot_loop(x, w, P, ws, poll, st);
+  if (rc != NFDPF_OK) return rc;
+  ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
+  return launch_status("nfdpf_ot_sinkhorn_local");
+}
+
+extern "C" int nfdpf_ot_sinkhorn_finish(const float *x, int B, int N, float eps, float scaling, float threshold,
+                                        int max_iter, int64_t row_base, float *x_out, float *w_out,
+                                        int64_t *idx_out, int32_t *iters_out, void *workspace, void *history,
+                                        const int32_t *gate, const int32_t *stop_at, void *stream) {
+  NFDPF_REQUIRE(x && x_out && w_out && idx_out && workspace && history && stop_at,
+                "nfdpf_ot_sinkhorn_finish: null pointer");
+  NFDPF_OT_CHECK_ARGS("nfdpf_ot_sinkhorn_finish");
+  if (B == 0) return NFDPF_OK;
+  hipStream_t st = as_stream(stream);
+  OtWs ws = carve(workspace, B, N);
+  OtParams P{B, N, ot_splits(N), max_iter, (double)eps, (double)scaling * (double)scaling,
+             (double)threshold, gate, stop_at, nullptr, 0, (double *)history};
+  ot_tail(x, P, ws, row_base, x_out, w_out, idx_out, iters_out, st);
+  return launch_status("nfdpf_ot_sinkhorn_finish");
 }
 
 extern "C" int nfdpf_ot_transport_backward(const float *g_out, int B, int N, float eps, float *g_x,
@@ -1328,7 +1409,7 @@ extern "C" int nfdpf_ot_transport_backward(const float *g_out, int B, int N, flo
   hipStream_t st = as_stream(stream);
   const int splits = ot_splits(N);
   OtWs ws = carve(workspace, B, N);
-  OtParams P{B, N, splits, 1, (double)eps, 1.0, 0.0, gate, nullptr, nullptr, 0};
+  OtParams P{B, N, splits, 1, (double)eps, 1.0, 0.0, gate, nullptr, nullptr, 0, nullptr};
   const dim3 g(splits, B);
   ot_bwd_table_kernel<<<g, kOtBlock, 0, st>>>(P, ws, g_out);
   ot_bwd_apply_kernel<<<g, kOtBlock, 0, st>>>(P, ws, g_out, g_x);

@@ -81,7 +81,13 @@ SIGNATURES = {
     "nfdpf_ot_resample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int, c_void_p]),
-    "nfdpf_ess_gate": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_ot_history_bytes": (c_int64, [c_int, c_int, c_int]),
+    "nfdpf_ot_sinkhorn_local": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "nfdpf_ot_sinkhorn_finish": (c_int, [c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_int64, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p]),
+    "nfdpf_ess_gate":(c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_maf_stack_backward_workspace": (c_int64, [c_int, c_int, c_int, c_int64]),
     "nfdpf_maf_stack_backward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -93,7 +99,7 @@ SIGNATURES = {
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_rqs": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_float, c_float,
                           c_float, c_float, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
-    "nfdpf_split_fault": (c_int, [c_int]),
+    "nfdpf_split_fault": (c_int, [c_int, c_void_p]),
     "nfdpf_normalize_log_probs": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "nfdpf_cglow_params_size": (c_int64, [c_int]),
     "nfdpf_cglow_measurement": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
@@ -152,10 +158,11 @@ def check(rc: int, what: str):
         raise NfdpfError(f"{what} failed (rc={rc}): {msg}")
 
 
-def check_split_fault(what: str = "tiled filter step"):
+def check_split_fault(what: str = "tiled filter step", device=None):
     """Raise if a wave-pair hand-off of the tiled step gave up on its partner (csrc/split.hpp
-    kSpinCap) since the last check: that launch ran on stale data.  Synchronous."""
-    n = lib().nfdpf_split_fault(1)
+    kSpinCap) since the last check: that launch ran on stale data.  Read in order on the
+    current stream of ``device`` (where the launches ran), then synchronises that stream."""
+    n = lib().nfdpf_split_fault(1, stream_ptr(device))
     if n != 0:
         raise NfdpfError(f"{what}: {n} wave-pair hand-off(s) timed out on the device (outputs invalid)"
                          if n > 0 else f"{what}: could not read the device fault counter")

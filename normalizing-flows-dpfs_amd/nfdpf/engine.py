@@ -12,8 +12,10 @@ Batch sharding (world size > 1, rows [rank B, (rank + 1) B) per rank):
   * soft resampling: the pass runs speculatively with every gate assumed off and no exchange,
     then ONE all-gather of all steps' partials verifies the T batch-global gates
     (DPFs.py:163-165); a fired gate reruns the pass with a per-step all-gather;
-  * OT: a per-step all-gather of the partials feeds the gate, and each Sinkhorn call takes
-    the MIN of the stop iteration over ranks (resamplers.py:126-129) and reruns to it;
+  * OT: a per-step all-gather of the partials feeds the gate (or the speculative pass, as
+    above), and each Sinkhorn call runs its rows with the local stop rule keeping every
+    state's potentials, takes the MIN of the stop iteration over ranks (resamplers.py:126-129)
+    and finishes at that state (ops.ot_resample_sharded: no iteration runs twice);
   * one all-reduce of the obs-likelihood sums at the end.
 """
 from __future__ import annotations
@@ -144,6 +146,14 @@ class FilterEngine:
         # OT, auto mode: did the last pass resample?  Then the next one reads its gates step by
         # step (as the reference: one host sync per step); otherwise it speculates
         self._ot_fired = False
+
+    def __getstate__(self):
+        # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
+        # buffers / process group and the profiling events are per-process state
+        st = dict(self.__dict__)
+        st.pop("_pending", None)
+        st["step_events"] = None
+        return st
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -378,10 +388,14 @@ class FilterEngine:
                 fire = fired[-1] if host_mode else (True if c.force_resample else bool(gate_buf.item()))
                 if fire:
                     self.last_ot_calls += 1
-                    xo, _, _, it = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,
-                                                   shard.row_base, gate=gate_buf)
                     if shard.world > 1:
-                        xo = self._ot_global_stop(xin, pin, it, shard, gate_buf)
+                        # batch-coupled stop over every rank's rows (resamplers.py:126-129): the
+                        # local loop, the MIN of the stop count, the tail at that state
+                        xo, _, _, it = ops.ot_resample_sharded(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,
+                                                               shard.row_base, group=shard.group, gate=gate_buf)
+                    else:
+                        xo, _, _, it = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,
+                                                       shard.row_base, gate=gate_buf)
                     keep.append(xo)
                     d.ot_x = xo.data_ptr()
                 else:
@@ -422,15 +436,19 @@ class FilterEngine:
             else:
                 ess_all = ess_bufs[t & 1]
         # a wave-pair hand-off that timed out leaves stale data (csrc/split.hpp): fail loudly
-        if tiled and d.split_nets and not torch.cuda.is_current_stream_capturing():
-            L.check_split_fault("nfdpf_filter_step_tiled")
+        # (a stream-ordered read and a sync: deferred to finish_pending when the caller asked
+        # for a pass free of host syncs)
+        check_split = tiled and d.split_nets and not torch.cuda.is_current_stream_capturing()
+        if check_split and (finish or not spec):
+            L.check_split_fault("nfdpf_filter_step_tiled", dev)
+            check_split = False
         if c.resampler == "ot" and not spec:
             self._ot_fired = self.last_ot_calls > 0
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = lw_sum.double().sum(0)
         if spec:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
-            self._pending = (ess_hist[:T], tot, shard, N, res)
+            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None)
             if not finish:
                 return res
             if self.finish_pending():
@@ -454,7 +472,9 @@ class FilterEngine:
         evaluate all T gates (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the
         obs-likelihood into the result.  False: some gate fired -- the pass is not the
         reference's and must be rerun without speculation (run(..., speculate=False))."""
-        parts, tot, shard, N, res = self._pending
+        parts, tot, shard, N, res, split_dev = self._pending
+        if split_dev is not None:
+            L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
         tot = tot.clone()
         parts = self._gather_steps(parts, shard)
         if shard.world > 1:
@@ -466,16 +486,6 @@ class FilterEngine:
         return True
 
     # -- helpers ----------------------------------------------------------------------------
-    def _ot_global_stop(self, xin, pin, it, shard: ShardInfo, gate_buf):
-        """Batch-coupled Sinkhorn stop across ranks (resamplers.py:126-129):
-        the loop ends when ANY row of the whole batch converges, i.e. at the MIN over ranks of
-        the local stop iteration; re-run this rank's rows for exactly that many iterations."""
-        c = self.cfg
-        dist.all_reduce(it, op=dist.ReduceOp.MIN, group=shard.group)
-        xo, _, _, _ = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter, shard.row_base,
-                                      gate=gate_buf, stop_at=it)
-        return xo
-
     @staticmethod
     def _global(t: torch.Tensor, shard: ShardInfo) -> torch.Tensor:
         """Host copy of a per-row tensor over the whole (sharded) batch."""

@@ -46,15 +46,13 @@ class GradBucket:
         if self._buf is None or self._buf.numel() != n + P or self._buf.device != dev:
             self._buf = torch.empty(n + P, device=dev, dtype=torch.float32)
         buf = self._buf
-        off = 0
-        for j, p in enumerate(self.params):  # a parameter with no gradient contributes zeros
-            k = p.numel()
-            if p.grad is None:
-                buf[off:off + k].zero_()
-            else:
-                buf[off:off + k].copy_(p.grad.reshape(-1))
-            buf[n + j] = 0.0 if p.grad is None else 1.0  # presence flag, reduced in the same bucket
-            off += k
+        # the gradients (zeros where a parameter has none) in one cat, the presence flags in one
+        # host->device copy: a few launches per step, not one per parameter
+        grads = [p.grad.reshape(-1).to(torch.float32) if p.grad is not None
+                 else torch.zeros(p.numel(), device=dev, dtype=torch.float32) for p in self.params]
+        torch.cat(grads, out=buf[:n])
+        flags = torch.tensor([0.0 if p.grad is None else 1.0 for p in self.params], dtype=torch.float32)
+        buf[n:].copy_(flags)
         dist.all_reduce(buf, group=self.group)
         present = buf[n:].cpu()
         buf = buf[:n]

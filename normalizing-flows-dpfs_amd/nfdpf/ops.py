@@ -288,6 +288,60 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_b
     return xo, wo, idx, it
 
 
+def ot_history(B, N, max_iter, device) -> torch.Tensor:
+    """A private potential history for ot_sinkhorn_local / ot_sinkhorn_finish."""
+    nb = int(lib().nfdpf_ot_history_bytes(B, N, int(max_iter)))
+    return torch.empty(max(nb, 256) + 256, dtype=torch.uint8, device=device)
+
+
+def ot_sinkhorn_local(x, w, eps, scaling, threshold, max_iter, ws, hist, gate=None, poll=None):
+    """Phase 1 of a sharded Sinkhorn call (include/nfdpf.h): the loop with this rank's stop
+    rule, every state's potentials kept in ``hist`` -> the local count (int32[1])."""
+    require_device(x, "ot_sinkhorn_local")
+    B, N, D = x.shape
+    if D != 2:
+        raise L.NfdpfError("ot_sinkhorn_local: the HIP Sinkhorn is built for 2-D particles (state_dim = 2)")
+    it = torch.zeros(1, device=x.device, dtype=torch.int32)
+    if poll is None:
+        poll = not torch.cuda.is_current_stream_capturing()
+    check(lib().nfdpf_ot_sinkhorn_local(ptr(x), ptr(w), B, N, float(eps), float(scaling), float(threshold),
+                                        int(max_iter), ptr(it), _aligned_ptr(ws), _aligned_ptr(hist), ptr(gate),
+                                        int(bool(poll)), stream_ptr(x.device)), "nfdpf_ot_sinkhorn_local")
+    return it
+
+
+def ot_sinkhorn_finish(x, eps, scaling, threshold, max_iter, row_base, ws, hist, stop_at, gate=None):
+    """Phase 2: the tail of the call at state ``stop_at`` (the MIN over ranks of phase 1's
+    counts) -> (x', w', flat idx)."""
+    B, N, _ = x.shape
+    xo = torch.empty_like(x)
+    wo = torch.empty((B, N), device=x.device, dtype=f32)
+    idx = torch.empty((B, N), device=x.device, dtype=torch.int64)
+    check(lib().nfdpf_ot_sinkhorn_finish(ptr(x), B, N, float(eps), float(scaling), float(threshold), int(max_iter),
+                                         int(row_base), ptr(xo), ptr(wo), ptr(idx), None, _aligned_ptr(ws),
+                                         _aligned_ptr(hist), ptr(gate), ptr(stop_at), stream_ptr(x.device)),
+          "nfdpf_ot_sinkhorn_finish")
+    return xo, wo, idx
+
+
+def ot_resample_sharded(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_base=0, group=None,
+                        gate=None, poll=None, keep=None):
+    """ot_resample for this rank's rows of a batch sharded over ``group`` -- the unsharded
+    call's result bit for bit, no Sinkhorn iteration run twice (include/nfdpf.h): the loop
+    with the local stop rule keeping every state's potentials, the MIN of the stop count over
+    the ranks (one int32 all-reduce on the stream, resamplers.py:126-129: the first row to
+    converge anywhere ends the loop), then the tail at that state."""
+    import torch.distributed as dist
+    B, N, _ = x.shape
+    x, w = _c(x), _c(w)
+    ws = workspace(int(lib().nfdpf_ot_workspace_bytes(B, N)), x.device) if keep is None else keep
+    hist = workspace(int(lib().nfdpf_ot_history_bytes(B, N, int(max_iter))), x.device, tag="ot_hist")
+    it = ot_sinkhorn_local(x, w, eps, scaling, threshold, max_iter, ws, hist, gate, poll)
+    dist.all_reduce(it, op=dist.ReduceOp.MIN, group=group)
+    xo, wo, idx = ot_sinkhorn_finish(x, eps, scaling, threshold, max_iter, row_base, ws, hist, it, gate)
+    return xo, wo, idx, it
+
+
 def ot_workspace(B, N, device) -> torch.Tensor:
     """A private OT workspace (the forward state of one call, for its backward)."""
     nb = int(lib().nfdpf_ot_workspace_bytes(B, N))

@@ -10,7 +10,6 @@
   autograd.grad result is discarded, :241-245) -- nfdpf_ot_transport_backward.
 """
 import torch
-import torch.distributed as dist
 import torch.nn as nn
 
 from nfdpf import ops as _ops
@@ -70,18 +69,22 @@ def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, 
     return (xo, wo, idx) if index else (xo, wo)
 
 
+# The process group a batch-sharded DPF filters over (None: the default group); set by
+# DPFs.DPF from its shard, so the Sinkhorn stop is reduced over the same ranks as the rest.
+SHARD_GROUP = None
+
+
 def _ot_call(particles, weights, eps, scaling, threshold, max_iter, keep=None):
     """One Sinkhorn resampling with the reference's batch-coupled stop rule (the loop ends
     when ANY row converges, resamplers.py:126-129).  Batch-sharded (world > 1): each rank
-    runs its rows with the local rule, the ranks take the MIN of the stop iteration (the
-    first row to converge anywhere) and rerun to exactly that count -- the unsharded loop's
-    result (nfdpf.engine._ot_global_stop does the same in the no-grad engine)."""
-    xo, wo, idx, it = _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=keep)
-    if world_size() > 1:
-        dist.all_reduce(it, op=dist.ReduceOp.MIN)
-        xo, wo, idx, _ = _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=keep,
-                                          stop_at=it)
-    return xo, wo, idx, it
+    runs its rows with the local rule keeping every state's potentials, the ranks take the
+    MIN of the stop iteration (the first row to converge anywhere) and each finishes at that
+    state -- the unsharded loop's result, no iteration run twice (ops.ot_resample_sharded,
+    as the no-grad engine)."""
+    if world_size(SHARD_GROUP) > 1:
+        return _ops.ot_resample_sharded(particles, weights, eps, scaling, threshold, max_iter,
+                                        group=SHARD_GROUP, keep=keep)
+    return _ops.ot_resample(particles, weights, eps, scaling, threshold, max_iter, keep=keep)
 
 
 class _OtTransport(torch.autograd.Function):

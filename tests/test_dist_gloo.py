@@ -226,14 +226,16 @@ def _ot_stop_worker(rank, world, port, q):
         import resamplers.resamplers as R
         calls = []
 
-        def fake_ot(x, w, eps, scaling, threshold, max_iter, row_base=0, gate=None, stop_at=None, poll=None,
-                    keep=None):
+        def fake_local(x, w, eps, scaling, threshold, max_iter, ws, hist, gate=None, poll=None):
             # local stop rule: rank r's rows converge after 20 + 9 r iterations
-            it = stop_at.clone() if stop_at is not None else torch.tensor([20 + 9 * rank], dtype=torch.int32)
-            calls.append(None if stop_at is None else int(stop_at.item()))
-            return x + int(it.item()), w, torch.zeros(w.shape, dtype=torch.int64), it
+            calls.append("local")
+            return torch.tensor([20 + 9 * rank], dtype=torch.int32)
 
-        R._ops.ot_resample = fake_ot
+        def fake_finish(x, eps, scaling, threshold, max_iter, row_base, ws, hist, stop_at, gate=None):
+            calls.append(int(stop_at.item()))
+            return x + int(stop_at.item()), torch.full(x.shape[:2], 0.2), torch.zeros(x.shape[:2], dtype=torch.int64)
+
+        R._ops.ot_sinkhorn_local, R._ops.ot_sinkhorn_finish = fake_local, fake_finish
         x = torch.zeros(2, 5, 2)
         w = torch.full((2, 5), 0.2)
         xo, _, _ = R.resampler_ot(x, w)
@@ -244,7 +246,8 @@ def _ot_stop_worker(rank, world, port, q):
 
 def test_ot_stop_exchange_in_autograd_loop_world2():
     """resampler_ot under batch sharding (the e2e_train loop, resamplers.py:126-129): each rank
-    runs its local stop rule, the ranks take the MIN iteration, and every rank reruns to it."""
+    runs its local stop rule, the ranks take the MIN iteration, and every rank finishes at that
+    state (ops.ot_resample_sharded: one local loop, no rerun)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -257,5 +260,5 @@ def test_ot_stop_exchange_in_autograd_loop_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, calls, x0 in res:
-        assert calls == [None, 20], calls
+        assert calls == ["local", 20], calls
         assert x0 == 20.0

@@ -1,0 +1,107 @@
+"""Batch sharding through nfdpf.engine.FilterEngine on the GPU: two ranks (gloo, both on
+cuda:0 -- RCCL refuses two ranks on one device; the exchange code is the same) each filter
+half of the batch's rows and must return exactly the unsharded pass's rows (SURVEY.md §4.4,
+§8(e); DPFs.py:163-166 batch-global ESS gate, resamplers.py:126-129 batch-coupled Sinkhorn
+stop).  GPU box only.
+
+Cases (tests/_fullsize.py workloads, device RNG keyed on the GLOBAL row):
+  * soft_gated -- C2 flags (NF dyn + NF proposal, cos, soft), aligned frame encodings: the ESS
+    gate fires on some steps, so the auto mode's speculative pass misses and reruns with the
+    per-step exchange of the tiled partials;
+  * ot_gated -- C3 flags (CRNVP, OT): the speculative OT pass misses, the per-step pass reads
+    every gate and runs the two-phase sharded Sinkhorn (ops.ot_resample_sharded);
+  * ot_forced -- C4 flags (MAF dyn flow, NF proposal, cos, OT every step).
+Histories and indices must be bit-identical; the obs-likelihood is an fp64 sum reduced in a
+different order (per rank, then across ranks), then rounded to float32: 1e-6 relative.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+# name: (_fullsize case, B, N, T)
+CASES = {
+    "soft_gated": ("c2_full", 8, 1000, 12),
+    "ot_gated": ("c3_full", 8, 1000, 6),
+    "ot_forced": ("c4_n4000", 4, 2000, 3),
+}
+FIELDS = ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(case, rows, shard=None):
+    import _fullsize as F
+    from nfdpf.engine import FilterConfig, FilterEngine
+    name, B, N, T = CASES[case]
+    wl = F.workload(name, B=B, N=N, T=T)
+    c = F.cfg_dict(wl["flags"], N)
+    cfg = FilterConfig(N=N, NF_dyn=c["NF_dyn"], NF_cond=c["NF_cond"], measurement=c["measurement"],
+                       resampler=c["resampler"], dyn_flow=c["dyn_flow"], force_resample=wl["force"], seed=123,
+                       kernel="tiled")
+    eng = FilterEngine(cfg, wl["models"].to(DEV))
+    sl = slice(*rows)
+    res = eng.run(wl["enc"][sl].to(DEV), wl["start"][sl].to(DEV), wl["vel"][sl].to(DEV), shard=shard)
+    torch.cuda.synchronize()
+    out = {f: getattr(res, f).cpu() for f in FIELDS if getattr(res, f) is not None}
+    out["obs_likelihood"] = res.obs_likelihood.cpu()
+    out["ot_calls"] = eng.last_ot_calls
+    return out
+
+
+def _worker(rank, world, port, case, path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root, os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf import _lib
+        from nfdpf.engine import ShardInfo
+        _lib.load()
+        B = CASES[case][1] // world
+        out = _run(case, (rank * B, (rank + 1) * B), ShardInfo.from_env(B))
+        torch.save(out, f"{path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("case", list(CASES))
+def test_sharded_engine_matches_unsharded(case, tmp_path):
+    import torch.multiprocessing as mp
+    from nfdpf import _lib
+    _lib.load()
+    B = CASES[case][1]
+    full = _run(case, (0, B))
+    world = 2
+    path = str(tmp_path / "shard")
+    mp.start_processes(_worker, args=(world, _free_port(), case, path), nprocs=world, start_method="spawn")
+    parts = [torch.load(f"{path}.{r}", weights_only=True) for r in range(world)]
+    h = B // world
+    for f in FIELDS:
+        if f not in full:
+            continue
+        for r, part in enumerate(parts):
+            assert torch.equal(part[f], full[f][r * h:(r + 1) * h]), (case, f, r)
+    for part in parts:
+        a, b = float(part["obs_likelihood"]), float(full["obs_likelihood"])
+        assert abs(a - b) <= 1e-6 * abs(b), (a, b)  # float32 of the fp64 sums
+        assert part["ot_calls"] == full["ot_calls"]
+    ident = torch.arange(CASES[case][2]) + CASES[case][2] * torch.arange(B)[:, None]
+    fired = int((full["index"] != ident[:, None, :]).any(-1).any(0).sum())
+    print(f"\n{case}: B={B} over {world} ranks, resampling fired in {fired} steps, OT calls {full['ot_calls']}")
+    assert fired > 0 or full["ot_calls"] > 0

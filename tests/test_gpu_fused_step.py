@@ -52,7 +52,7 @@ def _run(eng, inputs, fused, monkeypatch):
     res = eng.run(*inputs)
     torch.cuda.synchronize()
     assert eng.last_fused == fused
-    assert _lib.lib().nfdpf_split_fault(1) == 0
+    assert _lib.lib().nfdpf_split_fault(1, _lib.stream_ptr(DEV)) == 0
     return {k: getattr(res, k).clone() for k in FIELDS}, float(res.obs_likelihood)
 
 
@@ -99,4 +99,4 @@ def test_fused_step_graph_replay(monkeypatch):
         assert torch.equal(outs[0][k], outs[1][k]), k
         assert torch.equal(outs[0][k], ref[k]), k
     from nfdpf import _lib
-    assert _lib.lib().nfdpf_split_fault(1) == 0
+    assert _lib.lib().nfdpf_split_fault(1, _lib.stream_ptr(DEV)) == 0

@@ -236,26 +236,58 @@ def test_ot_poll_matches_enqueue_all():
     assert int(z[3].item()) == 0
 
 
-def test_ot_sharded_stop_matches_unsharded():
-    """A batch split over two 'ranks' reproduces the unsharded Sinkhorn loop: each half runs
-    with the local stop rule, the MIN of the iteration counts is the batch-global stop
-    (resamplers.py:126-129), and each half re-runs to exactly that count (stop_at)."""
+def _ot_two_phase(parts, max_iter=100):
+    """A batch split over 'ranks' the way ops.ot_resample_sharded runs it, the ranks simulated
+    in turn: every part's local loop (private workspace + potential history), the MIN of the
+    counts (the all-reduce), every part's tail at that state."""
     from nfdpf import ops
-    fx = load("ot.npz")
-    c = group(fx, "c1")
-    x, p = t(c["x"]).to(DEV), t(c["p"]).to(DEV)
+    st = []
+    for xx, pp, rb in parts:
+        B, N, _ = xx.shape
+        ws, hist = ops.ot_workspace(B, N, DEV), ops.ot_history(B, N, max_iter, DEV)
+        st.append((ws, hist, ops.ot_sinkhorn_local(xx, pp, 0.1, 0.75, 1e-3, max_iter, ws, hist)))
+    local = [int(s_[2].item()) for s_ in st]
+    stop = torch.tensor([min(local)], dtype=torch.int32, device=DEV)
+    outs = [ops.ot_sinkhorn_finish(xx, 0.1, 0.75, 1e-3, max_iter, rb, ws, hist, stop)
+            for (xx, pp, rb), (ws, hist, _) in zip(parts, st)]
+    return outs, local, min(local)
+
+
+@pytest.mark.parametrize("kind", ["fixture", "mixed"])
+def test_ot_sharded_stop_matches_unsharded(kind):
+    """A batch split over 'ranks' reproduces the unsharded Sinkhorn loop bit for bit
+    (resamplers.py:126-129): each part runs its rows with the local
+    stop rule keeping every state's potentials, the MIN of the counts is the batch-global stop,
+    and each part finishes at that state -- no iteration runs twice.  'mixed' gives the parts
+    clouds of different spread, so one part's own rule stops later than the global MIN and its
+    tail must resume from the history (its tables were overwritten since); also the old
+    two-pass form (rerun with stop_at) for comparison."""
+    from nfdpf import ops
+    if kind == "fixture":
+        c = group(load("ot.npz"), "c1")
+        x, p = t(c["x"]).to(DEV), t(c["p"]).to(DEV)
+    else:
+        g = torch.Generator().manual_seed(17)
+        B, N = 6, 700
+        spread = torch.tensor([1.0, 1.0, 1.0, 30.0, 60.0, 90.0])[:, None, None]
+        x = (torch.randn(B, N, 2, generator=g) * spread).to(DEV)
+        p = torch.softmax(torch.randn(B, N, generator=g) * 2, -1).to(DEV)
     B = x.shape[0]
-    full, _, _, it_full = ops.ot_resample(x, p)
+    full, wfull, ifull, it_full = ops.ot_resample(x, p)
     h = B // 2
     parts = [(x[:h].contiguous(), p[:h].contiguous(), 0), (x[h:].contiguous(), p[h:].contiguous(), h)]
-    its = [ops.ot_resample(xx, pp, row_base=rb)[3] for xx, pp, rb in parts]
-    stop = torch.minimum(its[0], its[1])
-    assert int(stop.item()) == int(it_full.item())
-    outs = [ops.ot_resample(xx, pp, row_base=rb, stop_at=stop) for xx, pp, rb in parts]
-    for o in outs:
-        assert int(o[3].item()) == int(it_full.item())
+    outs, local, stop = _ot_two_phase(parts)
+    assert stop == int(it_full.item()), (local, int(it_full.item()))
     assert torch.equal(torch.cat([outs[0][0], outs[1][0]]), full)
-    assert torch.equal(torch.cat([outs[0][2], outs[1][2]]), ops.ot_resample(x, p)[2])
+    assert torch.equal(torch.cat([outs[0][1], outs[1][1]]), wfull)
+    assert torch.equal(torch.cat([outs[0][2], outs[1][2]]), ifull)
+    if kind == "mixed":
+        assert max(local) > stop, local  # a part resumed behind its own stop
+    # the two-pass form (local run, rerun to the MIN) agrees
+    its = [ops.ot_resample(xx, pp, row_base=rb)[3] for xx, pp, rb in parts]
+    mn = torch.minimum(its[0], its[1])
+    rerun = [ops.ot_resample(xx, pp, row_base=rb, stop_at=mn)[0] for xx, pp, rb in parts]
+    assert torch.equal(torch.cat(rerun), full)
 
 
 @pytest.mark.parametrize("meas", ["cos", "CRNVP", "NN", "gaussian"])
