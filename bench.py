@@ -58,6 +58,10 @@ F_EXEC = {"c2": 5696.0, "c4": 4768.0}
 # inverse's executed 1,280 (4 coupling halves x 2 nets x (1 + 8x8 + 8) MAC; 4 of its 5 inputs are
 # the per-row context, folded)
 F_EXEC_STEP = {"c2": 6976.0}
+# the merged front launch (tiled_fdyn_kernel): the nf_dyn inverse, 1,792 matmul FLOP (A9) scaled
+# by 13.1 / 12.608 for the elementwise work; executed 1,280 (its [mean, std] context folded)
+F_DYN_INV = 1792.0 * 13.1 / 12.608
+F_DYN_INV_EXEC = 1280.0
 B_ALG = 52.0            # algorithmic HBM bytes per particle-step
 B_SOFT = 36.0           # soft resampling, HBM bytes per particle: read x 8 + p 4,
 #                         write x' 8 + w' 4 + index 8, + 4 for the row's CDF pass
@@ -217,11 +221,26 @@ def ot_call_ms(res, T, iters=10):
     return best
 
 
+def rocprof_avg_ms(tag, kname):
+    """Average duration (ms) of ``kname`` in the committed rocprofv3 --kernel-trace --stats
+    summary of this workload's bench command (scripts/r03_measure.sh -> profiles/rocprof_<tag>.csv,
+    tag = config [+ _force]), and the file; (None, None) when there is none."""
+    path = os.path.join(ROOT, "profiles", f"rocprof_{tag}.csv")
+    if not os.path.exists(path):
+        return None, None
+    import csv
+    for row in csv.DictReader(open(path)):
+        name = row["Name"].split("(")[0].split("::")[-1].split("<")[0].strip()
+        if name == kname:
+            return float(row["AverageNs"]) * 1e-6, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def pmc_traffic(cfg_name, kname):
     """HBM bytes per launch of ``kname`` from the committed PMC summary of this workload
-    (scripts/pmc.sh + scripts/pmc_summary.py -> profiles/pmc_<config>.csv): FETCH_SIZE and
-    WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts half the bytes of a streaming read
-    (MI355X_MICROARCH.md, HBM / rocprofv3), so it is doubled.  None when no summary exists."""
+    (scripts/pmc.sh + scripts/pmc_summary.py -> profiles/pmc_<tag>.csv, tag = config [+ _force]):
+    FETCH_SIZE and WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts half the bytes of a streaming
+    read (MI355X_MICROARCH.md, HBM / rocprofv3), so it is doubled.  None when no summary exists."""
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.csv")
     if not os.path.exists(path):
         return None, None
@@ -304,8 +323,7 @@ def main():
     ot = flags["resampler_type"] == "ot"
     # auto (engine.FilterEngine.run): speculative gates when sharded, and for OT at any world size
     # unless the previous pass resampled (then its gates are read step by step)
-    spec_on = (world > 1 or ot) if args.speculate < 0 else bool(args.speculate)
-    spec = spec_on and args.kernel == "tiled" and not args.force_resample and not (ot and eng._ot_fired)
+    spec = eng.speculates(shard)  # the engine's own decision for the next pass (engine._decide_spec)
     if args.graph and ((flags["resampler_type"] == "soft" and world == 1) or spec):
         # the pass has no host synchronisation in this mode: capture it once, replay per step
         # (every launch of every time step runs on each replay; only the Python launch path goes).
@@ -373,19 +391,31 @@ def main():
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
     F_EX = F_EXEC.get(args.config, F_ALG) if kname.startswith("tiled_prop") else F_ALG
+    bound = "mfma" if kname == "cglow_kernel" else "valu"
     if args.kernel == "tiled" and eng.last_fused:  # the whole step in one launch: all of its FLOP
         kname, F_ALG = "tiled_step_fused_kernel", F_STEP
         F_EX = F_EXEC_STEP.get(args.config, F_ALG)
+    elif front_ms is not None and front_ms > kernel_ms:
+        # the step's front launch (gate + resampling + motion [+ nf_dyn inverse]) is the longer
+        # one (--force-resample): it is the dominant kernel
+        kernel_ms = front_ms
+        if kname == "tiled_prop_quad_kernel":  # merged front + nf_dyn inverse (use_merged)
+            kname, F_ALG, F_EX = "tiled_fdyn_kernel", F_DYN_INV, F_DYN_INV_EXEC
+        else:  # gate + soft resampling + motion: bytes, not FLOP
+            kname, F_ALG, F_EX, bound = "tiled_front_kernel", 0.0, 0.0, "hbm"
+            launch_bytes = (B_SOFT + 8.0 + 8.0) * B * N  # resampling + motion's noise / x' writes
     ot_iter_ms = None
     if flags["resampler_type"] == "ot" and eng.last_ot_calls:
         ot_iter_ms = ot_iteration_ms(res, T)
         if ot_iter_ms * eng.last_ot_calls * 10 > kernel_ms * T:  # the Sinkhorn loop dominates
-            kname, kernel_ms = "ot_iter_kernel", ot_iter_ms
+            kname, kernel_ms, bound = "ot_iter_kernel", ot_iter_ms, "valu"
             F_ALG, launch_units = F_OT_PAIR, B * N * N
             F_EX = F_ALG
             # per particle: x~ (8 B) + logw (4) + both potentials read and written (fp64, 32)
             launch_bytes = 44.0 * B * N
-    traffic, traffic_src = pmc_traffic(args.config, kname)
+    tag = args.config + ("_force" if args.force_resample else "")
+    traffic, traffic_src = pmc_traffic(tag, kname)
+    rp_ms, rp_src = rocprof_avg_ms(tag, kname)
     # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
     se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
     cnt = torch.tensor(float(res.pred.numel()), device=dev, dtype=torch.float64)
@@ -393,6 +423,19 @@ def main():
         dist.all_reduce(se)
         dist.all_reduce(cnt)
     rmse = float(torch.sqrt(se / cnt))
+    # the same filter on INFORMATIVE frame encodings (the particle encoder at the true
+    # positions, what a trained frame encoder approximates): the timed passes' N(0,1) encodings
+    # carry no information, so their RMSE is not a filtering-quality number.  One untimed pass
+    # on its own engine (the timed engine's speculation state is left alone).
+    rmse_inf = None
+    if not args.enc_from_state:
+        with torch.no_grad():
+            enc_inf = dpf.particle_encoder(state[:, :, :2].float()).contiguous()
+        res_inf = FilterEngine(fcfg, dpf).run(enc_inf, start, vel_in, shard=shard)
+        se = ((res_inf.pred - state[:, :, :2]) ** 2).sum().double()
+        if world > 1:
+            dist.all_reduce(se)
+        rmse_inf = float(torch.sqrt(se / cnt))
     # steps whose ESS gate fired (DPFs.py:165) in the last pass: OT calls are counted on the
     # host by the engine; a soft resample leaves a non-identity index row
     if flags["resampler_type"] == "ot":
@@ -441,14 +484,20 @@ def main():
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
                        "parallelism": f"batch-sharded x{world}"},
             "rmse": rmse,
+            "rmse_informative_encodings": rmse_inf,
             "resampled_steps": resampled,
             # bound: the FP32 issue rate of the CU -- VALU for the coupling nets / Sinkhorn
             # (v_pk_fma_f32, v_exp_f32), f32 MFMA + VALU for CGLOW; same 157.3 TFLOP/s peak
-            "roofline": {"bound": "mfma" if kname == "cglow_kernel" else "valu", "achieved": achieved_tf,
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "traffic_source": traffic_src,
+            "roofline": {"bound": bound,
+                         "achieved": achieved_tf if bound != "hbm" else hbm_gbs,
+                         "peak": PEAK_FP32_TFLOPS if bound != "hbm" else PEAK_HBM_GBS,
+                         "unit": "TFLOP/s" if bound != "hbm" else "GB/s",
+                         "frac": achieved_tf / PEAK_FP32_TFLOPS if bound != "hbm" else hbm_gbs / PEAK_HBM_GBS,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_avg_ms": kernel_ms,
+                         # the same kernel's average in the committed rocprofv3 summary of this
+                         # bench command (profiles/rocprof_<config>.csv), beside the live figure
+                         "kernel_avg_ms_rocprof": rp_ms, "rocprof_source": rp_src,
                          "flop_per_unit": F_ALG, "units_per_launch": per_launch_units,
                          "flop_per_unit_executed": F_EX,
                          "frac_executed": F_EX * per_launch_units / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,

@@ -56,6 +56,13 @@ struct TiledWs {
   float *cb_cond;   // [B][kCb] proposal fold over the encoding columns (K1, tile 0)
   double *fin;      // [B][T][tiles][4] sum p^2, sum p x0, sum p x1, sum logw
   uint64_t *rowx;   // [B][tiles][8] the fused step's x_dyn partials as tagged granules
+  // tiled_rows_kernel's outputs (long rows, soft resampler): the step's gate, each row's
+  // normaliser of the deferred slot t-1 and, when the gate fired, each particle's source and
+  // resampled log-weight
+  int32_t *rs_gate;  // [1]
+  float *rs_rn;      // [B][4] RowNorm {shift, Ssum, Lmax}
+  int32_t *rs_src;   // [B][N]
+  float *rs_lr;      // [B][N]
 };
 // The step's softmax partials live in the caller's ess_out / ess_all (include/nfdpf.h):
 // per (row, tile) {max u, sum e^(u-max), sum e^(2(u-max)), max raw likelihood}.
@@ -68,7 +75,8 @@ __host__ __device__ static inline int n_tiles(int N) { return (N + kTile - 1) / 
 
 static int64_t tiled_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(bt * 32) * 2 + al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32) + al256(bt * 64);
+  return al256(bt * 32) * 2 + al256((int64_t)B * kCb * 4) * 2 + al256(bt * T * 32) + al256(bt * 64) + al256(4) +
+         al256((int64_t)B * 16) + al256((int64_t)B * N * 4) * 2;
 }
 
 static TiledWs tiled_carve(void *ws, int B, int N, int T) {
@@ -86,6 +94,14 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
   w.fin = (double *)p;
   p += al256(bt * T * 32);
   w.rowx = (uint64_t *)p;
+  p += al256(bt * 64);
+  w.rs_gate = (int32_t *)p;
+  p += al256(4);
+  w.rs_rn = (float *)p;
+  p += al256((int64_t)B * 16);
+  w.rs_src = (int32_t *)p;
+  p += al256((int64_t)B * N * 4);
+  w.rs_lr = (float *)p;
   return w;
 }
 
@@ -257,13 +273,84 @@ __device__ __forceinline__ void store_sums4(double *dst, double a, double b, dou
 // gathered weights), keeping its own particles' sources in registers -- so resampling and
 // motion share one launch and the resampled state never round-trips through HBM.
 // Dynamic LDS: C[max(N, B_global)] then w'[N].
+//
+// ROWS (long rows: tiled_rows_kernel ran first): the gate, the deferred slot's row normaliser
+// and -- when the gate fired -- every particle's source and resampled log-weight come from
+// that launch, so this one holds no dynamic LDS and no per-tile copy of the row's search.
+
+// ---- K0 for long rows with the soft resampler, one 1024-thread workgroup per row: the step's
+// ESS gate (the same block-parallel cascade-order evaluation, every workgroup alike), the row
+// normaliser of the deferred slot t-1 and, when the gate fires, the row's soft resampling
+// (resamplers.py:20-60, the soft.hpp recipe) ONCE per row.  tiled_front_kernel otherwise
+// rebuilds the row's CDF and searches all N markers in each of the row's N / 256 tiles and
+// evaluates the batch gate in every one of them (C5: 2,560 workgroups each reading the 64 x 40
+// partials, with 120 KB of LDS each: one workgroup per CU -- 235 us per step, round 2).
+__global__ __launch_bounds__(1024) void tiled_rows_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  extern __shared__ float dyn_lds[];
+  __shared__ double shd[16];
+  __shared__ float shf[16];
+  __shared__ int fire_sh;
+  __shared__ RowNorm rn_sh;
+  const int tiles = n_tiles(d.N), N = d.N;
+  const int b = blockIdx.x;
+  const int64_t grow = d.row_base + b;
+  const bool defer = d.defer_norm && d.t > 0;
+  const bool shifted = shifted_meas(d.measurement);
+  float *Cbuf = dyn_lds;
+  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh, defer ? ess_row(d, b) : -1, &rn_sh, shifted);
+  if (threadIdx.x == 0) {
+    if (b == 0) ws.rs_gate[0] = fire ? 1 : 0;
+    if (defer) {
+      ws.rs_rn[4 * b] = rn_sh.shift;
+      ws.rs_rn[4 * b + 1] = rn_sh.Ssum;
+      ws.rs_rn[4 * b + 2] = rn_sh.Lmax;
+    }
+  }
+  if (!fire || d.resampler != NFDPF_RESAMPLE_SOFT) return;
+  const float *pprev = d.p_prev + b * d.p_prev_rs;
+  float *wbuf = dyn_lds + max(N, d.B_global);
+  if (defer) {  // the row's p_{t-1} into LDS for the resampler
+    const RowNorm rn = rn_sh;
+    const RowSlot Sp = row_slot(d, b, d.t - 1);
+    float *pbuf = wbuf + N;
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
+      float lw, lk;
+      pbuf[j] = norm_value(Sp, j, rn, shifted, lw, lk);
+    }
+    __syncthreads();
+    pprev = pbuf;
+  }
+  SoftRow row{pprev, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
+  float off;
+  if (d.rng_mode == NFDPF_RNG_HOST && d.host_offsets)
+    off = d.host_offsets[b];
+  else
+    off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)d.t, grow, 0u).x) * (1.0f / (float)N);
+  int32_t *src_out = ws.rs_src + (int64_t)b * N;
+  soft_row_search(row, d.lin, off, Cbuf, shd, shf, [&](int j, int src) {
+    // src == N: the reference's out-of-range edge (next row's first particle, weight 0)
+    wbuf[j] = src < N ? row.w(src) : 0.f;
+    src_out[j] = src;
+  });
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const float s2 = cascade_row_sum([&](int j) { return wbuf[j]; }, N);
+    if (threadIdx.x == 0) shf[8] = s2;
+  }
+  __syncthreads();
+  const float s2 = shf[8];
+  float *lr_out = ws.rs_lr + (int64_t)b * N;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) lr_out[j] = logf(wbuf[j] / s2);
+}
+
+template <bool ROWS>
 __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   extern __shared__ float dyn_lds[];
   __shared__ double shd[16];
   __shared__ float shf[16];
   __shared__ int fire_sh;
-  __shared__ float xr_sh[kTile][2];
-  __shared__ int src_sh[kTile];
+  __shared__ float xr_sh[ROWS ? 1 : kTile][2];
+  __shared__ int src_sh[ROWS ? 1 : kTile];
   TRACE(0, 0)
   const int tiles = n_tiles(d.N), N = d.N;
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -276,9 +363,13 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   float e0 = 0.f, e1 = 0.f;
   if (i < N) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: computed under its latency
   __shared__ RowNorm rn_sh;
-  const int64_t my_row = ess_row(d, b);
-  const bool fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh, defer ? my_row : -1, &rn_sh,
-                                     shifted_meas(d.measurement));
+  bool fire;
+  if constexpr (ROWS) {
+    fire = ws.rs_gate[0] != 0;
+  } else {
+    const int64_t my_row = ess_row(d, b);
+    fire = tiled_gate_block(d, tiles, Cbuf, &fire_sh, defer ? my_row : -1, &rn_sh, shifted_meas(d.measurement));
+  }
   TRACE(0, 1)
   const int mode = !fire ? kSrcPrev : (d.resampler == NFDPF_RESAMPLE_SOFT ? kSrcSoft : kSrcOt);
   const RowSlot S = row_slot(d, b);
@@ -289,7 +380,10 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   RowNorm rn{0.f, 1.f, 0.f};
   RowSlot Sp = S;
   if (defer) {
-    rn = rn_sh;  // left by the gate staging (same partials)
+    if constexpr (ROWS)
+      rn = RowNorm{ws.rs_rn[4 * b], ws.rs_rn[4 * b + 1], ws.rs_rn[4 * b + 2]};
+    else
+      rn = rn_sh;  // left by the gate staging (same partials)
     Sp = row_slot(d, b, d.t - 1);
   }
   auto prev_p = [&](int j) {
@@ -297,7 +391,16 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
     return norm_value(Sp, j, rn, shifted_meas(d.measurement), lw, lk);
   };
   float x0 = 0.f, x1 = 0.f, lr = 0.f;
-  if (mode == kSrcSoft) {
+  if (ROWS && mode == kSrcSoft) {
+    if (i < N) {  // the row's resampling, done once by tiled_rows_kernel
+      const int src = ws.rs_src[(int64_t)b * N + i];
+      const float *xs = src < N ? xprev + 2 * src : (b + 1 < d.B ? xprev + d.x_prev_rs : xprev + 2 * (N - 1));
+      x0 = xs[0];
+      x1 = xs[1];
+      lr = ws.rs_lr[(int64_t)b * N + i];
+      S.hidx[i] = (int64_t)N * grow + src;
+    }
+  } else if (mode == kSrcSoft) {
     float *wbuf = dyn_lds + max(N, d.B_global);
     if (defer) {  // the row's p_{t-1} into LDS for the resampler
       float *pbuf = wbuf + N;
@@ -1507,6 +1610,16 @@ static bool use_merged(const nfdpf_filter_desc &d) {
          d.B_global <= kMergedMaxN;
 }
 
+// Rows longer than this (soft resampler, not the merged path) take the gate, the deferred row
+// normaliser and the row's resampling from tiled_rows_kernel, once per row.
+// (NFDPF_TILED_ROWS_MIN_N overrides the threshold, read per call: tests compare both paths.)
+constexpr int kRowsMinN = 1024;
+static bool use_rows(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_TILED_ROWS_MIN_N");
+  const int min_n = e ? atoi(e) : kRowsMinN;
+  return d.resampler == NFDPF_RESAMPLE_SOFT && !use_merged(d) && d.N > min_n;
+}
+
 // One launch per step (tiled_step_fused_kernel), opt-in with NFDPF_FUSED_STEP=1, when every
 // workgroup of the grid can be resident at once -- one 1024-thread workgroup per CU -- since a
 // row's four workgroups wait for each other inside it.  Measured SLOWER than the two launches
@@ -1718,10 +1831,17 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
         hipExtLaunchKernelGGL(tiled_fdyn_kernel, g, dim3(2 * kTile), mlds, st, fev[0], fev[1], 0, d, ws);
       else
         tiled_fdyn_kernel<<<g, 2 * kTile, mlds, st>>>(d, ws);
+    } else if (use_rows(d)) {
+      // the gate / row normaliser / row resampling once per row, then the tiles without LDS
+      tiled_rows_kernel<<<d.B, 1024, lds, st>>>(d, ws);
+      if (fev)
+        hipExtLaunchKernelGGL(tiled_front_kernel<true>, g, dim3(kTile), 0, st, fev[0], fev[1], 0, d, ws);
+      else
+        tiled_front_kernel<true><<<g, kTile, 0, st>>>(d, ws);
     } else if (fev) {
-      hipExtLaunchKernelGGL(tiled_front_kernel, g, dim3(kTile), lds, st, fev[0], fev[1], 0, d, ws);
+      hipExtLaunchKernelGGL(tiled_front_kernel<false>, g, dim3(kTile), lds, st, fev[0], fev[1], 0, d, ws);
     } else {
-      tiled_front_kernel<<<g, kTile, lds, st>>>(d, ws);
+      tiled_front_kernel<false><<<g, kTile, lds, st>>>(d, ws);
     }
     if (use_fused(d))
       ;  // the whole step ran in tiled_step_fused_kernel

@@ -155,6 +155,35 @@ class FilterEngine:
         st["step_events"] = None
         return st
 
+    def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False) -> bool:
+        """Does the next pass run with the speculative ESS gate (every gate taken as off, the T
+        gates verified once after the pass from all steps' partials, a fired gate rerunning the
+        pass step by step)?  Auto mode (``speculate`` and cfg.speculate_gate None): yes for the
+        tiled pipeline at any world size -- the reference reads its gate before every step
+        (DPFs.py:163-165), which in the tiled step is a chain of dependent loads and fp64
+        arithmetic at the head of every front launch (and, sharded, a per-step collective; with
+        OT, a device->host sync per step) -- unless the previous pass resampled (OT: its gates
+        are then read step by step) or a recent miss is backing off (a miss costs a whole second
+        pass; the next 1, 2, 4 ... 64 passes run step by step).  ``consume``: count this pass
+        against the back-off (run() only)."""
+        c = self.cfg
+        tiled = c.kernel == "tiled"
+        auto = speculate is None and c.speculate_gate is None
+        if speculate is None:
+            speculate = c.speculate_gate if c.speculate_gate is not None else tiled
+        if auto and tiled and c.resampler == "ot" and self._ot_fired:
+            speculate = False  # the last pass resampled: per-step gates, no wasted speculative pass
+        elif auto and speculate and self._spec_skip > 0:
+            if consume:
+                self._spec_skip -= 1
+            speculate = False
+        return bool(speculate and tiled and c.resampler in ("soft", "ot") and not host_mode and not teacher
+                    and not c.force_resample and c.measurement != "CGLOW")
+
+    def speculates(self, shard=None) -> bool:
+        """Whether run() (auto arguments, device RNG) will speculate the gates of its next pass."""
+        return self._decide_spec(shard or ShardInfo(), None, self.cfg.rng_mode == "host")
+
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
         c, m = self.cfg, self.m
@@ -225,21 +254,7 @@ class FilterEngine:
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
         ot_auto = auto and tiled and c.resampler == "ot"
-        if speculate is None:
-            # auto: sharded (one exchange per pass instead of one per step), and OT at any world
-            # size -- its gate is read on the host before every Sinkhorn call (DPFs.py:165), a
-            # device->host sync per step that keeps the pass out of a graph; speculating, a pass
-            # whose gates all stay off has no sync and no Sinkhorn launch at all
-            speculate = c.speculate_gate if c.speculate_gate is not None else (shard.world > 1 or ot_auto)
-        if ot_auto and self._ot_fired:
-            speculate = False  # the last pass resampled: per-step gates, no wasted speculative pass
-        elif auto and speculate and self._spec_skip > 0:
-            # auto mode after a fired gate: the per-step exchange for the next passes (a miss
-            # costs a whole second pass -- profiles/r02_dist_*.json), retried with backoff
-            self._spec_skip -= 1
-            speculate = False
-        spec = bool(speculate and tiled and c.resampler in ("soft", "ot") and not host_mode and teacher is None
-                    and not c.force_resample and not external)
+        spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True)
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)

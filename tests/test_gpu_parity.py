@@ -670,3 +670,30 @@ def test_gate_batch_matches_single():
     single = torch.stack([ops.ess_gate_tiled(parts[k].contiguous(), N, k).cpu()[0] for k in range(T)])
     assert torch.equal(batch, single)
     assert 0 < int(batch.sum()) < T
+
+
+@pytest.mark.parametrize("N,force", [(2000, True), (2000, False), (700, True)])
+def test_rows_kernel_matches_per_tile_resampling(N, force, monkeypatch):
+    """Long rows (soft resampler off the merged path): tiled_rows_kernel takes the gate, the
+    deferred row normaliser and the row's resampling once per row; the per-tile path does all
+    three in every tile.  Same arithmetic, so the passes are bit-identical (both forced through
+    NFDPF_TILED_ROWS_MIN_N)."""
+    import _fullsize as F
+    from nfdpf.engine import FilterConfig, FilterEngine
+    wl = F.workload("c2_full", B=6, N=N, T=6)
+    models = wl["models"].to(DEV)
+    out = {}
+    for min_n in (0, 1 << 30):  # rows kernel for every N / never
+        monkeypatch.setenv("NFDPF_TILED_ROWS_MIN_N", str(min_n))
+        # NF_cond off: not the merged C2 path, so the front launch is tiled_front_kernel
+        cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=False, measurement="cos", resampler="soft",
+                           force_resample=force, seed=5, kernel="tiled")
+        out[min_n] = FilterEngine(cfg, models).run(wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+    a, b = out[0], out[1 << 30]
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    ident = torch.arange(N, device=DEV) + N * torch.arange(6, device=DEV)[:, None]
+    fired = int((a.index != ident[:, None, :]).any(-1).any(0).sum())
+    print(f"\nN={N} force={force}: resampled in {fired} of 6 steps")
+    if force:
+        assert fired == 6
