@@ -155,7 +155,8 @@ class FilterEngine:
         st["step_events"] = None
         return st
 
-    def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False) -> bool:
+    def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False,
+                     finish=True) -> bool:
         """Does the next pass run with the speculative ESS gate (every gate taken as off, the T
         gates verified once after the pass from all steps' partials, a fired gate rerunning the
         pass step by step)?  Auto mode (``speculate`` and cfg.speculate_gate None): yes for the
@@ -165,12 +166,16 @@ class FilterEngine:
         OT, a device->host sync per step) -- unless the previous pass resampled (OT: its gates
         are then read step by step) or a recent miss is backing off (a miss costs a whole second
         pass; the next 1, 2, 4 ... 64 passes run step by step).  ``consume``: count this pass
-        against the back-off (run() only)."""
+        against the back-off (run() only).  A pass captured into a graph (``finish`` with a
+        capturing stream) cannot verify its gates on the host: auto mode does not speculate
+        there (run(finish=False) does, leaving finish_pending to the caller)."""
         c = self.cfg
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
         if speculate is None:
             speculate = c.speculate_gate if c.speculate_gate is not None else tiled
+            if auto and finish and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                speculate = False
         if auto and tiled and c.resampler == "ot" and self._ot_fired:
             speculate = False  # the last pass resampled: per-step gates, no wasted speculative pass
         elif auto and speculate and self._spec_skip > 0:
@@ -180,9 +185,9 @@ class FilterEngine:
         return bool(speculate and tiled and c.resampler in ("soft", "ot") and not host_mode and not teacher
                     and not c.force_resample and c.measurement != "CGLOW")
 
-    def speculates(self, shard=None) -> bool:
+    def speculates(self, shard=None, finish=True) -> bool:
         """Whether run() (auto arguments, device RNG) will speculate the gates of its next pass."""
-        return self._decide_spec(shard or ShardInfo(), None, self.cfg.rng_mode == "host")
+        return self._decide_spec(shard or ShardInfo(), None, self.cfg.rng_mode == "host", finish=finish)
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -254,7 +259,7 @@ class FilterEngine:
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
         ot_auto = auto and tiled and c.resampler == "ot"
-        spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True)
+        spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish)
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)

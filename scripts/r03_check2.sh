@@ -2,8 +2,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 500 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_dist.py \
-  tests/test_gpu_fused_step.py tests/test_gpu_parity.py -k "dist or fused or rows_kernel or speculative or ot_sharded" \
+timeout -k 10 500 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread \
+  tests/test_gpu_fused_step.py tests/test_gpu_parity.py -k "fused or rows_kernel or speculative or ot_sharded" \
   > gpurun_out/r03_dist_tests2.log 2>&1 || { echo "dist tests failed"; tail -40 gpurun_out/r03_dist_tests2.log; exit 1; }
 tail -3 gpurun_out/r03_dist_tests2.log
 for a in 1 2; do
