@@ -160,12 +160,14 @@ class FilterEngine:
         """Does the next pass run with the speculative ESS gate (every gate taken as off, the T
         gates verified once after the pass from all steps' partials, a fired gate rerunning the
         pass step by step)?  Auto mode (``speculate`` and cfg.speculate_gate None): yes for the
-        tiled pipeline at any world size -- the reference reads its gate before every step
-        (DPFs.py:163-165), which in the tiled step is a chain of dependent loads and fp64
-        arithmetic at the head of every front launch (and, sharded, a per-step collective; with
-        OT, a device->host sync per step) -- unless the previous pass resampled (OT: its gates
-        are then read step by step) or a recent miss is backing off (a miss costs a whole second
-        pass; the next 1, 2, 4 ... 64 passes run step by step).  ``consume``: count this pass
+        tiled pipeline when the batch is sharded (one exchange per pass instead of one per step)
+        and for OT at any world size (its gate is read on the host before every Sinkhorn call,
+        DPFs.py:165: a device->host sync per step) -- unless the previous pass resampled (OT:
+        its gates are then read step by step) or a recent miss is backing off (a miss costs a
+        whole second pass; the next 1, 2, 4 ... 64 passes run step by step).  Not for the soft
+        resampler on one GPU: its per-step gate is device-side already, and speculating saved
+        0.33 us of the front launch per step against ~30 us of verification per pass (C2, round
+        3: 2.09e9 vs 2.13e9 particle-steps/s).  ``consume``: count this pass
         against the back-off (run() only).  A pass captured into a graph (``finish`` with a
         capturing stream) cannot verify its gates on the host: auto mode does not speculate
         there (run(finish=False) does, leaving finish_pending to the caller)."""
@@ -173,7 +175,8 @@ class FilterEngine:
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
         if speculate is None:
-            speculate = c.speculate_gate if c.speculate_gate is not None else tiled
+            speculate = c.speculate_gate if c.speculate_gate is not None else \
+                (tiled and (shard.world > 1 or c.resampler == "ot"))
             if auto and finish and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 speculate = False
         if auto and tiled and c.resampler == "ot" and self._ot_fired:
