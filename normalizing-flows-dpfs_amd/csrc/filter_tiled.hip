@@ -45,8 +45,13 @@ __device__ unsigned long long g_trace[4][2048][8];
 #define TRACE(K, P)                                                                        \
   if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < 2048)                     \
     g_trace[K][blockIdx.y * gridDim.x + blockIdx.x][P] = __builtin_amdgcn_s_memrealtime();
+// the same from lane 0 of the executing wave (several waves of one workgroup record slots)
+#define TRACEW(K, P)                                                                       \
+  if ((threadIdx.x & 63) == 0 && blockIdx.y * gridDim.x + blockIdx.x < 2048)              \
+    g_trace[K][blockIdx.y * gridDim.x + blockIdx.x][P] = __builtin_amdgcn_s_memrealtime();
 #else
 #define TRACE(K, P)
+#define TRACEW(K, P)
 #endif
 
 struct TiledWs {
@@ -750,8 +755,10 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
       __builtin_amdgcn_wave_barrier();
+      TRACEW(0, 4)
       const float s = cascade_row_sum([&](int r) { return Cbuf[r]; }, d.B_global);
       if (threadIdx.x == 0) fire_sh = (s / (float)d.B_global) < 0.5f * (float)N;
+      TRACEW(0, 5)
     }
   } else if (spec && (!FUSED || threadIdx.x < 2 * kTile)) {
     // every source load of this thread first (one memory latency instead of one per
@@ -766,11 +773,20 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
       xs0[k] = j < N ? src[2 * j] : 0.f;
       xs1[k] = j < N ? src[2 * j + 1] : 0.f;
     }
+#ifdef NFDPF_EXP_TRACE
+    if (threadIdx.x >> 6 == 1) {  // wave 1: when its source loads have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      TRACEW(0, 6)
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int j = j0 + k * js;
       if (j < N) acc(j, xs0[k], xs1[k]);
     }
+#ifdef NFDPF_EXP_TRACE
+    if (threadIdx.x >> 6 == 1) TRACEW(0, 7)
+#endif
   }
   __syncthreads();
   const bool fire = fire_sh != 0;
@@ -1126,7 +1142,7 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   __syncthreads();
   if (flows && valid) {
     float lik;
-    if (ROLES == 3) {
+    if constexpr (ROLES == 3) {
       lik = cos_lik(ssx[1][pl] + ssx[2][pl], dotx[1][pl] + dotx[2][pl], L.vinv);
       S.hlik[i] = lik;
     } else {
