@@ -351,8 +351,8 @@ __device__ float cascade_row_sum(const Get &v, int n) {
   if (W == 1) return __shfl(ps, 0);
   float tot = 0.f;
   for (int r = nv * 8; r < n; ++r) tot += v(r);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) tot += __shfl(ps, q);
+#pragma unroll  // lanes 0..7 in order; v_readlane (SGPR broadcast) instead of an LDS permute each
+  for (int q = 0; q < 8; ++q) tot += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ps), q));
   return tot;
 }
 

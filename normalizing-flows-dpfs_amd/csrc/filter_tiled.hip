@@ -686,13 +686,26 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
   if (threadIdx.x < 16) xflag[threadIdx.x] = 0;
   pair_clear(xbuf, kTile);
   float e0 = 0.f, e1 = 0.f;
-  if (valid) motion_noise(d, b, grow, i, e0, e1);  // independent of the gate: under its latency
   const int64_t my_row = ess_row(d, b);
   const RowSlot S = row_slot(d, b);
   const float *xprev = d.x_prev + b * d.x_prev_rs;
   const float *pprev = d.p_prev + b * d.p_prev_rs;
   const RowSlot Sp = defer ? row_slot(d, b, d.t - 1) : S;
   const float v0 = d.vel[2 * b], v1 = d.vel[2 * b + 1];
+  const double *parts = reinterpret_cast<const double *>(d.ess_all);
+  // Phase 1 is memory latency (the previous launch's outputs: ~2.4 us from the workgroup's start,
+  // round-3 trace) plus Philox draws that depend on no load: every wave issues its loads first
+  // and draws while they are in flight.  The gate wave's partials of rows lane (tiles <= 4, the
+  // merged C2 path) are loaded into registers before anything else.
+  const bool gate_wave = threadIdx.x < 64 && !d.gate && !d.force_resample;
+  constexpr int kPreT = 4;
+  double pre[kPreT * kSm];
+  const bool pre_ok = gate_wave && tiles <= kPreT && (int)threadIdx.x < d.B_global;
+  if (pre_ok) {
+    const double *pr = parts + (int64_t)threadIdx.x * tiles * kSm;
+#pragma unroll
+    for (int k = 0; k < kPreT * kSm; ++k) pre[k] = k < tiles * kSm ? pr[k] : 0.0;
+  }
   // fold operands that depend on nothing computed in this launch, loaded now so their latency
   // hides under the gate / speculative motion: the nf_dyn fold's bias and context weights
   // (threads < n_flows*4*H) and, in tile 0, the proposal fold over the encoding columns
@@ -723,26 +736,29 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
   float enc_fold = 0.f;
   if (enc_fold_lane) {  // proposal fold over the encoding columns (model/models.py:338-346); K3 adds mean/std
     const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(d.E + 4), threadIdx.x - enc_fold_t0);
-    enc_fold = fold_acc(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
+    enc_fold = fold_acc_pipe(r, d.E + 4, fold_bias0(r, d.E + 4), S.enc, 0, d.E);
   }
   // the row's sums over x_phys = (x_src + vel) + eps (motion_apply_eps's arithmetic)
   double a0 = 0, a1 = 0, c0 = 0, c1 = 0;
-  auto acc = [&](int j, float xs0, float xs1) {
-    float n0, n1;
-    motion_noise(d, b, grow, j, n0, n1);
+  auto acc_n = [&](float xs0, float xs1, float n0, float n1) {
     const float p0 = (xs0 + v0) + n0, p1 = (xs1 + v1) + n1;
     a0 += p0;
     a1 += p1;
     c0 += (double)p0 * p0;
     c1 += (double)p1 * p1;
   };
+  auto acc = [&](int j, float xs0, float xs1) {
+    float n0, n1;
+    motion_noise(d, b, grow, j, n0, n1);
+    acc_n(xs0, xs1, n0, n1);
+  };
   // The ESS gate (DPFs.py:163-165) is a chain of dependent loads and fp64 arithmetic on one
   // wave: wave 0 evaluates it (tiled_gate_block's arithmetic) while waves 1..7 run the
   // no-resampling motion of the row speculatively -- kept when the gate stays off (every
   // step of the C2 bench), recomputed from the resampled sources when it fires.
-  const double *parts = reinterpret_cast<const double *>(d.ess_all);
   const bool spec = !d.force_resample && !(d.gate && d.gate[0] != 0);
   if (threadIdx.x < 64) {
+    if (valid) motion_noise(d, b, grow, i, e0, e1);  // under the partials' latency
     if (d.gate || d.force_resample) {
       if (threadIdx.x == 0) {
         fire_sh = d.gate ? d.gate[0] != 0 : 1;
@@ -750,8 +766,11 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
       }
     } else {
       for (int r = threadIdx.x; r < d.B_global; r += 64) {
-        Cbuf[r] = row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, N, d.t > 0);
-        if (defer && r == my_row) rn_sh = row_norm(parts + (int64_t)r * tiles * kSm, tiles, shifted);
+        // rows < 64 from the registers loaded at the launch's start (the row normaliser of this
+        // workgroup's own row too: no second round trip)
+        const double *sm = (pre_ok && r == (int)threadIdx.x) ? pre : parts + (int64_t)r * tiles * kSm;
+        Cbuf[r] = row_inv_ess(sm, tiles, N, d.t > 0);
+        if (defer && r == my_row) rn_sh = row_norm(sm, tiles, shifted);
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
       __builtin_amdgcn_wave_barrier();
@@ -773,20 +792,31 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
       xs0[k] = j < N ? src[2 * j] : 0.f;
       xs1[k] = j < N ? src[2 * j + 1] : 0.f;
     }
+    // the draws while the sources are in flight (they depend on no load), then the sums
+    float n0[kPer], n1[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int j = j0 + k * js;
+      n0[k] = n1[k] = 0.f;
+      if (j < N) motion_noise(d, b, grow, j, n0[k], n1[k]);
+    }
+    if (valid) motion_noise(d, b, grow, i, e0, e1);
 #ifdef NFDPF_EXP_TRACE
-    if (threadIdx.x >> 6 == 1) {  // wave 1: when its source loads have landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x >> 6 == 1) {  // wave 1: draws done / its source loads landed
       TRACEW(0, 6)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 #endif
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int j = j0 + k * js;
-      if (j < N) acc(j, xs0[k], xs1[k]);
+      if (j < N) acc_n(xs0[k], xs1[k], n0[k], n1[k]);
     }
 #ifdef NFDPF_EXP_TRACE
     if (threadIdx.x >> 6 == 1) TRACEW(0, 7)
 #endif
+  } else if (valid) {
+    motion_noise(d, b, grow, i, e0, e1);
   }
   __syncthreads();
   const bool fire = fire_sh != 0;

@@ -37,9 +37,15 @@ __device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) {
 
 // context from (sum x, sum y, sum x^2, sum y^2) over N particles
 __device__ __forceinline__ Ctx4 ctx_from_sums(double a0, double a1, double b0, double b1, int N) {
+#ifdef NFDPF_CTX_RCP  // experiment: reciprocal multiplies and a float sqrt (1-ulp differences)
+  const double rn = 1.0 / N, rn1 = 1.0 / (N - 1);
+  const double m0 = a0 * rn, m1 = a1 * rn;
+  return Ctx4{(float)m0, (float)m1, sqrtf((float)((b0 - a0 * m0) * rn1)), sqrtf((float)((b1 - a1 * m1) * rn1))};
+#else
   const double m0 = a0 / N, m1 = a1 / N;
   return Ctx4{(float)m0, (float)m1, (float)sqrt((b0 - a0 * m0) / (N - 1)),
               (float)sqrt((b1 - a1 * m1) / (N - 1))};
+#endif
 }
 
 // source of the particle before motion
@@ -147,6 +153,38 @@ __device__ __forceinline__ float fold_acc(const FoldRef &r, int O, float a, cons
     for (int q = 0; q < 12; ++q) wv[q] = wr[2 * (c + q)];
 #pragma unroll
     for (int q = 0; q < 12; ++q) a = fmaf(wv[q], ctx[c + q - c0], a);
+  }
+  for (; c < c1; ++c) a = fmaf(wr[2 * c], ctx[c - c0], a);
+  return a;
+}
+
+// fold_acc with the next 12 weights in flight while the current 12 are accumulated (the same
+// fma sequence): for the long folds (the proposal's 192 encoding columns), whose 16 batches
+// would otherwise each wait a full load latency
+__device__ __forceinline__ float fold_acc_pipe(const FoldRef &r, int O, float a, const float *ctx, int c0, int c1) {
+  const float *wr = r.w1c + 2 * r.j * O + r.w;
+  int c = c0;
+  if (c + 12 <= c1) {
+    float wa[12], wb[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) wa[q] = wr[2 * (c + q)];
+    for (; c + 24 <= c1; c += 24) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) wb[q] = wr[2 * (c + 12 + q)];
+#pragma unroll
+      for (int q = 0; q < 12; ++q) a = fmaf(wa[q], ctx[c + q - c0], a);
+      if (c + 36 <= c1) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) wa[q] = wr[2 * (c + 24 + q)];
+      }
+#pragma unroll
+      for (int q = 0; q < 12; ++q) a = fmaf(wb[q], ctx[c + 12 + q - c0], a);
+    }
+    if (c + 12 <= c1) {  // an odd batch left in wa
+#pragma unroll
+      for (int q = 0; q < 12; ++q) a = fmaf(wa[q], ctx[c + q - c0], a);
+      c += 12;
+    }
   }
   for (; c < c1; ++c) a = fmaf(wr[2 * c], ctx[c - c0], a);
   return a;
