@@ -386,6 +386,8 @@ def main():
             kname = "tiled_prop_quad_kernel"  # coupling nets on wave pairs beside the encoder pair
         elif flags["NF_cond"] and flags["measurement"] != "CGLOW":
             kname = "tiled_prop2_kernel"       # two roles: flow chain, measurement
+        elif flags["measurement"] == "CRNVP" and os.environ.get("NFDPF_CM_TWO_CHAIN", "0") == "1":
+            kname = "tiled_prop_cm_kernel"     # two chains: encoder + context folds, coupling nets
         else:
             kname = "tiled_prop_kernel"
     if flags["measurement"] == "CGLOW":

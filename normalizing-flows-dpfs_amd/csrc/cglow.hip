@@ -179,6 +179,52 @@ __device__ float logabsdet12(float (&a)[kC], int q, float *) {
   }
   return ld;
 }
+#elif !defined(NFDPF_CG_EXACT_LU)
+// The pivot search as ONE unsigned max per DPP step: the key of a lane is |a[k]|'s bit pattern
+// (monotonic in the value for non-negative floats) with its low 4 mantissa bits replaced by
+// 15 - lane, so the 16-lane max picks the largest |value| -- to 2^-19 relative; among values
+// that equal to that precision, the lowest lane -- and names its lane.  Lanes whose row was a
+// pivot already (and lanes 12..15) hold key 0 and never win: a live lane's key is >= 4.  The
+// multiplier is a[k] times the pivot's reciprocal (v_rcp_f32, 1 ulp).  Round 2's search (an
+// exact compare-and-select argmax, branchy after compilation: ~70 instructions per pivot) and
+// IEEE division (11) stay behind -DNFDPF_CG_EXACT_LU.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_max_u(uint32_t v) {
+  return max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float logabsdet12(float (&a)[kC], int q, float *prow_lds) {
+  float ld = 0.f;
+  bool done = q >= kC;  // lanes 12..15 hold no row
+  const uint32_t tag = 15u - (uint32_t)q;
+#pragma unroll
+  for (int k = 0; k < kC; ++k) {
+    uint32_t key = done ? 0u : ((__float_as_uint(fabsf(a[k])) & ~0xFu) | tag);
+    key = dpp_max_u<kDppXor1>(key);
+    key = dpp_max_u<kDppXor2>(key);
+    key = dpp_max_u<kDppHalfMirror>(key);
+    key = dpp_max_u<kDppMirror>(key);
+    const int who = 15 - (int)(key & 0xFu);
+    if (q == who)
+#pragma unroll
+      for (int j = k; j < kC; ++j) prow_lds[j] = a[j];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float prow[kC];
+#pragma unroll
+    for (int j = k; j < kC; ++j) prow[j] = prow_lds[j];
+    const float piv = prow[k];
+    ld += logf(fabsf(piv));
+    if (q == who) done = true;
+    if (!done) {
+      const float f = a[k] * __builtin_amdgcn_rcpf(piv);
+#pragma unroll
+      for (int j = k + 1; j < kC; ++j) a[j] = fmaf(-f, prow[j], a[j]);
+    }
+    __builtin_amdgcn_wave_barrier();  // every lane has read the row before the next is written
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  return ld;
+}
 #else
 template <int CTRL>
 __device__ __forceinline__ void argmax_step(float &v, int &who) {
@@ -318,7 +364,12 @@ __device__ __noinline__ void phase_resize(const float *glow_, int p, int q) {
 #pragma unroll
     for (int ab = 0; ab < 4; ++ab) hb[ab][m] = bias;
   }
-#pragma unroll 1
+// tap loop unrolled by 9 (one (dr) row of taps: its weight loads issue ahead of the fmas):
+// 2.33 -> 2.28 ms per C5 launch against unroll 3; unroll 1 2.43 ms; 27 spills to scratch
+#ifndef NFDPF_CG_RESIZE_UNROLL
+#define NFDPF_CG_RESIZE_UNROLL 9
+#endif
+#pragma unroll NFDPF_CG_RESIZE_UNROLL
   for (int t = 0; t < 27; ++t) {  // taps (dr, ds, c) of the 3x3x3 window
     F2 = (cf2 *)wptr(glow + kOffF);
     const int dr = t / 9, ds = (t / 3) % 3, c = t % 3;
@@ -383,7 +434,11 @@ __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int 
   }
 #else
   constexpr int kChunk = CIN % 4 == 0 ? 4 : (CIN % 3 == 0 ? 3 : 2);
-#pragma unroll 1
+// (unrolled by 3: 2.71 vs 2.33 ms per C5 launch, 32 B of scratch; by 9: 724 B of scratch)
+#ifndef NFDPF_CG_CONV_UNROLL
+#define NFDPF_CG_CONV_UNROLL 1
+#endif
+#pragma unroll NFDPF_CG_CONV_UNROLL
   for (int t9 = 0; t9 < 9; ++t9) {
     const int dr = t9 / 3, ds = t9 - 3 * (t9 / 3);
     const int rr = qi + dr - 1, ss = qj + ds - 1;

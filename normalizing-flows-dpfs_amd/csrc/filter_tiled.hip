@@ -1189,6 +1189,127 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   TRACE(2, 3)
 }
 
+// ---- K3 for the conditional-RealNVP measurement without an NF proposal (C3, DPF-CM): 512
+// threads per tile of 256 particles.  The measurement's flow input is the row's frame encoding
+// and its condition the particle encoding (model/models.py:256-278), so a particle's work is two
+// chains: waves 4-7 ("cond") encode the proposal and fold the encoding into every coupling
+// half's first-layer bias pairs (the context columns of nf/flows.py:215-226's nets), publishing
+// them half by half through LDS; waves 0-3 ("flow", the same particles as cond wave w + 4) take
+// the densities while the encoder runs, then the coupling nets on the frame encoding as each
+// half's biases arrive.  Two waves per SIMD instead of one at C3's 64 000 particles: one chain's
+// scalar-load stalls are the other's issue slots.  The arithmetic is measure<CRNVP>'s, split at
+// the fold (bit-identical).  Not the default: measured slower (use_cm).
+static __host__ __device__ constexpr size_t cm_lds_bytes(int n_flows) {
+  return (size_t)2 * n_flows * kH * kTile * sizeof(f2);
+}
+template <bool NFD>
+__global__ __launch_bounds__(2 * kTile) void tiled_prop_cm_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  extern __shared__ f2 cbx[];  // [half h = 2 flow + n][kH][kTile] folded bias pairs
+  __shared__ StepShared L;
+  __shared__ int cflag[4];     // halves published by cond wave w + 4 (for flow wave w)
+  __shared__ float smf[16];
+  __shared__ double smd[48];
+  TRACE(2, 0)
+  constexpr int HALF = kE / 2;
+  constexpr int ns = net_size<HALF, kH>(kE);
+  const int tiles = n_tiles(d.N);
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int pl = threadIdx.x & (kTile - 1);
+  const bool flows = threadIdx.x < kTile;
+  const int i = tile * kTile + pl;
+  const RowSlot S = row_slot(d, b);
+  const bool valid = i < d.N;
+  PropIn in{};
+  float lr = 0.f;
+  if (valid) {  // issued before the row prologue so they overlap it
+    if (flows) {
+      in = load_prop_in<NFD>(S, i);
+      lr = S.hp[i];
+    } else {  // the proposal (= x_dyn without --NF-cond, stage_propose_inverse)
+      in.xd0 = NFD ? S.scr[4 * i] : S.hx[2 * i];
+      in.xd1 = NFD ? S.scr[4 * i + 1] : S.hx[2 * i + 1];
+    }
+  }
+  measure_row_setup<NFDPF_MEAS_CRNVP>(S.enc, d.meas_params, L);
+  if (threadIdx.x < 4) cflag[threadIdx.x] = 0;
+  __syncthreads();
+  if (!NFD && d.defer_norm && d.t > 0)  // no K2 in this config
+    finish_prev(d, ws, b, tile, i, flows, flows && i < d.N ? load_prev_in(row_slot(d, b, d.t - 1), i) : PrevIn{},
+                L.d);
+  TRACE(2, 1)
+  const int nh = 2 * d.n_flows;
+  lds_vint *flag = (lds_vint *)&cflag[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3];
+  float lk = -INFINITY, u = 0.f;
+  if (!flows) {
+    float e[kE];
+    particle_encode<kE>(wptr(d.pe_params), in.xd0, in.xd1, e);
+    for (int h = 0; h < nh; ++h) {
+      cf2 *fw = wptr2(d.meas_params) + h * ns;  // flow h / 2, coupling half h % 2
+#pragma unroll
+      for (int j = 0; j < kH; ++j) cbx[(h * kH + j) * kTile + pl] = fold_pair_c<HALF, kH, kE>(fw, j, e);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pairs land before the count
+      *flag = h + 1;
+    }
+  } else {
+    float propose = 0.f, prior = 0.f;
+    if (valid) stage_prior<NFD, false>(d, S, i, in, nullptr, in.xd0, in.xd1, 0.f, propose, prior);
+    float lo[HALF], up[HALF];
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) {
+      lo[k] = L.encv[k];
+      up[k] = L.encv[HALF + k];
+    }
+    float ld = 0.f;
+    for (int f = 0; f < d.n_flows; ++f) {
+      cf2 *fw = wptr2(d.meas_params) + f * 2 * ns;
+      f2 cb[kH];
+      float t[HALF], s[HALF];
+      // coupling_forward, half by half as the cond wave publishes the bias pairs
+      int it = 0;
+      for (; __builtin_amdgcn_readfirstlane(*flag) < 2 * f + 1 && it < kSpinCap; ++it) __builtin_amdgcn_s_sleep(1);
+      if (it == kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < kH; ++j) cb[j] = cbx[(2 * f * kH + j) * kTile + pl];
+      ts_pair<HALF, kH>(fw, lo, cb, t, s);
+#pragma unroll
+      for (int k = 0; k < HALF; ++k) up[k] = t[k] + up[k] * expf(s[k]);
+      const float l1 = half_sum<HALF>(s);
+      it = 0;
+      for (; __builtin_amdgcn_readfirstlane(*flag) < 2 * f + 2 && it < kSpinCap; ++it) __builtin_amdgcn_s_sleep(1);
+      if (it == kSpinCap && (threadIdx.x & 63) == 0) atomicAdd(&g_split_fault, 1);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < kH; ++j) cb[j] = cbx[((2 * f + 1) * kH + j) * kTile + pl];
+      ts_pair<HALF, kH>(fw + ns, up, cb, t, s);
+#pragma unroll
+      for (int k = 0; k < HALF; ++k) lo[k] = t[k] + lo[k] * expf(s[k]);
+      ld += l1 + half_sum<HALF>(s);
+    }
+    // the prior's quadratic form in fp64, as measure<CRNVP>
+    const double is = 1.0 / (double)d.meas_prior_std;
+    double m = 0.0;
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) {
+      const double a = lo[k] * is, c = up[k] * is;
+      m = fma(a, a, m);
+      m = fma(c, c, m);
+    }
+    const double lp = -0.5 * (kE * 1.8378770664093453 + m) - kE * log((double)d.meas_prior_std);
+    if (valid) {
+      lk = (float)(lp + (double)ld);
+      S.hlik[i] = lk;
+      u = logw(lr, lk, prior, propose);
+    }
+  }
+  TRACE(2, 2)
+  double *sm = reinterpret_cast<double *>(d.ess_out) + ((int64_t)b * tiles + tile) * kSm;
+  const float lm = block_max_dpp(lk, L.f);  // the cond waves hold -inf
+  if (threadIdx.x == 0) sm[3] = lm;
+  store_softmax(u, valid && flows, sm, smf, smd);
+  TRACE(2, 3)
+}
+
 // ---- K3 on wave pairs (split.hpp; --NF-dyn RealNVP, --NF-cond, cosine measurement): the
 // t-wave and the s-wave of a particle group run the proposal inverse and the nf_dyn forward
 // net by net, then split the particle encoder's output layer (each computes the hidden
@@ -1666,6 +1787,14 @@ static bool use_rows(const nfdpf_filter_desc &d) {
   return d.resampler == NFDPF_RESAMPLE_SOFT && !use_merged(d) && d.N > min_n;
 }
 
+// The two-chain CRNVP proposal launch (tiled_prop_cm_kernel), opt-in with NFDPF_CM_TWO_CHAIN=1
+// (read per call: tests compare both).  Measured SLOWER than the one-chain tiled_prop_kernel at
+// C3 (33.7 vs 30.7 us per launch, 1.455e9 vs 1.566e9 particle-steps/s, one box, bit-identical).
+static bool use_cm(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_CM_TWO_CHAIN");
+  return e && e[0] == '1' && d.n_flows <= kMaxFlows;
+}
+
 // One launch per step (tiled_step_fused_kernel), opt-in with NFDPF_FUSED_STEP=1, when every
 // workgroup of the grid can be resident at once -- one 1024-thread workgroup per CU -- since a
 // row's four workgroups wait for each other inside it.  Measured SLOWER than the two launches
@@ -1717,6 +1846,22 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
         hipExtLaunchKernelGGL(tiled_prop_split_kernel<false>, g, dim3(2 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
       else
         tiled_prop_split_kernel<false><<<g, 2 * kTile, 0, st>>>(d, ws);
+      return;
+    }
+  }
+  if constexpr (!NFC && MEAS == NFDPF_MEAS_CRNVP) {
+    if (use_cm(d)) {
+      const size_t lds = cm_lds_bytes(d.n_flows);
+      static bool attr = false;  // the fold buffer exceeds the default 64 KB at 3-4 flows
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void *)tiled_prop_cm_kernel<NFD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)cm_lds_bytes(kMaxFlows));
+        attr = true;
+      }
+      if (ev)
+        hipExtLaunchKernelGGL(tiled_prop_cm_kernel<NFD>, g, dim3(2 * kTile), lds, st, ev[0], ev[1], 0, d, ws);
+      else
+        tiled_prop_cm_kernel<NFD><<<g, 2 * kTile, lds, st>>>(d, ws);
       return;
     }
   }

@@ -37,15 +37,9 @@ __device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) {
 
 // context from (sum x, sum y, sum x^2, sum y^2) over N particles
 __device__ __forceinline__ Ctx4 ctx_from_sums(double a0, double a1, double b0, double b1, int N) {
-#ifdef NFDPF_CTX_RCP  // experiment: reciprocal multiplies and a float sqrt (1-ulp differences)
-  const double rn = 1.0 / N, rn1 = 1.0 / (N - 1);
-  const double m0 = a0 * rn, m1 = a1 * rn;
-  return Ctx4{(float)m0, (float)m1, sqrtf((float)((b0 - a0 * m0) * rn1)), sqrtf((float)((b1 - a1 * m1) * rn1))};
-#else
   const double m0 = a0 / N, m1 = a1 / N;
   return Ctx4{(float)m0, (float)m1, (float)sqrt((b0 - a0 * m0) / (N - 1)),
               (float)sqrt((b1 - a1 * m1) / (N - 1))};
-#endif
 }
 
 // source of the particle before motion

@@ -461,7 +461,9 @@ class FilterEngine:
         # a wave-pair hand-off that timed out leaves stale data (csrc/split.hpp): fail loudly
         # (a stream-ordered read and a sync: deferred to finish_pending when the caller asked
         # for a pass free of host syncs)
-        check_split = tiled and d.split_nets and not torch.cuda.is_current_stream_capturing()
+        # (the split nets, and the CRNVP launch's cond -> flow hand-off without --NF-cond)
+        handoffs = d.split_nets or (d.measurement == L.MEAS["CRNVP"] and not d.nf_cond)
+        check_split = tiled and handoffs and not torch.cuda.is_current_stream_capturing()
         if check_split and (finish or not spec):
             L.check_split_fault("nfdpf_filter_step_tiled", dev)
             check_split = False

@@ -697,3 +697,33 @@ def test_rows_kernel_matches_per_tile_resampling(N, force, monkeypatch):
     print(f"\nN={N} force={force}: resampled in {fired} of 6 steps")
     if force:  # step 0 resamples uniform weights: the identity map, not counted here
         assert fired >= 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,nf_dyn,resampler,force", [(1000, False, "ot", False), (1000, False, "soft", True),
+                                                      (777, True, "soft", True), (300, False, "ot", True)])
+def test_crnvp_two_chain_matches_one_chain(N, nf_dyn, resampler, force, monkeypatch):
+    """CRNVP without --NF-cond (C3): tiled_prop_cm_kernel splits each particle's measurement
+    into the encoder + context folds (cond waves) and the coupling nets (flow waves), handing the
+    folded bias pairs over half by half; tiled_prop_kernel runs both on one lane.  Same
+    arithmetic, so the passes are bit-identical (NFDPF_CM_TWO_CHAIN=1 selects the two-chain launch,
+    an opt-in: measured slower at C3)."""
+    import _fullsize as F
+    from nfdpf import _lib
+    from nfdpf.engine import FilterConfig, FilterEngine
+    wl = F.workload("c3_full", B=5, N=N, T=5)
+    models = wl["models"].to(DEV)
+    out = {}
+    for single in ("1", "0"):
+        monkeypatch.setenv("NFDPF_CM_TWO_CHAIN", "0" if single == "1" else "1")
+        cfg = FilterConfig(N=N, NF_dyn=nf_dyn, NF_cond=False, measurement="CRNVP", resampler=resampler,
+                           force_resample=force, seed=7, kernel="tiled")
+        out[single] = FilterEngine(cfg, models).run(wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+        torch.cuda.synchronize()
+    _lib.check_split_fault("tiled_prop_cm_kernel", DEV)
+    a, b = out["1"], out["0"]
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert (x is None) == (y is None), f
+        assert x is None or torch.equal(x, y), f
+    assert torch.isfinite(b.lik).all()
