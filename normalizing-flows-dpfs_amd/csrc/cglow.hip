@@ -113,6 +113,15 @@ __device__ __forceinline__ f4 mfma_tile(const FA &fa, const FB &fb) {
   for (int s = 0; s < KSTEPS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa(r, 4 * s + kk), fb(4 * s + kk, r), acc, 0, 0, 0);
   return acc;
 }
+// the same with this lane's B operands already in registers: b[s] = B[4 s + l / 16][l % 16]
+template <int KSTEPS, class FA>
+__device__ __forceinline__ f4 mfma_tile_b(const FA &fa, const float (&b)[KSTEPS]) {
+  const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa(r, 4 * s + kk), b[s], acc, 0, 0, 0);
+  return acc;
+}
 template <class FE>
 __device__ __forceinline__ void mfma_store(const f4 &acc, const FE &epi) {
   const int l = threadIdx.x & 63;
@@ -445,8 +454,12 @@ __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int 
     const bool in = rr >= 0 && rr < 4 && ss >= 0 && ss < 4;
     const float *src = S.ex[p][in ? rr * 4 + ss : q];  // a valid row either way
     float v[CIN];
+    // loads first, unconditionally (src is a valid row either way), then the selects: written as
+    // `in ? src[c] : 0` the compiler guarded every load with an exec-mask branch
 #pragma unroll
-    for (int c = 0; c < CIN; ++c) v[c] = in ? src[c] : 0.f;
+    for (int c = 0; c < CIN; ++c) v[c] = src[c];
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) v[c] = in ? v[c] : 0.f;
 #pragma unroll
     for (int c0 = 0; c0 < CIN; c0 += kChunk) {
       cf2 *F2 = (cf2 *)wptr(glow + kOffF);
@@ -644,17 +657,36 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
         }
       }
       SYNC();
-      for (int nt = w; nt < kE / 16; nt += 4) {
-        const int n0 = nt * 16;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {  // N tiles w, w + 4, w + 8 of kE / 16 = 12
+        const int n0 = (w + 4 * j) * 16;
+#ifdef NFDPF_CG_BPRE_ENC
+        const f4 acc = mfma_tile_b<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; }, bL3[j]);
+        mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + bb3[j]; });
+#else
         const f4 acc = mfma_tile<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; },
                                             [&](int k, int c) { return W3(n0 + c, k); });
         mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + pb3[n0 + c]; });
+#endif
       }
       SYNC();
     }
     CGTRACE(1)
     // ---- conditioning nets, conv1 (3 -> 8, 2x2 stride 2, 8x8 -> 4x4) for actnorm (A) and
     //      1x1-conv (I) nets: VALU, lane = (particle, 4x4 position)
+    // This wave's B operands (weights) and epilogue biases of the conditioning nets' MFMA
+    // layers are lane-dependent vector loads; in place each layer paid a global round trip for
+    // them (and another for its bias) between two barriers.  Each is issued one phase ahead.
+    // (lane l: column c = l % 16, k = 4 s + l / 16 -- mfma_tile's operand order)
+    const int fc = l & 15, fk = l >> 4;
+    float bC2[2][8], bbC2[2];              // cond conv2 of net 0 (A) and 1 (I), row tile w
+#pragma unroll
+    for (int net = 0; net < 2; ++net) {
+      const float *G = net ? gI : gA;
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) bC2[net][s2] = fc < kXH ? G[CondA::c2w + fc * 32 + 4 * s2 + fk] : 0.f;
+      bbC2[net] = G[CondA::c2b + (fc & 7)];
+    }
     const int p = w * 4 + (l >> 4), q = l & 15, qi = q >> 2, qj = q & 3;
     {
       float in[12];
@@ -678,35 +710,58 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
     }
     SYNC();
     CGTRACE(2)
+    float bC3[8], bbC3, bL0[2], bbL0, bL2[4], bbL2;  // cond conv3, x_Linear of net w (w < 2)
+    {
+      const float *G = w ? gI : gA;
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) bC3[s2] = fc < kXH ? G[CondA::c4w + fc * 32 + 4 * s2 + fk] : 0.f;
+      bbC3 = G[CondA::c4b + (fc & 7)];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) bL0[s2] = G[CondA::l0w + fc * kXH + 4 * s2 + fk];
+      bbL0 = G[CondA::l0b + fc];
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) bL2[s2] = G[CondA::l2w + fc * kXS + 4 * s2 + fk];
+      bbL2 = G[CondA::l2b + fc];
+    }
     // conv2 (8 -> 8, 2x2 stride 2, 4x4 -> 2x2): GEMM, rows (particle, 2x2 pos), k (ci, a, b)
-    for (int job = w; job < 8; job += 4) {
-      const int net = job >> 2, mt = job & 3;  // 4 row tiles of 16 = 64 rows
-      const float *G = net ? gI : gA;
-      const f4 acc = mfma_tile<8>(
+#pragma unroll
+    for (int net = 0; net < 2; ++net) {  // jobs w (net 0) and w + 4 (net 1), row tile mt = w
+      const int mt = w;  // 4 row tiles of 16 = 64 rows
+      const f4 acc = mfma_tile_b<8>(
           [&](int r, int k) {
             const int row = mt * 16 + r, pp = row >> 2, pos = row & 3;
             const int ci = k >> 2, a = (k >> 1) & 1, b2 = k & 1;
             return S.cv1[pp][(2 * (pos >> 1) + a) * 4 + 2 * (pos & 1) + b2][net * kXH + ci];
           },
-          [&](int k, int c) { return c < kXH ? G[CondA::c2w + c * 32 + k] : 0.f; });
+          bC2[net]);
       mfma_store(acc, [&](int r, int c, float v) {
         if (c < kXH) {
           const int row = mt * 16 + r;
-          S.cv2[row >> 2][row & 3][net * kXH + c] = relu(v + G[CondA::c2b + c]);
+          S.cv2[row >> 2][row & 3][net * kXH + c] = relu(v + bbC2[net]);
         }
       });
     }
     SYNC();
     CGTRACE(3)
+    float bL4[3][4], bbL4[3];  // last layer: jobs w, w + 4, w + 8 (< 11)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int job = w + 4 * j;
+      const bool isI = job >= 2;
+      const int n = (isI ? job - 2 : job) * 16 + fc, nout = isI ? kC * kC : 2 * kC;
+      const float *G = isI ? gI : gA;
+      const int lw = isI ? CondI::l4w : CondA::l4w, lb = isI ? CondI::l4b : CondA::l4b;
+      const bool ok = job < 11 && n < nout;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) bL4[j][s2] = ok ? G[lw + n * kXS + 4 * s2 + fk] : 0.f;
+      bbL4[j] = ok ? G[lb + n] : 0.f;
+    }
     // conv3 (8 -> 8, 2x2 stride 2, 2x2 -> 1x1): rows = particles, k = (ci, a, b)
     if (w < 2) {
       const int net = w;
-      const float *G = net ? gI : gA;
-      const f4 acc = mfma_tile<8>(
-          [&](int r, int k) { return S.cv2[r][k & 3][net * kXH + (k >> 2)]; },
-          [&](int k, int c) { return c < kXH ? G[CondA::c4w + c * 32 + k] : 0.f; });
+      const f4 acc = mfma_tile_b<8>([&](int r, int k) { return S.cv2[r][k & 3][net * kXH + (k >> 2)]; }, bC3);
       mfma_store(acc, [&](int r, int c, float v) {
-        if (c < kXH) S.cv3[r][net * kXH + c] = relu(v + G[CondA::c4b + c]);
+        if (c < kXH) S.cv3[r][net * kXH + c] = relu(v + bbC3);
       });
     }
     SYNC();
@@ -714,33 +769,29 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
     // x_Linear: 8 -> 16 -> 16 (ReLU)
     if (w < 2) {
       const int net = w;
-      const float *G = net ? gI : gA;
-      const f4 acc = mfma_tile<2>([&](int r, int k) { return S.cv3[r][net * kXH + k]; },
-                                  [&](int k, int c) { return G[CondA::l0w + c * kXH + k]; });
-      mfma_store(acc, [&](int r, int c, float v) { S.v0[r][net * kXS + c] = relu(v + G[CondA::l0b + c]); });
+      const f4 acc = mfma_tile_b<2>([&](int r, int k) { return S.cv3[r][net * kXH + k]; }, bL0);
+      mfma_store(acc, [&](int r, int c, float v) { S.v0[r][net * kXS + c] = relu(v + bbL0); });
     }
     SYNC();
     if (w < 2) {
       const int net = w;
-      const float *G = net ? gI : gA;
-      const f4 acc = mfma_tile<4>([&](int r, int k) { return S.v0[r][net * kXS + k]; },
-                                  [&](int k, int c) { return G[CondA::l2w + c * kXS + k]; });
-      mfma_store(acc, [&](int r, int c, float v) { S.v1[r][net * kXS + c] = relu(v + G[CondA::l2b + c]); });
+      const f4 acc = mfma_tile_b<4>([&](int r, int k) { return S.v0[r][net * kXS + k]; }, bL2);
+      mfma_store(acc, [&](int r, int c, float v) { S.v1[r][net * kXS + c] = relu(v + bbL2); });
     }
     SYNC();
     CGTRACE(5)
     // last layer + tanh: actnorm (24 = 2 tiles) and 1x1 conv (144 = 9 tiles)
-    for (int job = w; job < 11; job += 4) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int job = w + 4 * j;
+      if (job >= 11) break;
       const bool isI = job >= 2;
       const int n0 = (isI ? job - 2 : job) * 16, nout = isI ? kC * kC : 2 * kC;
-      const float *G = isI ? gI : gA;
-      const int lw = isI ? CondI::l4w : CondA::l4w, lb = isI ? CondI::l4b : CondA::l4b;
-      const f4 acc = mfma_tile<4>([&](int r, int k) { return S.v1[r][(isI ? kXS : 0) + k]; },
-                                  [&](int k, int c) { return n0 + c < nout ? G[lw + (n0 + c) * kXS + k] : 0.f; });
+      const f4 acc = mfma_tile_b<4>([&](int r, int k) { return S.v1[r][(isI ? kXS : 0) + k]; }, bL4[j]);
       mfma_store(acc, [&](int r, int c, float v) {
         const int n = n0 + c;
         if (n < nout) {
-          const float t = cg_tanh(v + G[lb + n]);
+          const float t = cg_tanh(v + bbL4[j]);
           if (isI)
             S.wm[r][n] = t;
           else
