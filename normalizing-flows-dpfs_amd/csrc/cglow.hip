@@ -282,6 +282,12 @@ __device__ __forceinline__ float logabsdet12(float (&a)[kC], int q, float *prow_
 
 using namespace cg;
 
+// phase_resize / phase_f as calls (default) or inlined (-DNFDPF_CG_PHASE_INLINE=__forceinline__:
+// 156 B of scratch, not run)
+#ifndef NFDPF_CG_PHASE_INLINE
+#define NFDPF_CG_PHASE_INLINE __noinline__
+#endif
+
 // workgroup barrier that is also a scheduling fence
 #define SYNC()                            \
   do {                                    \
@@ -354,7 +360,7 @@ __device__ __forceinline__ void phase_y(float (&y)[kC], int p, int q) {
 // 2x2 block of 8x8 conv1 outputs stays in registers) -> S.ex[p][q][0:6].  Weights are stored
 // tap-major, output channel fastest (nfdpf.pack.cglow_tensors), so each input value feeds a
 // contiguous run of output-channel pairs (v_pk_fma_f32 with an SGPR pair).
-__device__ __noinline__ void phase_resize(const float *glow_, int p, int q) {
+__device__ NFDPF_CG_PHASE_INLINE void phase_resize(const float *glow_, int p, int q) {
   const float *glow = sgpr_ptr(glow_);
   const int qi = q >> 2, qj = q & 3;
   // The 4x4 window (rows 2qi-1 .. 2qi+2, cols 2qj-1 .. 2qj+2, zero outside) is read from LDS per
@@ -475,7 +481,7 @@ __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int 
 
 // resize conv3, the coupling net f, the affine update of z2 and the Gaussian log-prob;
 // returns this particle's sum (over its 16 positions) of log scale + logp
-__device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *zrow) {
+__device__ NFDPF_CG_PHASE_INLINE float phase_f(const float *glow_, int p, int q, float *zrow) {
   const float *glow = sgpr_ptr(glow_);
   cfloat *F = wptr(glow + kOffF);
   float fin[kC];  // cat(resize_x(x), z1)
@@ -566,7 +572,10 @@ __device__ __noinline__ float phase_f(const float *glow_, int p, int q, float *z
 // 3 workgroups per CU: 50 KB of LDS each (the stage union of Lds) and <= 168 VGPRs (162) for
 // 3 waves per SIMD.  (r01f: min-blocks 2 with 80 KB of LDS spilled 182 SGPRs and ran 5.24 ms
 // at C5; min-blocks 1, same occupancy, 5.09 ms; the union + min-blocks 3 4.72 ms -- A/B, 3 runs.)
-__global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restrict__ pe,
+#ifndef NFDPF_CG_WGS
+#define NFDPF_CG_WGS 3  // resident workgroups per CU (LDS 50 KB, <= 168 VGPRs); 2: 2.52 vs 2.12 ms
+#endif
+__global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const float *__restrict__ pe,
                                                             const float *__restrict__ glow,
                                                             const float *__restrict__ enc,
                                                             int64_t enc_rs, const float *__restrict__ x,
@@ -660,14 +669,9 @@ __global__ __launch_bounds__(kThreads, 3) void cglow_kernel(const float *__restr
 #pragma unroll
       for (int j = 0; j < 3; ++j) {  // N tiles w, w + 4, w + 8 of kE / 16 = 12
         const int n0 = (w + 4 * j) * 16;
-#ifdef NFDPF_CG_BPRE_ENC
-        const f4 acc = mfma_tile_b<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; }, bL3[j]);
-        mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + bb3[j]; });
-#else
         const f4 acc = mfma_tile<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; },
                                             [&](int k, int c) { return W3(n0 + c, k); });
         mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + pb3[n0 + c]; });
-#endif
       }
       SYNC();
     }
@@ -850,7 +854,7 @@ extern "C" int nfdpf_cglow_measurement(const float *pe_params, const float *glow
   }
   // a persistent grid of exactly the resident workgroups (3 per CU: LDS 50 KB, 162 VGPRs):
   // more would start a second, late round of workgroups and leave the tail unbalanced
-  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * 3);
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)cus * NFDPF_CG_WGS);
   cglow_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(pe_params, glow_params, enc, enc_rs, x, x_rs, B, N,
                                                         lik, lik_rs, nullptr, nullptr, 1.0f);
   return launch_status("nfdpf_cglow_measurement");
@@ -862,7 +866,7 @@ static int cglow_grid(int64_t tiles) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
   }
-  return (int)std::min<int64_t>(tiles, (int64_t)cus * 3);
+  return (int)std::min<int64_t>(tiles, (int64_t)cus * NFDPF_CG_WGS);
 }
 
 extern "C" int nfdpf_cglow_flow(const float *glow_params, int K, const float *x, const float *y, int64_t M,
