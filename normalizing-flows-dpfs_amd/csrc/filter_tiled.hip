@@ -1046,9 +1046,15 @@ __device__ __forceinline__ void store_softmax_fin(float u, bool valid, double *s
 }
 
 // ---- K3: proposal + measurement
-template <bool NFD, bool NFC, int MEAS>
+// STAGE (CRNVP, use_stage, opt-in): the measurement's encoder and flow weights copied into LDS
+// once per workgroup and read from there (ds_read) instead of streamed through the scalar cache
+// (26 KB, more than it holds).  Measured slower: not the default.
+constexpr int kCrnvpPe = pe_size(kE);                                  // encoder floats
+constexpr int kCrnvpFlow = 2 * 2 * net_size<kE / 2, kH>(kE);           // floats per flow
+template <bool NFD, bool NFC, int MEAS, bool STAGE = false>
 __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_desc d, TiledWs ws) {
   __shared__ StepShared L;
+  extern __shared__ float4 wstage[];  // STAGE: [encoder | flows] weights
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   const int b = blockIdx.y, tile = blockIdx.x;
@@ -1057,6 +1063,13 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   const bool valid = i < d.N;
   PropIn in{};
   float lr = 0.f;
+  if constexpr (STAGE) {  // 16-B aligned blobs, whole float4s (checked on the host)
+    const float4 *pe4 = reinterpret_cast<const float4 *>(d.pe_params);
+    const float4 *mp4 = reinterpret_cast<const float4 *>(d.meas_params);
+    const int nmp4 = d.n_flows * kCrnvpFlow / 4;
+    for (int k = threadIdx.x; k < kCrnvpPe / 4; k += kTile) wstage[k] = pe4[k];
+    for (int k = threadIdx.x; k < nmp4; k += kTile) wstage[kCrnvpPe / 4 + k] = mp4[k];
+  }
   if (valid) {  // issued before the row prologue so they overlap it
     in = load_prop_in<NFD>(S, i);
     lr = S.hp[i];
@@ -1080,7 +1093,15 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   float lk = -INFINITY, u = 0.f;
   if (valid) {
     float q0x, q1x, propose, prior;
-    lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, in, L.cb_dyn, L.cb_cond, q0x, q1x, propose, prior);
+    if constexpr (STAGE) {
+      static_assert(!STAGE || MEAS == NFDPF_MEAS_CRNVP, "staged weights: CRNVP only");
+      const float jp = stage_propose_inverse<NFC>(d, in, L.cb_cond, q0x, q1x);
+      stage_prior<NFD, NFC>(d, S, i, in, L.cb_dyn, q0x, q1x, jp, propose, prior);
+      const float *wl = reinterpret_cast<const float *>(wstage);
+      lk = crnvp_lik(wl, wl + kCrnvpPe, d.n_flows, d.meas_prior_std, L.encv, q0x, q1x);
+    } else {
+      lk = stage_proposal<NFD, NFC, MEAS>(d, S, L, i, in, L.cb_dyn, L.cb_cond, q0x, q1x, propose, prior);
+    }
     if (MEAS != NFDPF_MEAS_EXTERNAL) {
       S.hlik[i] = lk;
       u = logw(lr, lk, prior, propose);
@@ -1787,6 +1808,18 @@ static bool use_rows(const nfdpf_filter_desc &d) {
   return d.resampler == NFDPF_RESAMPLE_SOFT && !use_merged(d) && d.N > min_n;
 }
 
+// CRNVP weights staged in LDS per workgroup (tiled_prop_kernel<..., true>), opt-in with
+// NFDPF_CRNVP_STAGE=1 (read per call: tests compare both): 16-B aligned blobs and at most
+// kMaxFlows flows (<= 58 KB).  Measured SLOWER than the scalar-cache stream at C3 (48 vs 31 us
+// per launch, 1.11e9 vs 1.58e9; one ds_read_b128 per two v_pk_fma, 254 VGPRs leave the
+// compiler two or three reads in flight).
+static bool use_stage(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_CRNVP_STAGE");
+  if (!(e && e[0] == '1')) return false;
+  return d.n_flows >= 0 && d.n_flows <= kMaxFlows && ((uintptr_t)d.pe_params & 15) == 0 &&
+         ((uintptr_t)d.meas_params & 15) == 0;
+}
+
 // The two-chain CRNVP proposal launch (tiled_prop_cm_kernel), opt-in with NFDPF_CM_TWO_CHAIN=1
 // (read per call: tests compare both).  Measured SLOWER than the one-chain tiled_prop_kernel at
 // C3 (33.7 vs 30.7 us per launch, 1.455e9 vs 1.566e9 particle-steps/s, one box, bit-identical).
@@ -1872,6 +1905,17 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
     else
       tiled_prop2_kernel<NFD, NFC, MEAS, 2><<<g, 2 * kTile, 0, st>>>(d, ws);
   } else {
+    if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
+      if (use_stage(d)) {
+        const size_t lds = (size_t)(kCrnvpPe + d.n_flows * kCrnvpFlow) * sizeof(float);
+        if (ev)
+          hipExtLaunchKernelGGL(tiled_prop_kernel<NFD, NFC, MEAS, true>, g, dim3(kTile), lds, st, ev[0], ev[1], 0,
+                                d, ws);
+        else
+          tiled_prop_kernel<NFD, NFC, MEAS, true><<<g, kTile, lds, st>>>(d, ws);
+        return;
+      }
+    }
     if (ev)
       hipExtLaunchKernelGGL(tiled_prop_kernel<NFD, NFC, MEAS>, g, dim3(kTile), 0, st, ev[0], ev[1], 0, d, ws);
     else

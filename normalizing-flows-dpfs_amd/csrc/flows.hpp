@@ -32,6 +32,12 @@ __device__ __forceinline__ f2 tanh2(f2 x) {
   return pfma(splat(-2.0f), f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, splat(1.0f));
 }
 __device__ __forceinline__ cf2 *wptr2(const float *p) { return (cf2 *)wptr(p); }
+// The weight-pointer types the per-particle helpers below take: constant address space (cfloat /
+// cf2: scalar loads, the default) or a plain pointer into LDS (weights staged per workgroup:
+// ds_read, the address space inferred after inlining).  pair_ptr maps a float pointer to the
+// pair pointer of the same kind.
+__device__ __forceinline__ cf2 *pair_ptr(cfloat *p) { return (cf2 *)p; }
+__device__ __forceinline__ const f2 *pair_ptr(const float *p) { return (const f2 *)p; }
 __device__ __forceinline__ f2 relu2(f2 x) { return f2{relu(x.x), relu(x.y)}; }
 
 // pairs in a (t, s) core / a whole (t, s) coupling half
@@ -52,9 +58,9 @@ __device__ __forceinline__ f2 fold_pair(cf2 *w, int O, int j, const float *ctx) 
   for (int c = 0; c < O; ++c) a = pfma(w1c[j * O + c], splat(ctx[c]), a);
   return a;
 }
-template <int HALF, int H, int O>
-__device__ __forceinline__ f2 fold_pair_c(cf2 *w, int j, const float (&ctx)[O]) {
-  cf2 *w1c = w + net_core<HALF, H>();
+template <int HALF, int H, int O, class WP>
+__device__ __forceinline__ f2 fold_pair_c(WP w, int j, const float (&ctx)[O]) {
+  const WP w1c = w + net_core<HALF, H>();
   f2 a = w1c[H * O + j];
 #pragma unroll
   for (int c = 0; c < O; ++c) a = pfma(w1c[j * O + c], splat(ctx[c]), a);
@@ -63,8 +69,8 @@ __device__ __forceinline__ f2 fold_pair_c(cf2 *w, int j, const float (&ctx)[O]) 
 
 // Nets t and s of one coupling half on input u, first layer on the HALF leading columns plus
 // the folded bias pairs cb[H].  Outputs t[HALF], s[HALF].
-template <int HALF, int H>
-__device__ __forceinline__ void ts_pair(cf2 *w, const float (&u)[HALF], const f2 *cb,
+template <int HALF, int H, class WP>
+__device__ __forceinline__ void ts_pair(WP w, const float (&u)[HALF], const f2 *cb,
                                         float (&t)[HALF], float (&s)[HALF]) {
   f2 h[H];
 #pragma unroll
@@ -74,7 +80,7 @@ __device__ __forceinline__ void ts_pair(cf2 *w, const float (&u)[HALF], const f2
     for (int k = 0; k < HALF; ++k) a = pfma(w[j * HALF + k], splat(u[k]), a);
     h[j] = tanh2(a);
   }
-  cf2 *w2 = w + H * HALF;
+  const WP w2 = w + H * HALF;
   f2 g[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
@@ -83,7 +89,7 @@ __device__ __forceinline__ void ts_pair(cf2 *w, const float (&u)[HALF], const f2
     for (int k = 0; k < H; ++k) a = pfma(w2[j * H + k], h[k], a);
     g[j] = tanh2(a);
   }
-  cf2 *w3 = w2 + H * H + H;
+  const WP w3 = w2 + H * H + H;
 #pragma unroll
   for (int o = 0; o < HALF; ++o) {
     f2 a = w3[HALF * H + o];
@@ -119,8 +125,8 @@ __device__ __forceinline__ float half_sum(const float (&s)[HALF]) {
 // One RealNVP_cond flow: pair (t1, s1) then pair (t2, s2), net_size(O) pairs each; cb = the
 // folded bias pairs [2][H].  Forward: nf/flows.py:215-226; inverse: :228-239.  Returns the
 // flow's log-det.
-template <int HALF, int H>
-__device__ __forceinline__ float coupling_forward(cf2 *fw, int O, float (&lo)[HALF],
+template <int HALF, int H, class WP>
+__device__ __forceinline__ float coupling_forward(WP fw, int O, float (&lo)[HALF],
                                                   float (&up)[HALF], const f2 *cb) {
   const int ns = net_size<HALF, H>(O);
   float t[HALF], s[HALF];
@@ -272,13 +278,14 @@ constexpr int kPeB1 = kPeH1 * 2, kPeW2 = kPeB1 + kPeH1, kPeB2 = kPeW2 + kPeH2 * 
 
 __device__ __forceinline__ float pick(const f2 *h, int k) { return (k & 1) ? h[k >> 1].y : h[k >> 1].x; }
 
-__device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, f2 (&h2)[kPeH2 / 2]) {
-  cf2 *w1 = (cf2 *)pe, *b1 = (cf2 *)(pe + kPeB1);
+template <class WF>
+__device__ __forceinline__ void pe_hidden(WF pe, float x0, float x1, f2 (&h2)[kPeH2 / 2]) {
+  const auto w1 = pair_ptr(pe), b1 = pair_ptr(pe + kPeB1);
   f2 h1[kPeH1 / 2];
 #pragma unroll
   for (int m = 0; m < kPeH1 / 2; ++m)
     h1[m] = relu2(pfma(w1[2 * m + 1], splat(x1), pfma(w1[2 * m], splat(x0), b1[m])));
-  cf2 *w2 = (cf2 *)(pe + kPeW2), *b2 = (cf2 *)(pe + kPeB2);
+  const auto w2 = pair_ptr(pe + kPeW2), b2 = pair_ptr(pe + kPeB2);
   constexpr int M = kPeH2 / 2;
 #pragma unroll
   for (int m = 0; m < M; ++m) h2[m] = b2[m];
@@ -293,10 +300,10 @@ __device__ __forceinline__ void pe_hidden(cfloat *pe, float x0, float x1, f2 (&h
 }
 
 // output pairs [m0, m0 + MP) of the last layer, input-major
-template <int E, int MP>
-__device__ __forceinline__ void pe_out(cfloat *pe, const f2 (&h2)[kPeH2 / 2], int m0, f2 (&a)[MP]) {
+template <int E, int MP, class WF>
+__device__ __forceinline__ void pe_out(WF pe, const f2 (&h2)[kPeH2 / 2], int m0, f2 (&a)[MP]) {
   constexpr int M = E / 2;
-  cf2 *w3 = (cf2 *)(pe + kPeW3) + m0, *b3 = (cf2 *)(pe + kPeW3 + E * kPeH2) + m0;
+  const auto w3 = pair_ptr(pe + kPeW3) + m0, b3 = pair_ptr(pe + kPeW3 + E * kPeH2) + m0;
 #pragma unroll
   for (int m = 0; m < MP; ++m) a[m] = b3[m];
 #pragma unroll
@@ -307,8 +314,8 @@ __device__ __forceinline__ void pe_out(cfloat *pe, const f2 (&h2)[kPeH2 / 2], in
   }
 }
 
-template <int E>
-__device__ __forceinline__ void particle_encode(cfloat *pe, float x0, float x1, float (&e)[E]) {
+template <int E, class WF>
+__device__ __forceinline__ void particle_encode(WF pe, float x0, float x1, float (&e)[E]) {
   f2 h2[kPeH2 / 2];
   pe_hidden(pe, x0, x1, h2);
   f2 a[E / 2];

@@ -37,6 +37,46 @@ struct MeasArgs {
   float meas_prior_std;
 };
 
+// measurement_model_cnf (model/models.py:256-278): flow input = the row's frame encoding encv,
+// condition = the particle encoding; N(0, prior_std^2 I) prior + log-det.  pe / mp: the encoder
+// and flow blobs behind constant-address-space pointers (scalar loads) or plain pointers into
+// LDS (tiled_prop_kernel stages them per workgroup) -- the same arithmetic either way.
+template <class WF>
+__device__ __forceinline__ float crnvp_lik(WF pe, WF mp, int n_flows, float prior_std, const float *encv,
+                                           float x0, float x1) {
+  float e[kE];
+  particle_encode<kE>(pe, x0, x1, e);
+  constexpr int HALF = kE / 2;
+  constexpr int ns = net_size<HALF, kH>(kE);
+  float lo[HALF], up[HALF];
+#pragma unroll
+  for (int k = 0; k < HALF; ++k) {
+    lo[k] = encv[k];
+    up[k] = encv[HALF + k];
+  }
+  float ld = 0.f;
+  for (int f = 0; f < n_flows; ++f) {
+    const auto fw = pair_ptr(mp) + f * 2 * ns;
+    f2 cb[2 * kH];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_pair_c<HALF, kH, kE>(fw + n * ns, j, e);
+    ld += coupling_forward<HALF, kH>(fw, kE, lo, up, cb);
+  }
+  // the prior's quadratic form in fp64 (32 terms of ~10 each: fp32 lost ~1e-4 absolute)
+  const double is = 1.0 / (double)prior_std;
+  double m = 0.0;
+#pragma unroll
+  for (int k = 0; k < HALF; ++k) {
+    const double a = lo[k] * is, c = up[k] * is;
+    m = fma(a, a, m);
+    m = fma(c, c, m);
+  }
+  const double lp = -0.5 * (kE * 1.8378770664093453 + m) - kE * log((double)prior_std);
+  return (float)(lp + (double)ld);
+}
+
 template <int MEAS>
 __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L, float x0,
                                          float x1) {
@@ -47,39 +87,7 @@ __device__ __forceinline__ float measure(const MeasArgs &d, const StepShared &L,
     encode_dot<kE>(wptr(d.pe_params), x0, x1, L.encv, ss, dot);
     return cos_lik(ss, dot, L.vinv);
   } else if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
-    // measurement_model_cnf (model/models.py:256-278): flow input = frame encoding,
-    // condition = particle encoding; N(0, prior_std^2 I) prior + log-det
-    float e[kE];
-    particle_encode<kE>(wptr(d.pe_params), x0, x1, e);
-    constexpr int HALF = kE / 2;
-    constexpr int ns = net_size<HALF, kH>(kE);
-    float lo[HALF], up[HALF];
-#pragma unroll
-    for (int k = 0; k < HALF; ++k) {
-      lo[k] = L.encv[k];
-      up[k] = L.encv[HALF + k];
-    }
-    float ld = 0.f;
-    for (int f = 0; f < d.n_flows; ++f) {
-      cf2 *fw = wptr2(d.meas_params) + f * 2 * ns;
-      f2 cb[2 * kH];
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < kH; ++j) cb[n * kH + j] = fold_pair_c<HALF, kH, kE>(fw + n * ns, j, e);
-      ld += coupling_forward<HALF, kH>(fw, kE, lo, up, cb);
-    }
-    // the prior's quadratic form in fp64 (32 terms of ~10 each: fp32 lost ~1e-4 absolute)
-    const double is = 1.0 / (double)d.meas_prior_std;
-    double m = 0.0;
-#pragma unroll
-    for (int k = 0; k < HALF; ++k) {
-      const double a = lo[k] * is, c = up[k] * is;
-      m = fma(a, a, m);
-      m = fma(c, c, m);
-    }
-    const double lp = -0.5 * (kE * 1.8378770664093453 + m) - kE * log((double)d.meas_prior_std);
-    return (float)(lp + (double)ld);
+    return crnvp_lik(wptr(d.pe_params), wptr(d.meas_params), d.n_flows, d.meas_prior_std, L.encv, x0, x1);
   } else if constexpr (MEAS == NFDPF_MEAS_GAUSSIAN) {
     // measurement_model_Gaussian with N(1, 100 I) (DPFs.py:84-86, model/models.py:237-254)
     float e[kE];

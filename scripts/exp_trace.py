@@ -14,7 +14,8 @@ from nfdpf import _lib  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 SPLIT = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-flags, _, N, T, _, _ = bench.CONFIGS["c2"]
+CFG = os.environ.get("TRACE_CONFIG", "c2")
+flags, _, N, T, _, _ = bench.CONFIGS[CFG]
 torch.manual_seed(2)
 a = bench.make_args(flags, B, N, T, {})
 from DPFs import DPF  # noqa: E402

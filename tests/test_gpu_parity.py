@@ -727,3 +727,30 @@ def test_crnvp_two_chain_matches_one_chain(N, nf_dyn, resampler, force, monkeypa
         assert (x is None) == (y is None), f
         assert x is None or torch.equal(x, y), f
     assert torch.isfinite(b.lik).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,nf_dyn,resampler,force", [(1000, False, "ot", False), (777, True, "soft", True),
+                                                      (300, False, "ot", True)])
+def test_crnvp_staged_weights_match_scalar(N, nf_dyn, resampler, force, monkeypatch):
+    """CRNVP without --NF-cond: tiled_prop_kernel reads the measurement's encoder and flow weights
+    from LDS (staged once per workgroup) instead of through the scalar cache.  Same arithmetic,
+    so the passes are bit-identical (NFDPF_CRNVP_STAGE=1 selects the staged weights, an opt-in:
+    measured slower at C3)."""
+    import _fullsize as F
+    from nfdpf.engine import FilterConfig, FilterEngine
+    wl = F.workload("c3_full", B=5, N=N, T=5)
+    models = wl["models"].to(DEV)
+    out = {}
+    for scalar in ("1", "0"):
+        monkeypatch.setenv("NFDPF_CRNVP_STAGE", "0" if scalar == "1" else "1")
+        cfg = FilterConfig(N=N, NF_dyn=nf_dyn, NF_cond=False, measurement="CRNVP", resampler=resampler,
+                           force_resample=force, seed=7, kernel="tiled")
+        out[scalar] = FilterEngine(cfg, models).run(wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+        torch.cuda.synchronize()
+    a, b = out["1"], out["0"]
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert (x is None) == (y is None), f
+        assert x is None or torch.equal(x, y), f
+    assert torch.isfinite(b.lik).all()
