@@ -397,6 +397,9 @@ NFDPF_API int nfdpf_filter_tiled_tiles(int N);
  * the (tiles, B) grid resident on the current device; opt-in: NFDPF_FUSED_STEP=1), else 0.
  * prof_front is then ignored (no separate front launch).  No reference counterpart: a query. */
 NFDPF_API int nfdpf_filter_tiled_fused(const nfdpf_filter_desc *d);
+/* sizeof(nfdpf_filter_desc) as this library was built: a binding checks its mirror of the
+ * struct against it (nfdpf._lib does, at load).  No reference counterpart: a query. */
+NFDPF_API int64_t nfdpf_filter_desc_size(void);
 /* the t = 0 gate input from p0 [B,N] -> ess_parts [B][tiles][4] */
 NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
                             void *stream);

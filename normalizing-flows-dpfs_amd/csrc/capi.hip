@@ -27,4 +27,5 @@ int launch_status(const char *what) {
 }  // namespace nfdpf
 
 extern "C" int nfdpf_version(void) { return 1; }
+extern "C" int64_t nfdpf_filter_desc_size(void) { return (int64_t)sizeof(nfdpf_filter_desc); }
 extern "C" const char *nfdpf_last_error(void) { return nfdpf::g_err; }

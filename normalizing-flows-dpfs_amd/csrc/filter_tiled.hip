@@ -2030,8 +2030,10 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_step_tiled: EXTERNAL measurement runs as phase 1 + phase 2");
   NFDPF_REQUIRE(d.measurement != NFDPF_MEAS_EXTERNAL || d.phase != 2 || d.lik_ext,
                 "nfdpf_filter_step_tiled: phase 2 needs lik_ext");
-  NFDPF_REQUIRE(!d.defer_norm || d.resampler == NFDPF_RESAMPLE_SOFT,
-                "nfdpf_filter_step_tiled: defer_norm needs the soft resampler (OT reads p_prev before the step)");
+  // OT reads p_prev before the step, so its steps defer only in a speculative pass (every gate
+  // taken as off: d.gate given and zero, the shard's own partials -- ess_local)
+  NFDPF_REQUIRE(!d.defer_norm || d.resampler == NFDPF_RESAMPLE_SOFT || (d.ess_local && d.gate && !d.force_resample),
+                "nfdpf_filter_step_tiled: defer_norm needs the soft resampler or a speculative OT pass");
   if (d.resampler == NFDPF_RESAMPLE_SOFT) {
     NFDPF_REQUIRE(d.N <= kStepMaxN, "nfdpf_filter_step_tiled: soft resampling supports N <= %d", kStepMaxN);
     NFDPF_REQUIRE(d.lin || d.phase == 2, "nfdpf_filter_step_tiled: soft resampling needs lin");

@@ -113,6 +113,7 @@ SIGNATURES = {
     "nfdpf_filter_tiled_workspace_bytes": (c_int64, [c_int, c_int, c_int]),
     "nfdpf_filter_tiled_tiles": (c_int, [c_int]),
     "nfdpf_filter_tiled_fused": (c_int, [POINTER(FilterDesc)]),
+    "nfdpf_filter_desc_size": (c_int64, []),
     "nfdpf_filter_tiled_init": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_filter_step_tiled": (c_int, [POINTER(FilterDesc), c_void_p, c_void_p]),
     "nfdpf_ess_gate_tiled": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
@@ -144,6 +145,13 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if hasattr(lib, "nfdpf_filter_desc_size"):  # the struct mirror must match the library's
+        n = int(lib.nfdpf_filter_desc_size())
+        if n != ctypes.sizeof(FilterDesc):
+            raise NfdpfError(f"{path}: nfdpf_filter_desc is {n} bytes, nfdpf._lib.FilterDesc "
+                             f"{ctypes.sizeof(FilterDesc)} (stale library or binding)")
+    elif not partial:
+        raise NfdpfError(f"{path}: no nfdpf_filter_desc_size (stale library)")
     _lib = lib
     return lib
 

@@ -315,8 +315,9 @@ class FilterEngine:
         d.rng_mode = L.RNG_HOST if host_mode else L.RNG_DEVICE
         d.force_resample, d.n_flows, d.hidden = int(c.force_resample), c.n_flows, c.hidden
         # tiled + soft: step t's weights are normalised inside step t+1 (one launch fewer per
-        # step); not when the caller feeds p_prev itself (teacher forcing) or OT reads it first
-        d.defer_norm = int(tiled and c.resampler == "soft" and teacher is None)
+        # step); not when the caller feeds p_prev itself (teacher forcing) or OT reads it first --
+        # except in a speculative pass, whose gates are all taken as off (no Sinkhorn call in it)
+        d.defer_norm = int(tiled and teacher is None and (c.resampler == "soft" or (c.resampler == "ot" and spec)))
         d.split_nets = int(tiled and c.split_nets and c.NF_dyn and splittable(self.m.nf_dyn.flows)
                            and (not c.NF_cond or splittable(self.m.cond_model.flows)))
         d.alpha, d.pos_noise = c.alpha, c.pos_noise

@@ -82,3 +82,11 @@ def test_ctypes_signatures_match_header_arity():
         params = protos[name].strip()
         n = 0 if params in ("", "void") else params.count(",") + 1
         assert len(argtypes) == n, f"{name}: ctypes passes {len(argtypes)} arguments, the header declares {n}"
+
+
+def test_filter_desc_mirror_matches_library():
+    """nfdpf._lib.FilterDesc mirrors nfdpf_filter_desc field by field; the library reports the
+    struct size it was built with (load() refuses a mismatch -- a stale .so or binding)."""
+    import ctypes
+    from nfdpf import _lib
+    assert int(_lib.load().nfdpf_filter_desc_size()) == ctypes.sizeof(_lib.FilterDesc)
