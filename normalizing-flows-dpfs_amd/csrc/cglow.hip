@@ -71,6 +71,7 @@ struct Lds {
   float ld[kTileP];                    // per-particle log-det of actnorm + 1x1 conv
   int row[kTileP];
   float escale[2 * kYH + kC];          // exp of the coupling net's log-scales (once per launch)
+  float zrow[kC + 1];                  // zeros: the 3x3 convolutions' out-of-grid neighbour
   union {
     struct {  // particle encoder
       float h1[kTileP][kPeH1 + 1];
@@ -141,6 +142,13 @@ __device__ __forceinline__ float cg_tanh(float x) {
   return tanhf(x);
 #endif
 }
+
+// A lane-dependent weight load through a GLOBAL pointer (a generic one compiles to flat_load,
+// which also counts on lgkmcnt: every LDS wait would then wait for it too), unconditional --
+// the callers clamp the index and select afterwards (a guarded load became an exec-mask branch
+// per element).
+typedef const float __attribute__((address_space(1))) gfloat;
+__device__ __forceinline__ float gld(const float *p, int i) { return ((gfloat *)p)[i]; }
 
 // A pointer argument of a non-inlined function arrives in VGPRs; it is wave-uniform, so move
 // it to SGPRs (readfirstlane) before making it a scalar-load weight pointer.
@@ -321,7 +329,7 @@ __device__ __forceinline__ void y_fetch(const float *__restrict__ enc, int64_t e
 #pragma unroll
   for (int c = 0; c < 3; ++c)
 #pragma unroll
-    for (int f = 0; f < 4; ++f) y[c * 4 + f] = er[c * 64 + (2 * qi + (f >> 1)) * 8 + 2 * qj + (f & 1)];
+    for (int f = 0; f < 4; ++f) y[c * 4 + f] = gld(er, c * 64 + (2 * qi + (f >> 1)) * 8 + 2 * qj + (f & 1));
 }
 __device__ __forceinline__ void phase_y(float (&y)[kC], int p, int q) {
   float sl = 0.f;
@@ -458,14 +466,13 @@ __device__ __forceinline__ void conv3x3(const float *glow, int wofs, int p, int 
     const int dr = t9 / 3, ds = t9 - 3 * (t9 / 3);
     const int rr = qi + dr - 1, ss = qj + ds - 1;
     const bool in = rr >= 0 && rr < 4 && ss >= 0 && ss < 4;
-    const float *src = S.ex[p][in ? rr * 4 + ss : q];  // a valid row either way
+    // an out-of-grid neighbour reads the zero row (one address select per tap instead of a
+    // select per channel; written as `in ? src[c] : 0` the compiler had also guarded every load
+    // with an exec-mask branch)
+    const float *src = in ? S.ex[p][rr * 4 + ss] : S.zrow;
     float v[CIN];
-    // loads first, unconditionally (src is a valid row either way), then the selects: written as
-    // `in ? src[c] : 0` the compiler guarded every load with an exec-mask branch
 #pragma unroll
     for (int c = 0; c < CIN; ++c) v[c] = src[c];
-#pragma unroll
-    for (int c = 0; c < CIN; ++c) v[c] = in ? v[c] : 0.f;
 #pragma unroll
     for (int c0 = 0; c0 < CIN; c0 += kChunk) {
       cf2 *F2 = (cf2 *)wptr(glow + kOffF);
@@ -586,9 +593,10 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int64_t total = (int64_t)B * N;
   const int64_t ntiles = (total + kTileP - 1) / kTileP;
-  auto PW = [](const float *w, int o, int i, int K) { return w[((o >> 1) * K + i) * 2 + (o & 1)]; };
+  auto PW = [](const float *w, int o, int i, int K) { return gld(w, ((o >> 1) * K + i) * 2 + (o & 1)); };
   // the coupling net's per-channel scales exp(logs) (Conv2dNormy, nf/cglow/modules.py:214) and exp(3 logs)
   // (Conv2dZerosy, :233), once per launch (ordered before use by the tile's first SYNC)
+  if (tid <= kC) S.zrow[tid] = 0.f;  // read-only from here (ordered by the tile's first SYNC)
   if (tid < 2 * kYH + kC) {
     const float *F = glow + kOffF;
     S.escale[tid] = tid < kYH ? expf(F[Aff::f0al + tid])
@@ -618,7 +626,7 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
     const float *pw1 = pe_, *pb1 = pe_ + kPeB1, *pw2 = pe_ + kPeW2, *pb2 = pe_ + kPeB2, *pw3 = pe_ + kPeW3,
                 *pb3 = pe_ + kPeW3 + kE * kPeH2;
     // W2 / W3 in col_pairs order (nfdpf.pack.encoder_tensors): {W[2m, k], W[2m+1, k]} at [k][m]
-    auto W3 = [&](int n, int k) { return pw3[(k * (kE / 2) + (n >> 1)) * 2 + (n & 1)]; };
+    auto W3 = [&](int n, int k) { return gld(pw3, (k * (kE / 2) + (n >> 1)) * 2 + (n & 1)); };
     const int64_t g0 = tile * kTileP;
     if (xin) {
       // CondGlowModel.forward(x, y): the condition x (3 x 8 x 8) is given per sample and y is
@@ -639,8 +647,8 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
         if (gi < total) {
           rb = (int)(gi / N);
           const int i = (int)(gi - (int64_t)rb * N);
-          a = x[rb * x_rs + 2 * i];
-          c = x[rb * x_rs + 2 * i + 1];
+          a = gld(x, rb * x_rs + 2 * i);
+          c = gld(x, rb * x_rs + 2 * i + 1);
         }
         S.pxy[tid][0] = a;
         S.pxy[tid][1] = c;
@@ -650,7 +658,7 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
       // ---- particle encoder (model/models.py:141-150): 2 -> 16 -> 32 (ReLU), then 32 -> 192
       {
         const int p = tid >> 4, j = tid & 15;
-        const float h = fmaf(PW(pw1, j, 1, 2), S.pxy[p][1], fmaf(PW(pw1, j, 0, 2), S.pxy[p][0], pb1[j]));
+        const float h = fmaf(PW(pw1, j, 1, 2), S.pxy[p][1], fmaf(PW(pw1, j, 0, 2), S.pxy[p][0], gld(pb1, j)));
         S.h1[p][j] = relu(h);
       }
       SYNC();
@@ -659,9 +667,9 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
   #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int o = j + 16 * hh;
-          float a = pb2[o];
+          float a = gld(pb2, o);
   #pragma unroll
-          for (int k = 0; k < kPeH1; ++k) a = fmaf(pw2[(k * (kPeH2 / 2) + (o >> 1)) * 2 + (o & 1)], S.h1[p][k], a);
+          for (int k = 0; k < kPeH1; ++k) a = fmaf(gld(pw2, (k * (kPeH2 / 2) + (o >> 1)) * 2 + (o & 1)), S.h1[p][k], a);
           S.h2[p][o] = relu(a);
         }
       }
@@ -671,7 +679,7 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
         const int n0 = (w + 4 * j) * 16;
         const f4 acc = mfma_tile<kPeH2 / 4>([&](int r, int k) { return S.h2[r][k]; },
                                             [&](int k, int c) { return W3(n0 + c, k); });
-        mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + pb3[n0 + c]; });
+        mfma_store(acc, [&](int r, int c, float v) { S.xs[r][n0 + c] = v + gld(pb3, n0 + c); });
       }
       SYNC();
     }
@@ -688,8 +696,10 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
     for (int net = 0; net < 2; ++net) {
       const float *G = net ? gI : gA;
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) bC2[net][s2] = fc < kXH ? G[CondA::c2w + fc * 32 + 4 * s2 + fk] : 0.f;
-      bbC2[net] = G[CondA::c2b + (fc & 7)];
+      for (int s2 = 0; s2 < 8; ++s2) bC2[net][s2] = gld(G, CondA::c2w + (fc & 7) * 32 + 4 * s2 + fk);
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) bC2[net][s2] = fc < kXH ? bC2[net][s2] : 0.f;
+      bbC2[net] = gld(G, CondA::c2b + (fc & 7));
     }
     const int p = w * 4 + (l >> 4), q = l & 15, qi = q >> 2, qj = q & 3;
     {
@@ -718,14 +728,16 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
     {
       const float *G = w ? gI : gA;
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) bC3[s2] = fc < kXH ? G[CondA::c4w + fc * 32 + 4 * s2 + fk] : 0.f;
-      bbC3 = G[CondA::c4b + (fc & 7)];
+      for (int s2 = 0; s2 < 8; ++s2) bC3[s2] = gld(G, CondA::c4w + (fc & 7) * 32 + 4 * s2 + fk);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) bL0[s2] = G[CondA::l0w + fc * kXH + 4 * s2 + fk];
-      bbL0 = G[CondA::l0b + fc];
+      for (int s2 = 0; s2 < 8; ++s2) bC3[s2] = fc < kXH ? bC3[s2] : 0.f;
+      bbC3 = gld(G, CondA::c4b + (fc & 7));
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) bL2[s2] = G[CondA::l2w + fc * kXS + 4 * s2 + fk];
-      bbL2 = G[CondA::l2b + fc];
+      for (int s2 = 0; s2 < 2; ++s2) bL0[s2] = gld(G, CondA::l0w + fc * kXH + 4 * s2 + fk);
+      bbL0 = gld(G, CondA::l0b + fc);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) bL2[s2] = gld(G, CondA::l2w + fc * kXS + 4 * s2 + fk);
+      bbL2 = gld(G, CondA::l2b + fc);
     }
     // conv2 (8 -> 8, 2x2 stride 2, 4x4 -> 2x2): GEMM, rows (particle, 2x2 pos), k (ci, a, b)
 #pragma unroll
@@ -757,8 +769,11 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
       const int lw = isI ? CondI::l4w : CondA::l4w, lb = isI ? CondI::l4b : CondA::l4b;
       const bool ok = job < 11 && n < nout;
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) bL4[j][s2] = ok ? G[lw + n * kXS + 4 * s2 + fk] : 0.f;
-      bbL4[j] = ok ? G[lb + n] : 0.f;
+      for (int s2 = 0; s2 < 4; ++s2) bL4[j][s2] = gld(G, lw + (ok ? n : 0) * kXS + 4 * s2 + fk);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) bL4[j][s2] = ok ? bL4[j][s2] : 0.f;
+      bbL4[j] = gld(G, lb + (ok ? n : 0));
+      bbL4[j] = ok ? bbL4[j] : 0.f;
     }
     // conv3 (8 -> 8, 2x2 stride 2, 2x2 -> 1x1): rows = particles, k = (ci, a, b)
     if (w < 2) {
