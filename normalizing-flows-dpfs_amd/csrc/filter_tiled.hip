@@ -114,12 +114,37 @@ static TiledWs tiled_carve(void *ws, int B, int N, int T) {
 // e_n = e^(u_n - M) and S = sum e_n, p_n = e_n / S (+ 1e-12 after a filter step, DPFs.py:192):
 // sum p^2 = sum e^2 / S^2 + 2e-12 + N 1e-24.  fp64 throughout; the reference sums fp32 p^2 in
 // cascade order, so the two agree to ~1e-7 relative.
-__device__ __forceinline__ float row_inv_ess(const double *sm, int tiles, int N, bool eps) {
+// The tile partials through an accessor sm(i) = partial word i of the row: a global pointer
+// (row_inv_ess / row_norm below), or a register array indexed by constants (KT: the tiles loop
+// fully unrolled, k < tiles masked -- the same operations in the same order, tiles <= KT).
+// Through a generic pointer these reads compiled to flat_load (which also counts on lgkmcnt);
+// a register array reached through a pointer lived in scratch.
+typedef const double __attribute__((address_space(1))) gdouble;
+template <int KT, class SM>
+__device__ __forceinline__ float row_inv_ess_t(const SM &sm, int tiles, int N, bool eps) {
+  double M = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KT; ++k)
+    if (KT == 0 || k < tiles) M = sm(kSm * k) > M ? sm(kSm * k) : M;
+  double S = 0.0, Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    if (!(KT == 0 || k < tiles)) continue;
+    // the tile rescale factors in f32 (relative error ~1e-7, the gate's own resolution)
+    const float f = expf((float)(sm(kSm * k) - M));
+    S += sm(kSm * k + 1) * (double)f;
+    Q += sm(kSm * k + 2) * ((double)f * (double)f);
+  }
+  double sp2 = Q / (S * S);
+  if (eps) sp2 += 2e-12 + (double)N * 1e-24;
+  return 1.0f / (float)sp2;
+}
+__device__ __forceinline__ float row_inv_ess(const double *sm_, int tiles, int N, bool eps) {
+  gdouble *sm = (gdouble *)sm_;
   double M = -INFINITY;
   for (int k = 0; k < tiles; ++k) M = sm[kSm * k] > M ? sm[kSm * k] : M;
   double S = 0.0, Q = 0.0;
   for (int k = 0; k < tiles; ++k) {
-    // the tile rescale factors in f32 (relative error ~1e-7, the gate's own resolution)
     const float f = expf((float)(sm[kSm * k] - M));
     S += sm[kSm * k + 1] * (double)f;
     Q += sm[kSm * k + 2] * ((double)f * (double)f);
@@ -134,7 +159,23 @@ __device__ __forceinline__ float row_inv_ess(const double *sm, int tiles, int N,
 struct RowNorm {
   float shift, Ssum, Lmax;
 };
-__device__ __forceinline__ RowNorm row_norm(const double *sm, int tiles, bool shifted) {
+template <int KT, class SM>
+__device__ __forceinline__ RowNorm row_norm_t(const SM &sm, int tiles, bool shifted) {
+  float M = -INFINITY, Lmax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    if (!(k < tiles)) continue;
+    M = fmaxf(M, (float)sm(kSm * k));
+    if (shifted) Lmax = fmaxf(Lmax, (float)sm(kSm * k + 3));
+  }
+  double Sd = 0.0;
+#pragma unroll
+  for (int k = 0; k < KT; ++k)
+    if (k < tiles) Sd += sm(kSm * k + 1) * (double)expf((float)sm(kSm * k) - M);
+  return RowNorm{shifted ? M - Lmax : M, (float)Sd, Lmax};
+}
+__device__ __forceinline__ RowNorm row_norm(const double *sm_, int tiles, bool shifted) {
+  gdouble *sm = (gdouble *)sm_;
   float M = -INFINITY, Lmax = -INFINITY;
   for (int k = 0; k < tiles; ++k) {
     M = fmaxf(M, (float)sm[kSm * k]);
@@ -702,9 +743,9 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
   double pre[kPreT * kSm];
   const bool pre_ok = gate_wave && tiles <= kPreT && (int)threadIdx.x < d.B_global;
   if (pre_ok) {
-    const double *pr = parts + (int64_t)threadIdx.x * tiles * kSm;
+    gdouble *pr = (gdouble *)(parts + (int64_t)threadIdx.x * tiles * kSm);
 #pragma unroll
-    for (int k = 0; k < kPreT * kSm; ++k) pre[k] = k < tiles * kSm ? pr[k] : 0.0;
+    for (int k = 0; k < kPreT * kSm; ++k) pre[k] = pr[k < tiles * kSm ? k : 0];
   }
   // fold operands that depend on nothing computed in this launch, loaded now so their latency
   // hides under the gate / speculative motion: the nf_dyn fold's bias and context weights
@@ -768,9 +809,15 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
       for (int r = threadIdx.x; r < d.B_global; r += 64) {
         // rows < 64 from the registers loaded at the launch's start (the row normaliser of this
         // workgroup's own row too: no second round trip)
-        const double *sm = (pre_ok && r == (int)threadIdx.x) ? pre : parts + (int64_t)r * tiles * kSm;
-        Cbuf[r] = row_inv_ess(sm, tiles, N, d.t > 0);
-        if (defer && r == my_row) rn_sh = row_norm(sm, tiles, shifted);
+        if (pre_ok && r == (int)threadIdx.x) {
+          const auto sm = [&](int k) { return pre[k]; };
+          Cbuf[r] = row_inv_ess_t<kPreT>(sm, tiles, N, d.t > 0);
+          if (defer && r == my_row) rn_sh = row_norm_t<kPreT>(sm, tiles, shifted);
+        } else {
+          const double *sm = parts + (int64_t)r * tiles * kSm;
+          Cbuf[r] = row_inv_ess(sm, tiles, N, d.t > 0);
+          if (defer && r == my_row) rn_sh = row_norm(sm, tiles, shifted);
+        }
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
       __builtin_amdgcn_wave_barrier();
