@@ -134,9 +134,10 @@ __device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf
 
 // tanh of the conditioning nets' outputs and of the coupling's shift / scale: libm tanhf.
 // (-DNFDPF_CG_FAST_TANH: tanh_fast, common.hpp -- 2 % faster per launch, but the golden
-// error grows from 1.8e-6 to 5.5e-6 against the reference's own 2.1e-6: not shipped.)
+// error grows from 1.8e-6 to 5.5e-6 against the reference's own 2.1e-6: not shipped.  Round 3:
+// libm's two regimes evaluated branch-free and selected, ~2 ulp -- 2.03 ms either way, removed.)
 __device__ __forceinline__ float cg_tanh(float x) {
-#ifdef NFDPF_CG_FAST_TANH
+#if defined(NFDPF_CG_FAST_TANH)
   return tanh_fast(x);
 #else
   return tanhf(x);
