@@ -54,6 +54,27 @@ __device__ unsigned long long g_trace[4][2048][8];
 #define TRACEW(K, P)
 #endif
 
+// (row b, tile) of this workgroup.  -DNFDPF_XCD_REMAP: blocks are dealt round-robin over the 8
+// XCDs (blocks k and k + 8 share one, MI355X_MICROARCH.md §Workgroup dispatch), so a row's tiles
+// (blocks 4b .. 4b + 3) sat on 4 different L2s; the remap gives each XCD group whole rows, so the
+// row-level data of the previous launch (the row's particles and partials) is read from the
+// reader's own L2.  Any bijection is correct: every kernel derives (b, tile) here.  Measured
+// SLOWER at C2 (2.05e9 vs 2.13e9: both launches ~0.5-0.8 us longer, one box) -- not the default.
+__device__ __forceinline__ void tile_row(int &b, int &tile) {
+#ifdef NFDPF_XCD_REMAP
+  const int n = gridDim.x * gridDim.y;
+  if ((n & 7) == 0) {
+    const int id = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (id & 7) * (n >> 3) + (id >> 3);
+    tile = lin % gridDim.x;
+    b = lin / gridDim.x;
+    return;
+  }
+#endif
+  b = blockIdx.y;
+  tile = blockIdx.x;
+}
+
 struct TiledWs {
   double *st_phys;  // [B][tiles][4] sum x0, x1, x0^2, x1^2 of x_phys
   double *st_dyn;   // [B][tiles][4] same for x_dyn
@@ -399,7 +420,8 @@ __global__ __launch_bounds__(kTile) void tiled_front_kernel(const nfdpf_filter_d
   __shared__ int src_sh[ROWS ? 1 : kTile];
   TRACE(0, 0)
   const int tiles = n_tiles(d.N), N = d.N;
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int i = tile * kTile + threadIdx.x;
   const int64_t grow = d.row_base + b;
   float *Cbuf = dyn_lds;
@@ -550,7 +572,9 @@ __device__ __forceinline__ void row_sync(const nfdpf_filter_desc &d, const Tiled
   const int tiles = n_tiles(d.N);
   const int ng = tiles * 8;
   if (threadIdx.x < 64) {
-    const uint64_t *g = ws.rowx + (int64_t)blockIdx.y * tiles * 8;
+    int b, tile;
+    tile_row(b, tile);
+    const uint64_t *g = ws.rowx + (int64_t)b * tiles * 8;
     for (int base = 0; base < ng; base += 64) {
       const int q = base + (int)threadIdx.x;
       uint64_t v = 0;
@@ -615,7 +639,8 @@ __global__ __launch_bounds__(SPLIT ? 2 * kTile : kTile) void tiled_dyn_kernel(co
   __shared__ int xflag[16];
   TRACE(1, 0)
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const SplitLane sl = SPLIT ? split_lane(8) : SplitLane{0, (int)threadIdx.x};
   const int role = sl.role, slot = sl.slot;
   const int i = tile * kTile + slot;
@@ -715,7 +740,8 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
   __shared__ int xflag[16];
   TRACE(0, 0)
   const int tiles = n_tiles(d.N), N = d.N;
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const SplitLane sl = split_lane(8);
   const int role = sl.role, slot = sl.slot;
   const int i = tile * kTile + slot;
@@ -1104,7 +1130,8 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
   extern __shared__ float4 wstage[];  // STAGE: [encoder | flows] weights
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int i = tile * kTile + threadIdx.x;
   const RowSlot S = row_slot(d, b);
   const bool valid = i < d.N;
@@ -1181,7 +1208,8 @@ __global__ __launch_bounds__(ROLES * kTile) void tiled_prop2_kernel(const nfdpf_
   __shared__ double smd[48];
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int pl = threadIdx.x & (kTile - 1);
   const bool flows = threadIdx.x < kTile;
   const int i = tile * kTile + pl;
@@ -1281,7 +1309,8 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_cm_kernel(const nfdpf_fi
   constexpr int HALF = kE / 2;
   constexpr int ns = net_size<HALF, kH>(kE);
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int pl = threadIdx.x & (kTile - 1);
   const bool flows = threadIdx.x < kTile;
   const int i = tile * kTile + pl;
@@ -1394,7 +1423,8 @@ __global__ __launch_bounds__(2 * kTile) void tiled_prop_split_kernel(const nfdpf
   __shared__ double smd[48];
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const SplitLane sl = split_lane(8);
   const int role = sl.role, slot = sl.slot;
   const int i = tile * kTile + slot;
@@ -1559,7 +1589,8 @@ __device__ __forceinline__ void quad_part(const nfdpf_filter_desc &d, const Tile
   TRACE(2, 0)
   QTRACE(0)
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool enc = w >= 8;
   const int role = w & 1, g = (w >> 1) & 3;
@@ -1735,7 +1766,8 @@ __global__ __launch_bounds__(kTile) void tiled_extlik_kernel(const nfdpf_filter_
   __shared__ double shd2[32];
   __shared__ float shf[16];
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int i = tile * kTile + threadIdx.x;
   const RowSlot S = row_slot(d, b);
   const bool valid = i < d.N;
@@ -1759,7 +1791,8 @@ __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_de
   TRACE(3, 0)
   __shared__ double shd[16];
   const int tiles = n_tiles(d.N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int i = tile * kTile + threadIdx.x;
   const RowNorm rn = row_norm(reinterpret_cast<const double *>(d.ess_out) + (int64_t)b * tiles * kSm, tiles, SHIFT);
   const RowSlot S = row_slot(d, b);
@@ -1800,7 +1833,8 @@ __global__ __launch_bounds__(kTile) void tiled_ess_init_kernel(const float *__re
                                                                double *__restrict__ parts) {
   __shared__ double shd[16];
   const int tiles = n_tiles(N);
-  const int b = blockIdx.y, tile = blockIdx.x;
+  int b, tile;
+  tile_row(b, tile);
   const int i = tile * kTile + threadIdx.x;
   double v = 0.0;
   if (i < N) {
