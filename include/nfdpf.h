@@ -278,6 +278,26 @@ NFDPF_API int nfdpf_cglow_measurement(const float *pe_params, const float *glow_
 NFDPF_API int nfdpf_cglow_flow(const float *glow_params, int K, const float *x, const float *y, int64_t M,
                                float *z, float *nll, void *stream);
 
+/* Backward of the two CGLOW entry points above (training; the autograd
+ * gradient of nf/cglow/modules.py + CGlowModel.py:167-176, d log|det W| / dW = W^-T).
+ * Deterministic (fixed-order per-workgroup partials in the workspace, reduced in order).
+ *   nfdpf_cglow_measurement_backward: inputs as nfdpf_cglow_measurement, g_lik (b, i) at
+ *     g_lik + b*glik_rs + i = dL/d(raw lik) -> g_x [B, N, 2], g_y [B*N, 192] = dL/d(frame
+ *     encoding) per particle (the caller sums each row's N), g_glow (glow blob layout),
+ *     g_pe (encoder blob layout).
+ *   nfdpf_cglow_flow_backward: inputs as nfdpf_cglow_flow, g_z [M, 192] (NULL = 0), g_nll [M]
+ *     -> g_x, g_y [M, 192], g_glow.
+ *   workspace: nfdpf_cglow_backward_workspace(B*N or M) bytes. */
+NFDPF_API int64_t nfdpf_cglow_backward_workspace(int64_t M);
+NFDPF_API int nfdpf_cglow_measurement_backward(const float *pe_params, const float *glow_params, int K,
+                                               const float *enc, int64_t enc_rs, const float *x, int64_t x_rs,
+                                               int B, int N, const float *g_lik, int64_t glik_rs, float *g_x,
+                                               float *g_y, float *g_glow, float *g_pe, void *workspace,
+                                               void *stream);
+NFDPF_API int nfdpf_cglow_flow_backward(const float *glow_params, int K, const float *x, const float *y, int64_t M,
+                                        const float *g_z, const float *g_nll, float *g_x, float *g_y,
+                                        float *g_glow, void *workspace, void *stream);
+
 /* Backward of nfdpf_maf_stack (training): g_out [rows, dim] = dL/d(output), g_logdet [rows]
  * (either may be NULL = 0) -> g_x [rows, dim] = dL/dx and g_params = dL/d(blob), the blob's
  * layout.  dim 2 or 4, hidden 8, n_flows <= 4 (dim 4: <= 2).  workspace: caller-owned,

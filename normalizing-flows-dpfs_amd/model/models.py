@@ -358,6 +358,23 @@ class _CglowRunner:
     def torch(self, enc, x):
         return (self.model.torch_forward_raw(enc, x),)
 
+    def hip_backward(self, enc, x, gouts):
+        """d/d(enc, x, encoder and CGLOW parameters) on nfdpf_cglow_measurement_backward
+        (csrc/cglow_bwd.hip); None (recompute) outside the kernel's configuration."""
+        from nfdpf.pack import blob_param_grads, cglow_tensors
+        m = self.model
+        if enc.dim() != 2 or enc.shape[-1] != 192 or x.dim() != 3 or x.shape[-1] != 2 \
+                or not m.CGLOW.kernel_supported():
+            return None
+        pe = blob(m, "pe", m.particle_encoder, lambda: encoder_tensors(m.particle_encoder), x.device)
+        glow = blob(m, "glow", m.CGLOW, lambda: cglow_tensors(m.CGLOW), x.device)
+        g = gouts[0] if gouts[0] is not None else torch.zeros(x.shape[:2], device=x.device)
+        g_enc, gx, g_glow, g_pe = _ops.cglow_measurement_backward(pe, glow, enc.float(), x.float(), g.float())
+        pe_params, gl_params = list(m.particle_encoder.parameters()), list(m.CGLOW.parameters())
+        res = blob_param_grads(m, "pe_grad", pe_params, lambda get: encoder_tensors(m.particle_encoder, get), g_pe)
+        res += blob_param_grads(m, "glow_grad", gl_params, lambda get: cglow_tensors(m.CGLOW, get), g_glow)
+        return (g_enc.to(enc.dtype), gx.to(x.dtype)), res
+
 
 class measurement_model_cglow(nn.Module):
     """Conditional-GLOW likelihood (model/models.py:280-303)."""

@@ -91,6 +91,17 @@ class _FlowRunner:
     def torch(self, x, y):
         return self.model.torch_forward(x, y)
 
+    def hip_backward(self, x, y, gouts):
+        """d/d(x, y, parameters) on nfdpf_cglow_flow_backward (csrc/cglow_bwd.hip)."""
+        from nfdpf import ops
+        from nfdpf.pack import blob, blob_param_grads, cglow_tensors
+        m = self.model
+        glow = blob(m, "glow", m, lambda: cglow_tensors(m), x.device)
+        g_z, g_nll = gouts
+        gx, gy, g_glow = ops.cglow_flow_backward(glow, x, y, g_z, g_nll)
+        res = blob_param_grads(m, "glow_grad", list(m.parameters()), lambda get: cglow_tensors(m, get), g_glow)
+        return (gx, gy), res
+
 
 class CondGlowModel(nn.Module):
     def __init__(self, args):

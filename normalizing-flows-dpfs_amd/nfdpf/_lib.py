@@ -105,6 +105,12 @@ SIGNATURES = {
     "nfdpf_cglow_measurement": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
                                         c_int, c_void_p, c_int64, c_void_p]),
     "nfdpf_cglow_flow": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_cglow_backward_workspace": (c_int64, [c_int64]),
+    "nfdpf_cglow_measurement_backward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64,
+                                                 c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p, c_void_p]),
+    "nfdpf_cglow_flow_backward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_measurement": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                   c_float, c_void_p, c_void_p]),
     "nfdpf_particle_init": (c_int, [c_void_p, c_int, c_int, c_float, c_int, c_uint64, c_int64, c_void_p, c_void_p,

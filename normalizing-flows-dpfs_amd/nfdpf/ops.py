@@ -428,6 +428,49 @@ def cglow_measurement(pe_blob, glow_blob, enc, x, K=1, out=None):
     return lik
 
 
+def cglow_measurement_backward(pe_blob, glow_blob, enc, x, g_lik, K=1):
+    """Backward of cglow_measurement (raw lik, no row-max shift): enc [B, 192], x [B, N, 2],
+    g_lik [B, N] -> (g_enc [B, 192], g_x [B, N, 2], g_glow [blob], g_pe [blob])
+    (nfdpf_cglow_measurement_backward: per-particle dL/dy summed over each row's N here)."""
+    require_device(x, "cglow_measurement_backward")
+    B, N, _ = x.shape
+    x, enc, g_lik = _c(x), _c(enc), _c(g_lik)
+    if enc.shape[-1] != 192:
+        raise L.NfdpfError("cglow_measurement_backward: frame encodings must be 192 wide (--hiddensize 192)")
+    if int(glow_blob.numel()) != int(lib().nfdpf_cglow_params_size(int(K))):
+        raise L.NfdpfError("cglow_measurement_backward: parameter blob does not match flow_depth K")
+    gx = torch.empty_like(x)
+    gy = torch.empty((B * N, 192), device=x.device, dtype=f32)
+    g_glow = torch.empty_like(glow_blob)
+    g_pe = torch.empty_like(pe_blob)
+    nb = int(lib().nfdpf_cglow_backward_workspace(B * N))
+    ws = torch.empty(max(1, nb // 4), device=x.device, dtype=f32)
+    check(lib().nfdpf_cglow_measurement_backward(ptr(pe_blob), ptr(glow_blob), int(K), ptr(enc), enc.stride(0), ptr(x),
+                                                 x.stride(0), B, N, ptr(g_lik), g_lik.stride(0), ptr(gx), ptr(gy),
+                                                 ptr(g_glow), ptr(g_pe), ptr(ws), stream_ptr(x.device)),
+          "nfdpf_cglow_measurement_backward")
+    return gy.view(B, N, 192).sum(1), gx, g_glow, g_pe
+
+
+def cglow_flow_backward(glow_blob, x, y, g_z, g_nll, K=1):
+    """Backward of cglow_flow: x, y [M,3,8,8], g_z [M,12,4,4] (or None), g_nll [M] -> (g_x, g_y
+    [M,3,8,8], g_glow [blob]) (nfdpf_cglow_flow_backward)."""
+    require_device(x, "cglow_flow_backward")
+    M = x.shape[0]
+    x, y = _c(x), _c(y)
+    g_nll = _c(g_nll) if g_nll is not None else torch.zeros((M,), device=x.device, dtype=f32)
+    g_z = _c(g_z) if g_z is not None else None
+    gx = torch.empty_like(x)
+    gy = torch.empty_like(y)
+    g_glow = torch.empty_like(glow_blob)
+    nb = int(lib().nfdpf_cglow_backward_workspace(M))
+    ws = torch.empty(max(1, nb // 4), device=x.device, dtype=f32)
+    check(lib().nfdpf_cglow_flow_backward(ptr(_c(glow_blob)), int(K), ptr(x), ptr(y), int(M),
+                                          ptr(g_z) if g_z is not None else None, ptr(g_nll), ptr(gx), ptr(gy),
+                                          ptr(g_glow), ptr(ws), stream_ptr(x.device)), "nfdpf_cglow_flow_backward")
+    return gx, gy, g_glow
+
+
 def cglow_flow(glow_blob, x, y, K=1):
     """CondGlowModel.forward(x, y) (nf/cglow/CGlowModel.py:167-176) -> (z [M,12,4,4], nll [M]);
     x, y [M,3,8,8] (the condition and the flow input, per sample)."""

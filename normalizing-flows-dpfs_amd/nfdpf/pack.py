@@ -46,11 +46,12 @@ def col_pairs(w: torch.Tensor) -> torch.Tensor:
     return w.t().reshape(i, o // 2, 2)
 
 
-def encoder_tensors(seq: nn.Module):
+def encoder_tensors(seq: nn.Module, get=_same):
     """Particle encoder Linear(2,16) Linear(16,32) Linear(32,E) (model/models.py:130-150) in
     the kernel layout: W1 row_pairs, W2 and W3 col_pairs, biases as they are."""
     l1, l2, l3 = _linears(seq)
-    return [row_pairs(l1.weight), l1.bias, col_pairs(l2.weight), l2.bias, col_pairs(l3.weight), l3.bias]
+    return [row_pairs(get(l1.weight)), get(l1.bias), col_pairs(get(l2.weight)), get(l2.bias),
+            col_pairs(get(l3.weight)), get(l3.bias)]
 
 
 def coupling_pair_tensors(t_net: nn.Module, s_net: nn.Module, half: int, get=_same):
@@ -102,16 +103,18 @@ def _taps_last(w: torch.Tensor) -> torch.Tensor:
     return w.permute(2, 3, 1, 0)
 
 
-def _cond_net_tensors(m: nn.Module):
+def _cond_net_tensors(m: nn.Module, get=_same):
     """CondActNorm / Cond1x1Conv conditioning net (nf/cglow/modules.py:84-101, 145-162):
     x_Con conv 0 as [k][out] (k = in, kh, kw), convs 2, 4 and the x_Linear layers as stored."""
     c0, c2, c4 = [l for l in m.x_Con if isinstance(l, nn.Conv2d)]
     l0, l2, l4 = _linears(m.x_Linear)
-    return [c0.weight.reshape(c0.weight.shape[0], -1).t(), c0.bias, c2.weight, c2.bias, c4.weight, c4.bias,
-            l0.weight, l0.bias, l2.weight, l2.bias, l4.weight, l4.bias]
+    w0 = get(c0.weight)
+    return [w0.reshape(w0.shape[0], -1).t()] + [get(t) for t in (c0.bias, c2.weight, c2.bias, c4.weight, c4.bias,
+                                                                   l0.weight, l0.bias, l2.weight, l2.bias,
+                                                                   l4.weight, l4.bias)]
 
 
-def cglow_tensors(glow: nn.Module):
+def cglow_tensors(glow: nn.Module, get=_same):
     """CondGlowModel (nf/cglow/CGlowModel.py) with K = 1, L = 1: the CondGlowStep's actnorm
     net, 1x1-conv net, then the affine coupling (modules.py:258-303) in the kernel layout of
     csrc/cglow.hip (Aff): resize_x / f convolutions tap-major, output channel fastest."""
@@ -122,11 +125,13 @@ def cglow_tensors(glow: nn.Module):
     a = st.affine
     r0, r2, r4 = [l for l in a.resize_x if isinstance(l, nn.Conv2d)]
     f0, f2, f4 = [l for l in a.f if isinstance(l, nn.Conv2d)]
-    return (_cond_net_tensors(st.actnorm) + _cond_net_tensors(st.invconv) +
-            [_taps_last(r0.weight), r0.bias, _taps_last(r2.weight), r2.bias, _taps_last(r4.weight), r4.bias,
-             _taps_last(f0.weight), f0.actnorm.bias, f0.actnorm.logs,
-             f2.weight.reshape(f2.weight.shape[0], -1).t(), f2.actnorm.bias, f2.actnorm.logs,
-             _taps_last(f4.weight), f4.bias, f4.logs, f4.newbias])
+    w2 = get(f2.weight)
+    return (_cond_net_tensors(st.actnorm, get) + _cond_net_tensors(st.invconv, get) +
+            [_taps_last(get(r0.weight)), get(r0.bias), _taps_last(get(r2.weight)), get(r2.bias),
+             _taps_last(get(r4.weight)), get(r4.bias),
+             _taps_last(get(f0.weight)), get(f0.actnorm.bias), get(f0.actnorm.logs),
+             w2.reshape(w2.shape[0], -1).t(), get(f2.actnorm.bias), get(f2.actnorm.logs),
+             _taps_last(get(f4.weight)), get(f4.bias), get(f4.logs), get(f4.newbias)])
 
 
 def flows_tensors(flows, get=_same):
@@ -165,6 +170,22 @@ def blob_grad_to_params(owner: nn.Module, name: str, params, build, g_blob: torc
         out.append(flat[off:off + p.numel()].view(p.shape).to(p.dtype))
         off += p.numel()
     return out
+
+
+def blob_param_grads(owner: nn.Module, name: str, params, build, g_blob: torch.Tensor):
+    """blob_grad_to_params for a parameter list of which the blob may pack only a subset:
+    gradients of the packed parameters, None for the others (a parameter the forward does not
+    read gets no gradient under autograd either, e.g. CondGlowModel's new_mean / new_logs with
+    learn_top off)."""
+    seen = {}
+
+    def rec(p):
+        seen[id(p)] = p
+        return p
+    build(rec)
+    used = [p for p in params if id(p) in seen]
+    grads = dict(zip([id(p) for p in used], blob_grad_to_params(owner, name, used, build, g_blob)))
+    return [grads.get(id(p)) for p in params]
 
 
 def splittable(flows) -> bool:
