@@ -33,30 +33,34 @@ constexpr int kThreads = 256;
 constexpr int kPeE = pe_size(kE);  // particle encoder 2 -> 16 -> 32 -> 192
 
 // ---- parameter layers of the two blobs (glow, then the particle encoder at kStep) ----
+// mf: the layer's gradient is a GEMM over the tile's (particle, position) terms, accumulated on
+// f32 MFMA (v_mfma_f32_16x16x4f32, an exact k-ordered fmaf chain) in registers that persist
+// across tiles; the others have owner threads (contract below).
 struct LayerDef {
   int off, n;
+  bool mf;
 };
 #define COND_LAYERS(O, C)                                                                          \
-  {O + C::c0w, C::c0b - C::c0w}, {O + C::c0b, C::c2w - C::c0b}, {O + C::c2w, C::c2b - C::c2w},   \
+  {O + C::c0w, C::c0b - C::c0w, true}, {O + C::c0b, C::c2w - C::c0b}, {O + C::c2w, C::c2b - C::c2w, true}, \
       {O + C::c2b, C::c4w - C::c2b}, {O + C::c4w, C::c4b - C::c4w}, {O + C::c4b, C::l0w - C::c4b}, \
       {O + C::l0w, C::l0b - C::l0w}, {O + C::l0b, C::l2w - C::l0b}, {O + C::l2w, C::l2b - C::l2w}, \
       {O + C::l2b, C::l4w - C::l2b}, {O + C::l4w, C::l4b - C::l4w}, {O + C::l4b, C::size - C::l4b}
 constexpr LayerDef kLayers[] = {
     COND_LAYERS(kOffA, CondA),
     COND_LAYERS(kOffI, CondI),
-    {kOffF + Aff::r0w, Aff::r0b - Aff::r0w},
+    {kOffF + Aff::r0w, Aff::r0b - Aff::r0w, true},
     {kOffF + Aff::r0b, Aff::r2w - Aff::r0b},
-    {kOffF + Aff::r2w, Aff::r2b - Aff::r2w},
+    {kOffF + Aff::r2w, Aff::r2b - Aff::r2w, true},
     {kOffF + Aff::r2b, Aff::r4w - Aff::r2b},
-    {kOffF + Aff::r4w, Aff::r4b - Aff::r4w},
+    {kOffF + Aff::r4w, Aff::r4b - Aff::r4w, true},
     {kOffF + Aff::r4b, Aff::f0w - Aff::r4b},
-    {kOffF + Aff::f0w, Aff::f0ab - Aff::f0w},
+    {kOffF + Aff::f0w, Aff::f0ab - Aff::f0w, true},
     {kOffF + Aff::f0ab, kYH},
     {kOffF + Aff::f0al, kYH},
-    {kOffF + Aff::f2w, kYH * kYH},
+    {kOffF + Aff::f2w, kYH * kYH, true},
     {kOffF + Aff::f2ab, kYH},
     {kOffF + Aff::f2al, kYH},
-    {kOffF + Aff::f4w, Aff::f4b - Aff::f4w},
+    {kOffF + Aff::f4w, Aff::f4b - Aff::f4w, true},
     {kOffF + Aff::f4b, kC},
     {kOffF + Aff::f4l, kC},
     {kOffF + Aff::f4nb, kC},
@@ -64,7 +68,7 @@ constexpr LayerDef kLayers[] = {
     {kStep + kPeB1, kPeW2 - kPeB1},
     {kStep + kPeW2, kPeB2 - kPeW2},
     {kStep + kPeB2, kPeW3 - kPeB2},
-    {kStep + kPeW3, kE * kPeH2},
+    {kStep + kPeW3, kE * kPeH2, true},
     {kStep + kPeW3 + kE * kPeH2, kE},
 };
 #undef COND_LAYERS
@@ -72,11 +76,12 @@ constexpr int kNumLayers = sizeof(kLayers) / sizeof(kLayers[0]);
 constexpr int kTotParams = kStep + kPeE;  // one workspace row
 
 constexpr int slots_of(int n) { return (n + kThreads - 1) / kThreads; }
+constexpr int layer_slots(int i) { return kLayers[i].mf ? 0 : slots_of(kLayers[i].n); }
 constexpr int slot_base(int off) {
   int s = 0;
   for (int i = 0; i < kNumLayers; ++i) {
-    if (kLayers[i].off == off) return s;
-    s += slots_of(kLayers[i].n);
+    if (kLayers[i].off == off) return kLayers[i].mf ? -1 : s;
+    s += layer_slots(i);
   }
   return -1;
 }
@@ -87,7 +92,7 @@ constexpr int layer_n(int off) {
 }
 constexpr int count_slots() {
   int s = 0;
-  for (int i = 0; i < kNumLayers; ++i) s += slots_of(kLayers[i].n);
+  for (int i = 0; i < kNumLayers; ++i) s += layer_slots(i);
   return s;
 }
 constexpr bool layers_tile() {  // the layers cover both blobs exactly, in order
@@ -122,11 +127,27 @@ __device__ __forceinline__ void store_acc(const Acc &acc, float *row) {
   if constexpr (L < kNumLayers) {
     constexpr int off = kLayers[L].off, n = kLayers[L].n, base = slot_base(off);
 #pragma unroll
-    for (int i = 0; i < slots_of(n); ++i) {
+    for (int i = 0; i < layer_slots(L); ++i) {
       const int j = (int)threadIdx.x + kThreads * i;
       if (n % kThreads == 0 || j < n) row[off + j] = acc[base + i];
     }
     store_acc<L + 1>(acc, row);
+  }
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// C (16 x 16 tile, this lane: rows 4 (l / 16) + i, column l % 16) into the workgroup's row:
+// row[idx(m, n)] for m < M, n = n0 + l % 16 < NC
+template <class IDX>
+__device__ __forceinline__ void store_tile(const f4 &c, float *row, int M, int n0, int NC, const IDX &idx) {
+  const int l = threadIdx.x & 63, n = n0 + (l & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = 4 * (l >> 4) + i;
+    if (m < M && n < NC) row[idx(m, n)] = c[i];
   }
 }
 
@@ -205,6 +226,10 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
   Acc acc;
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) acc[s] = 0.f;
+  // this wave's MFMA jobs (column tiles of the mf layers), persistent across tiles
+  const int lr = tid & 15, lk = (tid >> 4) & 3;  // MFMA lane: row / column l % 16, k offset l / 16
+  f4 cF4a = {}, cF4b = {}, cF0a = {}, cF0b = {}, cR4 = {}, cR2 = {}, cR0 = {}, cF2 = {}, cC0 = {}, cC2 = {};
+  f4 cW3[6] = {};
   // per-channel scales of f (Conv2dNormy exp(logs), Conv2dZerosy exp(3 logs))
   const float *F = glow + kOffF;
   float es0[kYH], es2[kYH], e3[kC];
@@ -258,8 +283,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         S.h2[p][o] = relu(a);
       }
       __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < kE / 16; ++kk) {  // xs (W3 col_pairs: W3[n][k] at (k * 96 + (n >> 1)) * 2 + (n & 1))
+      _Pragma("unroll 1") for (int kk = 0; kk < kE / 16; ++kk) {  // xs (W3 col_pairs: W3[n][k] at (k * 96 + (n >> 1)) * 2 + (n & 1))
         const int n = q + 16 * kk;
         float a = pe[kPeW3 + kE * kPeH2 + n];
 #pragma unroll 8
@@ -296,8 +320,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     {  // conv2 (8 -> 8, 4x4 -> 2x2): lane q = (net, output channel), the four positions
       const int net = q >> 3, o = q & 7;
       const float *G = net ? gI : gA;
-#pragma unroll
-      for (int pos = 0; pos < 4; ++pos) {
+      _Pragma("unroll 1") for (int pos = 0; pos < 4; ++pos) {
         float a = G[CondA::c2b + o];
 #pragma unroll
         for (int ci = 0; ci < kXH; ++ci)
@@ -455,16 +478,23 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     }
     __syncthreads();
     float fin[kC];
+    {  // conv3x3 (6 -> 6), ReLU
+      float a[kCh];
 #pragma unroll
-    for (int o = 0; o < kCh; ++o) {  // conv3x3 (6 -> 6), ReLU
-      float a = F[Aff::r4b + o];
+      for (int o = 0; o < kCh; ++o) a[o] = F[Aff::r4b + o];
       _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
         const int rr = qi + t9 / 3 - 1, ss = qj + t9 % 3 - 1;
         if (!in4(rr, ss)) continue;
+        float v[kCh];
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) a = fmaf(F[Aff::r4w + (t9 * kCh + c) * kCh + o], S.r2[p][rr * 4 + ss][c], a);
+        for (int c = 0; c < kCh; ++c) v[c] = S.r2[p][rr * 4 + ss][c];
+#pragma unroll
+        for (int c = 0; c < kCh; ++c)
+#pragma unroll
+          for (int o = 0; o < kCh; ++o) a[o] = fmaf(F[Aff::r4w + (t9 * kCh + c) * kCh + o], v[c], a[o]);
       }
-      fin[o] = relu(a);
+#pragma unroll
+      for (int o = 0; o < kCh; ++o) fin[o] = relu(a[o]);
     }
 #pragma unroll
     for (int c = 0; c < kCh; ++c) fin[kCh + c] = yw[c];
@@ -473,17 +503,24 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     __syncthreads();
     // f: Conv2dNormy(12 -> 8, 3x3) ReLU, Conv2dNormy(8 -> 8, 1x1) ReLU, Conv2dZerosy(8 -> 12) tanh
     float g1[kYH], g2[kYH], u[kC], h[kC];
-#pragma unroll
-    for (int o = 0; o < kYH; ++o) {
-      float a = 0.f;
+    {
+      float a[kYH] = {};
       _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
         const int rr = qi + t9 / 3 - 1, ss = qj + t9 % 3 - 1;
         if (!in4(rr, ss)) continue;
+        float v[kC];
 #pragma unroll
-        for (int c = 0; c < kC; ++c) a = fmaf(F[Aff::f0w + (t9 * kC + c) * kYH + o], S.fin[p][rr * 4 + ss][c], a);
+        for (int c = 0; c < kC; ++c) v[c] = S.fin[p][rr * 4 + ss][c];
+#pragma unroll
+        for (int c = 0; c < kC; ++c)
+#pragma unroll
+          for (int o = 0; o < kYH; ++o) a[o] = fmaf(F[Aff::f0w + (t9 * kC + c) * kYH + o], v[c], a[o]);
       }
-      g1[o] = relu((a + F[Aff::f0ab + o]) * es0[o]);
-      S.g1[p][q][o] = g1[o];
+#pragma unroll
+      for (int o = 0; o < kYH; ++o) {
+        g1[o] = relu((a[o] + F[Aff::f0ab + o]) * es0[o]);
+        S.g1[p][q][o] = g1[o];
+      }
     }
 #pragma unroll
     for (int o = 0; o < kYH; ++o) {
@@ -494,17 +531,24 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       S.g2[p][q][o] = g2[o];
     }
     __syncthreads();
-#pragma unroll
-    for (int o = 0; o < kC; ++o) {
-      float a = 0.f;
+    {
+      float a[kC] = {};
       _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
         const int rr = qi + t9 / 3 - 1, ss = qj + t9 % 3 - 1;
         if (!in4(rr, ss)) continue;
+        float v[kYH];
 #pragma unroll
-        for (int c = 0; c < kYH; ++c) a = fmaf(F[Aff::f4w + (t9 * kYH + c) * kC + o], S.g2[p][rr * 4 + ss][c], a);
+        for (int c = 0; c < kYH; ++c) v[c] = S.g2[p][rr * 4 + ss][c];
+#pragma unroll
+        for (int c = 0; c < kYH; ++c)
+#pragma unroll
+          for (int o = 0; o < kC; ++o) a[o] = fmaf(F[Aff::f4w + (t9 * kYH + c) * kC + o], v[c], a[o]);
       }
-      u[o] = (a + F[Aff::f4b + o] + F[Aff::f4nb + o]) * e3[o];
-      h[o] = tanhf(u[o]);
+#pragma unroll
+      for (int o = 0; o < kC; ++o) {
+        u[o] = (a[o] + F[Aff::f4b + o] + F[Aff::f4nb + o]) * e3[o];
+        h[o] = tanhf(u[o]);
+      }
     }
 
     // ---------------- backward ----------------
@@ -556,17 +600,25 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
-    contract<kOffF + Aff::f4w>(acc, [&](int j) {
-      const int o = j % kC, c = (j / kC) % kYH, t9 = j / (kC * kYH);
-      const int dr = t9 / 3 - 1, ds = t9 % 3 - 1;
-      float a = 0.f;
-      _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
-        for (int qq = 0; qq < 16; ++qq) {
-          const int rr = (qq >> 2) + dr, ss = (qq & 3) + ds;
-          if (in4(rr, ss)) a = fmaf(S.D[pp][qq][o], S.g2[pp][rr * 4 + ss][c], a);
+    {  // f4w: dW[o][n = (t9, c)] = sum_(p,q) D[p][q][o] g2[p][q + tap][c] (K = 256): column
+       // tiles w, and 4 in wave 0
+      auto job = [&](f4 &cc, int nt) {
+        const int n = nt * 16 + lr, t9 = n >> 3, ch = n & 7, dr = t9 / 3 - 1, ds = t9 % 3 - 1;
+        const bool nok = n < 9 * kYH, mok = lr < kC;
+        const int orow = mok ? lr : 0;
+#pragma unroll 4
+        for (int s2 = 0; s2 < 64; ++s2) {
+          const int k = 4 * s2 + lk, pp = k >> 4, q2 = k & 15;
+          const int rr = (q2 >> 2) + dr, ss = (q2 & 3) + ds;
+          const bool ok = nok && in4(rr, ss);
+          const float bv = S.g2[pp][ok ? rr * 4 + ss : 0][ch];
+          const float av = S.D[pp][q2][orow];
+          cc = mfma4(mok ? av : 0.f, ok ? bv : 0.f, cc);
         }
-      return a;
-    });
+      };
+      job(cF4a, w);
+      if (w == 0) job(cF4b, 4);
+    }
     contract<kOffF + Aff::f4b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][j];
@@ -584,15 +636,21 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     });
     // transposed conv -> dL/dg2 at q; ReLU; Conv2dNormy(1x1) with actnorm scale es2
     float d2[kYH];
+    float tg2[kYH] = {};
+    _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
+      const int rr = qi - (t9 / 3 - 1), ss = qj - (t9 % 3 - 1);  // the output whose tap t9 reads q
+      if (!in4(rr, ss)) continue;
+      float dd[kC];
+#pragma unroll
+      for (int o = 0; o < kC; ++o) dd[o] = S.D[p][rr * 4 + ss][o];
+#pragma unroll
+      for (int c = 0; c < kYH; ++c)
+#pragma unroll
+        for (int o = 0; o < kC; ++o) tg2[c] = fmaf(F[Aff::f4w + (t9 * kYH + c) * kC + o], dd[o], tg2[c]);
+    }
 #pragma unroll
     for (int c = 0; c < kYH; ++c) {
-      float a = 0.f;
-      _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
-        const int rr = qi - (t9 / 3 - 1), ss = qj - (t9 % 3 - 1);  // the output whose tap t9 reads q
-        if (!in4(rr, ss)) continue;
-#pragma unroll
-        for (int o = 0; o < kC; ++o) a = fmaf(F[Aff::f4w + (t9 * kYH + c) * kC + o], S.D[p][rr * 4 + ss][o], a);
-      }
+      const float a = tg2[c];
       const float gv = g2[c] > 0.f ? a : 0.f;  // dL/d(v2), v2 = (conv + ab) es2
       d2[c] = gv * es2[c];
       sb[c] = d2[c];          // ab2
@@ -610,13 +668,16 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kYH; ++o) S.D[p][q][o] = d2[o];
     __syncthreads();
-    contract<kOffF + Aff::f2w>(acc, [&](int j) {
-      const int o = j % kYH, c = j / kYH;
-      float a = 0.f;
-      _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
-        for (int qq = 0; qq < 16; ++qq) a = fmaf(S.D[pp][qq][o], S.g1[pp][qq][c], a);
-      return a;
-    });
+    if (w == 1) {  // f2w: dW[o][c] = sum_(p,q) D[p][q][o] g1[p][q][c]
+      const bool ok = lr < kYH;
+      const int o = ok ? lr : 0;
+#pragma unroll 4
+      for (int s2 = 0; s2 < 64; ++s2) {
+        const int k = 4 * s2 + lk, pp = k >> 4, q2 = k & 15;
+        const float av = S.D[pp][q2][o], bv = S.g1[pp][q2][o];
+        cF2 = mfma4(ok ? av : 0.f, ok ? bv : 0.f, cF2);
+      }
+    }
     contract<kOffF + Aff::f2ab>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][24 + j];
@@ -650,17 +711,24 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kYH; ++o) S.D[p][q][o] = d0[o];
     __syncthreads();
-    contract<kOffF + Aff::f0w>(acc, [&](int j) {
-      const int o = j % kYH, c = (j / kYH) % kC, t9 = j / (kYH * kC);
-      const int dr = t9 / 3 - 1, ds = t9 % 3 - 1;
-      float a = 0.f;
-      _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
-        for (int qq = 0; qq < 16; ++qq) {
-          const int rr = (qq >> 2) + dr, ss = (qq & 3) + ds;
-          if (in4(rr, ss)) a = fmaf(S.D[pp][qq][o], S.fin[pp][rr * 4 + ss][c], a);
+    {  // f0w: dW[o][n = (t9, c)] = sum D[p][q][o] fin[p][q + tap][c]: column tiles w, w + 4 (< 7)
+      auto job = [&](f4 &cc, int nt) {
+        const int n = nt * 16 + lr, t9 = n / kC, ch = n % kC, dr = t9 / 3 - 1, ds = t9 % 3 - 1;
+        const bool nok = n < 9 * kC, mok = lr < kYH;
+        const int orow = mok ? lr : 0;
+#pragma unroll 4
+        for (int s2 = 0; s2 < 64; ++s2) {
+          const int k = 4 * s2 + lk, pp = k >> 4, q2 = k & 15;
+          const int rr = (q2 >> 2) + dr, ss = (q2 & 3) + ds;
+          const bool ok = nok && in4(rr, ss);
+          const float bv = S.fin[pp][ok ? rr * 4 + ss : 0][ok ? ch : 0];
+          const float av = S.D[pp][q2][orow];
+          cc = mfma4(mok ? av : 0.f, ok ? bv : 0.f, cc);
         }
-      return a;
-    });
+      };
+      job(cF0a, w);
+      if (w + 4 < 7) job(cF0b, w + 4);
+    }
     contract<kOffF + Aff::f0ab>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][j];
@@ -671,17 +739,17 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][8 + j];
       return a;
     });
-    float gfin[kC];
+    float gfin[kC] = {};
+    _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
+      const int rr = qi - (t9 / 3 - 1), ss = qj - (t9 % 3 - 1);
+      if (!in4(rr, ss)) continue;
+      float dd[kYH];
 #pragma unroll
-    for (int c = 0; c < kC; ++c) {
-      float a = 0.f;
-      _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
-        const int rr = qi - (t9 / 3 - 1), ss = qj - (t9 % 3 - 1);
-        if (!in4(rr, ss)) continue;
+      for (int o = 0; o < kYH; ++o) dd[o] = S.D[p][rr * 4 + ss][o];
 #pragma unroll
-        for (int o = 0; o < kYH; ++o) a = fmaf(F[Aff::f0w + (t9 * kC + c) * kYH + o], S.D[p][rr * 4 + ss][o], a);
-      }
-      gfin[c] = a;
+      for (int c = 0; c < kC; ++c)
+#pragma unroll
+        for (int o = 0; o < kYH; ++o) gfin[c] = fmaf(F[Aff::f0w + (t9 * kC + c) * kYH + o], dd[o], gfin[c]);
     }
 #pragma unroll
     for (int c = 0; c < kCh; ++c) gz1[c] += gfin[kCh + c];
@@ -701,32 +769,41 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kCh; ++o) S.D[p][q][o] = d4[o];
     __syncthreads();
-    contract<kOffF + Aff::r4w>(acc, [&](int j) {
-      const int o = j % kCh, c = (j / kCh) % kCh, t9 = j / (kCh * kCh);
-      const int dr = t9 / 3 - 1, ds = t9 % 3 - 1;
-      float a = 0.f;
-      _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
-        for (int qq = 0; qq < 16; ++qq) {
-          const int rr = (qq >> 2) + dr, ss = (qq & 3) + ds;
-          if (in4(rr, ss)) a = fmaf(S.D[pp][qq][o], S.r2[pp][rr * 4 + ss][c], a);
-        }
-      return a;
-    });
+    {  // r4w: dW[o][n = (t9, c)] = sum D[p][q][o] r2[p][q + tap][c]: column tile w (54 columns)
+      const int n = w * 16 + lr, t9 = n / kCh, ch = n % kCh, dr = t9 / 3 - 1, ds = t9 % 3 - 1;
+      const bool nok = n < 9 * kCh, mok = lr < kCh;
+      const int orow = mok ? lr : 0;
+#pragma unroll 4
+      for (int s2 = 0; s2 < 64; ++s2) {
+        const int k = 4 * s2 + lk, pp = k >> 4, q2 = k & 15;
+        const int rr = (q2 >> 2) + dr, ss = (q2 & 3) + ds;
+        const bool ok = nok && in4(rr, ss);
+        const float bv = S.r2[pp][ok ? rr * 4 + ss : 0][ok ? ch : 0];
+        const float av = S.D[pp][q2][orow];
+        cR4 = mfma4(mok ? av : 0.f, ok ? bv : 0.f, cR4);
+      }
+    }
     contract<kOffF + Aff::r4b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][16 + j];
       return a;
     });
     float dr2[kCh];  // dL/d(resize conv2 pre-activation)
+    float tr2[kCh] = {};
+    _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
+      const int rr = qi - (t9 / 3 - 1), ss = qj - (t9 % 3 - 1);
+      if (!in4(rr, ss)) continue;
+      float dd[kCh];
+#pragma unroll
+      for (int o = 0; o < kCh; ++o) dd[o] = S.D[p][rr * 4 + ss][o];
+#pragma unroll
+      for (int c = 0; c < kCh; ++c)
+#pragma unroll
+        for (int o = 0; o < kCh; ++o) tr2[c] = fmaf(F[Aff::r4w + (t9 * kCh + c) * kCh + o], dd[o], tr2[c]);
+    }
 #pragma unroll
     for (int c = 0; c < kCh; ++c) {
-      float a = 0.f;
-      _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
-        const int rr = qi - (t9 / 3 - 1), ss = qj - (t9 % 3 - 1);
-        if (!in4(rr, ss)) continue;
-#pragma unroll
-        for (int o = 0; o < kCh; ++o) a = fmaf(F[Aff::r4w + (t9 * kCh + c) * kCh + o], S.D[p][rr * 4 + ss][o], a);
-      }
+      const float a = tr2[c];
       dr2[c] = r2v[c] > 0.f ? a : 0.f;
       sb[c] = dr2[c];
     }
@@ -735,98 +812,100 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       const float a = row16_sum(sb[o]);
       if (q == 0) S.sm[p][24 + o] = a;
     }
-    // resize conv1 gradients at this lane's 2x2 block (r1 recomputed: ReLU outputs)
-    float r1[4][16];
-    resize1(r1);
-    float d1[4][16];
-#pragma unroll
-    for (int ab = 0; ab < 4; ++ab)
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        float a = 0.f;
-#pragma unroll
-        for (int o = 0; o < kCh; ++o) a = fmaf(F[Aff::r2w + (ab * 16 + c) * kCh + o], dr2[o], a);
-        d1[ab][c] = r1[ab][c] > 0.f ? a : 0.f;
-      }
-    float s1[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) s1[c] = row16_sum((d1[0][c] + d1[1][c]) + (d1[2][c] + d1[3][c]));
-    if (q == 0)
-#pragma unroll
-      for (int c = 0; c < 16; ++c) S.sm[p][32 + c] = s1[c];
     __syncthreads();  // D (r4), g1 / g2 (aliased by R1) no longer read; sm complete
     contract<kOffF + Aff::r2b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][24 + j];
       return a;
     });
+#pragma unroll
+    for (int o = 0; o < kCh; ++o) S.D[p][q][o] = dr2[o];
+    // four rounds of one wave's particles: r1 recomputed (ReLU outputs) at the wave's 2x2 blocks
+    // -> r2w; then d r1 in its place -> r0w and dL/dx
+    for (int rw = 0; rw < 4; ++rw) {
+      float r1[4][16];
+      if (w == rw) {
+        resize1(r1);
+#pragma unroll
+        for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+          for (int c = 0; c < 16; ++c) S.R1[p & 3][q][ab][c] = r1[ab][c];
+      }
+      __syncthreads();
+      {  // r2w: dW[o][n = (ab, c)] = sum_(p4,q) D[4 rw + p4][q][o] r1[p4][q][ab][c]: tile ab = w
+        const bool mok = lr < kCh;
+        const int orow = mok ? lr : 0;
+#pragma unroll 4
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const int k = 4 * s2 + lk, p4 = k >> 4, q2 = k & 15;
+          const float av = S.D[4 * rw + p4][q2][orow], bv = S.R1[p4][q2][w][lr];
+          cR2 = mfma4(mok ? av : 0.f, bv, cR2);
+        }
+      }
+      __syncthreads();
+      if (w == rw) {  // d r1 (in r1's registers), its per-particle sums (r0b)
+#pragma unroll
+        for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+          for (int c = 0; c < 16; ++c) {
+            float a = 0.f;
+#pragma unroll
+            for (int o = 0; o < kCh; ++o) a = fmaf(F[Aff::r2w + (ab * 16 + c) * kCh + o], dr2[o], a);
+            r1[ab][c] = r1[ab][c] > 0.f ? a : 0.f;
+            S.R1[p & 3][q][ab][c] = r1[ab][c];
+          }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const float s1 = row16_sum((r1[0][c] + r1[1][c]) + (r1[2][c] + r1[3][c]));
+          if (q == 0) S.sm[p][32 + c] = s1;
+        }
+      }
+      __syncthreads();
+      {  // r0w: dW[o][t] = sum_(p4, 8x8 pos) d1[p4][pos][o] x[p4][c][pos + tap]; wave w: column
+         // tile w & 1, particles 2 (w >> 1) .. +1 of the round (the halves are added at the end)
+        const int n = (w & 1) * 16 + lr, dr = n / 9 - 1, ds = (n / 3) % 3 - 1, c = n % 3;
+        const bool nok = n < 27;
+#pragma unroll 4
+        for (int s2 = 0; s2 < 32; ++s2) {
+          const int k = 4 * s2 + lk, p4 = 2 * (w >> 1) + (k >> 6), pos = k & 63, r = pos >> 3, s8 = pos & 7;
+          const int rr = r + dr, ss = s8 + ds;
+          const bool ok = nok && rr >= 0 && rr < 8 && ss >= 0 && ss < 8;
+          const float bv = S.X[4 * rw + p4][ok ? c * 64 + rr * 8 + ss : 0];
+          const float av = S.R1[p4][(r >> 1) * 4 + (s8 >> 1)][(r & 1) * 2 + (s8 & 1)][lr];
+          cR0 = mfma4(av, ok ? bv : 0.f, cR0);
+        }
+      }
+      if (w == rw) {  // dL/dx from resize conv1 at this lane's 2x2 block, 3 channels
+        _Pragma("unroll 1") for (int ab = 0; ab < 4; ++ab) {
+          const int r = 2 * qi + (ab >> 1), s = 2 * qj + (ab & 1);
+          float a[3] = {};
+          _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
+            const int ro = r - (t9 / 3 - 1), so = s - (t9 % 3 - 1);  // output reading (r, s) by tap t9
+            if (ro < 0 || ro >= 8 || so < 0 || so >= 8) continue;
+            const f4 *dd4 = reinterpret_cast<const f4 *>(S.R1[p & 3][(ro >> 1) * 4 + (so >> 1)][(ro & 1) * 2 + (so & 1)]);
+            float dd[16];
+#pragma unroll
+            for (int o4 = 0; o4 < 4; ++o4) {
+              const f4 v = dd4[o4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dd[4 * o4 + e] = v[e];
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+              for (int o = 0; o < 16; ++o) a[c] = fmaf(F[Aff::r0w + ((t9 * 3) + c) * 16 + o], dd[o], a[c]);
+          }
+#pragma unroll
+          for (int c = 0; c < 3; ++c) S.gX[p][c * 64 + r * 8 + s] += a[c];
+        }
+      }
+      __syncthreads();
+    }
     contract<kOffF + Aff::r0b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][32 + j];
       return a;
     });
-#pragma unroll
-    for (int o = 0; o < kCh; ++o) S.D[p][q][o] = dr2[o];
-    // four rounds of one wave's particles: r2w from (d r2, r1), then r0w and dL/dx from d r1
-    for (int rw = 0; rw < 4; ++rw) {
-      if (w == rw)
-#pragma unroll
-        for (int ab = 0; ab < 4; ++ab)
-#pragma unroll
-          for (int c = 0; c < 16; ++c) S.R1[p & 3][q][ab][c] = r1[ab][c];
-      __syncthreads();
-      contract<kOffF + Aff::r2w>(acc, [&](int j) {
-        const int o = j % kCh, c = (j / kCh) % 16, ab = j / (kCh * 16);
-        float a = 0.f;
-        _Pragma("unroll 1") for (int p4 = 0; p4 < 4; ++p4)
-          for (int qq = 0; qq < 16; ++qq) a = fmaf(S.D[4 * rw + p4][qq][o], S.R1[p4][qq][ab][c], a);
-        return a;
-      });
-      __syncthreads();
-      if (w == rw)
-#pragma unroll
-        for (int ab = 0; ab < 4; ++ab)
-#pragma unroll
-          for (int c = 0; c < 16; ++c) S.R1[p & 3][q][ab][c] = d1[ab][c];
-      __syncthreads();
-      contract<kOffF + Aff::r0w>(acc, [&](int j) {
-        const int o = j % 16, t = j / 16;
-        const int dr = t / 9 - 1, ds = (t / 3) % 3 - 1, c = t % 3;
-        float a = 0.f;
-        _Pragma("unroll 1") for (int p4 = 0; p4 < 4; ++p4) {
-          const float *Xp = S.X[4 * rw + p4] + c * 64;
-          _Pragma("unroll 1") for (int r = 0; r < 8; ++r) {
-            const int rr = r + dr;
-            if (rr < 0 || rr >= 8) continue;
-            for (int s = 0; s < 8; ++s) {
-              const int ss = s + ds;
-              if (ss < 0 || ss >= 8) continue;
-              a = fmaf(S.R1[p4][(r >> 1) * 4 + (s >> 1)][(r & 1) * 2 + (s & 1)][o], Xp[rr * 8 + ss], a);
-            }
-          }
-        }
-        return a;
-      });
-      if (w == rw) {  // dL/dx from resize conv1 at this lane's 2x2 block, 3 channels
-#pragma unroll
-        for (int ab = 0; ab < 4; ++ab) {
-          const int r = 2 * qi + (ab >> 1), s = 2 * qj + (ab & 1);
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            float a = 0.f;
-            _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
-              const int ro = r - (t9 / 3 - 1), so = s - (t9 % 3 - 1);  // output reading (r, s) by tap t9
-              if (ro < 0 || ro >= 8 || so < 0 || so >= 8) continue;
-              const float *dd = S.R1[p & 3][(ro >> 1) * 4 + (so >> 1)][(ro & 1) * 2 + (so & 1)];
-#pragma unroll
-              for (int o = 0; o < 16; ++o) a = fmaf(F[Aff::r0w + ((t9 * 3) + c) * 16 + o], dd[o], a);
-            }
-            S.gX[p][c * 64 + r * 8 + s] += a;
-          }
-        }
-      }
-      __syncthreads();
-    }
     // 1x1 conv and actnorm: dL/dyw = (g_z1, g_z2)
     float gyw[kC];
 #pragma unroll
@@ -910,9 +989,9 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       const int net = hh, k = q;
       float a = 0.f;
       if (net == 0) {
-        for (int n = 0; n < 2 * kC; ++n) a = fmaf(gA[CondA::l4w + n * kXS + k], S.gan[p][n], a);
+        _Pragma("unroll 4") for (int n = 0; n < 2 * kC; ++n) a = fmaf(gA[CondA::l4w + n * kXS + k], S.gan[p][n], a);
       } else {
-        for (int n = 0; n < kC * kC; ++n) a = fmaf(gI[CondI::l4w + n * kXS + k], S.gw[p][n], a);
+        _Pragma("unroll 4") for (int n = 0; n < kC * kC; ++n) a = fmaf(gI[CondI::l4w + n * kXS + k], S.gw[p][n], a);
       }
       Gp[net * kXS + k] = S.l1[p][net * kXS + k] > 0.f ? a : 0.f;
     }
@@ -1013,16 +1092,6 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     __syncthreads();
 #pragma unroll
     for (int net = 0; net < 2; ++net) {
-      auto c2w = [&](int j) {
-        const int o = j / 32, ci = (j / 4) % kXH, ab = j % 4;
-        float a = 0.f;
-        _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
-#pragma unroll
-          for (int pos = 0; pos < 4; ++pos)
-            a = fmaf(S.D[pp][0][80 + pos * 16 + net * kXH + o],
-                     S.c1[pp][(2 * (pos >> 1) + (ab >> 1)) * 4 + 2 * (pos & 1) + (ab & 1)][net * kXH + ci], a);
-        return a;
-      };
       auto c2b = [&](int j) {
         float a = 0.f;
         _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
@@ -1030,12 +1099,20 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
           for (int pos = 0; pos < 4; ++pos) a += S.D[pp][0][80 + pos * 16 + net * kXH + j];
         return a;
       };
-      if (net == 0) {
-        contract<kOffA + CondA::c2w>(acc, c2w);
+      if (net == 0)
         contract<kOffA + CondA::c2b>(acc, c2b);
-      } else {
-        contract<kOffI + CondI::c2w>(acc, c2w);
+      else
         contract<kOffI + CondI::c2b>(acc, c2b);
+    }
+    {  // c2w of net w >> 1, column tile w & 1: dW[o][n = (ci, ab)] = sum_(p, pos) g[p][pos][o] c1[p][..][ci]
+      const int net = w >> 1, n = (w & 1) * 16 + lr, ci = n >> 2, ab = n & 3;
+      const bool mok = lr < kXH;
+#pragma unroll 4
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int k = 4 * s2 + lk, pp = k >> 2, pos = k & 3;
+        const float av = S.D[pp][0][80 + pos * 16 + net * kXH + (mok ? lr : 0)];
+        const float bv = S.c1[pp][(2 * (pos >> 1) + (ab >> 1)) * 4 + 2 * (pos & 1) + (ab & 1)][net * kXH + ci];
+        cC2 = mfma4(mok ? av : 0.f, bv, cC2);
       }
     }
     {  // dL/dc1 at position q (both nets)
@@ -1053,29 +1130,28 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
+    if (w == 2) {  // c0w of both nets (rows net * 8 + o): dW[k = (ci, a, b)][o] = sum_(p,q) g1c x
+      const int n = lr < 12 ? lr : 0, ci = n >> 2, a2 = (n >> 1) & 1, b2 = n & 1;
+#pragma unroll 4
+      for (int s2 = 0; s2 < 64; ++s2) {
+        const int k = 4 * s2 + lk, pp = k >> 4, q2 = k & 15;
+        const float av = S.G1c[pp][q2][lr];
+        const float bv = S.X[pp][ci * 64 + (2 * (q2 >> 2) + a2) * 8 + 2 * (q2 & 3) + b2];
+        cC0 = mfma4(av, lr < 12 ? bv : 0.f, cC0);
+      }
+    }
 #pragma unroll
     for (int net = 0; net < 2; ++net) {
-      auto c0w = [&](int j) {  // [k = (ci, a, b)][o]
-        const int o = j % kXH, k = j / kXH, ci = k >> 2, a2 = (k >> 1) & 1, b2 = k & 1;
-        float a = 0.f;
-        _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
-          for (int qq = 0; qq < 16; ++qq)
-            a = fmaf(S.G1c[pp][qq][net * kXH + o], S.X[pp][ci * 64 + (2 * (qq >> 2) + a2) * 8 + 2 * (qq & 3) + b2], a);
-        return a;
-      };
       auto c0b = [&](int j) {
         float a = 0.f;
         _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp)
           for (int qq = 0; qq < 16; ++qq) a += S.G1c[pp][qq][net * kXH + j];
         return a;
       };
-      if (net == 0) {
-        contract<kOffA + CondA::c0w>(acc, c0w);
+      if (net == 0)
         contract<kOffA + CondA::c0b>(acc, c0b);
-      } else {
-        contract<kOffI + CondI::c0w>(acc, c0w);
+      else
         contract<kOffI + CondI::c0b>(acc, c0b);
-      }
     }
     // dL/dx from both conditioning conv1s at this lane's 2x2 block
 #pragma unroll
@@ -1097,12 +1173,15 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < kE / 16; ++k) g_x[m * kE + q + 16 * k] = S.gX[p][q + 16 * k];
     } else {
-      contract<kStep + kPeW3>(acc, [&](int j) {  // col_pairs: pair (k, n / 2), n & 1
-        const int pr = j >> 1, k = pr / (kE / 2), n = (pr % (kE / 2)) * 2 + (j & 1);
-        float a = 0.f;
-        _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a = fmaf(S.gX[pp][n], S.h2[pp][k], a);
-        return a;
-      });
+#pragma unroll
+      for (int jj = 0; jj < 6; ++jj) {  // W3: dW[n][k] = sum_p gX[p][n] h2[p][k]; job w + 4 jj = (n tile, k tile)
+        const int j = w + 4 * jj, mt = j >> 1, kt = j & 1;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int k = 4 * s2 + lk;
+          cW3[jj] = mfma4(S.gX[k][mt * 16 + lr], S.h2[k][kt * 16 + lr], cW3[jj]);
+        }
+      }
       contract<kStep + kPeW3 + kE * kPeH2>(acc, [&](int j) {
         float a = 0.f;
         _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.gX[pp][j];
@@ -1112,8 +1191,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       for (int hh = 0; hh < 2; ++hh) {  // dL/dh2 -> D[p][0][0..31]
         const int k = q + 16 * hh;
         float a = 0.f;
-#pragma unroll 8
-        for (int n = 0; n < kE; ++n) a = fmaf(pe[kPeW3 + (k * (kE / 2) + (n >> 1)) * 2 + (n & 1)], S.gX[p][n], a);
+        _Pragma("unroll 4") for (int n = 0; n < kE; ++n) a = fmaf(pe[kPeW3 + (k * (kE / 2) + (n >> 1)) * 2 + (n & 1)], S.gX[p][n], a);
         Gp[k] = S.h2[p][k] > 0.f ? a : 0.f;
       }
       __syncthreads();
@@ -1158,7 +1236,45 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     __syncthreads();
   }
   // this workgroup's parameter-gradient row
-  store_acc<0>(acc, partial + (int64_t)blockIdx.x * kTotParams);
+  float *row = partial + (int64_t)blockIdx.x * kTotParams;
+  store_acc<0>(acc, row);
+  store_tile(cF4a, row, kC, w * 16, 9 * kYH, [](int m, int n) { return kOffF + Aff::f4w + n * kC + m; });
+  if (w == 0) store_tile(cF4b, row, kC, 64, 9 * kYH, [](int m, int n) { return kOffF + Aff::f4w + n * kC + m; });
+  store_tile(cF0a, row, kYH, w * 16, 9 * kC, [](int m, int n) { return kOffF + Aff::f0w + n * kYH + m; });
+  if (w + 4 < 7)
+    store_tile(cF0b, row, kYH, (w + 4) * 16, 9 * kC, [](int m, int n) { return kOffF + Aff::f0w + n * kYH + m; });
+  store_tile(cR4, row, kCh, w * 16, 9 * kCh, [](int m, int n) { return kOffF + Aff::r4w + n * kCh + m; });
+  store_tile(cR2, row, kCh, 0, 16, [w](int m, int n) { return kOffF + Aff::r2w + (w * 16 + n) * kCh + m; });
+  if (w == 1) store_tile(cF2, row, kYH, 0, kYH, [](int m, int n) { return kOffF + Aff::f2w + n * kYH + m; });
+  if (w == 2)
+    store_tile(cC0, row, 16, 0, 12, [](int m, int n) { return ((m >> 3) ? kOffI : kOffA) + CondA::c0w + n * kXH + (m & 7); });
+  {
+    const int net = w >> 1;
+    store_tile(cC2, row, kXH, (w & 1) * 16, 32,
+               [net](int m, int n) { return (net ? kOffI : kOffA) + CondA::c2w + m * 32 + n; });
+  }
+  if (PART)
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj) {
+      const int j = w + 4 * jj, mt = j >> 1, kt = j & 1;
+      store_tile(cW3[jj], row, 16, kt * 16, 32, [mt](int m, int n) {
+        const int nx = mt * 16 + m;
+        return kStep + kPeW3 + (n * (kE / 2) + (nx >> 1)) * 2 + (nx & 1);
+      });
+    }
+  // r0w: the two particle halves (waves w and w + 2) added in a fixed order
+  float *cmb = &S.D[0][0][0];
+  const int l = tid & 63;
+  if (w >= 2)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cmb[((w - 2) * 64 + l) * 4 + i] = cR0[i];
+  __syncthreads();
+  if (w < 2) {
+    f4 t = cR0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[i] += cmb[(w * 64 + l) * 4 + i];
+    store_tile(t, row, 16, w * 16, 27, [](int m, int n) { return kOffF + Aff::r0w + n * 16 + m; });
+  }
 }
 
 // out[j] = sum over the workgroup rows, in row order

@@ -26,7 +26,8 @@ def main():
     x = (torch.randn(B, N, 2, generator=g) * 20).to(dev).requires_grad_(True)
     gl = torch.randn(B, N, generator=g).to(dev)
     out = {"B": B, "N": N}
-    for mode in (True, False):
+    modes = (True,) if os.environ.get("CGB_HIP_ONLY") else (True, False)
+    for mode in modes:
         ag.HIP_BACKWARD = mode
         times = []
         for it in range(4):
@@ -41,7 +42,8 @@ def main():
         out["hip_backward_ms" if mode else "recompute_backward_ms"] = 1e3 * min(times[1:])
         print(json.dumps(out), flush=True)
     ag.HIP_BACKWARD = True
-    out["speedup"] = out["recompute_backward_ms"] / out["hip_backward_ms"]
+    if "recompute_backward_ms" in out:
+        out["speedup"] = out["recompute_backward_ms"] / out["hip_backward_ms"]
     print(json.dumps(out), flush=True)
 
 
