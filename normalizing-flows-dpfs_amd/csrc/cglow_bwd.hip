@@ -182,7 +182,17 @@ struct BLds {
     float G1c[kTP][16][2 * kXH];     // conditioning conv1 output gradients
   };
   float D[kTP][16][kC];  // output gradients of the layer being differentiated (exchange)
+  float esc[2 * kYH + kC];                     // exp(f0 logs), exp(f2 logs), exp(3 f4 logs)
+  float w4A[2 * kC * kXS], w4I[kC * kC * kXS];  // the nets' last layers [n][k] (lane-indexed reads)
 };
+
+#ifdef NFDPF_EXP_CBTRACE  // experiment: per-phase timestamps of one tile per workgroup
+__device__ uint64_t g_cbtrace[256][16];
+#define CBT(k)                                                              \
+  if (cbt_on && threadIdx.x == 0) g_cbtrace[blockIdx.x & 255][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define CBT(k)
+#endif
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_max_u(uint32_t v) {
@@ -230,16 +240,17 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
   const int lr = tid & 15, lk = (tid >> 4) & 3;  // MFMA lane: row / column l % 16, k offset l / 16
   f4 cF4a = {}, cF4b = {}, cF0a = {}, cF0b = {}, cR4 = {}, cR2 = {}, cR0 = {}, cF2 = {}, cC0 = {}, cC2 = {};
   f4 cW3[6] = {};
-  // per-channel scales of f (Conv2dNormy exp(logs), Conv2dZerosy exp(3 logs))
-  const float *F = glow + kOffF;
-  float es0[kYH], es2[kYH], e3[kC];
-#pragma unroll
-  for (int o = 0; o < kYH; ++o) {
-    es0[o] = expf(F[Aff::f0al + o]);
-    es2[o] = expf(F[Aff::f2al + o]);
+  // per-channel scales of f (Conv2dNormy exp(logs), Conv2dZerosy exp(3 logs)) and the
+  // conditioning nets' last layers, once per workgroup (ordered by the tile's first barrier)
+  {
+    const float *F = glow + kOffF;
+    if (tid < 2 * kYH + kC)
+      S.esc[tid] = tid < kYH ? expf(F[Aff::f0al + tid])
+                   : tid < 2 * kYH ? expf(F[Aff::f2al + tid - kYH]) : expf(F[Aff::f4l + tid - 2 * kYH] * 3.0f);
+    for (int k = tid; k < 2 * kC * kXS; k += kThreads) S.w4A[k] = glow[kOffA + CondA::l4w + k];
+    for (int k = tid; k < kC * kC * kXS; k += kThreads) S.w4I[k] = glow[kOffI + CondI::l4w + k];
   }
-#pragma unroll
-  for (int o = 0; o < kC; ++o) e3[o] = expf(F[Aff::f4l + o] * 3.0f);
+  const float *es0 = S.esc, *es2 = S.esc + kYH, *e3 = S.esc + 2 * kYH;
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // weight pointers laundered per tile: the compiler re-reads the weights from the caches in
@@ -247,10 +258,14 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     const float *gw_ = glow, *pe = pe_;
     asm volatile("" : "+s"(gw_), "+s"(pe));
     const float *gA = gw_ + kOffA, *gI = gw_ + kOffI, *F = gw_ + kOffF;
+#ifdef NFDPF_EXP_CBTRACE
+    const bool cbt_on = tile == blockIdx.x + 2 * (int64_t)gridDim.x;
+#endif
     const int64_t m_raw = tile * kTP + p;
     const bool valid = m_raw < M;
     const int64_t m = valid ? m_raw : M - 1;  // invalid lanes recompute a real particle, upstream 0
     const int rowb = PART ? (int)(m / N) : (int)m;
+    CBT(0)
     // ---------------- forward recompute ----------------
     float yq[kC];  // squeezed y at position q: channel c * 4 + f
     {
@@ -283,18 +298,32 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         S.h2[p][o] = relu(a);
       }
       __syncthreads();
-      _Pragma("unroll 1") for (int kk = 0; kk < kE / 16; ++kk) {  // xs (W3 col_pairs: W3[n][k] at (k * 96 + (n >> 1)) * 2 + (n & 1))
-        const int n = q + 16 * kk;
-        float a = pe[kPeW3 + kE * kPeH2 + n];
-#pragma unroll 8
-        for (int k = 0; k < kPeH2; ++k) a = fmaf(pe[kPeW3 + (k * (kE / 2) + (n >> 1)) * 2 + (n & 1)], S.h2[p][k], a);
-        S.X[p][n] = a;
+      {  // xs = W3 h2 + b3 on MFMA (the forward kernel's arithmetic): C[p][n], A = h2, B[k][n] =
+         // W3[n][k] (col_pairs: (k * 96 + n / 2) * 2 + n % 2); wave w: column tiles w, w + 4, w + 8
+        float bw[3][8];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int n = (w + 4 * j) * 16 + lr;
+#pragma unroll
+          for (int s2 = 0; s2 < 8; ++s2) bw[j][s2] = pe[kPeW3 + ((4 * s2 + lk) * (kE / 2) + (n >> 1)) * 2 + (n & 1)];
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int n0 = (w + 4 * j) * 16;
+          f4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s2 = 0; s2 < 8; ++s2) c = mfma4(S.h2[lr][4 * s2 + lk], bw[j][s2], c);
+          const float bias = pe[kPeW3 + kE * kPeH2 + n0 + lr];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) S.X[4 * lk + i][n0 + lr] = c[i] + bias;
+        }
       }
     } else {
 #pragma unroll
       for (int k = 0; k < kE / 16; ++k) S.X[p][q + 16 * k] = x[m * kE + q + 16 * k];
     }
     __syncthreads();
+    CBT(1)
     // conditioning nets: conv1 (3 -> 8, 2x2 stride 2, 8x8 -> 4x4) at position q
     {
       float in[12];
@@ -367,10 +396,11 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       const bool isI = idx >= 2 * kC;
       const int n = isI ? idx - 2 * kC : idx;
       const float *G = isI ? gI : gA;
-      const int lw = isI ? CondI::l4w : CondA::l4w, lb = isI ? CondI::l4b : CondA::l4b;
+      const int lb = isI ? CondI::l4b : CondA::l4b;
+      const float *W = isI ? S.w4I : S.w4A;
       float a = G[lb + n];
 #pragma unroll
-      for (int k = 0; k < kXS; ++k) a = fmaf(G[lw + n * kXS + k], S.l1[p][(isI ? kXS : 0) + k], a);
+      for (int k = 0; k < kXS; ++k) a = fmaf(W[n * kXS + k], S.l1[p][(isI ? kXS : 0) + k], a);
       const float t = tanhf(a);
       if (isI)
         S.wm[p][n] = t;
@@ -378,20 +408,28 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         S.an[p][n] = t;
     }
     __syncthreads();
+    CBT(2)
     // actnorm, 1x1 conv at position q
-    float ya[kC], yw[kC], els[kC];
+    float yw[kC];
+    {
+      float ya[kC];
 #pragma unroll
-    for (int c = 0; c < kC; ++c) {
-      els[c] = expf(S.an[p][c]);
-      ya[c] = (yq[c] + S.an[p][kC + c]) * els[c];
-      S.ya[p][q][c] = ya[c];
-    }
+      for (int c = 0; c < kC; ++c) {
+        ya[c] = (yq[c] + S.an[p][kC + c]) * expf(S.an[p][c]);
+        S.ya[p][q][c] = ya[c];
+      }
+      const f4 *wr = reinterpret_cast<const f4 *>(S.wm[p]);
 #pragma unroll
-    for (int o = 0; o < kC; ++o) {
-      float a = 0.f;
+      for (int o = 0; o < kC; ++o) {
+        float a = 0.f;
 #pragma unroll
-      for (int c = 0; c < kC; ++c) a = fmaf(S.wm[p][o * kC + c], ya[c], a);
-      yw[o] = a;
+        for (int c4 = 0; c4 < kC / 4; ++c4) {
+          const f4 wv = wr[o * (kC / 4) + c4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a = fmaf(wv[e], ya[4 * c4 + e], a);
+        }
+        yw[o] = a;
+      }
     }
     // W^-1: Gauss-Jordan with partial pivoting, lane q < 12 holding row q of [W | I]
     {
@@ -417,16 +455,26 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
           for (int j = 0; j < 2 * kC; ++j) S.prow[p][j] = a[j];
         WFENCE();
-        const float inv = 1.0f / S.prow[p][k];
+        float pr[2 * kC];
+        {
+          const f4 *pv = reinterpret_cast<const f4 *>(S.prow[p]);
+#pragma unroll
+          for (int j4 = 0; j4 < 2 * kC / 4; ++j4) {
+            const f4 v = pv[j4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pr[4 * j4 + e] = v[e];
+          }
+        }
+        const float inv = 1.0f / pr[k];
         if (q == who) {
           done = true;
           mycol = k;
 #pragma unroll
-          for (int j = 0; j < 2 * kC; ++j) a[j] = S.prow[p][j] * inv;
+          for (int j = 0; j < 2 * kC; ++j) a[j] = pr[j] * inv;
         } else if (q < kC) {
           const float f = a[k];
 #pragma unroll
-          for (int j = 0; j < 2 * kC; ++j) a[j] = fmaf(-f, S.prow[p][j] * inv, a[j]);
+          for (int j = 0; j < 2 * kC; ++j) a[j] = fmaf(-f, pr[j] * inv, a[j]);
         }
         WFENCE();
       }
@@ -477,6 +525,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
+    CBT(3)
     float fin[kC];
     {  // conv3x3 (6 -> 6), ReLU
       float a[kCh];
@@ -501,6 +550,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int c = 0; c < kC; ++c) S.fin[p][q][c] = fin[c];
     __syncthreads();
+    CBT(4)
     // f: Conv2dNormy(12 -> 8, 3x3) ReLU, Conv2dNormy(8 -> 8, 1x1) ReLU, Conv2dZerosy(8 -> 12) tanh
     float g1[kYH], g2[kYH], u[kC], h[kC];
     {
@@ -600,6 +650,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
+    CBT(5)
     {  // f4w: dW[o][n = (t9, c)] = sum_(p,q) D[p][q][o] g2[p][q + tap][c] (K = 256): column
        // tiles w, and 4 in wave 0
       auto job = [&](f4 &cc, int nt) {
@@ -668,6 +719,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kYH; ++o) S.D[p][q][o] = d2[o];
     __syncthreads();
+    CBT(6)
     if (w == 1) {  // f2w: dW[o][c] = sum_(p,q) D[p][q][o] g1[p][q][c]
       const bool ok = lr < kYH;
       const int o = ok ? lr : 0;
@@ -769,6 +821,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kCh; ++o) S.D[p][q][o] = d4[o];
     __syncthreads();
+    CBT(7)
     {  // r4w: dW[o][n = (t9, c)] = sum D[p][q][o] r2[p][q + tap][c]: column tile w (54 columns)
       const int n = w * 16 + lr, t9 = n / kCh, ch = n % kCh, dr = t9 / 3 - 1, ds = t9 % 3 - 1;
       const bool nok = n < 9 * kCh, mok = lr < kCh;
@@ -813,6 +866,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       if (q == 0) S.sm[p][24 + o] = a;
     }
     __syncthreads();  // D (r4), g1 / g2 (aliased by R1) no longer read; sm complete
+    CBT(8)
     contract<kOffF + Aff::r2b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][24 + j];
@@ -900,6 +954,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         }
       }
       __syncthreads();
+      CBT(9)
     }
     contract<kOffF + Aff::r0b>(acc, [&](int j) {
       float a = 0.f;
@@ -936,9 +991,9 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       float *gyr = g_y + m * kE;
 #pragma unroll
       for (int c = 0; c < kC; ++c) {
-        const float gy0 = gya[c] * els[c];
+        const float gy0 = gya[c] * expf(S.an[p][c]);
         if (valid) gyr[(c >> 2) * 64 + (2 * qi + ((c & 3) >> 1)) * 8 + 2 * qj + (c & 1)] = gy0;
-        const float gls = row16_sum(gya[c] * ya[c]), gb = row16_sum(gy0);
+        const float gls = row16_sum(gya[c] * S.ya[p][q][c]), gb = row16_sum(gy0);
         if (q == 0) {
           S.gan[p][c] = fmaf(16.0f, gobj, gls);
           S.gan[p][kC + c] = gb;
@@ -946,6 +1001,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
+    CBT(10)
     // ---------------- conditioning nets backward (A: actnorm, I: 1x1 conv) ----------------
     for (int idx = q; idx < 2 * kC + kC * kC; idx += 16) {  // through the tanh
       const bool isI = idx >= 2 * kC;
@@ -989,9 +1045,9 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       const int net = hh, k = q;
       float a = 0.f;
       if (net == 0) {
-        _Pragma("unroll 4") for (int n = 0; n < 2 * kC; ++n) a = fmaf(gA[CondA::l4w + n * kXS + k], S.gan[p][n], a);
+        _Pragma("unroll 8") for (int n = 0; n < 2 * kC; ++n) a = fmaf(S.w4A[n * kXS + k], S.gan[p][n], a);
       } else {
-        _Pragma("unroll 4") for (int n = 0; n < kC * kC; ++n) a = fmaf(gI[CondI::l4w + n * kXS + k], S.gw[p][n], a);
+        _Pragma("unroll 8") for (int n = 0; n < kC * kC; ++n) a = fmaf(S.w4I[n * kXS + k], S.gw[p][n], a);
       }
       Gp[net * kXS + k] = S.l1[p][net * kXS + k] > 0.f ? a : 0.f;
     }
@@ -1167,6 +1223,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       S.gX[p][ci * 64 + (2 * qi + a2) * 8 + 2 * qj + b2] += a;
     }
     __syncthreads();
+    CBT(11)
     // ---------------- the condition's gradient: out, or through the particle encoder ----------------
     if (!PART) {
       if (valid)
@@ -1187,12 +1244,30 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.gX[pp][j];
         return a;
       });
+      {  // dL/dh2[p][k] = sum_n gX[p][n] W3[n][k] on MFMA -> D[p][0][0..31]: wave w: k tile w & 1,
+         // n half w >> 1 (the halves added in a fixed order through LDS)
+        const int kt = w & 1, nh = w >> 1, kk = kt * 16 + lr;
+        float bw[24];
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {  // dL/dh2 -> D[p][0][0..31]
-        const int k = q + 16 * hh;
-        float a = 0.f;
-        _Pragma("unroll 4") for (int n = 0; n < kE; ++n) a = fmaf(pe[kPeW3 + (k * (kE / 2) + (n >> 1)) * 2 + (n & 1)], S.gX[p][n], a);
-        Gp[k] = S.h2[p][k] > 0.f ? a : 0.f;
+        for (int s2 = 0; s2 < 24; ++s2) {
+          const int n = nh * 96 + 4 * s2 + lk;
+          bw[s2] = pe[kPeW3 + (kk * (kE / 2) + (n >> 1)) * 2 + (n & 1)];
+        }
+        f4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 24; ++s2) c = mfma4(S.gX[lr][nh * 96 + 4 * s2 + lk], bw[s2], c);
+        float *cmb = &S.R1[0][0][0][0];
+        if (nh == 1)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cmb[(kt * 64 + (tid & 63)) * 4 + i] = c[i];
+        __syncthreads();
+        if (nh == 0)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int pp = 4 * lk + i;
+            const float v = c[i] + cmb[(kt * 64 + (tid & 63)) * 4 + i];
+            S.D[pp][0][kk] = S.h2[pp][kk] > 0.f ? v : 0.f;
+          }
       }
       __syncthreads();
       contract<kStep + kPeW2>(acc, [&](int j) {
@@ -1234,6 +1309,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
+    CBT(12)
   }
   // this workgroup's parameter-gradient row
   float *row = partial + (int64_t)blockIdx.x * kTotParams;
@@ -1324,6 +1400,12 @@ static int launch_bwd(const float *pe, const float *glow, const float *enc, int6
 }  // namespace nfdpf
 
 using namespace nfdpf;
+
+#ifdef NFDPF_EXP_CBTRACE
+extern "C" NFDPF_API int nfdpf_exp_cbtrace_read(void *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(cgb::g_cbtrace), sizeof(cgb::g_cbtrace)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int64_t nfdpf_cglow_backward_workspace(int64_t M) {
   if (M < 0) return -1;

@@ -7,4 +7,4 @@ cd "$(dirname "$0")/../normalizing-flows-dpfs_amd/csrc"
 mkdir -p ../../exp
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fvisibility=hidden --offload-arch=gfx950 -w "$@" -shared \
   capi.hip flows.hip flows_bwd.hip resample_soft.hip resample_soft_bwd.hip filter_step.hip filter_tiled.hip resample_ot.hip measure.hip measure_bwd.hip misc.hip \
-  cglow.hip rqs.hip maf_bwd.hip pseudo_lik.hip nn_bwd.hip -o ../../exp/lib_${TAG}.so
+  cglow.hip cglow_bwd.hip rqs.hip maf_bwd.hip pseudo_lik.hip nn_bwd.hip -o ../../exp/lib_${TAG}.so
