@@ -184,14 +184,21 @@ struct BLds {
   float D[kTP][16][kC];  // output gradients of the layer being differentiated (exchange)
   float esc[2 * kYH + kC];                     // exp(f0 logs), exp(f2 logs), exp(3 f4 logs)
   float w4A[2 * kC * kXS], w4I[kC * kC * kXS];  // the nets' last layers [n][k] (lane-indexed reads)
+  float b4[2 * kC + kC * kC];                   // ... their biases (A then I)
+  float wc2[2][kXH * kXH * 4], wc4[2][kXH * kXH * 4];  // conv2 / conv3 of nets A, I [o][ci][a][b]
 };
+static_assert(sizeof(BLds) <= 160 * 1024, "cglow_bwd: LDS above 160 KB");
 
 #ifdef NFDPF_EXP_CBTRACE  // experiment: per-phase timestamps of one tile per workgroup
 __device__ uint64_t g_cbtrace[256][16];
-#define CBT(k)                                                              \
-  if (cbt_on && threadIdx.x == 0) g_cbtrace[blockIdx.x & 255][k] = __builtin_amdgcn_s_memrealtime();
+#define CBT(k)                                                                        \
+  do {                                                                                \
+    if (cbt_on && threadIdx.x == 0) g_cbtrace[blockIdx.x & 255][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
-#define CBT(k)
+#define CBT(k) \
+  do {         \
+  } while (0)
 #endif
 
 template <int CTRL>
@@ -249,6 +256,13 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
                    : tid < 2 * kYH ? expf(F[Aff::f2al + tid - kYH]) : expf(F[Aff::f4l + tid - 2 * kYH] * 3.0f);
     for (int k = tid; k < 2 * kC * kXS; k += kThreads) S.w4A[k] = glow[kOffA + CondA::l4w + k];
     for (int k = tid; k < kC * kC * kXS; k += kThreads) S.w4I[k] = glow[kOffI + CondI::l4w + k];
+    if (tid < 2 * kC + kC * kC)
+      S.b4[tid] = tid < 2 * kC ? glow[kOffA + CondA::l4b + tid] : glow[kOffI + CondI::l4b + tid - 2 * kC];
+    for (int k = tid; k < 2 * kXH * kXH * 4; k += kThreads) {
+      const int net = k >> 8, j = k & 255;
+      S.wc2[net][j] = glow[(net ? kOffI : kOffA) + CondA::c2w + j];
+      S.wc4[net][j] = glow[(net ? kOffI : kOffA) + CondA::c4w + j];
+    }
   }
   const float *es0 = S.esc, *es2 = S.esc + kYH, *e3 = S.esc + 2 * kYH;
 
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     const bool valid = m_raw < M;
     const int64_t m = valid ? m_raw : M - 1;  // invalid lanes recompute a real particle, upstream 0
     const int rowb = PART ? (int)(m / N) : (int)m;
-    CBT(0)
+    CBT(0);
     // ---------------- forward recompute ----------------
     float yq[kC];  // squeezed y at position q: channel c * 4 + f
     {
@@ -323,7 +337,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       for (int k = 0; k < kE / 16; ++k) S.X[p][q + 16 * k] = x[m * kE + q + 16 * k];
     }
     __syncthreads();
-    CBT(1)
+    CBT(1);
     // conditioning nets: conv1 (3 -> 8, 2x2 stride 2, 8x8 -> 4x4) at position q
     {
       float in[12];
@@ -355,7 +369,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         for (int ci = 0; ci < kXH; ++ci)
 #pragma unroll
           for (int ab = 0; ab < 4; ++ab)
-            a = fmaf(G[CondA::c2w + o * 32 + ci * 4 + ab],
+            a = fmaf(S.wc2[net][o * 32 + ci * 4 + ab],
                      S.c1[p][(2 * (pos >> 1) + (ab >> 1)) * 4 + 2 * (pos & 1) + (ab & 1)][net * kXH + ci], a);
         S.c2[p][pos][net * kXH + o] = relu(a);
       }
@@ -368,7 +382,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
       for (int ci = 0; ci < kXH; ++ci)
 #pragma unroll
-        for (int ab = 0; ab < 4; ++ab) a = fmaf(G[CondA::c4w + o * 32 + ci * 4 + ab], S.c2[p][ab][net * kXH + ci], a);
+        for (int ab = 0; ab < 4; ++ab) a = fmaf(S.wc4[net][o * 32 + ci * 4 + ab], S.c2[p][ab][net * kXH + ci], a);
       S.c3[p][net * kXH + o] = relu(a);
     }
     __syncthreads();
@@ -395,10 +409,8 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     for (int idx = q; idx < 2 * kC + kC * kC; idx += 16) {  // last layer + tanh: A (24) then I (144)
       const bool isI = idx >= 2 * kC;
       const int n = isI ? idx - 2 * kC : idx;
-      const float *G = isI ? gI : gA;
-      const int lb = isI ? CondI::l4b : CondA::l4b;
       const float *W = isI ? S.w4I : S.w4A;
-      float a = G[lb + n];
+      float a = S.b4[idx];
 #pragma unroll
       for (int k = 0; k < kXS; ++k) a = fmaf(W[n * kXS + k], S.l1[p][(isI ? kXS : 0) + k], a);
       const float t = tanhf(a);
@@ -408,7 +420,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         S.an[p][n] = t;
     }
     __syncthreads();
-    CBT(2)
+    CBT(2);
     // actnorm, 1x1 conv at position q
     float yw[kC];
     {
@@ -489,7 +501,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       for (int ab = 0; ab < 4; ++ab)
 #pragma unroll
         for (int o = 0; o < 16; ++o) h[ab][o] = F[Aff::r0b + o];
-      for (int t = 0; t < 27; ++t) {
+      _Pragma("unroll 3") for (int t = 0; t < 27; ++t) {
         const int dr = t / 9, ds = (t / 3) % 3, c = t % 3;
         float v[4];
 #pragma unroll
@@ -525,7 +537,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
-    CBT(3)
+    CBT(3);
     float fin[kC];
     {  // conv3x3 (6 -> 6), ReLU
       float a[kCh];
@@ -550,7 +562,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int c = 0; c < kC; ++c) S.fin[p][q][c] = fin[c];
     __syncthreads();
-    CBT(4)
+    CBT(4);
     // f: Conv2dNormy(12 -> 8, 3x3) ReLU, Conv2dNormy(8 -> 8, 1x1) ReLU, Conv2dZerosy(8 -> 12) tanh
     float g1[kYH], g2[kYH], u[kC], h[kC];
     {
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
-    CBT(5)
+    CBT(5);
     {  // f4w: dW[o][n = (t9, c)] = sum_(p,q) D[p][q][o] g2[p][q + tap][c] (K = 256): column
        // tiles w, and 4 in wave 0
       auto job = [&](f4 &cc, int nt) {
@@ -719,7 +731,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kYH; ++o) S.D[p][q][o] = d2[o];
     __syncthreads();
-    CBT(6)
+    CBT(6);
     if (w == 1) {  // f2w: dW[o][c] = sum_(p,q) D[p][q][o] g1[p][q][c]
       const bool ok = lr < kYH;
       const int o = ok ? lr : 0;
@@ -821,7 +833,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
     for (int o = 0; o < kCh; ++o) S.D[p][q][o] = d4[o];
     __syncthreads();
-    CBT(7)
+    CBT(7);
     {  // r4w: dW[o][n = (t9, c)] = sum D[p][q][o] r2[p][q + tap][c]: column tile w (54 columns)
       const int n = w * 16 + lr, t9 = n / kCh, ch = n % kCh, dr = t9 / 3 - 1, ds = t9 % 3 - 1;
       const bool nok = n < 9 * kCh, mok = lr < kCh;
@@ -866,7 +878,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       if (q == 0) S.sm[p][24 + o] = a;
     }
     __syncthreads();  // D (r4), g1 / g2 (aliased by R1) no longer read; sm complete
-    CBT(8)
+    CBT(8);
     contract<kOffF + Aff::r2b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.sm[pp][24 + j];
@@ -874,87 +886,122 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     });
 #pragma unroll
     for (int o = 0; o < kCh; ++o) S.D[p][q][o] = dr2[o];
-    // four rounds of one wave's particles: r1 recomputed (ReLU outputs) at the wave's 2x2 blocks
-    // -> r2w; then d r1 in its place -> r0w and dL/dx
+    // Four rounds of four particles (the resize stage's 8x8 grids do not fit LDS for the whole
+    // tile).  In round rw every wave works on particles 4 rw + l / 16 (lane l of the wave) at
+    // block q = l % 16, wave w on the channel group 4w .. 4w + 3: r1 recomputed (ReLU outputs)
+    // and staged -> r2w (MFMA); d r1 in its place -> r0w (MFMA) and dL/dx (wave w: the block's
+    // position w).
     for (int rw = 0; rw < 4; ++rw) {
-      float r1[4][16];
-      if (w == rw) {
-        resize1(r1);
+      const int p4 = (tid & 63) >> 4, pp = 4 * rw + p4;
+      float hv[4][4];  // [ab][c4]: channel 4 w + c4
 #pragma unroll
-        for (int ab = 0; ab < 4; ++ab)
+      for (int ab = 0; ab < 4; ++ab)
 #pragma unroll
-          for (int c = 0; c < 16; ++c) S.R1[p & 3][q][ab][c] = r1[ab][c];
+        for (int c4 = 0; c4 < 4; ++c4) hv[ab][c4] = F[Aff::r0b + 4 * w + c4];
+      _Pragma("unroll 3") for (int t = 0; t < 27; ++t) {
+        const int dr = t / 9, ds = (t / 3) % 3, c = t % 3;
+        float v[4];
+#pragma unroll
+        for (int ab = 0; ab < 4; ++ab) {
+          const int r = 2 * qi + (ab >> 1) + dr - 1, s8 = 2 * qj + (ab & 1) + ds - 1;
+          const bool in = r >= 0 && r < 8 && s8 >= 0 && s8 < 8;
+          const float xv = S.X[pp][in ? c * 64 + r * 8 + s8 : 0];
+          v[ab] = in ? xv : 0.f;
+        }
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const float wt = F[Aff::r0w + t * 16 + 4 * w + c4];
+#pragma unroll
+          for (int ab = 0; ab < 4; ++ab) hv[ab][c4] = fmaf(wt, v[ab], hv[ab][c4]);
+        }
+      }
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        f4 v;
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) v[c4] = relu(hv[ab][c4]);
+        *reinterpret_cast<f4 *>(&S.R1[p4][q][ab][4 * w]) = v;
       }
       __syncthreads();
+      if (rw == 0) CBT(13);
       {  // r2w: dW[o][n = (ab, c)] = sum_(p4,q) D[4 rw + p4][q][o] r1[p4][q][ab][c]: tile ab = w
         const bool mok = lr < kCh;
         const int orow = mok ? lr : 0;
 #pragma unroll 4
         for (int s2 = 0; s2 < 16; ++s2) {
-          const int k = 4 * s2 + lk, p4 = k >> 4, q2 = k & 15;
-          const float av = S.D[4 * rw + p4][q2][orow], bv = S.R1[p4][q2][w][lr];
+          const int k = 4 * s2 + lk, k4 = k >> 4, q2 = k & 15;
+          const float av = S.D[4 * rw + k4][q2][orow], bv = S.R1[k4][q2][w][lr];
           cR2 = mfma4(mok ? av : 0.f, bv, cR2);
         }
       }
       __syncthreads();
-      if (w == rw) {  // d r1 (in r1's registers), its per-particle sums (r0b)
+      if (rw == 0) CBT(14);
+      {  // d r1 of this lane's entries (read, then overwritten in place), per-particle sums (r0b)
+        float dd[kCh];
 #pragma unroll
-        for (int ab = 0; ab < 4; ++ab)
+        for (int o = 0; o < kCh; ++o) dd[o] = S.D[pp][q][o];
+        float sum4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < 16; ++c) {
+        for (int ab = 0; ab < 4; ++ab) {
+          f4 *slot = reinterpret_cast<f4 *>(&S.R1[p4][q][ab][4 * w]);
+          const f4 rv = *slot;
+          f4 dv;
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
             float a = 0.f;
 #pragma unroll
-            for (int o = 0; o < kCh; ++o) a = fmaf(F[Aff::r2w + (ab * 16 + c) * kCh + o], dr2[o], a);
-            r1[ab][c] = r1[ab][c] > 0.f ? a : 0.f;
-            S.R1[p & 3][q][ab][c] = r1[ab][c];
+            for (int o = 0; o < kCh; ++o) a = fmaf(F[Aff::r2w + (ab * 16 + 4 * w + c4) * kCh + o], dd[o], a);
+            dv[c4] = rv[c4] > 0.f ? a : 0.f;
+            sum4[c4] += dv[c4];
           }
+          *slot = dv;
+        }
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const float s1 = row16_sum((r1[0][c] + r1[1][c]) + (r1[2][c] + r1[3][c]));
-          if (q == 0) S.sm[p][32 + c] = s1;
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const float s1 = row16_sum(sum4[c4]);
+          if (q == 0) S.sm[pp][32 + 4 * w + c4] = s1;
         }
       }
       __syncthreads();
+      if (rw == 0) CBT(15);
       {  // r0w: dW[o][t] = sum_(p4, 8x8 pos) d1[p4][pos][o] x[p4][c][pos + tap]; wave w: column
          // tile w & 1, particles 2 (w >> 1) .. +1 of the round (the halves are added at the end)
         const int n = (w & 1) * 16 + lr, dr = n / 9 - 1, ds = (n / 3) % 3 - 1, c = n % 3;
         const bool nok = n < 27;
 #pragma unroll 4
         for (int s2 = 0; s2 < 32; ++s2) {
-          const int k = 4 * s2 + lk, p4 = 2 * (w >> 1) + (k >> 6), pos = k & 63, r = pos >> 3, s8 = pos & 7;
+          const int k = 4 * s2 + lk, k4 = 2 * (w >> 1) + (k >> 6), pos = k & 63, r = pos >> 3, s8 = pos & 7;
           const int rr = r + dr, ss = s8 + ds;
           const bool ok = nok && rr >= 0 && rr < 8 && ss >= 0 && ss < 8;
-          const float bv = S.X[4 * rw + p4][ok ? c * 64 + rr * 8 + ss : 0];
-          const float av = S.R1[p4][(r >> 1) * 4 + (s8 >> 1)][(r & 1) * 2 + (s8 & 1)][lr];
+          const float bv = S.X[4 * rw + k4][ok ? c * 64 + rr * 8 + ss : 0];
+          const float av = S.R1[k4][(r >> 1) * 4 + (s8 >> 1)][(r & 1) * 2 + (s8 & 1)][lr];
           cR0 = mfma4(av, ok ? bv : 0.f, cR0);
         }
       }
-      if (w == rw) {  // dL/dx from resize conv1 at this lane's 2x2 block, 3 channels
-        _Pragma("unroll 1") for (int ab = 0; ab < 4; ++ab) {
-          const int r = 2 * qi + (ab >> 1), s = 2 * qj + (ab & 1);
-          float a[3] = {};
-          _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
-            const int ro = r - (t9 / 3 - 1), so = s - (t9 % 3 - 1);  // output reading (r, s) by tap t9
-            if (ro < 0 || ro >= 8 || so < 0 || so >= 8) continue;
-            const f4 *dd4 = reinterpret_cast<const f4 *>(S.R1[p & 3][(ro >> 1) * 4 + (so >> 1)][(ro & 1) * 2 + (so & 1)]);
-            float dd[16];
+      {  // dL/dx from resize conv1 at position w of this lane's 2x2 block, 3 channels
+        const int r = 2 * qi + (w >> 1), s8 = 2 * qj + (w & 1);
+        float a[3] = {0.f, 0.f, 0.f};
+        _Pragma("unroll 1") for (int t9 = 0; t9 < 9; ++t9) {
+          const int ro = r - (t9 / 3 - 1), so = s8 - (t9 % 3 - 1);  // output reading (r, s) by tap t9
+          if (ro < 0 || ro >= 8 || so < 0 || so >= 8) continue;
+          const f4 *dd4 = reinterpret_cast<const f4 *>(S.R1[p4][(ro >> 1) * 4 + (so >> 1)][(ro & 1) * 2 + (so & 1)]);
+          float dd[16];
 #pragma unroll
-            for (int o4 = 0; o4 < 4; ++o4) {
-              const f4 v = dd4[o4];
+          for (int o4 = 0; o4 < 4; ++o4) {
+            const f4 v = dd4[o4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) dd[4 * o4 + e] = v[e];
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-#pragma unroll
-              for (int o = 0; o < 16; ++o) a[c] = fmaf(F[Aff::r0w + ((t9 * 3) + c) * 16 + o], dd[o], a[c]);
+            for (int e = 0; e < 4; ++e) dd[4 * o4 + e] = v[e];
           }
 #pragma unroll
-          for (int c = 0; c < 3; ++c) S.gX[p][c * 64 + r * 8 + s] += a[c];
+          for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int o = 0; o < 16; ++o) a[c] = fmaf(F[Aff::r0w + ((t9 * 3) + c) * 16 + o], dd[o], a[c]);
         }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) S.gX[pp][c * 64 + r * 8 + s8] += a[c];
       }
       __syncthreads();
-      CBT(9)
+      CBT(9);
     }
     contract<kOffF + Aff::r0b>(acc, [&](int j) {
       float a = 0.f;
@@ -1001,7 +1048,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
-    CBT(10)
+    CBT(10);
     // ---------------- conditioning nets backward (A: actnorm, I: 1x1 conv) ----------------
     for (int idx = q; idx < 2 * kC + kC * kC; idx += 16) {  // through the tanh
       const bool isI = idx >= 2 * kC;
@@ -1136,12 +1183,11 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     }
     {  // dL/dc2: lane q = (net, ci), the four positions
       const int net = q >> 3, ci = q & 7;
-      const float *G = net ? gI : gA;
 #pragma unroll
       for (int ab = 0; ab < 4; ++ab) {
         float a = 0.f;
 #pragma unroll
-        for (int o = 0; o < kXH; ++o) a = fmaf(G[CondA::c4w + o * 32 + ci * 4 + ab], Gp[64 + net * kXH + o], a);
+        for (int o = 0; o < kXH; ++o) a = fmaf(S.wc4[net][o * 32 + ci * 4 + ab], Gp[64 + net * kXH + o], a);
         Gp[80 + ab * 16 + net * kXH + ci] = S.c2[p][ab][net * kXH + ci] > 0.f ? a : 0.f;
       }
     }
@@ -1175,12 +1221,11 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       const int pos = (qi >> 1) * 2 + (qj >> 1), ab = (qi & 1) * 2 + (qj & 1);
 #pragma unroll
       for (int net = 0; net < 2; ++net) {
-        const float *G = net ? gI : gA;
 #pragma unroll
         for (int ci = 0; ci < kXH; ++ci) {
           float a = 0.f;
 #pragma unroll
-          for (int o = 0; o < kXH; ++o) a = fmaf(G[CondA::c2w + o * 32 + ci * 4 + ab], Gp[80 + pos * 16 + net * kXH + o], a);
+          for (int o = 0; o < kXH; ++o) a = fmaf(S.wc2[net][o * 32 + ci * 4 + ab], Gp[80 + pos * 16 + net * kXH + o], a);
           S.G1c[p][q][net * kXH + ci] = S.c1[p][q][net * kXH + ci] > 0.f ? a : 0.f;
         }
       }
@@ -1223,7 +1268,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       S.gX[p][ci * 64 + (2 * qi + a2) * 8 + 2 * qj + b2] += a;
     }
     __syncthreads();
-    CBT(11)
+    CBT(11);
     // ---------------- the condition's gradient: out, or through the particle encoder ----------------
     if (!PART) {
       if (valid)
@@ -1309,7 +1354,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
-    CBT(12)
+    CBT(12);
   }
   // this workgroup's parameter-gradient row
   float *row = partial + (int64_t)blockIdx.x * kTotParams;

@@ -40,3 +40,8 @@ tot = (tr[:, 12] - tr[:, 0]) / 100.0
 print(f"workgroups {len(tr)}, tile total med {np.median(tot):.2f} us")
 for k, n in enumerate(names):
     print(f"  {n:18s} med {np.median(d[:, k]):8.2f} us  max {np.max(d[:, k]):8.2f}")
+full = buf.astype(np.int64)[ok]
+if (full[:, 13] > 0).all():  # round 0 of the resize stage: r1 staged, r2w, d r1 staged
+    sub = [full[:, 8], full[:, 13], full[:, 14], full[:, 15]]
+    for a, b, n in zip(sub[:-1], sub[1:], ["round0 r1 + stage", "round0 r2w", "round0 d r1 + stage"]):
+        print(f"  {n:18s} med {np.median((b - a) / 100.0):8.2f} us")
