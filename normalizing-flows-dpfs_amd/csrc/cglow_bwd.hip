@@ -44,7 +44,7 @@ struct LayerDef {
   {O + C::c0w, C::c0b - C::c0w, true}, {O + C::c0b, C::c2w - C::c0b}, {O + C::c2w, C::c2b - C::c2w, true}, \
       {O + C::c2b, C::c4w - C::c2b}, {O + C::c4w, C::c4b - C::c4w}, {O + C::c4b, C::l0w - C::c4b}, \
       {O + C::l0w, C::l0b - C::l0w}, {O + C::l0b, C::l2w - C::l0b}, {O + C::l2w, C::l2b - C::l2w}, \
-      {O + C::l2b, C::l4w - C::l2b}, {O + C::l4w, C::l4b - C::l4w}, {O + C::l4b, C::size - C::l4b}
+      {O + C::l2b, C::l4w - C::l2b}, {O + C::l4w, C::l4b - C::l4w, true}, {O + C::l4b, C::size - C::l4b}
 constexpr LayerDef kLayers[] = {
     COND_LAYERS(kOffA, CondA),
     COND_LAYERS(kOffI, CondI),
@@ -190,7 +190,7 @@ struct BLds {
 static_assert(sizeof(BLds) <= 160 * 1024, "cglow_bwd: LDS above 160 KB");
 
 #ifdef NFDPF_EXP_CBTRACE  // experiment: per-phase timestamps of one tile per workgroup
-__device__ uint64_t g_cbtrace[256][16];
+__device__ uint64_t g_cbtrace[256][24];
 #define CBT(k)                                                                        \
   do {                                                                                \
     if (cbt_on && threadIdx.x == 0) g_cbtrace[blockIdx.x & 255][k] = __builtin_amdgcn_s_memrealtime(); \
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
   // this wave's MFMA jobs (column tiles of the mf layers), persistent across tiles
   const int lr = tid & 15, lk = (tid >> 4) & 3;  // MFMA lane: row / column l % 16, k offset l / 16
   f4 cF4a = {}, cF4b = {}, cF0a = {}, cF0b = {}, cR4 = {}, cR2 = {}, cR0 = {}, cF2 = {}, cC0 = {}, cC2 = {};
-  f4 cW3[6] = {};
+  f4 cW3[6] = {}, cL4[3] = {};
   // per-channel scales of f (Conv2dNormy exp(logs), Conv2dZerosy exp(3 logs)) and the
   // conditioning nets' last layers, once per workgroup (ordered by the tile's first barrier)
   {
@@ -443,6 +443,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
         yw[o] = a;
       }
     }
+    CBT(16);
     // W^-1: Gauss-Jordan with partial pivoting, lane q < 12 holding row q of [W | I]
     {
       float a[2 * kC];
@@ -494,6 +495,7 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < kC; ++j) S.wi[p][mycol * kC + j] = a[kC + j];
     }
+    CBT(17);
     // resize_x: conv3x3 (3 -> 16) at this position's 2x2 block of the 8x8 grid, ReLU, conv 2x2/2
     // (16 -> 6), ReLU
     auto resize1 = [&](float (&h)[4][16]) {
@@ -1062,21 +1064,25 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
       }
     }
     __syncthreads();
-    contract<kOffA + CondA::l4w>(acc, [&](int j) {
-      const int n = j / kXS, k = j % kXS;
-      float a = 0.f;
-      _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a = fmaf(S.gan[pp][n], S.l1[pp][k], a);
-      return a;
-    });
+    // last layers: dW[n][k] = sum_p g[p][n] l1[p][k] (K = 16 particles) on MFMA: row tiles
+    // A 0-1, I 0-8 as jobs w, w + 4, w + 8 (< 11)
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const int job = w + 4 * jj;
+      if (job >= 11) break;
+      const bool isI = job >= 2;
+      const int n = (isI ? job - 2 : job) * 16 + lr, nout = isI ? kC * kC : 2 * kC;
+      const bool ok = n < nout;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int k = 4 * s2 + lk;
+        const float av = isI ? S.gw[k][ok ? n : 0] : S.gan[k][ok ? n : 0];
+        cL4[jj] = mfma4(ok ? av : 0.f, S.l1[k][(isI ? kXS : 0) + lr], cL4[jj]);
+      }
+    }
     contract<kOffA + CondA::l4b>(acc, [&](int j) {
       float a = 0.f;
       _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a += S.gan[pp][j];
-      return a;
-    });
-    contract<kOffI + CondI::l4w>(acc, [&](int j) {
-      const int n = j / kXS, k = j % kXS;
-      float a = 0.f;
-      _Pragma("unroll 1") for (int pp = 0; pp < kTP; ++pp) a = fmaf(S.gw[pp][n], S.l1[pp][kXS + k], a);
       return a;
     });
     contract<kOffI + CondI::l4b>(acc, [&](int j) {
@@ -1373,6 +1379,17 @@ __global__ __launch_bounds__(kThreads, 1) void cglow_bwd_kernel(
     const int net = w >> 1;
     store_tile(cC2, row, kXH, (w & 1) * 16, 32,
                [net](int m, int n) { return (net ? kOffI : kOffA) + CondA::c2w + m * 32 + n; });
+  }
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) {
+    const int job = w + 4 * jj;
+    if (job < 11) {
+      const bool isI = job >= 2;
+      const int m0 = (isI ? job - 2 : job) * 16;
+      const int rows = min(16, (isI ? kC * kC : 2 * kC) - m0);
+      store_tile(cL4[jj], row, rows, 0, kXS,
+                 [=](int m, int n) { return (isI ? kOffI + CondI::l4w : kOffA + CondA::l4w) + (m0 + m) * kXS + n; });
+    }
   }
   if (PART)
 #pragma unroll

@@ -28,7 +28,7 @@ g = torch.randn(B, N, device=dev)
 for _ in range(2):
     ops.cglow_measurement_backward(peb, glb, enc, x, g)
 torch.cuda.synchronize()
-buf = np.zeros((256, 16), dtype=np.uint64)
+buf = np.zeros((256, 24), dtype=np.uint64)
 assert _lib.lib().nfdpf_exp_cbtrace_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 tr = buf.astype(np.int64)[:, :13]
 ok = (tr[:, 0] > 0) & (tr[:, 12] > 0)
@@ -44,4 +44,8 @@ full = buf.astype(np.int64)[ok]
 if (full[:, 13] > 0).all():  # round 0 of the resize stage: r1 staged, r2w, d r1 staged
     sub = [full[:, 8], full[:, 13], full[:, 14], full[:, 15]]
     for a, b, n in zip(sub[:-1], sub[1:], ["round0 r1 + stage", "round0 r2w", "round0 d r1 + stage"]):
+        print(f"  {n:18s} med {np.median((b - a) / 100.0):8.2f} us")
+if (full[:, 16] > 0).all():  # inside the actnorm / 1x1 / GJ phase
+    sub = [full[:, 2], full[:, 16], full[:, 17], full[:, 3]]
+    for a, b, n in zip(sub[:-1], sub[1:], ["actnorm + 1x1", "Gauss-Jordan", "resize1 + conv2"]):
         print(f"  {n:18s} med {np.median((b - a) / 100.0):8.2f} us")
