@@ -5,7 +5,13 @@
 namespace nfdpf {
 
 constexpr int kSoftMaxN = 16384;  // C[] lives in LDS (64 KiB)
+constexpr size_t kSoftStageLds = 156 * 1024;  // C, p and the gathered weights in LDS: N <= 13 312
 
+// STAGE: the row's p and the gathered weights live in LDS next to C (3 N floats), so the two
+// cascade sums (one wave each, ~N / 32 dependent adds per lane) and the scan read LDS instead
+// of global memory (round 3: C5 112 us per call with every cascade term a global load).  The
+// arithmetic is the same either way (bit-identical, tests/test_gpu_backward.py / parity).
+template <bool STAGE>
 __global__ __launch_bounds__(1024) void soft_resample_kernel(
     const float *__restrict__ x, const float *__restrict__ p, const float *__restrict__ lin,
     const float *__restrict__ offsets, int B, int N, int D, float alpha, int64_t row_base,
@@ -13,9 +19,16 @@ __global__ __launch_bounds__(1024) void soft_resample_kernel(
   extern __shared__ float C[];
   __shared__ double shd[16];
   __shared__ float shf[2];
+  float *P = C + N, *Wg = C + 2 * N;
   const int b = blockIdx.x;
   const int64_t rowN = (int64_t)b * N;
-  SoftRow row{p + rowN, N, alpha, 1.0f / (float)N, (float)(1.0 - (double)alpha), 1.0f};
+  const float *prow = p + rowN;
+  if (STAGE) {
+    for (int j = threadIdx.x; j < N; j += blockDim.x) P[j] = prow[j];
+    __syncthreads();
+    prow = P;
+  }
+  SoftRow row{prow, N, alpha, 1.0f / (float)N, (float)(1.0 - (double)alpha), 1.0f};
   const int64_t flat_base = (int64_t)N * (row_base + b);
   soft_row_search(row, lin, offsets[b], C, shd, shf, [&](int i, int src) {
     // the reference gathers from the flattened batch: src == N reads the next row (:52-55)
@@ -24,18 +37,21 @@ __global__ __launch_bounds__(1024) void soft_resample_kernel(
     const int gj = (int)(g - gb * N);
     for (int k = 0; k < D; ++k) x_out[(rowN + i) * D + k] = x[g * D + k];
     const float wsrc = (gb == b) ? row.w(gj) : 0.0f;  // other-row weights: see DESIGN.md
-    w_out[rowN + i] = wsrc;
+    if (STAGE)
+      Wg[i] = wsrc;
+    else
+      w_out[rowN + i] = wsrc;
     idx_out[rowN + i] = flat_base + src;
   });
   __syncthreads();
+  const float *wr = STAGE ? Wg : w_out + rowN;
   if (threadIdx.x < 64) {
-    const float *wr = w_out + rowN;
     const float S2 = cascade_row_sum([&](int j) { return wr[j]; }, N);
     if (threadIdx.x == 0) shf[1] = S2;
   }
   __syncthreads();
   const float S2 = shf[1];
-  for (int i = threadIdx.x; i < N; i += blockDim.x) w_out[rowN + i] = w_out[rowN + i] / S2;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) w_out[rowN + i] = wr[i] / S2;
 }
 
 // p = exp(lw - max) / sum + add ; inv_ess = 1 / sum(p^2)
@@ -76,8 +92,20 @@ extern "C" int nfdpf_soft_resample(const float *x, const float *p, const float *
                 kSoftMaxN);
   NFDPF_REQUIRE(alpha > 0.f && alpha <= 1.f, "nfdpf_soft_resample: need 0 < alpha <= 1");
   if (B == 0) return NFDPF_OK;
-  soft_resample_kernel<<<B, row_threads(N), N * sizeof(float), as_stream(stream)>>>(
-      x, p, lin, offsets, B, N, D, alpha, row_base, x_out, w_out, idx_out);
+  const size_t stage_lds = 3 * (size_t)N * sizeof(float);
+  if (stage_lds <= kSoftStageLds) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void *)soft_resample_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kSoftStageLds);
+      attr = true;
+    }
+    soft_resample_kernel<true><<<B, row_threads(N), stage_lds, as_stream(stream)>>>(
+        x, p, lin, offsets, B, N, D, alpha, row_base, x_out, w_out, idx_out);
+  } else {
+    soft_resample_kernel<false><<<B, row_threads(N), N * sizeof(float), as_stream(stream)>>>(
+        x, p, lin, offsets, B, N, D, alpha, row_base, x_out, w_out, idx_out);
+  }
   return launch_status("nfdpf_soft_resample");
 }
 
