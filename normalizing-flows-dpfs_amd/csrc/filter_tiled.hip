@@ -836,9 +836,16 @@ __device__ __forceinline__ void fdyn_part(const nfdpf_filter_desc &d, const Tile
         // rows < 64 from the registers loaded at the launch's start (the row normaliser of this
         // workgroup's own row too: no second round trip)
         if (pre_ok && r == (int)threadIdx.x) {
+          // every lane evaluates its row's normaliser beside its 1 / sum p^2 (two independent
+          // chains the compiler interleaves) and the lane of this workgroup's row keeps it --
+          // instead of one lane's normaliser run after the batch's ESS terms, a divergent tail
+          // on the gate wave's critical path (same arithmetic: bit-identical)
           const auto sm = [&](int k) { return pre[k]; };
-          Cbuf[r] = row_inv_ess_t<kPreT>(sm, tiles, N, d.t > 0);
-          if (defer && r == my_row) rn_sh = row_norm_t<kPreT>(sm, tiles, shifted);
+          const float ie = row_inv_ess_t<kPreT>(sm, tiles, N, d.t > 0);
+          RowNorm rn_lane{0.f, 1.f, 0.f};
+          if (defer) rn_lane = row_norm_t<kPreT>(sm, tiles, shifted);
+          Cbuf[r] = ie;
+          if (defer && r == my_row) rn_sh = rn_lane;
         } else {
           const double *sm = parts + (int64_t)r * tiles * kSm;
           Cbuf[r] = row_inv_ess(sm, tiles, N, d.t > 0);
