@@ -1428,14 +1428,14 @@ __global__ __launch_bounds__(256) void cglow_param_reduce_kernel(const float *__
     g_pe[j - kStep] = a;
 }
 
+// One resident workgroup per CU (160 KB of LDS each), persistent over tiles.  A fixed cap (the
+// MI355X's 256 CUs), not the current device's CU count: the workspace the caller sized with
+// nfdpf_cglow_backward_workspace holds exactly this many partial rows, whichever device is
+// current at either call.
+constexpr int kBwdGrid = 256;
 static int bwd_grid(int64_t M) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
-  }
   const int64_t tiles = (M + kTP - 1) / kTP;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cus));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, kBwdGrid));
 }
 
 template <bool PART>
