@@ -185,8 +185,11 @@ def ot_iteration_ms(res, T):
         out[k] = best
     it = (out[20] - out[10]) / 10.0
     # ranks rehearsed on ONE shared GPU time each other's launches too; a difference the other
-    # rank's work swamped falls back to the 20-iteration call's share (an upper bound)
-    return it if it > 0 else out[20] / 20.0
+    # rank's work swamped falls back to the 20-iteration call's share, which includes the
+    # per-call fixed passes (an upper bound: flagged in the record, and no roofline from it)
+    if it > 0:
+        return it, False
+    return out[20] / 20.0, True
 
 
 def soft_resample_ms(res, T, reps=20):
@@ -397,7 +400,11 @@ def main():
         kname = "cglow_kernel"
     F_EX = F_EXEC.get(args.config, F_ALG) if kname.startswith("tiled_prop") else F_ALG
     bound = "mfma" if kname == "cglow_kernel" else "valu"
-    if args.kernel == "tiled" and eng.last_fused:  # the whole step in one launch: all of its FLOP
+    if args.kernel == "tiled" and eng.last_pass:  # the whole pass in one launch: every step's FLOP
+        kname, F_ALG = "tiled_pass_kernel", F_STEP
+        F_EX = F_EXEC_STEP.get(args.config, F_ALG)
+        launch_units, launch_bytes = B * N * T, B_ALG * B * N * T
+    elif args.kernel == "tiled" and eng.last_fused:  # the whole step in one launch: all of its FLOP
         kname, F_ALG = "tiled_step_fused_kernel", F_STEP
         F_EX = F_EXEC_STEP.get(args.config, F_ALG)
     elif front_ms is not None and front_ms > kernel_ms:
@@ -409,10 +416,10 @@ def main():
         else:  # gate + soft resampling + motion: bytes, not FLOP
             kname, F_ALG, F_EX, bound = "tiled_front_kernel", 0.0, 0.0, "hbm"
             launch_bytes = (B_SOFT + 8.0 + 8.0) * B * N  # resampling + motion's noise / x' writes
-    ot_iter_ms = None
+    ot_iter_ms, ot_iter_upper = None, False
     if flags["resampler_type"] == "ot" and eng.last_ot_calls:
-        ot_iter_ms = ot_iteration_ms(res, T)
-        if ot_iter_ms * eng.last_ot_calls * 10 > kernel_ms * T:  # the Sinkhorn loop dominates
+        ot_iter_ms, ot_iter_upper = ot_iteration_ms(res, T)
+        if not ot_iter_upper and ot_iter_ms * eng.last_ot_calls * 10 > kernel_ms * T:  # the Sinkhorn loop dominates
             kname, kernel_ms, bound = "ot_iter_kernel", ot_iter_ms, "valu"
             F_ALG, launch_units = F_OT_PAIR, B * N * N
             F_EX = F_ALG
@@ -458,14 +465,19 @@ def main():
                     "peak_GBs": PEAK_HBM_GBS, "frac": rs_gbs / PEAK_HBM_GBS,
                     "particles_per_s": B * N / (rs_ms * 1e-3)}
     else:
-        it_ms = ot_iter_ms if ot_iter_ms is not None else ot_iteration_ms(res, T)
+        if ot_iter_ms is None:
+            ot_iter_ms, ot_iter_upper = ot_iteration_ms(res, T)
+        it_ms = ot_iter_ms
         call10 = ot_call_ms(res, T, 10)
         tf = F_OT_PAIR * B * N * N / (it_ms * 1e-3) / 1e12
         resample = {"kernel": "ot_iter_kernel (one Sinkhorn iteration)", "avg_ms": it_ms, "bound": "valu",
                     "flop_per_pair": F_OT_PAIR, "pairs_per_launch": B * N * N, "achieved_TFLOPs": tf,
                     "peak_TFLOPs": PEAK_FP32_TFLOPS, "frac": tf / PEAK_FP32_TFLOPS,
-                    "call_ms_at_10_iterations": call10, "fixed_ms_per_call": call10 - 10 * it_ms,
-                    "calls_in_last_pass": eng.last_ot_calls}
+                    "call_ms_at_10_iterations": call10,
+                    "fixed_ms_per_call": None if ot_iter_upper else call10 - 10 * it_ms,
+                    "ot_iter_ms_is_upper_bound": ot_iter_upper, "calls_in_last_pass": eng.last_ot_calls}
+        if ot_iter_upper:  # the 10 / 20-iteration difference was swamped: no rate from an upper bound
+            resample["achieved_TFLOPs"] = resample["frac"] = None
     if front_ms is not None:
         resample["front_launch_ms"] = front_ms  # the step's gate + resampling + motion launch, live
 

@@ -420,6 +420,26 @@ NFDPF_API int nfdpf_filter_tiled_fused(const nfdpf_filter_desc *d);
 /* sizeof(nfdpf_filter_desc) as this library was built: a binding checks its mirror of the
  * struct against it (nfdpf._lib does, at load).  No reference counterpart: a query. */
 NFDPF_API int64_t nfdpf_filter_desc_size(void);
+/* The WHOLE T-step pass (DPFs.py:160-214, all of filtering_pos's loop) as one persistent launch,
+ * for a pass whose every ESS gate is taken as off (the speculative-gate mode: the caller verifies
+ * the T gates afterwards with nfdpf_ess_gate_tiled_batch over ess_out, and reruns the pass step
+ * by step with nfdpf_filter_step_tiled if one fired).  Replaces the T iterations of
+ * nfdpf_filter_step_tiled (+ the last normalisation and the pred / lw_sum reduction) for the
+ * configuration nfdpf_filter_pass_supported accepts: split RealNVP nf_dyn, NF_cond, the cosine
+ * measurement, device RNG, N <= 1024, n_flows <= 2, not forced, and a (tiles, B) grid of
+ * 1024-thread workgroups that is resident on the current device all at once.
+ * Descriptor fields as nfdpf_filter_step_tiled at t = 0, except:
+ *   x_prev / p_prev: the initial particles / probabilities;  vel: [T][B][2], every step's velocity;
+ *   ess_out: [T][B][tiles][4], step t's softmax partials (the gates' input; the next step's
+ *   partials in include/nfdpf.h's tiled layout);  gate / ess_all / scratch / defer_norm: unused;
+ *   prof_events: optional hipEvent_t[2] riding in the pass launch's own dispatch.
+ * Every history slot, pred and lw_sum are written as after the T steps of the tiled path.
+ * workspace: nfdpf_filter_pass_workspace_bytes(B, N, T) bytes, 256-B aligned.  A wait between
+ * the row's workgroups that times out is counted in nfdpf_split_fault (the outputs are then
+ * invalid).  No reference counterpart for the query / workspace functions. */
+NFDPF_API int nfdpf_filter_pass_supported(const nfdpf_filter_desc *d);
+NFDPF_API int64_t nfdpf_filter_pass_workspace_bytes(int B, int N, int T);
+NFDPF_API int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);
 /* the t = 0 gate input from p0 [B,N] -> ess_parts [B][tiles][4] */
 NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
                             void *stream);

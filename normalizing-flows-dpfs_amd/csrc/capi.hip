@@ -1,6 +1,9 @@
 // capi.hip -- error plumbing and version of the C ABI (include/nfdpf.h).
 #include <cstdarg>
 #include <cstdio>
+#include <mutex>
+#include <set>
+#include <utility>
 
 #include "common.hpp"
 
@@ -22,6 +25,16 @@ int launch_status(const char *what) {
     return NFDPF_ELAUNCH;
   }
   return NFDPF_OK;
+}
+
+void ensure_max_dynamic_lds(const void *fn, int bytes) {
+  // per (kernel, current device): the attribute belongs to the device's module
+  static std::mutex mu;
+  static std::set<std::pair<const void *, int>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.insert({fn, dev}).second) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 }  // namespace nfdpf

@@ -1445,12 +1445,7 @@ static int launch_bwd(const float *pe, const float *glow, const float *enc, int6
   const int64_t M = (int64_t)B * N;
   const int grid = bwd_grid(M);
   const size_t lds = sizeof(BLds);
-  static bool attr = false;  // per kernel instantiation
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void *)cglow_bwd_kernel<PART>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
+  ensure_max_dynamic_lds((const void *)cglow_bwd_kernel<PART>, (int)lds);
   float *partial = (float *)ws;
   cglow_bwd_kernel<PART><<<grid, kThreads, lds, st>>>(pe, glow, enc, enc_rs, x, x_rs, B, N, g_up, gup_rs, g_z, g_y,
                                                       g_x, partial);

@@ -22,6 +22,8 @@ namespace nfdpf {
 // ----------------------------------------------------------------------------------------
 void set_error(const char *fmt, ...);
 int launch_status(const char *what);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, current device), thread-safe
+void ensure_max_dynamic_lds(const void *fn, int bytes);
 
 #define NFDPF_REQUIRE(cond, ...)            \
   do {                                      \

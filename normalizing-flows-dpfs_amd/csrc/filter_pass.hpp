@@ -1,0 +1,524 @@
+// filter_pass.hpp -- the whole T-step filtering pass of DPF.filtering_pos (DPFs.py:160-214) as
+// ONE persistent launch, for the C2-shaped path (--NF-dyn RealNVP on split nets, --NF-cond, the
+// cosine measurement, N <= 1024) when every ESS gate of the pass is taken as off (the
+// speculative-gate mode: nfdpf_ess_gate_tiled_batch verifies the T gates after the pass from the
+// per-step partials this launch leaves, and a fired gate reruns the pass step by step).
+// Included by filter_tiled.hip (same translation unit: it shares g_split_fault).
+//
+// Why: the two-launch step (tiled_fdyn_kernel + tiled_prop_quad_kernel) is a chain of
+// latency-bound phases whose every launch starts by re-reading what the previous launch left in
+// HBM (the row's particles, partials and folds, from other XCDs) -- 50 steps x 2 launches of
+// ~13 + 15 us.  Without resampling a particle never leaves its lane: its state stays in
+// registers for the whole pass, and a step needs only three ROW-LOCAL reductions, exchanged
+// between the row's workgroups inside the launch as 8-byte {32 data bits, tag} granules
+// (agent-scope sc1 stores / loads, MI355X_MICROARCH.md handoff-1to1, ~1 us each):
+//
+//   A  sum x, x^2 of x_phys after motion      -> nf_dyn context [mean, std]   (model/models.py:309-315)
+//   B  sum x, x^2 of x_dyn after nf_dyn^-1    -> proposal context            (model/models.py:338-346)
+//   C  softmax partials {max, sum e, sum e^2} -> slot t's normalisation      (DPFs.py:187-192, utils.py:39-44)
+//
+// Grid (tiles, B) of 1024-thread workgroups, one per CU, ALL resident (the host checks the grid
+// against the occupancy; a row's workgroups wait for each other).  Waves 0-7 ("flow": the t- and
+// s-nets of 4 particle groups on wave pairs, split.hpp) and waves 8-15 ("encoder": the cosine
+// measurement's particle encoder on f32 MFMA, 32 particles per wave) run two independent loops
+// over the steps and meet only through LDS flags (step-tagged, monotonic):
+//
+//   flow t:  motion -> publish A -> [wave 0: poll A, nf_dyn fold -> fA] -> nf_dyn inverse ->
+//            publish B -> [wave 0: poll B, + the encoder's encoding-column fold (fE) -> fB] ->
+//            proposal inverse -> qbuf (qf) -> nf_dyn forward + densities -> rbuf (rf)
+//   enc  t:  [wave 8: poll C(t-1) -> slot t-1's row normaliser (fR), its ESS partial] ->
+//            [wave 8: the proposal fold over step t's encoding columns -> fE] ->
+//            normalise slot t-1 (hp, the prediction / obs-likelihood partials) ->
+//            encoder on qbuf -> likelihood -> log-weight -> publish C(t)
+//
+// so the encoder of step t runs beside the flow waves' step t+1 (motion and nf_dyn inverse).
+// Every step-indexed buffer (LDS and granules) is double-buffered by step parity; the
+// dependency chains make a second reuse safe (a tile can publish exchange X of step t+2 only
+// after every tile of its row has consumed X of step t; C: an encoder poller signals fE(t)
+// only after consuming C(t-1), and no flow wave passes the proposal fold of step t without it).
+//
+// Every wait is bounded (kPassWaitTicks of wall time) and a timed-out wait raises g_pass_abort so the whole grid
+// drains promptly; the host reads g_split_fault (nfdpf_split_fault) and fails loudly.
+//
+// Reductions have a fixed order (deterministic): A / B = per role-0 flow wave DPP sums, the row
+// total over (tile, wave) in order -- the order of the three-launch tiled path (tiled_front_kernel
+// -> store_sums4, block_sum_roles_store -> tiled_ctx); the tile's softmax partial = the quad
+// launch's merge over encoder waves 8..15.
+
+namespace nfdpf {
+
+constexpr int kPassMaxTiles = 4;   // N <= 1024: one poll sweep of <= 192 granules per exchange
+constexpr int kPassMaxT = 4000;    // tag = (epoch << 12) + t + 1
+constexpr int kGA = 8;             // granules per flow-wave publish: 4 doubles
+constexpr int kGC = 6;             // per encoder-wave publish: max (f32), sum e, sum e^2 (f64), pad
+
+__device__ uint32_t g_pass_epoch = 0;
+__device__ int g_pass_abort = 0;
+
+struct PassWs {
+  uint64_t *ga;  // [2][B][tiles][4 role-0 flow waves][kGA]  exchange A (x_phys sums)
+  uint64_t *gb;  // [2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
+  uint64_t *gc;  // [2][B][tiles][8 encoder waves][kGC]      exchange C (softmax partials)
+  double *fin;   // [B][T][tiles * 8][4] per encoder wave: sum p^2, sum p x0, sum p x1, sum logw
+};
+
+static int64_t pass_bytes(int B, int N, int T) {
+  const int64_t bt = (int64_t)B * n_tiles(N);
+  return al256(2 * bt * 4 * kGA * 8) * 2 + al256(2 * bt * 8 * kGC * 8) + al256(bt * T * 8 * 32);
+}
+
+static PassWs pass_carve(void *ws, int B, int N, int T) {
+  char *p = (char *)ws;
+  const int64_t bt = (int64_t)B * n_tiles(N);
+  PassWs w;
+  w.ga = (uint64_t *)p;
+  p += al256(2 * bt * 4 * kGA * 8);
+  w.gb = (uint64_t *)p;
+  p += al256(2 * bt * 4 * kGA * 8);
+  w.gc = (uint64_t *)p;
+  p += al256(2 * bt * 8 * kGC * 8);
+  w.fin = (double *)p;
+  return w;
+}
+
+struct PassLds {
+  float xbuf[8 * kTile];           // flow-pair hand-offs (pair_swap; 8-byte aligned, first member)
+  float Hws[8][32 * kHPitch];      // each encoder wave's MFMA layer outputs
+  float qbuf[2][2 * kTile];        // the proposal, flow t-wave -> encoder pair, by step parity
+  float rbuf[2][2 * kTile];        // prior | propose, flow t-wave -> encoder pair
+  float encq[8][kE];               // each encoder wave's copy of the step's frame encoding
+  f2 cbd[2][kMaxFlows * 2 * kH];   // nf_dyn folded biases (split order), by step parity
+  f2 cbc[2][kMaxFlows * 2 * kH];   // proposal folded biases (split order)
+  float encfold[2][kMaxFlows * 4 * kH];  // proposal fold over the encoding columns (pair order)
+  uint32_t rowa[kPassMaxTiles * 4 * kGA];  // wave 0's A / B sweep
+  uint32_t rowc[kPassMaxTiles * 8 * kGC];  // wave 8's C sweep
+  RowNorm rn[2];                   // slot s's row normaliser, by parity of s
+  int xflag[16];
+  int fA, fB, fE, fR;              // step-tagged flags (see the header comment)
+  int qf[4], rf[4];
+};
+
+__device__ __forceinline__ void gran_store(uint64_t *g, uint32_t data, uint32_t tag) {
+  __hip_atomic_store(g, ((uint64_t)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A bounded spin: false once the wait has timed out (counted once, and the whole grid told to
+// drain through g_pass_abort) or another wave's has.  The bound is wall time (s_memrealtime,
+// 100 MHz): kPassWaitTicks from the wait's first miss, far above any legitimate wait (a step
+// takes ~20 us) and short enough that a grid that cannot make progress drains within a second.
+constexpr uint64_t kPassWaitTicks = 20000000ull;  // 200 ms
+struct Spin {
+  uint64_t t0 = 0;
+  int it = 0;
+};
+__device__ __forceinline__ bool pass_spin(Spin &s) {
+  if ((s.it++ & 63) == 0) {
+    if (__hip_atomic_load(&g_pass_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (s.it == 1) {
+      s.t0 = now;
+    } else if (now - s.t0 > kPassWaitTicks) {
+      if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_split_fault, 1);
+        __hip_atomic_store(&g_pass_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+  }
+  __builtin_amdgcn_s_sleep(1);
+  return true;
+}
+
+// wait until the LDS flag reaches v (wave-uniform)
+__device__ __forceinline__ void wait_flag(const int *f, int v) {
+  Spin s;
+  while (__builtin_amdgcn_readfirstlane(*(lds_vint *)f) < v && pass_spin(s)) {
+  }
+  asm volatile("" ::: "memory");
+}
+// publish an LDS flag after this wave's LDS data writes have landed
+__device__ __forceinline__ void set_flag(int *f, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  *(lds_vint *)f = v;
+}
+
+// four wave-uniform doubles as 8 granules (lanes 0..7: value l / 2, low / high word by l & 1)
+__device__ __forceinline__ void publish4(uint64_t *g, const double (&v)[4], uint32_t tag) {
+  const int l = threadIdx.x & 63;
+  if (l < 8) {
+    const int k = l >> 1;
+    const double x = k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+    const uint64_t bits = (uint64_t)__double_as_longlong(x);
+    gran_store(g + l, (l & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits, tag);
+  }
+}
+
+// one wave sweeps granules [0, n) of a row (n <= 192) until every tag is `tag`, leaving the
+// data words in dst (LDS); false on abort
+__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst) {
+  const int l = threadIdx.x & 63;
+  uint64_t v[3] = {0, 0, 0};
+  bool ok[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) ok[c] = 64 * c + l >= n;
+  Spin sp;
+  for (;;) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (!ok[c]) v[c] = __hip_atomic_load(g + 64 * c + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (!ok[c]) ok[c] = (uint32_t)(v[c] >> 32) == tag;
+    if (__all(ok[0] && ok[1] && ok[2])) break;
+    if (!pass_spin(sp)) return false;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    if (64 * c + l < n) dst[64 * c + l] = (uint32_t)v[c];
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return true;
+}
+
+__device__ __forceinline__ double lds_double(const uint32_t *w, int q) {
+  return __longlong_as_double((long long)(((uint64_t)w[q + 1] << 32) | w[q]));
+}
+
+// the row context from an A / B sweep: lanes c < 4 add component c over (tile, wave) in order
+// (block_sum_roles_store, then tiled_ctx), every lane gets the context
+__device__ __forceinline__ Ctx4 row_ctx(const uint32_t *rw, int tiles, int N) {
+  const int c = threadIdx.x & 3;
+  double a = 0.0;
+  for (int k = 0; k < tiles; ++k) {
+    double tk = lds_double(rw, (k * 4 + 0) * kGA + 2 * c);
+#pragma unroll
+    for (int g = 1; g < 4; ++g) tk += lds_double(rw, (k * 4 + g) * kGA + 2 * c);
+    a += tk;
+  }
+  return ctx_from_sums(readlane_d(a, 0), readlane_d(a, 1), readlane_d(a, 2), readlane_d(a, 3), N);
+}
+
+// the motion noise of step t (motion_noise's device-RNG branch with an explicit step)
+__device__ __forceinline__ void pass_noise(const nfdpf_filter_desc &d, int t, int64_t grow, int i, float &e0,
+                                           float &e1) {
+  const U4 r = rng_draw(d.seed, kTagMotion, (uint32_t)t, grow, (uint32_t)i);
+  box_muller(r.x, r.y, e0, e1);
+  e0 *= d.pos_noise;
+  e1 *= d.pos_noise;
+}
+
+// ---- waves 0-7 ------------------------------------------------------------------------------
+__device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                          uint32_t tag0) {
+  const int tiles = n_tiles(d.N), N = d.N, nfl = d.n_flows, ncb = nfl * 4 * kH;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int role = w & 1, g = w >> 1, slot = g * 64 + lane;
+  const int i = tile * kTile + slot;
+  const bool valid = i < N;
+  const bool grp = tile * kTile + g * 64 < N;  // the pair has particles
+  const int64_t grow = d.row_base + b;
+  PairX px = pair_of(L.xbuf, L.xflag, role, slot);
+  float x0 = 0.f, x1 = 0.f;
+  if (valid) {
+    x0 = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i];
+    x1 = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i + 1];
+  }
+  // wave 0 folds both contexts: the weights of the context columns, once per launch
+  const bool fold_lane = w == 0 && lane < ncb;
+  float fwd[1 + kOctxDyn] = {}, fwc[4] = {};
+  if (fold_lane) {
+    const FoldRef r = fold_ref(d.dyn_params, kNsDyn, lane);
+    fwd[0] = fold_bias0(r, kOctxDyn);
+#pragma unroll
+    for (int c = 0; c < kOctxDyn; ++c) fwd[1 + c] = r.w1c[2 * (r.j * kOctxDyn + c) + r.w];
+    const int O = d.E + 4;
+    const FoldRef rc = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + d.E + c) + rc.w];
+  }
+  const float *dbase = d.dyn_params + split_suffix_offset(nfl, kOctxDyn);
+  const float *cbase = d.cond_params + split_suffix_offset(nfl, d.E + 4);
+  const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
+  for (int t = 0; t < d.T; ++t) {
+    const int par = t & 1;
+    const uint32_t tag = tag0 + (uint32_t)t + 1u;
+    const RowSlot S = row_slot(d, b, t);
+    const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
+    // motion (model/models.py:191-204), no resampling: x_phys = (x + vel) + eps
+    float e0 = 0.f, e1 = 0.f, p0 = 0.f, p1 = 0.f;
+    if (valid) {
+      pass_noise(d, t, grow, i, e0, e1);
+      p0 = (x0 + v0) + e0;
+      p1 = (x1 + v1) + e1;
+      if (role == 0) {
+        S.hnoise[2 * i] = e0;
+        S.hnoise[2 * i + 1] = e1;
+        S.hidx[i] = (int64_t)N * grow + i;
+      }
+    }
+    const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 4 + g;
+    const int64_t grow0 = ((int64_t)par * d.B + b) * tiles * 4;
+    if (role == 0) {  // exchange A: this wave's sums of x_phys
+      double s[4] = {p0, p1, (double)p0 * p0, (double)p1 * p1};
+      wave_sum_dpp_n(s);
+      publish4(ws.ga + gslot * kGA, s, tag);
+    }
+    if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
+      if (poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
+        const Ctx4 c = row_ctx(L.rowa, tiles, N);
+        if (fold_lane) {
+          const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
+          float v = fwd[0];
+#pragma unroll
+          for (int q = 0; q < kOctxDyn; ++q) v = fmaf(fwd[1 + q], cv[q], v);
+          reinterpret_cast<float *>(L.cbd[par])[split_cb_index(lane)] = v;
+        }
+      }
+      set_flag(&L.fA, t + 1);
+    } else {
+      wait_flag(&L.fA, t + 1);
+    }
+    // nf_dyn inverse (model/models.py:305-332) on the wave pair
+    float xd0 = p0, xd1 = p1, ld = 0.f;
+    if (valid)
+      for (int f = nfl - 1; f >= 0; --f)
+        ld += coupling_inverse_split(dbase + f * kSplitFlow, xd0, xd1, L.cbd[par] + f * 16, px, kTile);
+    const float jac = -ld;
+    if (role == 0) {
+      if (valid && S.hjac) S.hjac[i] = jac;
+      double s[4] = {valid ? xd0 : 0.0, valid ? xd1 : 0.0, valid ? (double)xd0 * xd0 : 0.0,
+                     valid ? (double)xd1 * xd1 : 0.0};
+      wave_sum_dpp_n(s);
+      publish4(ws.gb + gslot * kGA, s, tag);  // exchange B
+    }
+    if (w == 0) {  // the proposal fold: encoding columns (from wave 8), then [mean, std] of x_dyn
+      if (poll_row(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
+        const Ctx4 c = row_ctx(L.rowa, tiles, N);
+        wait_flag(&L.fE, t + 1);
+        if (fold_lane) {
+          const float c4[4] = {c.m0, c.m1, c.s0, c.s1};
+          float a = L.encfold[par][lane];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a = fmaf(fwc[q], c4[q], a);
+          reinterpret_cast<float *>(L.cbc[par])[split_cb_index(lane)] = a;
+        }
+      }
+      set_flag(&L.fB, t + 1);
+    } else {
+      wait_flag(&L.fB, t + 1);
+    }
+    // NF proposal inverse (model/models.py:334-356)
+    float q0 = xd0, q1 = xd1, ldp = 0.f;
+    if (valid)
+      for (int f = nfl - 1; f >= 0; --f)
+        ldp += coupling_inverse_split(cbase + f * kSplitFlow, q0, q1, L.cbc[par] + f * 16, px, kTile);
+    if (role == 0) {  // the proposal to the encoder pair
+      if (valid) {
+        L.qbuf[par][slot] = q0;
+        L.qbuf[par][kTile + slot] = q1;
+      }
+      set_flag(&L.qf[g], t + 1);
+    }
+    // nf_dyn forward of the proposal + densities (model/models.py:358-377, stage_prior_split)
+    if (grp && valid) {
+      const float de = density(e0, e1, K, two_var);
+      const float r0 = p0 - e0, r1 = p1 - e1;
+      float lo = q0, up = q1, ld2 = 0.f;
+      for (int f = 0; f < nfl; ++f)
+        ld2 += coupling_forward_split(dbase + f * kSplitFlow, lo, up, L.cbd[par] + f * 16, px, kTile);
+      const float prior = density(lo - r0, up - r1, K, two_var) - (-ld2);
+      const float propose = (de + jac) + (-ldp);
+      if (role == 0) {
+        L.rbuf[par][slot] = prior;
+        L.rbuf[par][kTile + slot] = propose;
+        S.hx[2 * i] = q0;
+        S.hx[2 * i + 1] = q1;
+        if (S.hprior) S.hprior[i] = prior;
+      }
+    }
+    if (role == 0) set_flag(&L.rf[g], t + 1);
+    x0 = q0;
+    x1 = q1;
+  }
+}
+
+// ---- waves 8-15 -----------------------------------------------------------------------------
+// wave 8: sweep C(s) of the row, leave its tile's merged ESS partial (the quad launch's merge,
+// include/nfdpf.h) at ess_out[s] and the row normaliser of slot s (row_norm) in L.rn
+__device__ __forceinline__ void pass_poll_c(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                            uint32_t tag0, int s) {
+  const int tiles = n_tiles(d.N), lane = threadIdx.x & 63;
+  const int64_t row0 = (((int64_t)(s & 1) * d.B + b) * tiles) * 8;
+  if (poll_row(ws.gc + row0 * kGC, tiles * 8 * kGC, tag0 + (uint32_t)s + 1u, L.rowc)) {
+    // lane k < tiles: tile k's {max, sum e, sum e^2} over its encoder waves in order
+    const int k = lane < tiles ? lane : 0;
+    float m = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) m = fmaxf(m, __uint_as_float(L.rowc[(k * 8 + v) * kGC]));
+    double sum = 0.0, sq = 0.0;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const int q = (k * 8 + v) * kGC;
+      const float mv = __uint_as_float(L.rowc[q]);
+      if (mv > -INFINITY) {
+        const double f = (double)expf(mv - m);
+        sum += lds_double(L.rowc, q + 1) * f;
+        sq += lds_double(L.rowc, q + 3) * f * f;
+      }
+    }
+    if (lane == tile) {
+      double *sm = reinterpret_cast<double *>(d.ess_out) + (((int64_t)s * d.B + b) * tiles + tile) * kSm;
+      sm[0] = m;
+      sm[1] = sum;
+      sm[2] = sq;
+      sm[3] = 0.0;
+    }
+    // row_norm's arithmetic over the tiles in order (the cosine likelihood is not shifted)
+    float M = -INFINITY;
+    for (int kk = 0; kk < tiles; ++kk) M = fmaxf(M, (float)(double)readlane_f(m, kk));
+    double Sd = 0.0;
+    for (int kk = 0; kk < tiles; ++kk) Sd += readlane_d(sum, kk) * (double)expf(readlane_f(m, kk) - M);
+    if (lane == 0) L.rn[s & 1] = RowNorm{M, (float)Sd, 0.f};
+  }
+  set_flag(&L.fR, s + 1);
+}
+
+// normalise slot s of this wave's particles (finish_prev's arithmetic, the cosine measurement:
+// unshifted): hp, and the wave's prediction / obs-likelihood partials; returns log p
+__device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                           int s, int i_e, bool valid_e, float u, float qx0, float qx1) {
+  wait_flag(&L.fR, s + 1);
+  const RowNorm rn = L.rn[s & 1];
+  double sf[4] = {0.0, 0.0, 0.0, 0.0};
+  float lp = 0.f;
+  if (valid_e) {
+    const float p = expf(u - rn.shift) / rn.Ssum + 1e-12f;
+    d.hist_p[((int64_t)b * d.T + s) * d.N + i_e] = p;
+    lp = logf(p);
+    sf[0] = (double)p * p;
+    sf[1] = (double)p * qx0;
+    sf[2] = (double)p * qx1;
+    sf[3] = u;
+  }
+  wave_sum_dpp_n(sf);
+  const int lane = threadIdx.x & 63, we = (threadIdx.x >> 6) - 8, tiles = n_tiles(d.N);
+  if (lane < 4)
+    ws.fin[((((int64_t)b * d.T + s) * tiles + tile) * 8 + we) * 4 + lane] =
+        lane == 0 ? sf[0] : lane == 1 ? sf[1] : lane == 2 ? sf[2] : sf[3];
+  return lp;
+}
+
+__device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                             uint32_t tag0) {
+  const int tiles = n_tiles(d.N), N = d.N, ncb = d.n_flows * 4 * kH;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, we = w - 8;
+  const int role = w & 1, g = (w >> 1) & 3;
+  // lanes 0-31: particles [32 role, 32 role + 32) of group g (encode_dot_mfma_half)
+  const int slot_e = g * 64 + 32 * role + (lane & 31), i_e = tile * kTile + slot_e;
+  const bool valid_e = lane < 32 && i_e < N;
+  const bool grp = tile * kTile + g * 64 < N;
+  const EncFrag2 ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
+  float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
+  float u = 0.f, qx0 = 0.f, qx1 = 0.f;
+  const int O = d.E + 4;
+  for (int t = 0; t < d.T; ++t) {
+    const int par = t & 1;
+    const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
+    if (we == 0) {
+      if (t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+      // the proposal fold over step t's encoding columns (model/models.py:338-346)
+      if (lane < ncb) {
+        const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
+        L.encfold[par][lane] = fold_acc(r, O, fold_bias0(r, O), enc_t, 0, d.E);
+      }
+      set_flag(&L.fE, t + 1);
+    }
+    // measure_row_setup (cosine), per wave into its own LDS copy
+    const float ve = lane < kE ? enc_t[lane] : 0.f;
+    const double vinv = 1.0 / fmax(sqrt(wave_sum((double)ve * ve)), 1e-12);
+    if (lane < kE) L.encq[we][lane] = ve;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+    // cosine measurement (model/models.py:206-219) and the log-weight (DPFs.py:187)
+    u = 0.f;
+    if (grp) {
+      wait_flag(&L.qf[g], t + 1);
+      double ss, dot;
+      encode_dot_mfma_half<kE>(ef, role, L.qbuf[par] + g * 64, L.qbuf[par] + kTile + g * 64, L.encq[we], ss, dot,
+                               L.Hws[we]);
+      const float lk = cos_lik(ss, dot, vinv);
+      if (valid_e) {
+        d.hist_lik[((int64_t)b * d.T + t) * N + i_e] = lk;
+        qx0 = L.qbuf[par][slot_e];
+        qx1 = L.qbuf[par][kTile + slot_e];
+      }
+      wait_flag(&L.rf[g], t + 1);
+      if (valid_e) u = logw(lr, lk, L.rbuf[par][slot_e], L.rbuf[par][kTile + slot_e]);
+    }
+    // exchange C: this wave's softmax partials (wave_partials_quad's arithmetic)
+    const float mw = wave_max_dpp(valid_e ? u : -INFINITY);
+    const float ev = valid_e ? expf(u - mw) : 0.f;
+    double r[2] = {(double)ev, (double)ev * ev};
+    wave_sum_dpp_n(r);
+    if (lane < kGC) {
+      const uint64_t eb = (uint64_t)__double_as_longlong(r[0]), qb = (uint64_t)__double_as_longlong(r[1]);
+      const uint32_t word = lane == 0 ? __float_as_uint(mw)
+                            : lane == 1 ? (uint32_t)eb
+                            : lane == 2 ? (uint32_t)(eb >> 32)
+                            : lane == 3 ? (uint32_t)qb
+                            : lane == 4 ? (uint32_t)(qb >> 32)
+                                        : 0u;
+      const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 8 + we;
+      gran_store(ws.gc + gslot * kGC + lane, word, tag0 + (uint32_t)t + 1u);
+    }
+  }
+  // the last slot's normalisation
+  if (we == 0) pass_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
+  pass_norm(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
+}
+
+__global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_filter_desc d, PassWs ws) {
+  __shared__ PassLds L;
+  int b, tile;
+  tile_row(b, tile);
+  const uint32_t tag0 = g_pass_epoch << 12;
+  // LDS is not cleared between workgroups: zero every flag and the pair buffers first
+  pair_clear(L.xbuf, kTile);
+  if (threadIdx.x < 16) L.xflag[threadIdx.x] = 0;
+  if (threadIdx.x < 4) {
+    L.qf[threadIdx.x] = 0;
+    L.rf[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = 0;
+  __syncthreads();
+  if (threadIdx.x < 8 * 64)
+    pass_flow(d, ws, L, b, tile, tag0);
+  else
+    pass_encoder(d, ws, L, b, tile, tag0);
+}
+
+__global__ void tiled_pass_epoch_kernel() {
+  g_pass_epoch = g_pass_epoch + 1u;
+  g_pass_abort = 0;
+}
+
+// The pass applies to this descriptor's configuration (the launcher also needs the speculative
+// gate: d.gate given, ess_local) and every workgroup of its grid can be resident at once.
+static bool pass_config_ok(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_PASS");  // read per call: NFDPF_PASS=0 keeps the step-by-step launches
+  if (e && e[0] == '0') return false;
+  if (!(d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP && d.nf_cond && d.measurement == NFDPF_MEAS_COS)) return false;
+  if (d.rng_mode != NFDPF_RNG_DEVICE || d.force_resample || d.phase != 0 || d.E != kE || d.hidden != kH) return false;
+  if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
+      d.B < 1)
+    return false;
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tiled_pass_kernel, 4 * kTile, 0) != hipSuccess || occ < 1)
+    return false;
+  return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;
+}
+
+}  // namespace nfdpf

@@ -1973,12 +1973,8 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
   if constexpr (!NFC && MEAS == NFDPF_MEAS_CRNVP) {
     if (use_cm(d)) {
       const size_t lds = cm_lds_bytes(d.n_flows);
-      static bool attr = false;  // the fold buffer exceeds the default 64 KB at 3-4 flows
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void *)tiled_prop_cm_kernel<NFD>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)cm_lds_bytes(kMaxFlows));
-        attr = true;
-      }
+      // the fold buffer exceeds the default 64 KB at 3-4 flows
+      ensure_max_dynamic_lds((const void *)tiled_prop_cm_kernel<NFD>, (int)cm_lds_bytes(kMaxFlows));
       if (ev)
         hipExtLaunchKernelGGL(tiled_prop_cm_kernel<NFD>, g, dim3(2 * kTile), lds, st, ev[0], ev[1], 0, d, ws);
       else
@@ -2025,7 +2021,40 @@ static void dispatch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStr
 
 }  // namespace nfdpf
 
+#include "filter_pass.hpp"  // the whole pass as one persistent launch (C2 shape, speculative gate)
+
 using namespace nfdpf;
+
+extern "C" int nfdpf_filter_pass_supported(const nfdpf_filter_desc *d) { return d && pass_config_ok(*d) ? 1 : 0; }
+
+extern "C" int64_t nfdpf_filter_pass_workspace_bytes(int B, int N, int T) {
+  return (B <= 0 || N <= 0 || T <= 0) ? 256 : pass_bytes(B, N, T);
+}
+
+extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *workspace, void *stream) {
+  NFDPF_REQUIRE(dp && workspace, "nfdpf_filter_pass_tiled: null argument");
+  const nfdpf_filter_desc &d = *dp;
+  NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_filter_pass_tiled: workspace not 256-B aligned");
+  NFDPF_REQUIRE(d.t == 0, "nfdpf_filter_pass_tiled: a pass starts at t = 0 (got t=%d)", d.t);
+  NFDPF_REQUIRE(d.hist_x && d.hist_p && d.hist_noise && d.hist_lik && d.hist_idx && d.hist_jac && d.hist_prior &&
+                    d.ess_out && d.enc && d.vel && d.x_prev && d.p_prev && d.lw_sum && d.pred,
+                "nfdpf_filter_pass_tiled: null input/output pointer");
+  NFDPF_REQUIRE(d.dyn_params && d.cond_params && d.pe_params, "nfdpf_filter_pass_tiled: parameters missing");
+  NFDPF_REQUIRE(pass_config_ok(d),
+                "nfdpf_filter_pass_tiled: configuration not supported here (nfdpf_filter_pass_supported == 0)");
+  hipStream_t st = as_stream(stream);
+  tiled_pass_epoch_kernel<<<1, 1, 0, st>>>();  // new granule tags for this pass
+  const PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
+  const dim3 g(n_tiles(d.N), d.B);
+  hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+  if (ev)
+    hipExtLaunchKernelGGL(tiled_pass_kernel, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
+  else
+    tiled_pass_kernel<<<g, 4 * kTile, 0, st>>>(d, ws);
+  const int BT = d.B * d.T;
+  tiled_finalize_kernel<<<(BT + 255) / 256, 256, 0, st>>>(ws.fin, BT, n_tiles(d.N) * 8, d.pred, d.lw_sum);
+  return launch_status("nfdpf_filter_pass_tiled");
+}
 
 extern "C" int64_t nfdpf_filter_tiled_workspace_bytes(int B, int N, int T) {
   return (B <= 0 || N <= 0 || T <= 0) ? 256 : tiled_bytes(B, N, T);
@@ -2060,9 +2089,10 @@ extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *es
 }
 
 extern "C" int nfdpf_split_fault(int reset, void *stream) {
-  // stream-ordered after the launches it checks (the caller's stream, not the null stream)
-  static int v = 0;
-  static const int z = 0;
+  // stream-ordered after the launches it checks (the caller's stream, not the null stream); the
+  // host words are this call's own (the stream is synchronised before they go out of scope)
+  int v = 0;
+  const int z = 0;
   hipStream_t st = as_stream(stream);
   if (hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_split_fault), sizeof(int), 0, hipMemcpyDeviceToHost, st) !=
           hipSuccess ||

@@ -94,12 +94,7 @@ extern "C" int nfdpf_soft_resample(const float *x, const float *p, const float *
   if (B == 0) return NFDPF_OK;
   const size_t stage_lds = 3 * (size_t)N * sizeof(float);
   if (stage_lds <= kSoftStageLds) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void *)soft_resample_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kSoftStageLds);
-      attr = true;
-    }
+    ensure_max_dynamic_lds((const void *)soft_resample_kernel<true>, (int)kSoftStageLds);
     soft_resample_kernel<true><<<B, row_threads(N), stage_lds, as_stream(stream)>>>(
         x, p, lin, offsets, B, N, D, alpha, row_base, x_out, w_out, idx_out);
   } else {

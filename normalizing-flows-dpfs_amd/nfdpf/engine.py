@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -146,6 +147,9 @@ class FilterEngine:
         # OT, auto mode: did the last pass resample?  Then the next one reads its gates step by
         # step (as the reference: one host sync per step); otherwise it speculates
         self._ot_fired = False
+        self.last_pass_ok = False  # the last run's shapes allow the one-launch pass
+        self.last_pass = False     # the last run's pass ran as one launch (nfdpf_filter_pass_tiled)
+        self.pass_launches = 0     # one-launch passes run by this engine (verified or not)
 
     def __getstate__(self):
         # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
@@ -156,15 +160,17 @@ class FilterEngine:
         return st
 
     def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False,
-                     finish=True) -> bool:
+                     finish=True, pass_ok=False) -> bool:
         """Does the next pass run with the speculative ESS gate (every gate taken as off, the T
         gates verified once after the pass from all steps' partials, a fired gate rerunning the
         pass step by step)?  Auto mode (``speculate`` and cfg.speculate_gate None): yes for the
-        tiled pipeline when the batch is sharded (one exchange per pass instead of one per step)
-        and for OT at any world size (its gate is read on the host before every Sinkhorn call,
-        DPFs.py:165: a device->host sync per step) -- unless the previous pass resampled (OT:
-        its gates are then read step by step) or a recent miss is backing off (a miss costs a
-        whole second pass; the next 1, 2, 4 ... 64 passes run step by step).  Not for the soft
+        tiled pipeline when the batch is sharded (one exchange per pass instead of one per step),
+        for OT at any world size (its gate is read on the host before every Sinkhorn call,
+        DPFs.py:165: a device->host sync per step), and wherever the whole pass runs as ONE
+        persistent launch (``pass_ok``: nfdpf_filter_pass_tiled, the C2 shape; it needs every
+        gate of the pass known in advance) -- unless the previous pass resampled (OT: its gates
+        are then read step by step) or a recent miss is backing off (a miss costs a whole second
+        pass; the next 1, 2, 4 ... 64 passes run step by step).  Not for the step-by-step soft
         resampler on one GPU: its per-step gate is device-side already, and speculating saved
         0.33 us of the front launch per step against ~30 us of verification per pass (C2, round
         3: 2.09e9 vs 2.13e9 particle-steps/s).  ``consume``: count this pass
@@ -176,7 +182,7 @@ class FilterEngine:
         auto = speculate is None and c.speculate_gate is None
         if speculate is None:
             speculate = c.speculate_gate if c.speculate_gate is not None else \
-                (tiled and (shard.world > 1 or c.resampler == "ot"))
+                (tiled and (shard.world > 1 or c.resampler == "ot" or pass_ok))
             if auto and finish and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 speculate = False
         if auto and tiled and c.resampler == "ot" and self._ot_fired:
@@ -189,8 +195,30 @@ class FilterEngine:
                     and not c.force_resample and c.measurement != "CGLOW")
 
     def speculates(self, shard=None, finish=True) -> bool:
-        """Whether run() (auto arguments, device RNG) will speculate the gates of its next pass."""
-        return self._decide_spec(shard or ShardInfo(), None, self.cfg.rng_mode == "host", finish=finish)
+        """Whether run() (auto arguments, device RNG) will speculate the gates of its next pass
+        (same shapes as the last run: whether the one-launch pass applies is taken from it)."""
+        return self._decide_spec(shard or ShardInfo(), None, self.cfg.rng_mode == "host", finish=finish,
+                                 pass_ok=self.last_pass_ok)
+
+    def _pass_supported(self, B, N, T, E, split_nets, shard) -> bool:
+        """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
+        the configuration, and the grid resident on the current device)?"""
+        c = self.cfg
+        if not (c.kernel == "tiled" and split_nets and c.rng_mode == "device" and not c.force_resample):
+            return False
+        # every workgroup of the grid must be resident at once: never on a device shared with
+        # another rank (the one-GPU rehearsals of a sharded run), whose kernels can hold CUs
+        if shard.world > 1 and torch.cuda.device_count() < shard.world:
+            return False
+        d = L.FilterDesc()
+        d.B, d.N, d.T, d.E, d.B_global, d.phase = B, N, T, E, shard.B_global, 0
+        d.nf_dyn = (L.DYN_MAF if c.dyn_flow == "MAF" else L.DYN_REALNVP) if c.NF_dyn else L.DYN_NONE
+        d.nf_cond = int(c.NF_cond)
+        d.measurement = L.MEAS.get(c.measurement, L.MEAS_EXTERNAL)
+        d.resampler = L.RESAMPLE[c.resampler]
+        d.rng_mode, d.force_resample = L.RNG_DEVICE, 0
+        d.n_flows, d.hidden, d.split_nets = c.n_flows, c.hidden, int(split_nets)
+        return bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -262,7 +290,14 @@ class FilterEngine:
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
         ot_auto = auto and tiled and c.resampler == "ot"
-        spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish)
+        split_nets = bool(tiled and c.split_nets and c.NF_dyn and splittable(self.m.nf_dyn.flows)
+                          and (not c.NF_cond or splittable(self.m.cond_model.flows)))
+        pass_ok = (not external and teacher is None and not host_mode
+                   and self._pass_supported(B, N, T, E, split_nets, shard))
+        self.last_pass_ok = pass_ok
+        spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish,
+                                 pass_ok=pass_ok)
+        use_pass = spec and pass_ok
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)
@@ -318,8 +353,7 @@ class FilterEngine:
         # step); not when the caller feeds p_prev itself (teacher forcing) or OT reads it first --
         # except in a speculative pass, whose gates are all taken as off (no Sinkhorn call in it)
         d.defer_norm = int(tiled and teacher is None and (c.resampler == "soft" or (c.resampler == "ot" and spec)))
-        d.split_nets = int(tiled and c.split_nets and c.NF_dyn and splittable(self.m.nf_dyn.flows)
-                           and (not c.NF_cond or splittable(self.m.cond_model.flows)))
+        d.split_nets = int(split_nets)
         d.alpha, d.pos_noise = c.alpha, c.pos_noise
         d.dens_const, d.meas_prior_std = density_const(c.pos_noise), c.meas_prior_std
         d.seed = int(c.seed) & (2 ** 64 - 1)
@@ -351,7 +385,24 @@ class FilterEngine:
             if rc != L.NFDPF_OK:
                 L.check(rc, "nfdpf_filter_step_tiled" if tiled else "nfdpf_filter_step")
 
-        for t in range(T):
+        self.last_pass = use_pass
+        if use_pass:
+            # the whole T-step pass as ONE persistent launch (nfdpf_filter_pass_tiled): every gate
+            # taken as off, step t's softmax partials into ess_hist[t + 1] for the verification
+            d.t = 0
+            d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = x0.data_ptr(), p0.data_ptr(), N * 2, N
+            d.vel = vel_p
+            d.ess_all, d.ess_out, d.gate = ess_in_p[0], ess_out_p[0], spec_gate_p
+            d.prof_events, d.prof_front = None, 0
+            if self.step_events is not None:
+                from .prof import EventPair
+                ev = EventPair(2)
+                self.step_events.append(ev)
+                d.prof_events = ev.ptr  # rides in the pass launch's own dispatch
+            pws = ops.pass_workspace(B, N, T, dev)
+            L.check(L.lib().nfdpf_filter_pass_tiled(d_ref, ops._aligned_ptr(pws), stream), "nfdpf_filter_pass_tiled")
+            self.pass_launches += 1
+        for t in range(0 if use_pass else T):
             if t == 0:
                 d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = x0.data_ptr(), p0.data_ptr(), N * 2, N
             elif teacher is not None:
@@ -463,7 +514,10 @@ class FilterEngine:
         # (a stream-ordered read and a sync: deferred to finish_pending when the caller asked
         # for a pass free of host syncs)
         # (the split nets, and the CRNVP launch's cond -> flow hand-off without --NF-cond)
-        handoffs = d.split_nets or (d.measurement == L.MEAS["CRNVP"] and not d.nf_cond)
+        # (the opt-in two-chain CRNVP launch hands off between its waves too; the default
+        # one-chain launch does not, and then no check -- a host sync -- is paid)
+        handoffs = d.split_nets or (d.measurement == L.MEAS["CRNVP"] and not d.nf_cond
+                                    and os.environ.get("NFDPF_CM_TWO_CHAIN", "0") == "1")
         check_split = tiled and handoffs and not torch.cuda.is_current_stream_capturing()
         if check_split and (finish or not spec):
             L.check_split_fault("nfdpf_filter_step_tiled", dev)
@@ -476,8 +530,11 @@ class FilterEngine:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None)
             if not finish:
-                return res
-            if self.finish_pending():
+                return res  # the caller verifies (finish_pending, e.g. after each graph replay)
+            ok = self.finish_pending()
+            # verified here: a kept engine (DPF keeps one) must not pin the pass's buffers
+            self._pending = None
+            if ok:
                 self._spec_backoff = 0
                 return res
             # a gate fired: the pass again, with the per-step exchange

@@ -532,6 +532,12 @@ def tiled_workspace(B: int, N: int, T: int, device) -> torch.Tensor:
     return workspace(int(lib().nfdpf_filter_tiled_workspace_bytes(B, N, T)), device, tag="tiled")
 
 
+def pass_workspace(B: int, N: int, T: int, device) -> torch.Tensor:
+    """Workspace of the one-launch pass (nfdpf_filter_pass_tiled): the row exchanges' granules
+    and the per-wave prediction / obs-likelihood partials."""
+    return workspace(int(lib().nfdpf_filter_pass_workspace_bytes(B, N, T)), device, tag="pass")
+
+
 def tiled_init(p0: torch.Tensor, out: torch.Tensor):
     B, N = p0.shape
     check(lib().nfdpf_filter_tiled_init(ptr(p0), B, N, ptr(out), stream_ptr(p0.device)), "nfdpf_filter_tiled_init")

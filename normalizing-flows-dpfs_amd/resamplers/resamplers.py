@@ -69,8 +69,9 @@ def soft_resampler(particles, particle_probs, alpha, num_resampled, index=True, 
     return (xo, wo, idx) if index else (xo, wo)
 
 
-# The process group a batch-sharded DPF filters over (None: the default group); set by
-# DPFs.DPF from its shard, so the Sinkhorn stop is reduced over the same ranks as the rest.
+# The process group the autograd loop's Sinkhorn stop is reduced over (None: the default
+# group -- the group DPFs.DPF's ShardInfo.from_env shards the batch over, so both paths agree).
+# A caller that shards a DPF over a subgroup must set this to that group as well.
 SHARD_GROUP = None
 
 

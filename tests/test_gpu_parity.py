@@ -622,12 +622,14 @@ def test_split_nets_match_pair_layout(gated):
 
 
 @pytest.mark.parametrize("aligned", [False, True])
-def test_speculative_gate_matches_exchange(aligned):
+def test_speculative_gate_matches_exchange(aligned, monkeypatch):
     """Speculative-gate mode (every gate assumed off, verified after the pass from all steps'
     partials, rerun on a fired gate) returns exactly the per-step-gate pass: bit-identical
     histories and obs-likelihood.  aligned=True uses the fixture's encodings aligned with the
-    true state, on which the gate fires -- the verification must catch it and rerun."""
+    true state, on which the gate fires -- the verification must catch it and rerun.  The
+    step-by-step speculative launches (NFDPF_PASS=0; the one-launch pass: tests/test_gpu_pass.py)."""
     from nfdpf.engine import FilterConfig, FilterEngine
+    monkeypatch.setenv("NFDPF_PASS", "0")
     fx = load("e2e_c2.npz")
     c = e2e_cfg(fx)
     models = _Models(weights(fx), c)

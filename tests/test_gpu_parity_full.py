@@ -172,12 +172,19 @@ def test_fullsize_teacher_forced(name):
     if cglow:
         # The CGLOW likelihood is steep in the particle position (|d lik / d x| up to ~2e3 at
         # C5, scripts/diag_c5.py), so a particle's own fp32 rounding (checked under "particles")
-        # moves it by ~1e-2 in any float32 evaluation.  The measurement's error is therefore taken
-        # at each run's OWN particles: ours and the reference's float32 likelihood against the
-        # float64 measurement at the same positions (the kernel alone, on identical particles:
-        # max 3.3e-3 vs the oracle float32's 7.2e-3, mean 3.4e-5 vs 3.6e-5).
+        # moves it by ~1e-2 in any float32 evaluation.  The measurement is therefore asserted on
+        # IDENTICAL particles: our CGLOW kernel on the reference's own teacher-forced proposals
+        # against the float64 measurement there, next to the reference's float32 likelihood
+        # (the same positions); the whole step's own-particle comparison is printed below.
         lik64_ours = _cglow_lik64_at(w, res.particles.cpu())
         lik64_ref = _cglow_lik64_at(w, ref[0])
+        k_lik = _cglow_kernel_lik_at(w, ref[0])
+        e_k, e_r = np.abs(k_lik - lik64_ref), np.abs(ref[3].numpy() - lik64_ref)
+        _table(f"  likelihood, kernel alone on the reference's particles vs float64: max err {e_k.max():.3e} "
+               f"(reference float32 {e_r.max():.3e}, ratio {e_k.max() / max(e_r.max(), 1e-30):.2f}), mean "
+               f"{e_k.mean():.3e} (reference {e_r.mean():.3e})")
+        assert e_k.max() <= 4 * e_r.max() + 2e-5, (e_k.max(), e_r.max())
+        assert e_k.mean() <= 2.5 * e_r.mean() + 2e-5, (e_k.mean(), e_r.mean())
     fails = []
     for what, i, k, atol in QUANTITIES:
         if ref[i] is None:
@@ -192,12 +199,11 @@ def test_fullsize_teacher_forced(name):
                    f"mean ours {e_o.mean():.3e} ref {e_r.mean():.3e}")
             if f_ours < f_ref - 2e-3:
                 fails.append((what, f_ours, f_ref, worst))
-            # max: 8x, not the 4x of the other quantities -- the case maximum is one element where
-            # the likelihood is steepest (|d lik / d x| ~ 2e3), whose float32 error is a draw of
-            # ~ulp x slope for ours and the reference alike (measured: 4.1x here, 1.27x over the
-            # 640 000 particles of test_cglow_measurement_fullsize, 0.46x on identical particles);
-            # the mean and the fraction carry the comparison
-            assert e_o.max() <= 8 * e_r.max() + atol, (e_o.max(), e_r.max())
+            # at each run's own particles the case maximum is one element where the likelihood
+            # is steepest, a draw of ~ulp x slope for ours and the reference alike (measured 4.6x
+            # in round 3): a diagnostic only -- the kernel is asserted on identical particles above
+            _table(f"  likelihood at own particles: max ratio {e_o.max() / max(e_r.max(), 1e-30):.2f}, "
+                   f"mean ratio {e_o.mean() / max(e_r.mean(), 1e-30):.2f} (diagnostic)")
             assert e_o.mean() <= 2.5 * e_r.mean() + atol, (e_o.mean(), e_r.mean())
             continue
         f32, _ = F.frac_within(o, ref[i], 1e-5, atol)
@@ -308,6 +314,22 @@ def _cglow_lik64_at(w, x):
     """The float64 CGLOW likelihood (row-max shifted, model/models.py:280-303) of a case's
     frame encodings at the particles x (B, T, N, 2), step by step."""
     out = [_cglow_oracle(w["params"], w["enc"][:, t], x[:, t].float(), torch.float64) for t in range(x.shape[1])]
+    return np.stack(out, 1)
+
+
+def _cglow_kernel_lik_at(w, x):
+    """Our CGLOW kernel (nfdpf_cglow_measurement, the row-max shift of model/models.py:301-302
+    applied after it, as the filter's phase 2) on the particles x (B, T, N, 2), step by step."""
+    from nfdpf import ops
+    from nfdpf.pack import cglow_tensors, encoder_tensors
+    m = w["models"]
+    pe = torch.cat([a.detach().reshape(-1) for a in encoder_tensors(m.particle_encoder)]).float().to(DEV)
+    glow = torch.cat([a.detach().reshape(-1) for a in cglow_tensors(m.cglow_measurement)]).float().to(DEV)
+    out = []
+    for t in range(x.shape[1]):
+        raw = ops.cglow_measurement(pe, glow, w["enc"][:, t].float().contiguous().to(DEV),
+                                    x[:, t].float().contiguous().to(DEV))
+        out.append((raw - raw.max(dim=-1, keepdim=True)[0]).cpu().numpy().astype(np.float64))
     return np.stack(out, 1)
 
 

@@ -1,0 +1,195 @@
+"""The whole filtering pass as ONE persistent launch (nfdpf_filter_pass_tiled, csrc/filter_pass.hpp)
+against (a) the step-by-step tiled launches on the same device-RNG draws and (b) the oracle
+(the reference's algorithm, float32 and float64) replaying those draws.  GPU box only.
+
+The pass runs every ESS gate as off (DPFs.py:163-165 speculated) and the engine verifies the T
+gates afterwards; a fired gate reruns the pass step by step (test_pass_gate_fired_reruns).
+Within a step the pass differs from the step launches only in the order of ONE reduction (the
+row's x_phys sums: per tile here, per row there), so (a) is a rounding-level comparison; (b)
+is the reference-parity check: every history within the reference's own float32 envelope.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _util import assert_close, e2e_cfg, load, t, weights
+from oracle import dpf_oracle as O
+from test_gpu_parity import _Models, _check_envelope
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from nfdpf import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+
+
+def _inputs(B, T, seed, scale=10.0):
+    g = torch.Generator().manual_seed(seed)
+    enc = torch.randn(B, T, 32, generator=g).to(DEV)
+    start = (torch.randn(B, 4, generator=g) * scale).to(DEV)
+    vel = (torch.randn(B, T, 2, generator=g) * 3).to(DEV)
+    return enc, start, vel
+
+
+def _models(fixture):
+    """The fixture's flows (e2e_c2: std 0.05, e2e_c2w: std 0.3) with a default-initialised
+    particle encoder: the fixtures' encoder is sharpened so that the ESS gate fires (what the
+    gate tests need); a pass whose gate fires is rerun step by step, and the comparison here is
+    of the one-launch pass itself."""
+    from model.models import build_particle_encoder
+    fx = load(fixture)
+    m = _Models(weights(fx), e2e_cfg(fx))
+    torch.manual_seed(12)
+    m.particle_encoder = build_particle_encoder(32, 2).to(DEV)
+    return m
+
+
+def _run(models, N, enc, start, vel, spec, seed=41, env=None, monkeypatch=None):
+    from nfdpf.engine import FilterConfig, FilterEngine
+    if monkeypatch is not None:
+        monkeypatch.setenv("NFDPF_PASS", env or "1")
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=seed,
+                       kernel="tiled", speculate_gate=spec)
+    eng = FilterEngine(cfg, models)
+    res = eng.run(enc, start, vel)
+    torch.cuda.synchronize()
+    return eng, res
+
+
+CASES = [(6, 1000, 8), (5, 777, 6), (3, 100, 5), (4, 257, 7), (2, 1024, 4), (64, 1000, 50)]
+
+
+@pytest.mark.parametrize("fixture", ["e2e_c2.npz", "e2e_c2w.npz"])
+@pytest.mark.parametrize("B,N,T", CASES)
+def test_pass_matches_step_launches(B, N, T, fixture, monkeypatch):
+    """One launch == T x (front + proposal launches): noise and indices bit-equal; histories to
+    rounding.  Ragged rows (777, 257: a last tile of 9 / 1 particles), one tile with empty wave
+    groups (N = 100), the maximum N (1024), the C2 shape (64 x 1000 x 50)."""
+    models = _models(fixture)
+    enc, start, vel = _inputs(B, T, seed=B * 1000 + N)
+    eng, a = _run(models, N, enc, start, vel, spec=True)
+    assert eng.pass_launches == 1 and eng.last_pass, "the one-launch pass did not run (or a gate fired)"
+    _, b = _run(models, N, enc, start, vel, spec=False)
+    assert torch.equal(a.noise, b.noise)
+    assert torch.equal(a.index, b.index)
+    ident = torch.arange(N, device=DEV) + N * torch.arange(B, device=DEV)[:, None]
+    assert torch.equal(a.index, ident[:, None, :].expand(B, T, N)), "a verified pass resamples nothing"
+    assert_close(a.particles.cpu(), b.particles.cpu(), 1e-5, 1e-4, "particles")
+    assert_close(a.probs.cpu(), b.probs.cpu(), 1e-4, 1e-9, "weights")
+    assert_close(a.lik.cpu(), b.lik.cpu(), 1e-4, 1e-5, "likelihood")
+    assert_close(a.jac.cpu(), b.jac.cpu(), 1e-5, 1e-5, "jac")
+    assert_close(a.prior.cpu(), b.prior.cpu(), 1e-5, 1e-4, "prior")
+    assert_close(a.pred.cpu(), b.pred.cpu(), 1e-5, 1e-3, "prediction")
+    assert abs(float(a.obs_likelihood) - float(b.obs_likelihood)) <= 1e-5 * abs(float(b.obs_likelihood)) + 1e-4
+
+
+class _Replay:
+    """The device draws of our own pass replayed into the oracle (HostRNG's interface)."""
+
+    def __init__(self, noise):
+        self.noise_t = noise.detach().cpu()
+        self.k = 0
+        self.gen = None
+
+    def offsets(self, B, N):
+        raise AssertionError("the oracle resampled: the gate fired")
+
+    def noise(self, B, N, std):
+        v = self.noise_t[:, self.k].clone()
+        self.k += 1
+        return v
+
+
+@pytest.mark.parametrize("fixture", ["e2e_c2.npz", "e2e_c2w.npz"])
+@pytest.mark.parametrize("B,N,T", [(4, 1000, 10), (3, 257, 6)])
+def test_pass_vs_oracle(B, N, T, fixture):
+    """The pass against the oracle run on the same initial particles and motion noise: ours vs
+    the oracle in float64 within 4x (max) / 2.5x (mean) of the oracle float32's own error
+    (test_gpu_parity._check_envelope, the one-step tests' bar), free-running over T steps (no
+    resampling: nothing discrete can diverge)."""
+    from nfdpf import ops
+    fx = load(fixture)
+    c = e2e_cfg(fx)
+    c["N"] = N
+    models = _models(fixture)
+    w = {k: v.detach().cpu() for k, v in models.state_dict().items()}
+    enc, start, vel = _inputs(B, T, seed=7 * N + B)
+    from nfdpf.engine import FilterConfig, FilterEngine
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=5,
+                       kernel="tiled", speculate_gate=True)
+    x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 5, 0, DEV)
+    eng = FilterEngine(cfg, models)
+    res = eng.run(enc, start, vel, init=(x0, logw0))
+    torch.cuda.synchronize()
+    assert eng.last_pass, "a gate fired: the one-launch pass was rerun step by step"
+    outs = {}
+    for dt in (torch.float32, torch.float64):
+        with O.precision(dt):
+            wd = O.cast_params(w, dt)
+            r = O.filtering(c, wd, enc.cpu().to(dt), start.cpu().to(dt), vel.cpu().to(dt), rng=_Replay(res.noise),
+                            init=(x0.cpu().to(dt), logw0.cpu().to(dt)))
+        outs[dt] = [a.double().numpy() if torch.is_tensor(a) else a for a in r]
+    r32, r64 = outs[torch.float32], outs[torch.float64]
+    np.testing.assert_array_equal(res.index.cpu().numpy(), r32[5])
+    _check_envelope(res.particles.cpu(), r32[0], r64[0], 1e-5, 1e-4, "particles")
+    _check_envelope(res.probs.cpu(), r32[1], r64[1], 1e-5, 1e-9, "weights")
+    _check_envelope(res.lik.cpu(), r32[3], r64[3], 1e-5, 2e-5, "likelihood")
+    _check_envelope(res.jac.cpu(), r32[6], r64[6], 1e-5, 1e-6, "jac")
+    _check_envelope(res.prior.cpu(), r32[7], r64[7], 1e-5, 1e-5, "prior")
+    obs64 = float(r64[8])
+    assert abs(float(res.obs_likelihood) - obs64) <= 4 * abs(float(r32[8]) - obs64) + 1e-5 * abs(obs64) + 1e-4
+
+
+def test_pass_gate_fired_reruns(monkeypatch):
+    """Encodings aligned with the true state: the ESS gate fires, the verification catches it
+    and the pass reruns step by step -- the result is the step-by-step pass, bit for bit."""
+    fx = load("e2e_c2.npz")
+    models = _Models(weights(fx), e2e_cfg(fx))
+    enc, start, vel = t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV)
+    N = int(fx["N"])
+    eng_a, a = _run(models, N, enc, start, vel, spec=True)
+    _, b = _run(models, N, enc, start, vel, spec=False)
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert torch.equal(a.obs_likelihood, b.obs_likelihood)
+    B, T = enc.shape[0], enc.shape[1]
+    ident = torch.arange(N, device=DEV) + N * torch.arange(B, device=DEV)[:, None]
+    assert int((a.index != ident[:, None, :]).any(-1).any(0).sum()) > 0, "the gate never fired"
+    assert not eng_a.last_pass  # the returned pass is the rerun
+
+
+def test_pass_deterministic_and_graph_replay():
+    """Two passes give identical bits; a hipGraph-captured pass (the bench's mode: run(finish=
+    False) captured, finish_pending after each replay) replays to the same result."""
+    models = _models("e2e_c2w.npz")
+    B, N, T = 8, 1000, 12
+    enc, start, vel = _inputs(B, T, seed=99)
+    eng, a = _run(models, N, enc, start, vel, spec=True)
+    assert eng.last_pass
+    _, b = _run(models, N, enc, start, vel, spec=True)
+    for f in ("particles", "probs", "lik", "jac", "prior", "pred"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cap = eng.run(enc, start, vel, finish=False, speculate=True)
+    for _ in range(3):
+        g.replay()
+        assert eng.finish_pending()
+        torch.cuda.synchronize()
+        for f in ("particles", "probs", "lik", "pred"):
+            assert torch.equal(getattr(cap, f), getattr(a, f)), f
+        assert torch.equal(cap.obs_likelihood, a.obs_likelihood)
+
+
+def test_pass_disabled_by_env(monkeypatch):
+    """NFDPF_PASS=0 keeps the step-by-step launches (the library reads it per call)."""
+    fx = load("e2e_c2.npz")
+    models = _Models(weights(fx), e2e_cfg(fx))
+    enc, start, vel = _inputs(2, 3, seed=3)
+    monkeypatch.setenv("NFDPF_PASS", "0")
+    eng, _ = _run(models, 300, enc, start, vel, spec=True)
+    assert not eng.last_pass
