@@ -235,10 +235,15 @@ def rocprof_avg_ms(tag, kname):
     if not os.path.exists(path):
         return None, None
     import csv
-    for row in csv.DictReader(open(path)):
-        name = row["Name"].split("(")[0].split("::")[-1].split("<")[0].strip()
-        if name == kname:
-            return float(row["AverageNs"]) * 1e-6, os.path.relpath(path, ROOT)
+    rows = list(csv.DictReader(open(path)))
+    # "<kernel>[full]" (scripts/rocprof_ot_split.py): the Sinkhorn launches that ran an iteration,
+    # without the early-exit tail the plain row averages in
+    for want in (kname + "[full]", kname):
+        for row in rows:
+            full = row["Name"].endswith("[full]")
+            name = row["Name"].split("(")[0].split("::")[-1].split("<")[0].strip() + ("[full]" if full else "")
+            if name == want and (full == want.endswith("[full]")):
+                return float(row["AverageNs"]) * 1e-6, os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -260,63 +265,11 @@ def pmc_traffic(cfg_name, kname):
     return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--force-resample", action="store_true")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--batch", type=int, default=None, help="override B per GPU (exploration only)")
-    ap.add_argument("--graph", type=int, default=1,
-                    help="1: capture the whole T-step pass (all launches of filtering_pos) in a hipGraph and "
-                         "replay it per step (device RNG, soft resampler, one GPU); 0: launch from Python")
-    ap.add_argument("--speculate", type=int, default=-1,
-                    help="speculative ESS gate (one exchange per pass, engine.FilterConfig.speculate_gate): "
-                         "-1 auto (on when sharded), 0 off (per-step exchange), 1 on (also at one GPU)")
-    ap.add_argument("--kernel", default="tiled", choices=["tiled", "fused"],
-                    help="tiled: multi-CU pipeline per step; fused: one workgroup per batch row")
-    ap.add_argument("--enc-from-state", action="store_true",
-                    help="frame encodings = the particle encoder applied to the true positions (what a "
-                         "trained frame encoder approximates): the likelihood peaks near the truth, the "
-                         "weights degenerate and the ESS gate fires (cos / CRNVP measurements, 32-wide)")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # more ranks than devices (a rehearsal on a one-GPU box) share devices round-robin
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        # "nccl" is RCCL over xGMI; NFDPF_DIST_BACKEND=gloo only for rehearsing several ranks on
-        # one device (RCCL refuses two ranks on one GPU)
-        backend = os.environ.get("NFDPF_DIST_BACKEND", "nccl")
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
-
-    from DPFs import DPF
-    from nfdpf.engine import FilterEngine, ShardInfo
-    flags, B, N, T, F_STEP, F_PROP = CONFIGS[args.config]
-    B = args.batch or B
-    F_ALG = F_PROP if (args.kernel == "tiled" or flags["measurement"] == "CGLOW") else F_STEP
-    launch_units = B * N  # particle-steps per launch of the step kernels
-    launch_bytes = B_ALG * B * N
-    torch.manual_seed(2)
-    a = make_args(flags, B, N, T, {"force_resample": args.force_resample})
-    dpf = DPF(a).to(dev).eval()
-    start, state, vel_in, enc = synthetic_disk(B * world, T, 2, a.hiddensize)
-    sl = slice(rank * B, (rank + 1) * B)
-    start, state, vel_in, enc = (t[sl].to(dev) for t in (start, state, vel_in, enc))
-    if args.enc_from_state:
-        with torch.no_grad():
-            enc = dpf.particle_encoder(state[:, :, :2].float()).contiguous()
-    shard = ShardInfo.from_env(B)
-    fcfg = dpf.filter_config()
-    fcfg.kernel = args.kernel
-    if args.speculate >= 0:
-        fcfg.speculate_gate = bool(args.speculate)
+def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
+    """W warm-up passes, then K passes timed between barriers + synchronisations (hipGraph
+    replay of the whole pass where the pass has no host synchronisation), then one more
+    Python-launched pass carrying the live kernel events.  -> dict."""
+    from nfdpf.engine import FilterEngine
     eng = FilterEngine(fcfg, dpf)
 
     def step():
@@ -326,17 +279,16 @@ def main():
         res = step()
     torch.cuda.synchronize()
     graph = None
-    ot = flags["resampler_type"] == "ot"
-    # auto (engine.FilterEngine.run): speculative gates when sharded, and for OT at any world size
-    # unless the previous pass resampled (then its gates are read step by step)
+    # auto (engine.FilterEngine.run): speculative gates when sharded, for OT at any world size
+    # unless the previous pass resampled, and wherever the whole pass runs as one launch
     spec = eng.speculates(shard)  # the engine's own decision for the next pass (engine._decide_spec)
-    if args.graph and ((flags["resampler_type"] == "soft" and world == 1) or spec):
+    if args.graph and ((fcfg.resampler == "soft" and world == 1) or spec):
         # the pass has no host synchronisation in this mode: capture it once, replay per step
         # (every launch of every time step runs on each replay; only the Python launch path goes).
-        # Sharded: the speculative-gate pass (engine.run(finish=False): no exchange inside) is
-        # captured; after each replay finish_pending() gathers all steps' partials once,
+        # Speculative gate: the pass (engine.run(finish=False): no exchange inside) is captured;
+        # after each replay finish_pending() gathers all steps' partials once (sharded),
         # verifies the T gates and reduces the obs-likelihood -- a fired gate (never at the
-        # bench's init weights) reruns the pass with the per-step exchange, inside the timing.
+        # bench's init weights) reruns the pass step by step, inside the timing.
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
@@ -385,8 +337,18 @@ def main():
     front_ms = float(np.mean(front)) if front else None
     for e in evs:
         e.close()
+    return dict(res=res, elapsed=elapsed, kernel_ms=kernel_ms, front_ms=front_ms, eng=eng, graph=graph, spec=spec)
+
+
+def dominant(cfg_name, flags, kernel, B, N, T, fcfg, run, force):
+    """The pass's dominant launch and its algorithmic cost per unit, timed
+    live (run['kernel_ms'] / run['front_ms']) or, for the Sinkhorn, by ot_iteration_ms."""
+    _, _, _, _, F_STEP, F_PROP = CONFIGS[cfg_name]
+    eng, kernel_ms, front_ms, res = run["eng"], run["kernel_ms"], run["front_ms"], run["res"]
+    F_ALG = F_PROP if (kernel == "tiled" or flags["measurement"] == "CGLOW") else F_STEP
+    units, nbytes = B * N, B_ALG * B * N  # per launch of the step kernels
     kname = "filter_step_kernel"
-    if args.kernel == "tiled":  # the proposal launch (csrc/filter_tiled.hip launch_prop)
+    if kernel == "tiled":  # the proposal launch (csrc/filter_tiled.hip launch_prop)
         if fcfg.split_nets and flags["NF_dyn"] and flags["NF_cond"] and flags["measurement"] == "cos" \
                 and flags.get("NF_dyn_flow", "RealNVP") == "RealNVP":
             kname = "tiled_prop_quad_kernel"  # coupling nets on wave pairs beside the encoder pair
@@ -398,15 +360,15 @@ def main():
             kname = "tiled_prop_kernel"
     if flags["measurement"] == "CGLOW":
         kname = "cglow_kernel"
-    F_EX = F_EXEC.get(args.config, F_ALG) if kname.startswith("tiled_prop") else F_ALG
+    F_EX = F_EXEC.get(cfg_name, F_ALG) if kname.startswith("tiled_prop") else F_ALG
     bound = "mfma" if kname == "cglow_kernel" else "valu"
-    if args.kernel == "tiled" and eng.last_pass:  # the whole pass in one launch: every step's FLOP
+    if kernel == "tiled" and eng.last_pass:  # the whole pass in one launch: every step's FLOP
         kname, F_ALG = "tiled_pass_kernel", F_STEP
-        F_EX = F_EXEC_STEP.get(args.config, F_ALG)
-        launch_units, launch_bytes = B * N * T, B_ALG * B * N * T
-    elif args.kernel == "tiled" and eng.last_fused:  # the whole step in one launch: all of its FLOP
+        F_EX = F_EXEC_STEP.get(cfg_name, F_ALG)
+        units, nbytes = B * N * T, B_ALG * B * N * T
+    elif kernel == "tiled" and eng.last_fused:  # the whole step in one launch: all of its FLOP
         kname, F_ALG = "tiled_step_fused_kernel", F_STEP
-        F_EX = F_EXEC_STEP.get(args.config, F_ALG)
+        F_EX = F_EXEC_STEP.get(cfg_name, F_ALG)
     elif front_ms is not None and front_ms > kernel_ms:
         # the step's front launch (gate + resampling + motion [+ nf_dyn inverse]) is the longer
         # one (--force-resample): it is the dominant kernel
@@ -415,19 +377,105 @@ def main():
             kname, F_ALG, F_EX = "tiled_fdyn_kernel", F_DYN_INV, F_DYN_INV_EXEC
         else:  # gate + soft resampling + motion: bytes, not FLOP
             kname, F_ALG, F_EX, bound = "tiled_front_kernel", 0.0, 0.0, "hbm"
-            launch_bytes = (B_SOFT + 8.0 + 8.0) * B * N  # resampling + motion's noise / x' writes
+            nbytes = (B_SOFT + 8.0 + 8.0) * B * N  # resampling + motion's noise / x' writes
     ot_iter_ms, ot_iter_upper = None, False
     if flags["resampler_type"] == "ot" and eng.last_ot_calls:
         ot_iter_ms, ot_iter_upper = ot_iteration_ms(res, T)
         if not ot_iter_upper and ot_iter_ms * eng.last_ot_calls * 10 > kernel_ms * T:  # the Sinkhorn loop dominates
             kname, kernel_ms, bound = "ot_iter_kernel", ot_iter_ms, "valu"
-            F_ALG, launch_units = F_OT_PAIR, B * N * N
+            F_ALG, units = F_OT_PAIR, B * N * N
             F_EX = F_ALG
             # per particle: x~ (8 B) + logw (4) + both potentials read and written (fp64, 32)
-            launch_bytes = 44.0 * B * N
-    tag = args.config + ("_force" if args.force_resample else "")
+            nbytes = 44.0 * B * N
+    tag = cfg_name + ("_force" if force else "")
     traffic, traffic_src = pmc_traffic(tag, kname)
     rp_ms, rp_src = rocprof_avg_ms(tag, kname)
+    achieved_tf = F_ALG * units / (kernel_ms * 1e-3) / 1e12
+    hbm_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
+    # bound: the FP32 issue rate of the CU -- VALU for the coupling nets / Sinkhorn
+    # (v_pk_fma_f32, v_exp_f32), f32 MFMA + VALU for CGLOW; same 157.3 TFLOP/s peak
+    roof = {"bound": bound,
+            "achieved": achieved_tf if bound != "hbm" else hbm_gbs,
+            "peak": PEAK_FP32_TFLOPS if bound != "hbm" else PEAK_HBM_GBS,
+            "unit": "TFLOP/s" if bound != "hbm" else "GB/s",
+            "frac": achieved_tf / PEAK_FP32_TFLOPS if bound != "hbm" else hbm_gbs / PEAK_HBM_GBS,
+            "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": kname, "kernel_avg_ms": kernel_ms,
+            # the same kernel's average in the committed rocprofv3 summary of this bench command
+            # (profiles/rocprof_<config>.csv; OT: the launches that ran the iteration, not the
+            # early-exit tail), beside the live figure
+            "kernel_avg_ms_rocprof": rp_ms, "rocprof_source": rp_src,
+            "flop_per_unit": F_ALG, "units_per_launch": units,
+            "flop_per_unit_executed": F_EX,
+            "frac_executed": F_EX * units / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+            "hbm_achieved_GBs": hbm_gbs, "hbm_frac": hbm_gbs / PEAK_HBM_GBS}
+    return roof, ot_iter_ms, ot_iter_upper
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--force-resample", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-forced", action="store_true",
+                    help="skip the line's `forced` object (the same workload with --force-resample, timed "
+                         "in a second loop; on by default for the configurations whose pass takes < 30 ms)")
+    ap.add_argument("--batch", type=int, default=None, help="override B per GPU (exploration only)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: capture the whole T-step pass (all launches of filtering_pos) in a hipGraph and "
+                         "replay it per step (device RNG, soft resampler, one GPU); 0: launch from Python")
+    ap.add_argument("--speculate", type=int, default=-1,
+                    help="speculative ESS gate (one exchange per pass, engine.FilterConfig.speculate_gate): "
+                         "-1 auto (on when sharded or when the pass runs as one launch), 0 off (per-step "
+                         "exchange), 1 on")
+    ap.add_argument("--kernel", default="tiled", choices=["tiled", "fused"],
+                    help="tiled: multi-CU pipeline per step; fused: one workgroup per batch row")
+    ap.add_argument("--enc-from-state", action="store_true",
+                    help="frame encodings = the particle encoder applied to the true positions (what a "
+                         "trained frame encoder approximates): the likelihood peaks near the truth, the "
+                         "weights degenerate and the ESS gate fires (cos / CRNVP measurements, 32-wide)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # more ranks than devices (a rehearsal on a one-GPU box) share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        # "nccl" is RCCL over xGMI; NFDPF_DIST_BACKEND=gloo only for rehearsing several ranks on
+        # one device (RCCL refuses two ranks on one GPU)
+        backend = os.environ.get("NFDPF_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+
+    import dataclasses
+    from DPFs import DPF
+    from nfdpf.engine import FilterEngine, ShardInfo
+    flags, B, N, T, F_STEP, F_PROP = CONFIGS[args.config]
+    B = args.batch or B
+    torch.manual_seed(2)
+    a = make_args(flags, B, N, T, {"force_resample": args.force_resample})
+    dpf = DPF(a).to(dev).eval()
+    start, state, vel_in, enc = synthetic_disk(B * world, T, 2, a.hiddensize)
+    sl = slice(rank * B, (rank + 1) * B)
+    start, state, vel_in, enc = (t[sl].to(dev) for t in (start, state, vel_in, enc))
+    if args.enc_from_state:
+        with torch.no_grad():
+            enc = dpf.particle_encoder(state[:, :, :2].float()).contiguous()
+    shard = ShardInfo.from_env(B)
+    fcfg = dpf.filter_config()
+    fcfg.kernel = args.kernel
+    if args.speculate >= 0:
+        fcfg.speculate_gate = bool(args.speculate)
+    run = timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev)
+    res, elapsed, eng, graph, spec = run["res"], run["elapsed"], run["eng"], run["graph"], run["spec"]
+    roof, ot_iter_ms, ot_iter_upper = dominant(args.config, flags, args.kernel, B, N, T, fcfg, run,
+                                               args.force_resample)
+    front_ms = run["front_ms"]
     # filtering RMSE of the last pass (losses.py:18-31, eval branch) over the whole job
     se = ((res.pred - state[:, :, :2]) ** 2).sum().double()
     cnt = torch.tensor(float(res.pred.numel()), device=dev, dtype=torch.float64)
@@ -481,12 +529,24 @@ def main():
     if front_ms is not None:
         resample["front_launch_ms"] = front_ms  # the step's gate + resampling + motion launch, live
 
+    # the same workload with the resampler every step (--force-resample), timed in its own loop
+    # right after: the ESS gate does not fire on the synthetic N(0,1) encodings at init weights,
+    # so the headline value times no resampler; this one times one per step
+    forced = None
+    cheap = args.config in ("c1", "c2", "c3")
+    if not args.force_resample and not args.no_forced and cheap:
+        fcfg_f = dataclasses.replace(fcfg, force_resample=True)
+        run_f = timed_passes(fcfg_f, dpf, enc, start, vel_in, shard, args, world, dev)
+        roof_f, _, _ = dominant(args.config, flags, args.kernel, B, N, T, fcfg_f, run_f, True)
+        forced = {"value": B * world * N * T * args.steps / run_f["elapsed"], "unit": "particle-steps/s",
+                  "ms_per_step": run_f["elapsed"] / args.steps * 1e3, "steps": args.steps,
+                  "resampler": flags["resampler_type"], "resampled_steps": T,
+                  "execution": "hipGraph replay of the pass" if run_f["graph"] is not None else "Python launches",
+                  "roofline": roof_f}
+
     if rank == 0:
         units = B * world * N * T * args.steps
         value = units / elapsed
-        per_launch_units = launch_units
-        achieved_tf = F_ALG * per_launch_units / (kernel_ms * 1e-3) / 1e12
-        hbm_gbs = launch_bytes / (kernel_ms * 1e-3) / 1e9
         out = {
             "metric": "particle-steps/sec (batch x N x T / s) + filtering RMSE, disk-tracking task",
             "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps,
@@ -496,6 +556,7 @@ def main():
                        + f", N={N}, batch={B} per GPU, seq_len={T}, state_dim=4 (2-D particles), "
                          f"{'forced' if args.force_resample else 'ESS-gated'} resampling, device RNG, "
                          f"{'hipGraph replay of the pass' if graph is not None else 'Python launches'}"
+                         + (", the whole pass as one launch" if eng.last_pass else "")
                          + (", speculative ESS gate verified once per pass" if spec else "")
                          + (", frame encodings = particle encoder(true positions)" if args.enc_from_state else ""),
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
@@ -503,24 +564,11 @@ def main():
             "rmse": rmse,
             "rmse_informative_encodings": rmse_inf,
             "resampled_steps": resampled,
-            # bound: the FP32 issue rate of the CU -- VALU for the coupling nets / Sinkhorn
-            # (v_pk_fma_f32, v_exp_f32), f32 MFMA + VALU for CGLOW; same 157.3 TFLOP/s peak
-            "roofline": {"bound": bound,
-                         "achieved": achieved_tf if bound != "hbm" else hbm_gbs,
-                         "peak": PEAK_FP32_TFLOPS if bound != "hbm" else PEAK_HBM_GBS,
-                         "unit": "TFLOP/s" if bound != "hbm" else "GB/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS if bound != "hbm" else hbm_gbs / PEAK_HBM_GBS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": kname, "kernel_avg_ms": kernel_ms,
-                         # the same kernel's average in the committed rocprofv3 summary of this
-                         # bench command (profiles/rocprof_<config>.csv), beside the live figure
-                         "kernel_avg_ms_rocprof": rp_ms, "rocprof_source": rp_src,
-                         "flop_per_unit": F_ALG, "units_per_launch": per_launch_units,
-                         "flop_per_unit_executed": F_EX,
-                         "frac_executed": F_EX * per_launch_units / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
-                         "hbm_achieved_GBs": hbm_gbs, "hbm_frac": hbm_gbs / PEAK_HBM_GBS},
+            "roofline": roof,
             "resample": resample,
         }
+        if forced is not None:
+            out["forced"] = forced
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.config, force=args.force_resample)
         print(json.dumps(out))

@@ -342,11 +342,19 @@ class measurement_model_cnf(nn.Module):
 
 class _CglowRunner:
     """measurement_model_cglow's raw likelihood -nll: the fused HIP kernel forward (particle
-    encoder + CGLOW, csrc/cglow.hip); backward differentiates the PyTorch restatement (the
-    particle encoder, then CondGlowModel.torch_forward) on the saved inputs (nfdpf.autograd)."""
+    encoder + CGLOW, csrc/cglow.hip) and the HIP backward (nfdpf_cglow_measurement_backward,
+    csrc/cglow_bwd.hip); ``torch`` is the PyTorch restatement (the particle encoder, then
+    CondGlowModel.torch_forward) that NFDPF_HIP_BACKWARD=0 differentiates instead, bounded to
+    RECOMPUTE_ROWS particles (nfdpf.autograd: 4 000 took 3.96 ms there, 64 000 did not finish in
+    3 minutes on the GPU box)."""
+
+    RECOMPUTE_ROWS = 16384
 
     def __init__(self, model):
         self.model = model
+
+    def recompute_limit(self, enc, x):
+        return self.RECOMPUTE_ROWS, x.numel() // x.shape[-1]
 
     def hip(self, enc, x):
         from nfdpf.pack import cglow_tensors

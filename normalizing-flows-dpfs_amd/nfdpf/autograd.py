@@ -1,10 +1,14 @@
 """Autograd for the HIP flow / measurement ops (training).
 
 The forward value always comes from the HIP kernel.  Backward: a runner with a HIP backward
-(``runner.hip_backward``: the RealNVP(_cond) coupling stacks, csrc/flows_bwd.hip) returns the
-input and parameter gradients from the kernel; the other runners (MAF, measurements) re-run
-the same math as PyTorch ops on the saved inputs and differentiate that (activation-recompute
-style).  ``NFDPF_HIP_BACKWARD=0`` sends every runner down the recompute path.
+(``runner.hip_backward``: the RealNVP(_cond) coupling stacks, MAF stacks, the cosine / CRNVP /
+NN / gaussian / CGLOW measurements -- csrc/*_bwd.hip) returns the input and parameter gradients
+from the kernel; where it declines (sizes or models its kernel does not cover), the runner's
+math is re-run as PyTorch ops on the saved inputs and differentiated (activation-recompute
+style).  ``NFDPF_HIP_BACKWARD=0`` sends every runner down the recompute path -- for comparison
+only: a runner may bound the recompute (``recompute_limit(*inputs)`` -> the largest size it
+finishes, with the input's size) and then refuses a larger one with NfdpfError instead of
+stalling the device (CGLOW's recompute did not finish a 64 x 1 000-particle backward in 3 min).
 """
 from __future__ import annotations
 
@@ -39,6 +43,13 @@ class _RecomputeFn(torch.autograd.Function):
                 gin = [g if (t is not None and t.requires_grad) else None for g, t in zip(gin, ins)]
                 gpar = [g if p.requires_grad else None for g, p in zip(gpar, params)]
                 return (None, None) + tuple(gin) + tuple(gpar)
+        lim = getattr(ctx.runner, "recompute_limit", None)
+        if lim is not None:
+            cap, size = lim(*ins)
+            if size > cap:
+                from ._lib import NfdpfError
+                raise NfdpfError(f"{type(ctx.runner).__name__}: the PyTorch-recompute backward is bounded to {cap} "
+                                 f"rows (got {size}); the HIP backward covers this size (NFDPF_HIP_BACKWARD=1)")
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(t.requires_grad) if t is not None and t.is_floating_point() else t
                       for t in ins]

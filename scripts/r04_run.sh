@@ -45,11 +45,14 @@ prof)
   for spec in ${PROFS:-c2}; do
     cfg=${spec%%:*}; extra=""; tag=$cfg
     case "$spec" in *:force) extra="--force-resample"; tag=${cfg}_force;; esac
-    A="--config $cfg $extra --no-cpu-baseline ${PROF_ARGS}"
+    A="--config $cfg $extra --no-cpu-baseline --no-forced ${PROF_ARGS}"
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof_$tag -o run -- \
       python3 bench.py $A > gpurun_out/fprof_$tag.log 2>&1
     rc=$?; echo "prof $tag rc=$rc"; tail -c 300 gpurun_out/fprof_$tag.log; echo; [ $rc -eq 0 ] || exit $rc
     find gpurun_out/fprof_$tag -name "*kernel_stats.csv" -exec cp {} gpurun_out/rocprof_$tag.csv \;
+    # OT: the iteration launches that ran an iteration, apart from the early-exit tail
+    tr=$(find gpurun_out/fprof_$tag -name "*kernel_trace.csv" | head -n 1)
+    [ -n "$tr" ] && python3 scripts/rocprof_ot_split.py "$tr" gpurun_out/rocprof_$tag.csv
     rm -rf gpurun_out/fprof_$tag
     [ -n "$NO_PMC" ] && continue
     for pass in "sq:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SMEM" \

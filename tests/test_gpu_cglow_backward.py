@@ -141,3 +141,23 @@ def test_cglow_backward_deterministic():
     b = ops.cglow_measurement_backward(peb, glb, enc, x, gl)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def test_cglow_recompute_backward_refuses_large(monkeypatch):
+    """The PyTorch-recompute backward (NFDPF_HIP_BACKWARD=0, a comparison path) refuses sizes it
+    cannot finish -- it once stalled a box on a 64 x 1 000-particle backward -- with NfdpfError
+    before any recompute runs; the HIP backward takes the same call."""
+    from model.models import build_particle_encoder_cglow, measurement_model_cglow
+    from nfdpf import autograd
+    from nfdpf._lib import NfdpfError
+    m = measurement_model_cglow(build_particle_encoder_cglow(192, 2), _glow()).to(DEV)
+    B, N = 2, 9000  # 18 000 particles > the 16 384 bound
+    enc = torch.randn(B, 192, device=DEV)
+    x = (torch.randn(B, N, 2, device=DEV) * 20).requires_grad_(True)
+    monkeypatch.setattr(autograd, "HIP_BACKWARD", False)
+    with pytest.raises(NfdpfError, match="recompute"):
+        m(enc, x).sum().backward()
+    monkeypatch.setattr(autograd, "HIP_BACKWARD", True)
+    x.grad = None
+    m(enc, x).sum().backward()
+    assert x.grad is not None and torch.isfinite(x.grad).all()
