@@ -60,11 +60,14 @@ struct PassWs {
   uint64_t *gb;  // [2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
   uint64_t *gc;  // [2][B][tiles][8 encoder waves][kGC]      exchange C (softmax partials)
   double *fin;   // [B][T][tiles * 8][4] per encoder wave: sum p^2, sum p x0, sum p x1, sum logw
+  // forced resampling (FORCE): one granule per tile and step parity, published once the tile's
+  // slot t weights (hist_p) and particles (hist_x), written through (sc1), have drained
+  uint64_t *gp;  // [2][B][tiles]
 };
 
 static int64_t pass_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(2 * bt * 4 * kGA * 8) * 2 + al256(2 * bt * 8 * kGC * 8) + al256(bt * T * 8 * 32);
+  return al256(2 * bt * 4 * kGA * 8) * 2 + al256(2 * bt * 8 * kGC * 8) + al256(bt * T * 8 * 32) + al256(2 * bt * 8);
 }
 
 static PassWs pass_carve(void *ws, int B, int N, int T) {
@@ -78,12 +81,29 @@ static PassWs pass_carve(void *ws, int B, int N, int T) {
   w.gc = (uint64_t *)p;
   p += al256(2 * bt * 8 * kGC * 8);
   w.fin = (double *)p;
+  p += al256(bt * T * 8 * 32);
+  w.gp = (uint64_t *)p;
   return w;
 }
 
+// forced resampling of the row (FORCE), at the top of a step while no wave is encoding
+struct PassRs {
+  float pl[kPassMaxTiles * kTile];   // the row's weights of the previous slot
+  float cdf[kPassMaxTiles * kTile];  // its CDF (soft_row_search)
+  float wg[kPassMaxTiles * kTile];   // the gathered weights w[idx_i] of every marker i
+  float lr_l[kTile];                 // this tile's particles: resampled log-weight,
+  float xr_l[kTile][2];              // source position,
+  int src_l[kTile];                  // source index (N: the reference's out-of-range edge)
+  double shd[16];
+  float shf[16];
+  uint32_t gpw[kPassMaxTiles];
+};
 struct PassLds {
   float xbuf[8 * kTile];           // flow-pair hand-offs (pair_swap; 8-byte aligned, first member)
-  float Hws[8][32 * kHPitch];      // each encoder wave's MFMA layer outputs
+  union {
+    float Hws[8][32 * kHPitch];    // each encoder wave's MFMA layer outputs
+    PassRs rs;
+  };
   float qbuf[2][2 * kTile];        // the proposal, flow t-wave -> encoder pair, by step parity
   float rbuf[2][2 * kTile];        // prior | propose, flow t-wave -> encoder pair
   float encq[8][kE];               // each encoder wave's copy of the step's frame encoding
@@ -96,6 +116,7 @@ struct PassLds {
   int xflag[16];
   int fA, fB, fE, fR;              // step-tagged flags (see the header comment)
   int qf[4], rf[4];
+  int fS, fbar, pcnt;              // FORCE: resampling done, flow-wave barrier, encoder weights drained
 };
 
 __device__ __forceinline__ void gran_store(uint64_t *g, uint32_t data, uint32_t tag) {
@@ -118,7 +139,7 @@ __device__ __forceinline__ bool pass_spin(Spin &s) {
     if (s.it == 1) {
       s.t0 = now;
     } else if (now - s.t0 > kPassWaitTicks) {
-      if ((threadIdx.x & 63) == 0) {
+      if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {  // first active lane
         atomicAdd(&g_split_fault, 1);
         __hip_atomic_store(&g_pass_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -207,7 +228,165 @@ __device__ __forceinline__ void pass_noise(const nfdpf_filter_desc &d, int t, in
   e1 *= d.pos_noise;
 }
 
+// write-through (sc1) stores of slot values another tile reads (FORCE)
+__device__ __forceinline__ void store_wt(float *p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_wt2(float *p, float a, float b) {  // p 8-B aligned
+  __hip_atomic_store(reinterpret_cast<uint64_t *>(p), ((uint64_t)__float_as_uint(b) << 32) | __float_as_uint(a),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float load_wt(const float *p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void load_wt2(const float *p, float &a, float &b) {
+  const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  a = __uint_as_float((uint32_t)v);
+  b = __uint_as_float((uint32_t)(v >> 32));
+}
+
+// barrier of the 8 flow waves (the encoder waves run their own loop meanwhile): each wave adds
+// to a monotonic LDS counter once its LDS writes have landed, then waits for the round's total
+__device__ __forceinline__ void flow_barrier(int *cnt, int &round) {
+  round += 8;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) atomicAdd(cnt, 1);
+  wait_flag(cnt, round);
+}
+
+// ---- FORCE: the soft resampling of the row at the top of step t (resamplers.py:20-60, the
+// soft.hpp recipe: bit-exact indices), by the 8 flow waves (512 threads) while the encoder
+// waves wait for its log-weights (flag fS).  Input: slot t-1's normalised weights (hist_p,
+// written by the encoder waves) and particles (hist_x, by the flow waves) of the whole row,
+// written through (sc1) by the row's tiles; a tile publishes one granule once every storing
+// wave has drained (MI355X_MICROARCH.md inter-workgroup visibility, row 1: sc1 stores,
+// vmcnt(0), the storing waves' LDS counter, one lane's sc1 flag; the polling wave, then a
+// barrier, then sc1 loads) -- or the initial state at t = 0.  Every tile searches all N
+// markers (the gathered weights' renormaliser is a cascade sum over the whole row in ATen's
+// order) and keeps its own particles' source, position and log-weight in LDS.  History slots
+// are never overwritten inside the pass, so the rare read of the NEXT row's first particle
+// (the reference's out-of-range edge, src == N) only waits for that row's tile 0 to have
+// published slot t-1 or a later one.
+__device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b,
+                                              int tile, uint32_t tag0, int t, int &round) {
+  PassRs &R = L.rs;
+  const int N = d.N, tiles = n_tiles(N), tid = threadIdx.x, nth = 8 * 64;
+  const int64_t grow = d.row_base + b;
+  const uint32_t tag = tag0 + (uint32_t)t;  // slot t - 1's
+  uint64_t *gp = ws.gp + ((int64_t)((t - 1) & 1) * d.B + b) * tiles;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through particle stores
+  flow_barrier(&L.fbar, round);
+  const float *xs;  // the previous slot's particles of this row
+  int64_t xs_next;  // ... and the offset of the next row's
+  if (t > 0) {
+    if (tid < 64) {
+      wait_flag(&L.pcnt, 8 * t);  // the encoder waves' weights of slot t - 1 have drained
+      if (tid == 0) gran_store(gp + tile, 1u, tag);
+      poll_row(gp, tiles, tag, R.gpw);
+    }
+    flow_barrier(&L.fbar, round);
+    const float *ps = d.hist_p + ((int64_t)b * d.T + t - 1) * N;
+    for (int j = tid; j < N; j += nth) R.pl[j] = load_wt(ps + j);
+    xs = d.hist_x + ((int64_t)b * d.T + t - 1) * N * 2;
+    xs_next = (int64_t)d.T * N * 2;
+  } else {
+    for (int j = tid; j < N; j += nth) R.pl[j] = d.p_prev[(int64_t)b * d.p_prev_rs + j];
+    xs = d.x_prev + (int64_t)b * d.x_prev_rs;
+    xs_next = d.x_prev_rs;
+  }
+  flow_barrier(&L.fbar, round);
+  // soft_row_search's steps on 512 threads (soft.hpp)
+  SoftRow row{R.pl, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
+  if (row.alpha < 1.0f) {
+    if (tid < 64) {
+      const float S = cascade_row_sum([&](int j) { return row.q_raw(j); }, N);
+      if (tid == 0) R.shf[0] = S;
+    }
+    flow_barrier(&L.fbar, round);
+    row.S = R.shf[0];
+  }
+  // the exact f64 prefix of q: 2 consecutive j per thread (N <= 1024), wave scans, wave order
+  {
+    const int j0 = 2 * tid;
+    const double a = j0 < N ? (double)row.q(j0) : 0.0, c = j0 + 1 < N ? (double)row.q(j0 + 1) : 0.0;
+    const double part = a + c;
+    const int lane = tid & 63, w = tid >> 6;
+    double inc = part;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) R.shd[w] = inc;
+    flow_barrier(&L.fbar, round);
+    double base = 0.0;
+    for (int k = 0; k < w; ++k) base += R.shd[k];
+    double run = base + inc - part;
+    if (j0 < N) {
+      run += a;
+      R.cdf[j0] = (float)run;
+    }
+    if (j0 + 1 < N) {
+      run += c;
+      R.cdf[j0 + 1] = (float)run;
+    }
+  }
+  flow_barrier(&L.fbar, round);
+  const float off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)t, grow, 0u).x) * (1.0f / (float)N);
+  const int i0 = tile * kTile;
+  for (int i = tid; i < N; i += nth) {
+    const float m = off + d.lin[i];
+    int lo = 0, hi = N - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (R.cdf[mid] < m)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const int sj = lo + (1.0f < m ? 1 : 0);
+    // sj == N: the reference's out-of-range edge (next row's first particle, weight 0)
+    R.wg[i] = sj < N ? row.w(sj) : 0.f;
+    if (i >= i0 && i < i0 + kTile) R.src_l[i - i0] = sj;
+  }
+  flow_barrier(&L.fbar, round);
+  if (tid < 64) {
+    const float s2 = cascade_row_sum([&](int j) { return R.wg[j]; }, N);
+    if (tid == 0) R.shf[8] = s2;
+  }
+  flow_barrier(&L.fbar, round);
+  if (tid < kTile && i0 + tid < N) {
+    const int sj = R.src_l[tid];
+    R.lr_l[tid] = logf(R.wg[i0 + tid] / R.shf[8]);
+    const float *src = xs + 2 * (sj < N ? sj : N - 1);
+    if (sj >= N && b + 1 < d.B) {
+      src = xs + xs_next;
+      if (t > 0) {  // row b + 1 has published slot t - 1 (or a later one): its history is final
+        const uint64_t *g = ws.gp + ((int64_t)((t - 1) & 1) * d.B + b + 1) * tiles;
+        Spin sp;
+        for (;;) {
+          const uint32_t v = (uint32_t)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
+          if ((v >= tag && v < tag0 + (1u << 12)) || !pass_spin(sp)) break;
+        }
+      }
+    }
+    float x0, x1;
+    if (t > 0) {
+      load_wt2(src, x0, x1);
+    } else {
+      x0 = src[0];
+      x1 = src[1];
+    }
+    R.xr_l[tid][0] = x0;
+    R.xr_l[tid][1] = x1;
+  }
+  flow_barrier(&L.fbar, round);
+  if (tid < 64) set_flag(&L.fS, t + 1);  // the encoder waves may read lr_l
+}
+
 // ---- waves 0-7 ------------------------------------------------------------------------------
+template <bool FORCE>
 __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                           uint32_t tag0) {
   const int tiles = n_tiles(d.N), N = d.N, nfl = d.n_flows, ncb = nfl * 4 * kH;
@@ -239,12 +418,22 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
   const float *dbase = d.dyn_params + split_suffix_offset(nfl, kOctxDyn);
   const float *cbase = d.cond_params + split_suffix_offset(nfl, d.E + 4);
   const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
+  int round = 0;  // flow_barrier rounds (FORCE)
   for (int t = 0; t < d.T; ++t) {
     const int par = t & 1;
     const uint32_t tag = tag0 + (uint32_t)t + 1u;
     const RowSlot S = row_slot(d, b, t);
     const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
-    // motion (model/models.py:191-204), no resampling: x_phys = (x + vel) + eps
+    int src = i;
+    if constexpr (FORCE) {  // soft resampling of the row every step (--force-resample)
+      pass_resample(d, ws, L, b, tile, tag0, t, round);
+      if (valid) {
+        x0 = L.rs.xr_l[slot][0];
+        x1 = L.rs.xr_l[slot][1];
+        src = L.rs.src_l[slot];
+      }
+    }
+    // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps
     float e0 = 0.f, e1 = 0.f, p0 = 0.f, p1 = 0.f;
     if (valid) {
       pass_noise(d, t, grow, i, e0, e1);
@@ -253,7 +442,7 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
       if (role == 0) {
         S.hnoise[2 * i] = e0;
         S.hnoise[2 * i + 1] = e1;
-        S.hidx[i] = (int64_t)N * grow + i;
+        S.hidx[i] = (int64_t)N * grow + src;
       }
     }
     const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 4 + g;
@@ -331,8 +520,12 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
       if (role == 0) {
         L.rbuf[par][slot] = prior;
         L.rbuf[par][kTile + slot] = propose;
-        S.hx[2 * i] = q0;
-        S.hx[2 * i + 1] = q1;
+        if (FORCE) {  // the next step's resampling reads the row's particles from other tiles
+          store_wt2(S.hx + 2 * i, q0, q1);
+        } else {
+          S.hx[2 * i] = q0;
+          S.hx[2 * i + 1] = q1;
+        }
         if (S.hprior) S.hprior[i] = prior;
       }
     }
@@ -385,6 +578,7 @@ __device__ __forceinline__ void pass_poll_c(const nfdpf_filter_desc &d, const Pa
 
 // normalise slot s of this wave's particles (finish_prev's arithmetic, the cosine measurement:
 // unshifted): hp, and the wave's prediction / obs-likelihood partials; returns log p
+template <bool FORCE>
 __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                            int s, int i_e, bool valid_e, float u, float qx0, float qx1) {
   wait_flag(&L.fR, s + 1);
@@ -393,7 +587,11 @@ __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const Pas
   float lp = 0.f;
   if (valid_e) {
     const float p = expf(u - rn.shift) / rn.Ssum + 1e-12f;
-    d.hist_p[((int64_t)b * d.T + s) * d.N + i_e] = p;
+    float *hp = d.hist_p + ((int64_t)b * d.T + s) * d.N + i_e;
+    if (FORCE)
+      store_wt(hp, p);  // the next step's resampling reads the row's weights from other tiles
+    else
+      *hp = p;
     lp = logf(p);
     sf[0] = (double)p * p;
     sf[1] = (double)p * qx0;
@@ -408,6 +606,7 @@ __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const Pas
   return lp;
 }
 
+template <bool FORCE>
 __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                              uint32_t tag0) {
   const int tiles = n_tiles(d.N), N = d.N, ncb = d.n_flows * 4 * kH;
@@ -439,7 +638,15 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     if (lane < kE) L.encq[we][lane] = ve;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+    if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+    if constexpr (FORCE) {  // the flow waves resample the row: the log-weight of the source
+      if (t > 0) {  // slot t - 1's weights (write-through) have drained: count this wave in
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((threadIdx.x & 63) == 0) atomicAdd(&L.pcnt, 1);
+      }
+      wait_flag(&L.fS, t + 1);
+      lr = valid_e ? L.rs.lr_l[slot_e] : 0.f;
+    }
     // cosine measurement (model/models.py:206-219) and the log-weight (DPFs.py:187)
     u = 0.f;
     if (grp) {
@@ -475,9 +682,10 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   }
   // the last slot's normalisation
   if (we == 0) pass_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
-  pass_norm(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
+  pass_norm<FORCE>(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
 }
 
+template <bool FORCE>
 __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_filter_desc d, PassWs ws) {
   __shared__ PassLds L;
   int b, tile;
@@ -490,12 +698,12 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
     L.qf[threadIdx.x] = 0;
     L.rf[threadIdx.x] = 0;
   }
-  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = 0;
+  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = L.pcnt = 0;
   __syncthreads();
   if (threadIdx.x < 8 * 64)
-    pass_flow(d, ws, L, b, tile, tag0);
+    pass_flow<FORCE>(d, ws, L, b, tile, tag0);
   else
-    pass_encoder(d, ws, L, b, tile, tag0);
+    pass_encoder<FORCE>(d, ws, L, b, tile, tag0);
 }
 
 __global__ void tiled_pass_epoch_kernel() {
@@ -509,14 +717,19 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   const char *e = getenv("NFDPF_PASS");  // read per call: NFDPF_PASS=0 keeps the step-by-step launches
   if (e && e[0] == '0') return false;
   if (!(d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP && d.nf_cond && d.measurement == NFDPF_MEAS_COS)) return false;
-  if (d.rng_mode != NFDPF_RNG_DEVICE || d.force_resample || d.phase != 0 || d.E != kE || d.hidden != kH) return false;
+  if (d.rng_mode != NFDPF_RNG_DEVICE || d.phase != 0 || d.E != kE || d.hidden != kH) return false;
+  // a forced pass resamples every step inside the launch (soft resampler only); otherwise the
+  // caller takes every gate as off and verifies them afterwards
+  if (d.force_resample && d.resampler != NFDPF_RESAMPLE_SOFT) return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
       d.B < 1)
     return false;
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tiled_pass_kernel, 4 * kTile, 0) != hipSuccess || occ < 1)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &occ, d.force_resample ? tiled_pass_kernel<true> : tiled_pass_kernel<false>, 4 * kTile, 0) != hipSuccess ||
+      occ < 1)
     return false;
   return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;
 }

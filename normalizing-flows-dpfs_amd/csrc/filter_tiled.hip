@@ -2040,6 +2040,8 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
                     d.ess_out && d.enc && d.vel && d.x_prev && d.p_prev && d.lw_sum && d.pred,
                 "nfdpf_filter_pass_tiled: null input/output pointer");
   NFDPF_REQUIRE(d.dyn_params && d.cond_params && d.pe_params, "nfdpf_filter_pass_tiled: parameters missing");
+  NFDPF_REQUIRE(!d.force_resample || (d.lin && ((uintptr_t)d.hist_x & 7) == 0),
+                "nfdpf_filter_pass_tiled: a forced pass needs lin and an 8-B aligned hist_x");
   NFDPF_REQUIRE(pass_config_ok(d),
                 "nfdpf_filter_pass_tiled: configuration not supported here (nfdpf_filter_pass_supported == 0)");
   hipStream_t st = as_stream(stream);
@@ -2047,10 +2049,11 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   const PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
   const dim3 g(n_tiles(d.N), d.B);
   hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+  const auto kern = d.force_resample ? tiled_pass_kernel<true> : tiled_pass_kernel<false>;
   if (ev)
-    hipExtLaunchKernelGGL(tiled_pass_kernel, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
+    hipExtLaunchKernelGGL(kern, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
   else
-    tiled_pass_kernel<<<g, 4 * kTile, 0, st>>>(d, ws);
+    kern<<<g, 4 * kTile, 0, st>>>(d, ws);
   const int BT = d.B * d.T;
   tiled_finalize_kernel<<<(BT + 255) / 256, 256, 0, st>>>(ws.fin, BT, n_tiles(d.N) * 8, d.pred, d.lw_sum);
   return launch_status("nfdpf_filter_pass_tiled");

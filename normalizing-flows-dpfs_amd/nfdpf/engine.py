@@ -204,7 +204,9 @@ class FilterEngine:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
         the configuration, and the grid resident on the current device)?"""
         c = self.cfg
-        if not (c.kernel == "tiled" and split_nets and c.rng_mode == "device" and not c.force_resample):
+        if not (c.kernel == "tiled" and split_nets and c.rng_mode == "device"):
+            return False
+        if c.force_resample and c.resampler != "soft":  # a forced pass resamples inside the launch
             return False
         # every workgroup of the grid must be resident at once: never on a device shared with
         # another rank (the one-GPU rehearsals of a sharded run), whose kernels can hold CUs
@@ -216,7 +218,7 @@ class FilterEngine:
         d.nf_cond = int(c.NF_cond)
         d.measurement = L.MEAS.get(c.measurement, L.MEAS_EXTERNAL)
         d.resampler = L.RESAMPLE[c.resampler]
-        d.rng_mode, d.force_resample = L.RNG_DEVICE, 0
+        d.rng_mode, d.force_resample = L.RNG_DEVICE, int(c.force_resample)
         d.n_flows, d.hidden, d.split_nets = c.n_flows, c.hidden, int(split_nets)
         return bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
 
@@ -297,7 +299,9 @@ class FilterEngine:
         self.last_pass_ok = pass_ok
         spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish,
                                  pass_ok=pass_ok)
-        use_pass = spec and pass_ok
+        # the one-launch pass: gates speculated (verified after it), or every step resampling
+        # (--force-resample: no gate to decide, the row's resampling runs inside the launch)
+        use_pass = pass_ok and (spec or c.force_resample)
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)
@@ -315,7 +319,7 @@ class FilterEngine:
             tiles = ops.tiled_tiles(N)
             # per-(row, tile) softmax partials {max u, sum e, sum e^2, max lik} of each step:
             # the next step's gate and (deferred) normalisation derive from them
-            if spec:  # every step's partials kept for the verification
+            if spec or use_pass:  # every step's partials kept for the verification
                 ess_hist = torch.empty((T + 1, B, tiles, 4), device=dev, dtype=torch.float64)
                 ess_bufs = [ess_hist[t] for t in range(1, T + 1)]
                 ess0 = ops.tiled_init(p0, ess_hist[0])
@@ -373,7 +377,7 @@ class FilterEngine:
         # time step, so it stays free of tensor slicing and per-call lookups
         hx_p, hp_p, vel_p = hx.data_ptr(), hp.data_ptr(), vel_steps.data_ptr()
         ess_out_p = [b.data_ptr() for b in ess_bufs]
-        ess_in_p = [ess0.data_ptr()] + ess_out_p[:-1] if spec else None
+        ess_in_p = [ess0.data_ptr()] + ess_out_p[:-1] if (spec or use_pass) else None
         spec_gate_p = spec_gate.data_ptr() if spec else None
         stream = ops.stream_ptr(dev)
         launch = L.lib().nfdpf_filter_step_tiled if tiled else L.lib().nfdpf_filter_step

@@ -193,3 +193,64 @@ def test_pass_disabled_by_env(monkeypatch):
     monkeypatch.setenv("NFDPF_PASS", "0")
     eng, _ = _run(models, 300, enc, start, vel, spec=True)
     assert not eng.last_pass
+
+
+def _philox_offsets(seed, T, B, N, row_base=0):
+    """The device RNG's soft-resampling offsets (csrc/common.hpp rng_draw(seed, kTagOffset = 1,
+    t, row, 0) -> u01 / N), restated on the host: offsets [T, B] float32."""
+    M = 0xFFFFFFFF
+
+    def philox(c, k0, k1):
+        x, y, z, w = c
+        for _ in range(10):
+            p0, p1 = x * 0xD2511F53, z * 0xCD9E8D57
+            x, y, z, w = ((p1 >> 32) ^ y ^ k0) & M, p1 & M, ((p0 >> 32) ^ w ^ k1) & M, p0 & M
+            k0, k1 = (k0 + 0x9E3779B9) & M, (k1 + 0xBB67AE85) & M
+        return x
+    out = np.zeros((T, B), dtype=np.float32)
+    for t in range(T):
+        for b in range(B):
+            row = row_base + b
+            u = philox((0, row & M, ((row >> 32) ^ (t << 8)) & M, 1), seed & M, (seed >> 32) & M)
+            out[t, b] = np.float32((u >> 8) * np.float32(2.0 ** -24)) * np.float32(np.float32(1.0) / np.float32(N))
+    return out
+
+
+@pytest.mark.parametrize("B,N,T", [(6, 1000, 8), (4, 257, 6), (3, 100, 5), (64, 1000, 50)])
+def test_forced_pass_resampling_bit_exact(B, N, T):
+    """--force-resample: the pass resamples every row every step inside the launch.  Every
+    step's indices equal the ORACLE's soft resampler (resamplers.py:20-60 restated, pinned to the
+    reference's golden vectors) on the pass's own previous slot and the device offsets, bit for
+    bit; the resampled log-weights likewise feed the same step; the whole pass against the
+    step-by-step launches: index agreement and predictions as test_gpu_parity's tiled == fused."""
+    models = _models("e2e_c2.npz")
+    enc, start, vel = _inputs(B, T, seed=B * 31 + N)
+    from nfdpf.engine import FilterConfig, FilterEngine
+    out = {}
+    for env in ("1", "0"):
+        import os
+        os.environ["NFDPF_PASS"] = env
+        try:
+            cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=77,
+                               kernel="tiled", force_resample=True)
+            eng = FilterEngine(cfg, models)
+            out[env] = eng.run(enc, start, vel)
+            torch.cuda.synchronize()
+            assert eng.last_pass == (env == "1")
+        finally:
+            os.environ.pop("NFDPF_PASS", None)
+    a, b = out["1"], out["0"]
+    off = _philox_offsets(77, T, B, N)
+    x, p, idx = a.particles.cpu(), a.probs.cpu(), a.index.cpu()
+    for t in range(1, T):
+        _, _, ref_idx = O.soft_resample(x[:, t - 1].contiguous(), p[:, t - 1].contiguous(), 0.5,
+                                        torch.from_numpy(off[t]))
+        assert torch.equal(idx[:, t], ref_idx.long()), f"step {t}: indices differ from the oracle's"
+    assert torch.equal(a.noise, b.noise)
+    agree = (a.index == b.index).float().mean().item()
+    assert agree > 0.99, agree  # a marker within rounding of a CDF step flips an index and the row then follows
+    assert torch.allclose(a.particles[:, :1], b.particles[:, :1], rtol=1e-4, atol=1e-2)
+    assert torch.allclose(a.pred[:, :2], b.pred[:, :2], rtol=1e-4, atol=1e-2)
+    assert torch.isfinite(a.probs).all()
+    s = a.probs.sum(-1)
+    assert torch.allclose(s, torch.ones_like(s) + N * 1e-12, atol=1e-5)
