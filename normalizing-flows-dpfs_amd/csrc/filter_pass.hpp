@@ -55,6 +55,23 @@ constexpr int kGC = 6;             // per encoder-wave publish: max (f32), sum e
 __device__ uint32_t g_pass_epoch = 0;
 __device__ int g_pass_abort = 0;
 
+#ifdef NFDPF_EXP_PTRACE
+// experiment-only: per-step phase timestamps (s_memrealtime, 100 MHz) of waves 0, 1 and 8 of
+// every workgroup, steps < 64 (scripts/exp_ptrace.py)
+__device__ unsigned long long g_ptrace[256][16][64][12];
+#define PT(t, k)                                                                                   \
+  do {                                                                                             \
+    const int w_ = threadIdx.x >> 6, wi_ = w_;          \
+    const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                           \
+    if (wi_ >= 0 && (threadIdx.x & 63) == 0 && wg_ < 256 && (t) < 64)                             \
+      g_ptrace[wg_][wi_][(t)][(k)] = __builtin_amdgcn_s_memrealtime();                             \
+  } while (0)
+#else
+#define PT(t, k) \
+  do {           \
+  } while (0)
+#endif
+
 struct PassWs {
   uint64_t *ga;  // [2][B][tiles][4 role-0 flow waves][kGA]  exchange A (x_phys sums)
   uint64_t *gb;  // [2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
@@ -99,13 +116,13 @@ struct PassRs {
   uint32_t gpw[kPassMaxTiles];
 };
 struct PassLds {
-  float xbuf[8 * kTile];           // flow-pair hand-offs (pair_swap; 8-byte aligned, first member)
   union {
     float Hws[8][32 * kHPitch];    // each encoder wave's MFMA layer outputs
     PassRs rs;
   };
-  float qbuf[2][2 * kTile];        // the proposal, flow t-wave -> encoder pair, by step parity
-  float rbuf[2][2 * kTile];        // prior | propose, flow t-wave -> encoder pair
+  float qbuf[2][2 * kTile];        // the proposal, chain wave -> prior wave + encoder pair, by step parity
+  float pbuf[2][2 * kTile];        // x_phys - eps, chain wave -> prior wave
+  float rbuf[2][2 * kTile];        // prior (prior wave) | propose (chain wave) -> encoder pair
   float encq[8][kE];               // each encoder wave's copy of the step's frame encoding
   f2 cbd[2][kMaxFlows * 2 * kH];   // nf_dyn folded biases (split order), by step parity
   f2 cbc[2][kMaxFlows * 2 * kH];   // proposal folded biases (split order)
@@ -113,9 +130,8 @@ struct PassLds {
   uint32_t rowa[kPassMaxTiles * 4 * kGA];  // wave 0's A / B sweep
   uint32_t rowc[kPassMaxTiles * 8 * kGC];  // wave 8's C sweep
   RowNorm rn[2];                   // slot s's row normaliser, by parity of s
-  int xflag[16];
   int fA, fB, fE, fR;              // step-tagged flags (see the header comment)
-  int qf[4], rf[4];
+  int qf[4], rf[4], pf[4], ef[8];
   int fS, fbar, pcnt;              // FORCE: resampling done, flow-wave barrier, encoder weights drained
 };
 
@@ -132,6 +148,10 @@ struct Spin {
   uint64_t t0 = 0;
   int it = 0;
 };
+#ifndef NFDPF_PASS_FLAG_SLEEP
+#define NFDPF_PASS_FLAG_SLEEP 1
+#endif
+template <int SLEEP = 1>
 __device__ __forceinline__ bool pass_spin(Spin &s) {
   if ((s.it++ & 63) == 0) {
     if (__hip_atomic_load(&g_pass_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
@@ -146,14 +166,14 @@ __device__ __forceinline__ bool pass_spin(Spin &s) {
       return false;
     }
   }
-  __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_s_sleep(SLEEP);
   return true;
 }
 
 // wait until the LDS flag reaches v (wave-uniform)
 __device__ __forceinline__ void wait_flag(const int *f, int v) {
   Spin s;
-  while (__builtin_amdgcn_readfirstlane(*(lds_vint *)f) < v && pass_spin(s)) {
+  while (__builtin_amdgcn_readfirstlane(*(lds_vint *)f) < v && pass_spin<NFDPF_PASS_FLAG_SLEEP>(s)) {
   }
   asm volatile("" ::: "memory");
 }
@@ -161,6 +181,9 @@ __device__ __forceinline__ void wait_flag(const int *f, int v) {
 __device__ __forceinline__ void set_flag(int *f, int v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   *(lds_vint *)f = v;
+#ifdef NFDPF_PASS_WAKE
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_wakeup" ::: "memory");
+#endif
 }
 
 // four wave-uniform doubles as 8 granules (lanes 0..7: value l / 2, low / high word by l & 1)
@@ -176,14 +199,22 @@ __device__ __forceinline__ void publish4(uint64_t *g, const double (&v)[4], uint
 
 // one wave sweeps granules [0, n) of a row (n <= 192) until every tag is `tag`, leaving the
 // data words in dst (LDS); false on abort
-__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst) {
+__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst,
+                         unsigned long long *tr = nullptr) {
   const int l = threadIdx.x & 63;
   uint64_t v[3] = {0, 0, 0};
   bool ok[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) ok[c] = 64 * c + l >= n;
   Spin sp;
+#ifdef NFDPF_EXP_PTRACE
+  unsigned long long iss = 0, its = 0;
+#endif
   for (;;) {
+#ifdef NFDPF_EXP_PTRACE
+    iss = __builtin_amdgcn_s_memrealtime();
+    ++its;
+#endif
 #pragma unroll
     for (int c = 0; c < 3; ++c)
       if (!ok[c]) v[c] = __hip_atomic_load(g + 64 * c + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -193,6 +224,12 @@ __device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst) 
     if (__all(ok[0] && ok[1] && ok[2])) break;
     if (!pass_spin(sp)) return false;
   }
+#ifdef NFDPF_EXP_PTRACE
+  if (tr && l == 0) {
+    tr[0] = iss;
+    tr[1] = its;
+  }
+#endif
 #pragma unroll
   for (int c = 0; c < 3; ++c)
     if (64 * c + l < n) dst[64 * c + l] = (uint32_t)v[c];
@@ -385,18 +422,66 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   if (tid < 64) set_flag(&L.fS, t + 1);  // the encoder waves may read lr_l
 }
 
-// ---- waves 0-7 ------------------------------------------------------------------------------
+// ---- waves 0-7: the flows, one wave per particle group and stage ---------------------------
+// The t- and s-nets of one coupling half on input u from the PAIR layout core (flows.hpp ts_pair,
+// HALF = 1: one v_pk_fma_f32 advances hidden unit j of both nets), layer 3 summed the way
+// split.hpp's net_split sums it (even and odd hidden units in two chains, then (even + odd) + b3):
+// every component sees net_split's fma sequence, so the result is bit-identical to the wave-pair
+// evaluation without its LDS hand-off.  cb = the half's folded bias pairs (fold_ref order).
+__device__ __forceinline__ f2 ts_half(cf2 *w, float u, const f2 *cb) {
+  f2 h[kH];
+#pragma unroll
+  for (int j = 0; j < kH; ++j) h[j] = tanh2(pfma(w[j], splat(u), cb[j]));
+  cf2 *w2 = w + kH;
+  f2 g[kH];
+#pragma unroll
+  for (int j = 0; j < kH; ++j) {
+    f2 a = w2[kH * kH + j];
+#pragma unroll
+    for (int k = 0; k < kH; ++k) a = pfma(w2[j * kH + k], h[k], a);
+    g[j] = tanh2(a);
+  }
+  cf2 *w3 = w2 + kH * kH + kH;
+  f2 e = w3[0] * g[0], o = w3[1] * g[1];
+#pragma unroll
+  for (int m = 1; m < kH / 2; ++m) {
+    e = pfma(w3[2 * m], g[2 * m], e);
+    o = pfma(w3[2 * m + 1], g[2 * m + 1], o);
+  }
+  return (e + o) + w3[kH];
+}
+// RealNVP_cond flow inverse (nf/flows.py:228-239) / forward (:215-226) on one wave: fw = the
+// flow's pair-layout block (half 1 at fw, half 2 at fw + ns), cb = its 16 folded bias pairs
+// (half 2 at cb + kH); the update arithmetic of split.hpp's coupling_*_split
+__device__ __forceinline__ float pass_inverse(cf2 *fw, int ns, float &lo, float &up, const f2 *cb) {
+  f2 ts = ts_half(fw + ns, up, cb + kH);
+  lo = (lo - ts.x) * expf(-ts.y);
+  const float l2 = -ts.y;
+  ts = ts_half(fw, lo, cb);
+  up = (up - ts.x) * expf(-ts.y);
+  return -ts.y + l2;
+}
+__device__ __forceinline__ float pass_forward(cf2 *fw, int ns, float &lo, float &up, const f2 *cb) {
+  f2 ts = ts_half(fw, lo, cb);
+  up = ts.x + up * expf(ts.y);
+  const float l1 = ts.y;
+  ts = ts_half(fw + ns, up, cb + kH);
+  lo = ts.x + lo * expf(ts.y);
+  return l1 + ts.y;
+}
+
+// waves 0-3 ("chain", group g = w): motion -> A -> nf_dyn inverse -> B -> proposal inverse, the
+// path from one step's particles to the next's; the proposal goes to the group's prior wave and
+// encoder pair through LDS (qbuf, pbuf, rbuf's propose half; flag qf[g])
 template <bool FORCE>
-__device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
-                                          uint32_t tag0) {
+__device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                           uint32_t tag0) {
   const int tiles = n_tiles(d.N), N = d.N, nfl = d.n_flows, ncb = nfl * 4 * kH;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int role = w & 1, g = w >> 1, slot = g * 64 + lane;
+  const int g = w, slot = g * 64 + lane;
   const int i = tile * kTile + slot;
   const bool valid = i < N;
-  const bool grp = tile * kTile + g * 64 < N;  // the pair has particles
   const int64_t grow = d.row_base + b;
-  PairX px = pair_of(L.xbuf, L.xflag, role, slot);
   float x0 = 0.f, x1 = 0.f;
   if (valid) {
     x0 = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i];
@@ -415,8 +500,8 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
 #pragma unroll
     for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + d.E + c) + rc.w];
   }
-  const float *dbase = d.dyn_params + split_suffix_offset(nfl, kOctxDyn);
-  const float *cbase = d.cond_params + split_suffix_offset(nfl, d.E + 4);
+  constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
+  cf2 *const dyn0 = wptr2(d.dyn_params), *const cond0 = wptr2(d.cond_params);
   const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
   int round = 0;  // flow_barrier rounds (FORCE)
   for (int t = 0; t < d.T; ++t) {
@@ -425,6 +510,11 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
     const RowSlot S = row_slot(d, b, t);
     const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
     int src = i;
+    // the nets' weights are re-read (scalar loads) every step: hoisted out of the step loop they
+    // would not fit the SGPRs and spill through VGPR lanes
+    cf2 *dyn = dyn0, *cond = cond0;
+    asm volatile("" : "+s"(dyn), "+s"(cond));
+    PT(t, 0);
     if constexpr (FORCE) {  // soft resampling of the row every step (--force-resample)
       pass_resample(d, ws, L, b, tile, tag0, t, round);
       if (valid) {
@@ -439,42 +529,46 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
       pass_noise(d, t, grow, i, e0, e1);
       p0 = (x0 + v0) + e0;
       p1 = (x1 + v1) + e1;
-      if (role == 0) {
-        S.hnoise[2 * i] = e0;
-        S.hnoise[2 * i + 1] = e1;
-        S.hidx[i] = (int64_t)N * grow + src;
-      }
+      S.hnoise[2 * i] = e0;
+      S.hnoise[2 * i + 1] = e1;
+      S.hidx[i] = (int64_t)N * grow + src;
     }
     const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 4 + g;
     const int64_t grow0 = ((int64_t)par * d.B + b) * tiles * 4;
-    if (role == 0) {  // exchange A: this wave's sums of x_phys
+    {  // exchange A: this wave's sums of x_phys
       double s[4] = {p0, p1, (double)p0 * p0, (double)p1 * p1};
       wave_sum_dpp_n(s);
       publish4(ws.ga + gslot * kGA, s, tag);
     }
+    PT(t, 1);
     if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
-      if (poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
+      const bool ok = poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa);
+      // cbd[par] was last read by the prior waves at step t - 2
+      if (t >= 2)
+        for (int q = 0; q < 4; ++q) wait_flag(&L.pf[q], t - 1);
+      if (ok) {
         const Ctx4 c = row_ctx(L.rowa, tiles, N);
         if (fold_lane) {
           const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
           float v = fwd[0];
 #pragma unroll
           for (int q = 0; q < kOctxDyn; ++q) v = fmaf(fwd[1 + q], cv[q], v);
-          reinterpret_cast<float *>(L.cbd[par])[split_cb_index(lane)] = v;
+          reinterpret_cast<float *>(L.cbd[par])[lane] = v;
         }
       }
       set_flag(&L.fA, t + 1);
     } else {
       wait_flag(&L.fA, t + 1);
     }
-    // nf_dyn inverse (model/models.py:305-332) on the wave pair
+    PT(t, 2);
+    // nf_dyn inverse (model/models.py:305-332)
     float xd0 = p0, xd1 = p1, ld = 0.f;
     if (valid)
-      for (int f = nfl - 1; f >= 0; --f)
-        ld += coupling_inverse_split(dbase + f * kSplitFlow, xd0, xd1, L.cbd[par] + f * 16, px, kTile);
+      for (int f = nfl - 1; f >= 0; --f) ld += pass_inverse(dyn + f * 2 * nsd, nsd, xd0, xd1, L.cbd[par] + f * 2 * kH);
     const float jac = -ld;
-    if (role == 0) {
-      if (valid && S.hjac) S.hjac[i] = jac;
+    PT(t, 3);
+    if (valid && S.hjac) S.hjac[i] = jac;
+    {
       double s[4] = {valid ? xd0 : 0.0, valid ? xd1 : 0.0, valid ? (double)xd0 * xd0 : 0.0,
                      valid ? (double)xd1 * xd1 : 0.0};
       wave_sum_dpp_n(s);
@@ -489,49 +583,82 @@ __device__ __forceinline__ void pass_flow(const nfdpf_filter_desc &d, const Pass
           float a = L.encfold[par][lane];
 #pragma unroll
           for (int q = 0; q < 4; ++q) a = fmaf(fwc[q], c4[q], a);
-          reinterpret_cast<float *>(L.cbc[par])[split_cb_index(lane)] = a;
+          reinterpret_cast<float *>(L.cbc[par])[lane] = a;
         }
       }
       set_flag(&L.fB, t + 1);
     } else {
       wait_flag(&L.fB, t + 1);
     }
+    PT(t, 4);
     // NF proposal inverse (model/models.py:334-356)
     float q0 = xd0, q1 = xd1, ldp = 0.f;
     if (valid)
-      for (int f = nfl - 1; f >= 0; --f)
-        ldp += coupling_inverse_split(cbase + f * kSplitFlow, q0, q1, L.cbc[par] + f * 16, px, kTile);
-    if (role == 0) {  // the proposal to the encoder pair
-      if (valid) {
-        L.qbuf[par][slot] = q0;
-        L.qbuf[par][kTile + slot] = q1;
-      }
-      set_flag(&L.qf[g], t + 1);
+      for (int f = nfl - 1; f >= 0; --f) ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
+    // the group's encoder pair has read qbuf / rbuf[par] of step t - 2
+    if (t >= 2) {
+      wait_flag(&L.ef[2 * g], t - 1);
+      wait_flag(&L.ef[2 * g + 1], t - 1);
     }
-    // nf_dyn forward of the proposal + densities (model/models.py:358-377, stage_prior_split)
-    if (grp && valid) {
-      const float de = density(e0, e1, K, two_var);
-      const float r0 = p0 - e0, r1 = p1 - e1;
-      float lo = q0, up = q1, ld2 = 0.f;
-      for (int f = 0; f < nfl; ++f)
-        ld2 += coupling_forward_split(dbase + f * kSplitFlow, lo, up, L.cbd[par] + f * 16, px, kTile);
-      const float prior = density(lo - r0, up - r1, K, two_var) - (-ld2);
-      const float propose = (de + jac) + (-ldp);
-      if (role == 0) {
-        L.rbuf[par][slot] = prior;
-        L.rbuf[par][kTile + slot] = propose;
-        if (FORCE) {  // the next step's resampling reads the row's particles from other tiles
-          store_wt2(S.hx + 2 * i, q0, q1);
-        } else {
-          S.hx[2 * i] = q0;
-          S.hx[2 * i + 1] = q1;
-        }
-        if (S.hprior) S.hprior[i] = prior;
+    if (valid) {  // to the prior wave and the encoder pair
+      L.qbuf[par][slot] = q0;
+      L.qbuf[par][kTile + slot] = q1;
+      L.pbuf[par][slot] = p0 - e0;
+      L.pbuf[par][kTile + slot] = p1 - e1;
+      L.rbuf[par][kTile + slot] = (density(e0, e1, K, two_var) + jac) + (-ldp);  // propose
+      if (FORCE) {  // the next step's resampling reads the row's particles from other tiles
+        store_wt2(S.hx + 2 * i, q0, q1);
+      } else {
+        S.hx[2 * i] = q0;
+        S.hx[2 * i + 1] = q1;
       }
     }
-    if (role == 0) set_flag(&L.rf[g], t + 1);
+    set_flag(&L.qf[g], t + 1);
+    PT(t, 5);
     x0 = q0;
     x1 = q1;
+  }
+}
+
+// waves 4-7 ("prior", group g = w - 4): the nf_dyn forward of the proposal and the prior density
+// (model/models.py:358-377, stage_prior_split) off the chain, into rbuf's prior half (flag rf[g])
+template <bool FORCE>
+__device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                           uint32_t tag0) {
+  const int N = d.N, nfl = d.n_flows;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int g = w - 4, slot = g * 64 + lane;
+  const int i = tile * kTile + slot;
+  const bool valid = i < N;
+  constexpr int nsd = kNsDyn;
+  cf2 *const dyn0 = wptr2(d.dyn_params);
+  const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
+  int round = 0;
+  for (int t = 0; t < d.T; ++t) {
+    const int par = t & 1;
+    const RowSlot S = row_slot(d, b, t);
+    cf2 *dyn = dyn0;
+    asm volatile("" : "+s"(dyn));
+    if constexpr (FORCE) pass_resample(d, ws, L, b, tile, tag0, t, round);
+    PT(t, 0);
+    wait_flag(&L.qf[g], t + 1);
+    PT(t, 1);
+    if (valid) {
+      float lo = L.qbuf[par][slot], up = L.qbuf[par][kTile + slot], ld2 = 0.f;
+      const float r0 = L.pbuf[par][slot], r1 = L.pbuf[par][kTile + slot];
+#ifndef NFDPF_EXP_NOFWD
+      for (int f = 0; f < nfl; ++f)
+#else
+      for (int f = 0; f < nfl && lo == 12345.f; ++f)  // experiment only: timing without the prior's forward
+#endif
+        ld2 += pass_forward(dyn + f * 2 * nsd, nsd, lo, up, L.cbd[par] + f * 2 * kH);
+      const float prior = density(lo - r0, up - r1, K, two_var) - (-ld2);
+      L.rbuf[par][slot] = prior;
+      if (S.hprior) S.hprior[i] = prior;
+    }
+    set_flag(&L.rf[g], t + 1);
+    set_flag(&L.pf[g], t + 1);
+    PT(t, 2);
   }
 }
 
@@ -623,14 +750,18 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   for (int t = 0; t < d.T; ++t) {
     const int par = t & 1;
     const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
+    PT(t, 0);
     if (we == 0) {
-      if (t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
-      // the proposal fold over step t's encoding columns (model/models.py:338-346)
+      // the proposal fold over step t's encoding columns (model/models.py:338-346); encfold[par]
+      // was last read by wave 0's fold of step t - 2, before qf(t - 1) this wave has waited for
       if (lane < ncb) {
         const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
         L.encfold[par][lane] = fold_acc(r, O, fold_bias0(r, O), enc_t, 0, d.E);
       }
       set_flag(&L.fE, t + 1);
+      PT(t, 1);
+      if (t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+      PT(t, 2);
     }
     // measure_row_setup (cosine), per wave into its own LDS copy
     const float ve = lane < kE ? enc_t[lane] : 0.f;
@@ -648,13 +779,20 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       lr = valid_e ? L.rs.lr_l[slot_e] : 0.f;
     }
     // cosine measurement (model/models.py:206-219) and the log-weight (DPFs.py:187)
+    PT(t, 3);
     u = 0.f;
     if (grp) {
       wait_flag(&L.qf[g], t + 1);
+      PT(t, 4);
       double ss, dot;
+#ifndef NFDPF_EXP_NOENC
       encode_dot_mfma_half<kE>(ef, role, L.qbuf[par] + g * 64, L.qbuf[par] + kTile + g * 64, L.encq[we], ss, dot,
                                L.Hws[we]);
+#else
+      ss = 1.0; dot = 0.5;  // experiment only: timing without the encoder
+#endif
       const float lk = cos_lik(ss, dot, vinv);
+      PT(t, 5);
       if (valid_e) {
         d.hist_lik[((int64_t)b * d.T + t) * N + i_e] = lk;
         qx0 = L.qbuf[par][slot_e];
@@ -663,6 +801,8 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       wait_flag(&L.rf[g], t + 1);
       if (valid_e) u = logw(lr, lk, L.rbuf[par][slot_e], L.rbuf[par][kTile + slot_e]);
     }
+    set_flag(&L.ef[we], t + 1);  // qbuf / rbuf[par] read: the chain wave may reuse them at t + 2
+    PT(t, 6);
     // exchange C: this wave's softmax partials (wave_partials_quad's arithmetic)
     const float mw = wave_max_dpp(valid_e ? u : -INFINITY);
     const float ev = valid_e ? expf(u - mw) : 0.f;
@@ -679,6 +819,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 8 + we;
       gran_store(ws.gc + gslot * kGC + lane, word, tag0 + (uint32_t)t + 1u);
     }
+    PT(t, 7);
   }
   // the last slot's normalisation
   if (we == 0) pass_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
@@ -691,17 +832,19 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
   int b, tile;
   tile_row(b, tile);
   const uint32_t tag0 = g_pass_epoch << 12;
-  // LDS is not cleared between workgroups: zero every flag and the pair buffers first
-  pair_clear(L.xbuf, kTile);
-  if (threadIdx.x < 16) L.xflag[threadIdx.x] = 0;
+  // LDS is not cleared between workgroups: zero every flag first
   if (threadIdx.x < 4) {
     L.qf[threadIdx.x] = 0;
     L.rf[threadIdx.x] = 0;
+    L.pf[threadIdx.x] = 0;
   }
+  if (threadIdx.x < 8) L.ef[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = L.pcnt = 0;
   __syncthreads();
-  if (threadIdx.x < 8 * 64)
-    pass_flow<FORCE>(d, ws, L, b, tile, tag0);
+  if (threadIdx.x < 4 * 64)
+    pass_chain<FORCE>(d, ws, L, b, tile, tag0);
+  else if (threadIdx.x < 8 * 64)
+    pass_prior<FORCE>(d, ws, L, b, tile, tag0);
   else
     pass_encoder<FORCE>(d, ws, L, b, tile, tag0);
 }

@@ -2113,6 +2113,11 @@ extern "C" int nfdpf_split_fault(int reset, void *stream) {
   return n;
 }
 
+#ifdef NFDPF_EXP_PTRACE
+extern "C" NFDPF_API int nfdpf_exp_ptrace_read(void *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ptrace), sizeof(g_ptrace)) == hipSuccess ? 0 : 1;
+}
+#endif
 #ifdef NFDPF_EXP_QTRACE
 extern "C" NFDPF_API int nfdpf_exp_qtrace_read(void *host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_qtrace), sizeof(g_qtrace)) == hipSuccess ? 0 : 1;

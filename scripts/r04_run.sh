@@ -57,7 +57,8 @@ prof)
     [ -n "$NO_PMC" ] && continue
     for pass in "sq:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SMEM" \
                 "mfma:SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-                "fetch:FETCH_SIZE" "write:WRITE_SIZE"; do
+                "fetch:FETCH_SIZE" "write:WRITE_SIZE" \
+                "inst:SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_BRANCH"; do
       name=${pass%%:*}; ctr=${pass#*:}
       timeout -k 10 -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/fpmc_${tag}_$name -o run -- \
         python3 bench.py $A --steps 1 --warmup 1 --graph 0 > gpurun_out/fpmc_${tag}_$name.log 2>&1
