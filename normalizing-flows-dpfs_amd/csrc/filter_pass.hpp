@@ -428,7 +428,13 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
 // split.hpp's net_split sums it (even and odd hidden units in two chains, then (even + odd) + b3):
 // every component sees net_split's fma sequence, so the result is bit-identical to the wave-pair
 // evaluation without its LDS hand-off.  cb = the half's folded bias pairs (fold_ref order).
+#ifndef NFDPF_PASS_SB
+#define NFDPF_PASS_SB 1
+#endif
 __device__ __forceinline__ f2 ts_half(cf2 *w, float u, const f2 *cb) {
+#if NFDPF_PASS_SB
+  __builtin_amdgcn_sched_barrier(0);  // no weight loads hoisted from here into the previous half
+#endif
   f2 h[kH];
 #pragma unroll
   for (int j = 0; j < kH; ++j) h[j] = tanh2(pfma(w[j], splat(u), cb[j]));
@@ -470,6 +476,24 @@ __device__ __forceinline__ float pass_forward(cf2 *fw, int ns, float &lo, float 
   return l1 + ts.y;
 }
 
+// The kernel's arguments re-read from the kernarg segment at the top of every step: LICM would
+// otherwise keep every step-invariant field and address live in SGPRs across the step loop,
+// and the nets' weight loads would then spill them through VGPR lanes (v_writelane /
+// v_readlane around every coupling)
+typedef const __attribute__((address_space(4))) nfdpf_filter_desc kdesc_t;
+typedef const __attribute__((address_space(4))) PassWs kws_t;
+__device__ __forceinline__ kdesc_t *kernarg_desc() {
+  kdesc_t *p = (kdesc_t *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ kws_t *kernarg_ws() {
+  constexpr size_t off = (sizeof(nfdpf_filter_desc) + alignof(PassWs) - 1) / alignof(PassWs) * alignof(PassWs);
+  kws_t *p = (kws_t *)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() + off);
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // waves 0-3 ("chain", group g = w): motion -> A -> nf_dyn inverse -> B -> proposal inverse, the
 // path from one step's particles to the next's; the proposal goes to the group's prior wave and
 // encoder pair through LDS (qbuf, pbuf, rbuf's propose half; flag qf[g])
@@ -501,19 +525,17 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + d.E + c) + rc.w];
   }
   constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
-  cf2 *const dyn0 = wptr2(d.dyn_params), *const cond0 = wptr2(d.cond_params);
-  const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
   int round = 0;  // flow_barrier rounds (FORCE)
   for (int t = 0; t < d.T; ++t) {
+    const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
+    const PassWs &ws = *(const PassWs *)kernarg_ws();
+    cf2 *dyn = wptr2(d.dyn_params), *cond = wptr2(d.cond_params);
+    const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const uint32_t tag = tag0 + (uint32_t)t + 1u;
     const RowSlot S = row_slot(d, b, t);
     const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
     int src = i;
-    // the nets' weights are re-read (scalar loads) every step: hoisted out of the step loop they
-    // would not fit the SGPRs and spill through VGPR lanes
-    cf2 *dyn = dyn0, *cond = cond0;
-    asm volatile("" : "+s"(dyn), "+s"(cond));
     PT(t, 0);
     if constexpr (FORCE) {  // soft resampling of the row every step (--force-resample)
       pass_resample(d, ws, L, b, tile, tag0, t, round);
@@ -543,6 +565,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     PT(t, 1);
     if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
       const bool ok = poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa);
+      PT(t, 7);
       // cbd[par] was last read by the prior waves at step t - 2
       if (t >= 2)
         for (int q = 0; q < 4; ++q) wait_flag(&L.pf[q], t - 1);
@@ -576,6 +599,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     }
     if (w == 0) {  // the proposal fold: encoding columns (from wave 8), then [mean, std] of x_dyn
       if (poll_row(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
+        PT(t, 8);
         const Ctx4 c = row_ctx(L.rowa, tiles, N);
         wait_flag(&L.fE, t + 1);
         if (fold_lane) {
@@ -631,14 +655,14 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
   const int i = tile * kTile + slot;
   const bool valid = i < N;
   constexpr int nsd = kNsDyn;
-  cf2 *const dyn0 = wptr2(d.dyn_params);
-  const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
   int round = 0;
   for (int t = 0; t < d.T; ++t) {
+    const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
+    const PassWs &ws = *(const PassWs *)kernarg_ws();
+    cf2 *dyn = wptr2(d.dyn_params);
+    const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const RowSlot S = row_slot(d, b, t);
-    cf2 *dyn = dyn0;
-    asm volatile("" : "+s"(dyn));
     if constexpr (FORCE) pass_resample(d, ws, L, b, tile, tag0, t, round);
     PT(t, 0);
     wait_flag(&L.qf[g], t + 1);
@@ -841,12 +865,21 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
   if (threadIdx.x < 8) L.ef[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = L.pcnt = 0;
   __syncthreads();
-  if (threadIdx.x < 4 * 64)
+#ifndef NFDPF_PRIO_CHAIN
+#define NFDPF_PRIO_CHAIN 0
+#define NFDPF_PRIO_PRIOR 0
+#define NFDPF_PRIO_ENC 0
+#endif
+  if (threadIdx.x < 4 * 64) {
+    __builtin_amdgcn_s_setprio(NFDPF_PRIO_CHAIN);
     pass_chain<FORCE>(d, ws, L, b, tile, tag0);
-  else if (threadIdx.x < 8 * 64)
+  } else if (threadIdx.x < 8 * 64) {
+    __builtin_amdgcn_s_setprio(NFDPF_PRIO_PRIOR);
     pass_prior<FORCE>(d, ws, L, b, tile, tag0);
-  else
+  } else {
+    __builtin_amdgcn_s_setprio(NFDPF_PRIO_ENC);
     pass_encoder<FORCE>(d, ws, L, b, tile, tag0);
+  }
 }
 
 __global__ void tiled_pass_epoch_kernel() {

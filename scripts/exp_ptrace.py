@@ -1,12 +1,12 @@
 """Experiment: per-step phase timestamps of the one-launch pass (lib built with
 -DNFDPF_EXP_PTRACE, loaded through NFDPF_LIB; scripts/exp_build.sh PTRACE -DNFDPF_EXP_PTRACE).
-C2 bench workload, the last of 3 passes; phases as durations (us), median over the 256
-workgroups and steps 4..45.
-Flow waves 0 (t-net + exchange poller) and 1 (s-net): 0 step start, 1 A published, 2 nf_dyn
-context folded (fA), 3 nf_dyn inverse done, 4 proposal folded (fB), 5 proposal inverse done,
-6 nf_dyn forward + densities done.  Encoder wave 8: 0 step start, 1 C(t-1) swept, 2 encoding
-fold (fE), 3 slot t-1 normalised, 4 proposal received, 5 encoder done, 6 log-weight, 7 C(t)
-published."""
+C2 bench workload, the last of 3 passes; durations in us, median over the 256 workgroups and
+steps 4..45.
+Chain waves 0-3: 0 step start, 1 A published, 2 nf_dyn context folded (fA), 3 nf_dyn inverse
+done, 4 proposal folded (fB), 5 proposal handed over (qf); wave 0 also 7 A swept, 8 B swept.
+Prior waves 4-7: 0 step start, 1 proposal received, 2 prior done.  Encoder wave 8: 0 step
+start, 1 encoding fold (fE), 2 C(t-1) swept, 3 slot t-1 normalised, 4 proposal received,
+5 encoder done, 6 log-weight, 7 C(t) published."""
 import ctypes
 import os
 import sys
@@ -32,52 +32,30 @@ for _ in range(3):
     eng.run(enc, start, vel, shard=ShardInfo.from_env(B))
 torch.cuda.synchronize()
 print("pass ran as one launch:", eng.last_pass)
-buf = np.zeros((256, 16, 64, 20), dtype=np.uint64)
+buf = np.zeros((256, 16, 64, 12), dtype=np.uint64)
 assert _lib.lib().nfdpf_exp_ptrace_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
-tr = buf.astype(np.int64)[:, [0, 1, 8, 2, 4, 6]]  # waves 0, 1, 8, then role-0 waves 2, 4, 6
-steps = slice(4, 46)
-for wi, name, nph in ((0, "flow w0", 7), (1, "flow w1", 7), (2, "enc w8", 8)):
-    x = tr[:, wi, :, :nph]
-    d = (np.diff(x, axis=-1) / 100.0)[:, steps]
-    per_step = (x[:, 5:47, 0] - x[:, 4:46, 0]) / 100.0
-    print(f"{name}: step {np.median(per_step):.2f} us |", " ".join(
-        f"{k}->{k + 1} {np.median(d[..., k]):.2f}" for k in range(nph - 1)))
-x = tr[:, 0, steps]
-print(f"flow w0: A poll wait {np.median((x[..., 7] - x[..., 1]) / 100):.2f} us, A ctx + fold {np.median((x[..., 2] - x[..., 7]) / 100):.2f} us")
-# skew between the row's tiles: A published (flow w0 phase 1) by the row's 4 workgroups
-pub = tr[:, 0, steps, 1].reshape(-1, 4, tr[:, 0, steps, 1].shape[-1])  # (row, tile, step)
-print(f"A publish skew within a row: med {np.median((pub.max(1) - pub.min(1)) / 100):.2f} us")
-done = tr[:, 0, steps, 7].reshape(-1, 4, pub.shape[-1])
-print(f"A poll done after the row's last publish: med {np.median((done - pub.max(1)[:, None, :]) / 100):.2f} us")
-st = tr[:, 0, steps, 8].reshape(done.shape)
-iss = tr[:, 0, steps, 9].reshape(done.shape)
-print(f"A store acked after own publish: med {np.median((x[..., 8] - x[..., 1]) / 100):.2f} us; "
-      f"poll iterations med {np.median(x[..., 10]):.0f}")
-print(f"successful A load: issued {np.median((iss - pub.max(1)[:, None, :]) / 100):.2f} us after the row's last "
-      f"publish, {np.median((iss - st.max(1)[:, None, :]) / 100):.2f} us after its last store ack; "
-      f"round trip {np.median((done - iss) / 100):.2f} us")
-allpub = tr[:, [0, 3, 4, 5]][:, :, steps, 1]  # (wg, wave, step)
-allpub = allpub.reshape(-1, 4, 4, allpub.shape[-1]).reshape(-1, 16, allpub.shape[-1])  # (row, tile*wave, step)
-lastall = allpub.max(1)
-print(f"A: last publish of all 16 role-0 waves after wave 0's last: med {np.median((lastall - pub.max(1)) / 100):.2f} us; "
-      f"poll done after it {np.median((done - lastall[:, None, :]) / 100):.2f} us; "
-      f"successful load issued after it {np.median((iss - lastall[:, None, :]) / 100):.2f} us")
-w0s = tr[:, [0, 3, 4, 5]][:, :, steps, 0]
-print("step start per role-0 wave rel. wave 0 (med us):", [round(float(np.median((w0s[:, k] - w0s[:, 0]) / 100)), 2) for k in range(4)])
-print("A publish per role-0 wave rel. wave 0 (med us):", [round(float(np.median((tr[:, [0, 3, 4, 5]][:, k, steps, 1] - tr[:, 0, steps, 1]) / 100)), 2) for k in range(4)])
-fl = tr[:, 0, steps]
-en = tr[:, 2, steps]
-print(f"B: poll done after wave 0's B publish-ready (phase 3) {np.median((fl[..., 11] - fl[..., 3]) / 100):.2f} us; "
-      f"fE set {np.median((en[..., 2] - fl[..., 3]) / 100):.2f} us after phase 3; fB set {np.median((fl[..., 4] - fl[..., 11]) / 100):.2f} us after the B poll")
-print(f"fraction of steps where fE is set after the B poll: {np.mean(en[..., 2] > fl[..., 11]):.2f}")
-full = buf.astype(np.int64)
-for wv in (0, 1, 4, 5):
-    z = full[:, wv, steps]
-    print(f"wave {wv} first nf_dyn coupling: net {np.median((z[..., 13] - z[..., 12]) / 100):.2f} swap {np.median((z[..., 14] - z[..., 13]) / 100):.2f} "
-          f"net {np.median((z[..., 15] - z[..., 14]) / 100):.2f} swap {np.median((z[..., 16] - z[..., 15]) / 100):.2f} | "
-          f"start rel. wave 0 {np.median((z[..., 12] - full[:, 0, steps, 12]) / 100):.2f}")
-# cross-wave: encoder's C(t) publish vs the flow step end
-f_end = tr[:, 0, :, 6]
-e_pub = tr[:, 2, :, 7]
-print(f"enc C(t) published after flow step end: med {np.median((e_pub - f_end)[:, steps]) / 100:.2f} us")
-print(f"enc proposal received after flow qf set: med {np.median((tr[:, 2, :, 4] - tr[:, 0, :, 5])[:, steps]) / 100:.2f} us")
+tr = buf.astype(np.int64)
+S = slice(4, 46)
+
+
+def med(x):
+    return float(np.median(x / 100.0))
+
+
+for wv, name, nph in ((0, "chain w0", 6), (3, "chain w3", 6), (4, "prior w4", 3), (7, "prior w7", 3), (8, "enc w8", 8)):
+    x = tr[:, wv, :, :nph]
+    d = np.diff(x, axis=-1)[:, S]
+    step = x[:, 5:47, 0] - x[:, 4:46, 0]
+    print(f"{name}: step {med(step):.2f} us |", " ".join(f"{k}->{k + 1} {med(d[..., k]):.2f}" for k in range(nph - 1)))
+ch = tr[:, 0:4, S]  # (wg, wave, step, k)
+print("chain step start rel. wave 0 (us):", [round(med(ch[:, k, :, 0] - ch[:, 0, :, 0]), 2) for k in range(4)])
+pub = ch[..., 1].reshape(-1, 4 * 4, ch.shape[2])  # (row, tile*wave, step)
+last = pub.max(1)
+w0 = tr[:, 0, S].reshape(-1, 4, ch.shape[2], 12)  # (row, tile, step, k)
+print(f"A: publish spread in a row {med(pub.max(1) - pub.min(1)):.2f}; swept {med(w0[..., 7] - last[:, None, :]):.2f} after the last "
+      f"publish; ctx + fold {med(w0[..., 2] - w0[..., 7]):.2f}")
+bp = tr[:, 0:4, S, 3].reshape(-1, 16, ch.shape[2]).max(1)
+print(f"B: swept {med(w0[..., 8] - bp[:, None, :]):.2f} after the last nf_dyn inverse; fold + fB {med(w0[..., 4] - w0[..., 8]):.2f}")
+en = tr[:, 8, S]
+print(f"fE(t) set rel. wave 0's B sweep: {med(en[..., 1] - tr[:, 0, S, 8]):.2f} (>0: the B fold waited for it)")
+print(f"prior done after qf: {med(tr[:, 4, S, 2] - tr[:, 0, S, 5]):.2f}; enc C(t) published after qf: {med(en[..., 7] - tr[:, 0, S, 5]):.2f}")
