@@ -426,7 +426,8 @@ NFDPF_API int64_t nfdpf_filter_desc_size(void);
  * by step with nfdpf_filter_step_tiled if one fired).  Replaces the T iterations of
  * nfdpf_filter_step_tiled (+ the last normalisation and the pred / lw_sum reduction) for the
  * configuration nfdpf_filter_pass_supported accepts: split RealNVP nf_dyn, NF_cond, the cosine
- * measurement, device RNG, N <= 1024, n_flows <= 2, not forced, and a (tiles, B) grid of
+ * measurement, device RNG, N <= 1024, n_flows <= 2, the soft resampler when forced (every step
+ * then resamples inside the launch and there is no gate to verify), and a (tiles, B) grid of
  * 1024-thread workgroups that is resident on the current device all at once.
  * Descriptor fields as nfdpf_filter_step_tiled at t = 0, except:
  *   x_prev / p_prev: the initial particles / probabilities;  vel: [T][B][2], every step's velocity;
@@ -453,6 +454,14 @@ NFDPF_API int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, int
  * the +1e-12 terms iff t0 + t > 0).  Verifies a speculative pass (every gate assumed off). */
 NFDPF_API int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int N, int t0, int force,
                                          int32_t *gates, void *stream);
+/* The verification of a speculative pass as ONE stream-ordered launch (capturable in a graph, no
+ * host synchronisation): the T gates as nfdpf_ess_gate_tiled_batch (not forced) -> gates [T], and
+ * flags [2] int32 = {how many of the T gates fired, the wave hand-off fault count since the last
+ * read -- nfdpf_split_fault's counter, read and cleared on the device}.  The caller reads flags
+ * once after the pass.  No reference counterpart (the reference checks each gate as it goes,
+ * DPFs.py:163-165). */
+NFDPF_API int nfdpf_pass_verify(const double *parts, int T, int B, int N, int t0, int32_t *gates, int32_t *flags,
+                                void *stream);
 
 #ifdef __cplusplus
 }

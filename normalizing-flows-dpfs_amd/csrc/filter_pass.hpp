@@ -131,7 +131,9 @@ struct PassLds {
   uint32_t rowc[kPassMaxTiles * 8 * kGC];  // wave 8's C sweep
   RowNorm rn[2];                   // slot s's row normaliser, by parity of s
   int fA, fB, fE, fR;              // step-tagged flags (see the header comment)
-  int qf[4], rf[4], pf[4], ef[8];
+  int qf[4], rf[4];
+  alignas(8) int pf[4];
+  alignas(8) int ef[8];
   int fS, fbar, pcnt;              // FORCE: resampling done, flow-wave barrier, encoder weights drained
 };
 
@@ -253,7 +255,24 @@ __device__ __forceinline__ Ctx4 row_ctx(const uint32_t *rw, int tiles, int N) {
     for (int g = 1; g < 4; ++g) tk += lds_double(rw, (k * 4 + g) * kGA + 2 * c);
     a += tk;
   }
-  return ctx_from_sums(readlane_d(a, 0), readlane_d(a, 1), readlane_d(a, 2), readlane_d(a, 3), N);
+  // ctx_from_sums's arithmetic with its two components on two lanes (lane k: mean and std of
+  // component k), one division chain per lane instead of both in sequence
+  const int k = threadIdx.x & 1;
+  const double s = k ? readlane_d(a, 1) : readlane_d(a, 0), q = k ? readlane_d(a, 3) : readlane_d(a, 2);
+  const double m = s / N;
+  const float sd = (float)sqrt((q - s * m) / (N - 1));
+  const float mf = (float)m;
+  return Ctx4{readlane_f(mf, 0), readlane_f(mf, 1), readlane_f(sd, 0), readlane_f(sd, 1)};
+}
+// wait until both adjacent LDS flags f[0], f[1] reach v (one 8-byte read per poll)
+__device__ __forceinline__ void wait_flag2(const int *f, int v) {
+  Spin s;
+  for (;;) {
+    const uint64_t w = *(volatile __attribute__((address_space(3))) uint64_t *)f;
+    const int a = __builtin_amdgcn_readfirstlane((int)(uint32_t)w), c = __builtin_amdgcn_readfirstlane((int)(w >> 32));
+    if ((a >= v && c >= v) || !pass_spin<NFDPF_PASS_FLAG_SLEEP>(s)) break;
+  }
+  asm volatile("" ::: "memory");
 }
 
 // the motion noise of step t (motion_noise's device-RNG branch with an explicit step)
@@ -526,6 +545,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
   }
   constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
   int round = 0;  // flow_barrier rounds (FORCE)
+  float en0 = 0.f, en1 = 0.f;  // the next step's motion noise
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
@@ -545,10 +565,13 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         src = L.rs.src_l[slot];
       }
     }
-    // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps
+    // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps; eps drawn during the
+    // previous step's B exchange (en0, en1)
     float e0 = 0.f, e1 = 0.f, p0 = 0.f, p1 = 0.f;
+    if (t == 0 && valid) pass_noise(d, 0, grow, i, en0, en1);
     if (valid) {
-      pass_noise(d, t, grow, i, e0, e1);
+      e0 = en0;
+      e1 = en1;
       p0 = (x0 + v0) + e0;
       p1 = (x1 + v1) + e1;
       S.hnoise[2 * i] = e0;
@@ -564,11 +587,13 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     }
     PT(t, 1);
     if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
+      // cbd[par] was last read by the prior waves at step t - 2
+      if (t >= 2) {
+        wait_flag2(&L.pf[0], t - 1);
+        wait_flag2(&L.pf[2], t - 1);
+      }
       const bool ok = poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa);
       PT(t, 7);
-      // cbd[par] was last read by the prior waves at step t - 2
-      if (t >= 2)
-        for (int q = 0; q < 4; ++q) wait_flag(&L.pf[q], t - 1);
       if (ok) {
         const Ctx4 c = row_ctx(L.rowa, tiles, N);
         if (fold_lane) {
@@ -597,6 +622,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       wave_sum_dpp_n(s);
       publish4(ws.gb + gslot * kGA, s, tag);  // exchange B
     }
+    if (valid && t + 1 < d.T) pass_noise(d, t + 1, grow, i, en0, en1);  // while the B sweep waits
     if (w == 0) {  // the proposal fold: encoding columns (from wave 8), then [mean, std] of x_dyn
       if (poll_row(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
         PT(t, 8);
@@ -620,10 +646,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     if (valid)
       for (int f = nfl - 1; f >= 0; --f) ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
     // the group's encoder pair has read qbuf / rbuf[par] of step t - 2
-    if (t >= 2) {
-      wait_flag(&L.ef[2 * g], t - 1);
-      wait_flag(&L.ef[2 * g + 1], t - 1);
-    }
+    if (t >= 2) wait_flag2(&L.ef[2 * g], t - 1);
     if (valid) {  // to the prior wave and the encoder pair
       L.qbuf[par][slot] = q0;
       L.qbuf[par][kTile + slot] = q1;

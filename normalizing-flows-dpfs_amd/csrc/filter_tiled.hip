@@ -1876,6 +1876,33 @@ __global__ void tiled_gate_batch_kernel(const double *__restrict__ parts, int B,
   if (threadIdx.x == 0) gates[k] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 
+// The verification of a speculative pass in one launch: the T gates (a wave per step, the
+// batch kernel's arithmetic), the number that fired and the hand-off fault counter (read and
+// cleared) into flags -- stream-ordered and capturable, so the host reads one word pair after
+// the pass instead of synchronising for the fault counter and again for the gates.
+__global__ __launch_bounds__(1024) void tiled_gate_verify_kernel(const double *__restrict__ parts, int T, int B,
+                                                                 int tiles, int N, int t0, int32_t *gates,
+                                                                 int32_t *flags) {
+  __shared__ int fired;
+  if (threadIdx.x == 0) fired = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int k = threadIdx.x >> 6; k < T; k += blockDim.x >> 6) {
+    const double *p = parts + (int64_t)k * B * tiles * kSm;
+    const float s =
+        cascade_row_sum([&](int r) { return row_inv_ess(p + (int64_t)r * tiles * kSm, tiles, N, t0 + k > 0); }, B);
+    const int gk = (s / (float)B) < 0.5f * (float)N ? 1 : 0;
+    if ((threadIdx.x & 63) == 0) gates[k] = gk;
+    mine += gk;
+  }
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&fired, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flags[0] = fired;
+    flags[1] = atomicExch(&g_split_fault, 0);
+  }
+}
+
 // the flows run on wave pairs when the blobs carry the split suffix (RealNVP nf_dyn)
 static bool use_split(const nfdpf_filter_desc &d) { return d.split_nets && d.nf_dyn == NFDPF_DYN_REALNVP; }
 // front + dyn in one launch (tiled_fdyn_kernel), the deferred normalisation in the proposal
@@ -2081,6 +2108,13 @@ extern "C" int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int
   if (T == 0) return NFDPF_OK;
   tiled_gate_batch_kernel<<<T, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, t0, force, gates);
   return launch_status("nfdpf_ess_gate_tiled_batch");
+}
+
+extern "C" int nfdpf_pass_verify(const double *parts, int T, int B, int N, int t0, int32_t *gates, int32_t *flags,
+                                 void *stream) {
+  NFDPF_REQUIRE(parts && gates && flags && T >= 1 && B >= 1 && N >= 1 && t0 >= 0, "nfdpf_pass_verify: bad arguments");
+  tiled_gate_verify_kernel<<<1, 1024, 0, as_stream(stream)>>>(parts, T, B, n_tiles(N), N, t0, gates, flags);
+  return launch_status("nfdpf_pass_verify");
 }
 
 extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,

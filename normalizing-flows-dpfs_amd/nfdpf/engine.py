@@ -523,7 +523,10 @@ class FilterEngine:
         handoffs = d.split_nets or (d.measurement == L.MEAS["CRNVP"] and not d.nf_cond
                                     and os.environ.get("NFDPF_CM_TWO_CHAIN", "0") == "1")
         check_split = tiled and handoffs and not torch.cuda.is_current_stream_capturing()
-        if check_split and (finish or not spec):
+        # one-shard speculative pass: the gates and the fault counter are verified by ONE queued
+        # launch (ops.pass_verify, capturable) and read once in finish_pending
+        verify_dev = spec and tiled and shard.world == 1
+        if check_split and (finish or not spec) and not verify_dev:
             L.check_split_fault("nfdpf_filter_step_tiled", dev)
             check_split = False
         if c.resampler == "ot" and not spec:
@@ -532,7 +535,12 @@ class FilterEngine:
         tot = lw_sum.double().sum(0)
         if spec:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
-            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None)
+            verify = None
+            if verify_dev:
+                flags = ops.pass_verify(ess_hist[:T], N)[1]
+                verify = (flags, (tot / (shard.B_global * N)).sum().float())
+                check_split = False
+            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify)
             if not finish:
                 return res  # the caller verifies (finish_pending, e.g. after each graph replay)
             ok = self.finish_pending()
@@ -559,7 +567,16 @@ class FilterEngine:
         evaluate all T gates (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the
         obs-likelihood into the result.  False: some gate fired -- the pass is not the
         reference's and must be rerun without speculation (run(..., speculate=False))."""
-        parts, tot, shard, N, res, split_dev = self._pending
+        parts, tot, shard, N, res, split_dev, verify = self._pending
+        if verify is not None:  # ops.pass_verify's flags: the one host synchronisation
+            fired, faults = verify[0].tolist()
+            if faults:
+                raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "
+                                   f"(outputs invalid)")
+            if fired:
+                return False
+            res.obs_likelihood = verify[1]
+            return True
         if split_dev is not None:
             L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
         tot = tot.clone()

@@ -564,5 +564,18 @@ def ess_gate_tiled_batch(parts, N, t0=0, force=False, out=None):
     return g
 
 
+def pass_verify(parts, N, t0=0):
+    """[T, B_global, tiles, 4] step partials of a speculative pass -> (gates int32 [T], flags int32
+    [2] = {gates fired, hand-off faults since the last read}), one launch, no host sync
+    (include/nfdpf.h nfdpf_pass_verify)."""
+    T, B = parts.shape[0], parts.shape[1]
+    parts = parts.to(torch.float64).contiguous()
+    g = torch.empty(T, device=parts.device, dtype=torch.int32)
+    flags = torch.empty(2, device=parts.device, dtype=torch.int32)
+    check(lib().nfdpf_pass_verify(ptr(parts), T, B, N, int(t0), ptr(g), ptr(flags), stream_ptr(parts.device)),
+          "nfdpf_pass_verify")
+    return g, flags
+
+
 def filter_step_tiled(desc: L.FilterDesc, ws: torch.Tensor, device):
     check(lib().nfdpf_filter_step_tiled(desc, _aligned_ptr(ws), stream_ptr(device)), "nfdpf_filter_step_tiled")

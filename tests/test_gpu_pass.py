@@ -202,6 +202,29 @@ def test_pass_deterministic_and_graph_replay():
         assert torch.equal(cap.obs_likelihood, a.obs_likelihood)
 
 
+@pytest.mark.parametrize("T,B,N", [(37, 5, 300), (50, 64, 1000), (1, 3, 1024)])
+def test_pass_verify_matches_gate_batch(T, B, N):
+    """ops.pass_verify (one launch: gates + fired count + the hand-off fault counter) == the
+    batch gate kernel on the same partials, with a mix of fired and quiet steps."""
+    from nfdpf import ops
+    tiles = (N + 255) // 256
+    g = torch.Generator().manual_seed(T * 7 + B)
+    odd = (torch.arange(T)[:, None, None] % 2 == 1).double()
+    m = torch.randn(T, B, tiles, generator=g, dtype=torch.float64) * odd
+    # even steps nearly uniform weights (ESS ~ N: quiet), odd steps peaked (fired)
+    spread = 0.01 + 30.0 * odd
+    e = torch.rand(T, B, tiles, generator=g, dtype=torch.float64) * 250 + 1
+    sq = e * e / 256 * (1 + spread)
+    parts = torch.stack([m, e, sq, torch.zeros_like(m)], -1).to(DEV)
+    ref = ops.ess_gate_tiled_batch(parts, N, 0, False)
+    gates, flags = ops.pass_verify(parts, N)
+    torch.cuda.synchronize()
+    assert torch.equal(gates, ref)
+    assert flags.tolist() == [int(ref.sum()), 0]
+    if T > 1:
+        assert 0 < int(ref.sum()) < T, "the case should mix fired and quiet steps"
+
+
 def test_pass_disabled_by_env(monkeypatch):
     """NFDPF_PASS=0 keeps the step-by-step launches (the library reads it per call)."""
     fx = load("e2e_c2.npz")
