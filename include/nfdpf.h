@@ -454,14 +454,15 @@ NFDPF_API int nfdpf_ess_gate_tiled(const double *parts, int B, int N, int t, int
  * the +1e-12 terms iff t0 + t > 0).  Verifies a speculative pass (every gate assumed off). */
 NFDPF_API int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int N, int t0, int force,
                                          int32_t *gates, void *stream);
-/* The verification of a speculative pass as ONE stream-ordered launch (capturable in a graph, no
- * host synchronisation): the T gates as nfdpf_ess_gate_tiled_batch (not forced) -> gates [T], and
+/* The verification of a one-shard speculative pass, stream-ordered (capturable in a graph, no
+ * host synchronisation): the T gates as nfdpf_ess_gate_tiled_batch (not forced) -> gates [T];
  * flags [2] int32 = {how many of the T gates fired, the wave hand-off fault count since the last
- * read -- nfdpf_split_fault's counter, read and cleared on the device}.  The caller reads flags
- * once after the pass.  No reference counterpart (the reference checks each gate as it goes,
- * DPFs.py:163-165). */
-NFDPF_API int nfdpf_pass_verify(const double *parts, int T, int B, int N, int t0, int32_t *gates, int32_t *flags,
-                                void *stream);
+ * read -- nfdpf_split_fault's counter, read and cleared on the device}; obs [1] = the
+ * obs-likelihood sum_t (sum_b lw_sum[b][t]) / (B N) (DPFs.py:191) from the pass's lw_sum [B][T].
+ * The caller reads flags once after the pass.  No reference counterpart (the reference checks
+ * each gate as it goes, DPFs.py:163-165). */
+NFDPF_API int nfdpf_pass_verify(const double *parts, const float *lw_sum, int T, int B, int N, int t0,
+                                int32_t *gates, int32_t *flags, float *obs, void *stream);
 
 #ifdef __cplusplus
 }

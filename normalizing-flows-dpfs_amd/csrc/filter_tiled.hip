@@ -1819,16 +1819,27 @@ __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_de
 }
 
 // per-row prediction / obs-likelihood sums of every step (after the last step)
+// (entries: a multiple of 8, read 8 at a time so the loads overlap; added in entry order)
 __global__ void tiled_finalize_kernel(const double *__restrict__ fin, int BT, int tiles,
                                       float *__restrict__ pred, float *__restrict__ lw_sum) {
   const int bt = blockIdx.x * blockDim.x + threadIdx.x;
   if (bt >= BT) return;
   double px = 0, py = 0, sw = 0;
-  for (int k = 0; k < tiles; ++k) {
-    const double *f = fin + ((int64_t)bt * tiles + k) * 4;
-    px += f[1];
-    py += f[2];
-    sw += f[3];
+  for (int k0 = 0; k0 < tiles; k0 += 8) {
+    double a[8][3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double *f = fin + ((int64_t)bt * tiles + k0 + j) * 4;
+      a[j][0] = f[1];
+      a[j][1] = f[2];
+      a[j][2] = f[3];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      px += a[j][0];
+      py += a[j][1];
+      sw += a[j][2];
+    }
   }
   pred[2 * bt] = (float)px;
   pred[2 * bt + 1] = (float)py;
@@ -1876,30 +1887,31 @@ __global__ void tiled_gate_batch_kernel(const double *__restrict__ parts, int B,
   if (threadIdx.x == 0) gates[k] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
 }
 
-// The verification of a speculative pass in one launch: the T gates (a wave per step, the
-// batch kernel's arithmetic), the number that fired and the hand-off fault counter (read and
-// cleared) into flags -- stream-ordered and capturable, so the host reads one word pair after
-// the pass instead of synchronising for the fault counter and again for the gates.
-__global__ __launch_bounds__(1024) void tiled_gate_verify_kernel(const double *__restrict__ parts, int T, int B,
-                                                                 int tiles, int N, int t0, int32_t *gates,
-                                                                 int32_t *flags) {
-  __shared__ int fired;
-  if (threadIdx.x == 0) fired = 0;
-  __syncthreads();
-  int mine = 0;
-  for (int k = threadIdx.x >> 6; k < T; k += blockDim.x >> 6) {
-    const double *p = parts + (int64_t)k * B * tiles * kSm;
-    const float s =
-        cascade_row_sum([&](int r) { return row_inv_ess(p + (int64_t)r * tiles * kSm, tiles, N, t0 + k > 0); }, B);
-    const int gk = (s / (float)B) < 0.5f * (float)N ? 1 : 0;
-    if ((threadIdx.x & 63) == 0) gates[k] = gk;
-    mine += gk;
+// The verification of a speculative pass, stream-ordered and capturable (the host then reads
+// one word pair instead of synchronising for the fault counter and again for the gates): the T
+// gates by tiled_gate_batch_kernel, then this one-wave launch -- the number that fired, the
+// hand-off fault counter (read and cleared) and the obs-likelihood sum_t (sum_b lw[b, t]) / (B N)
+// (DPFs.py:191; fp64 in row order per step, then step order) from the pass's lw_sum [B][T].
+__global__ __launch_bounds__(64) void tiled_verify_flags_kernel(const int32_t *__restrict__ gates,
+                                                                const float *__restrict__ lw_sum, int T, int B,
+                                                                double BN, int32_t *flags, float *obs) {
+  const int l = threadIdx.x;
+  int f = 0;
+  for (int k = l; k < T; k += 64) f += gates[k];
+  for (int o = 32; o >= 1; o >>= 1) f += __shfl_xor(f, o);
+  double acc = 0.0;  // lane 0 adds the steps in order; lanes hold the step sums of 64 steps at a time
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + l;
+    double tot = 0.0;
+    if (t < T)
+      for (int b = 0; b < B; ++b) tot += (double)lw_sum[(int64_t)b * T + t];
+    const double q = tot / BN;
+    for (int k = 0; k < 64 && t0 + k < T; ++k) acc += readlane_d(q, k);
   }
-  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&fired, mine);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    flags[0] = fired;
+  if (l == 0) {
+    flags[0] = f;
     flags[1] = atomicExch(&g_split_fault, 0);
+    obs[0] = (float)acc;
   }
 }
 
@@ -2110,10 +2122,13 @@ extern "C" int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int
   return launch_status("nfdpf_ess_gate_tiled_batch");
 }
 
-extern "C" int nfdpf_pass_verify(const double *parts, int T, int B, int N, int t0, int32_t *gates, int32_t *flags,
-                                 void *stream) {
-  NFDPF_REQUIRE(parts && gates && flags && T >= 1 && B >= 1 && N >= 1 && t0 >= 0, "nfdpf_pass_verify: bad arguments");
-  tiled_gate_verify_kernel<<<1, 1024, 0, as_stream(stream)>>>(parts, T, B, n_tiles(N), N, t0, gates, flags);
+extern "C" int nfdpf_pass_verify(const double *parts, const float *lw_sum, int T, int B, int N, int t0,
+                                 int32_t *gates, int32_t *flags, float *obs, void *stream) {
+  NFDPF_REQUIRE(parts && lw_sum && gates && flags && obs && T >= 1 && B >= 1 && N >= 1 && t0 >= 0,
+                "nfdpf_pass_verify: bad arguments");
+  hipStream_t st = as_stream(stream);
+  tiled_gate_batch_kernel<<<T, 64, 0, st>>>(parts, B, n_tiles(N), N, t0, 0, gates);
+  tiled_verify_flags_kernel<<<1, 64, 0, st>>>(gates, lw_sum, T, B, (double)B * (double)N, flags, obs);
   return launch_status("nfdpf_pass_verify");
 }
 

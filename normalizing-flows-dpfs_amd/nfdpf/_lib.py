@@ -127,7 +127,8 @@ SIGNATURES = {
     "nfdpf_filter_step_tiled": (c_int, [POINTER(FilterDesc), c_void_p, c_void_p]),
     "nfdpf_ess_gate_tiled": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_ess_gate_tiled_batch": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "nfdpf_pass_verify": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "nfdpf_pass_verify": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
 }
 
 _lib = None

@@ -532,13 +532,12 @@ class FilterEngine:
         if c.resampler == "ot" and not spec:
             self._ot_fired = self.last_ot_calls > 0
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
-        tot = lw_sum.double().sum(0)
+        tot = None if verify_dev else lw_sum.double().sum(0)  # (pass_verify reduces it on the device)
         if spec:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             verify = None
             if verify_dev:
-                flags = ops.pass_verify(ess_hist[:T], N)[1]
-                verify = (flags, (tot / (shard.B_global * N)).sum().float())
+                verify = ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]
                 check_split = False
             self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify)
             if not finish:

@@ -564,17 +564,20 @@ def ess_gate_tiled_batch(parts, N, t0=0, force=False, out=None):
     return g
 
 
-def pass_verify(parts, N, t0=0):
-    """[T, B_global, tiles, 4] step partials of a speculative pass -> (gates int32 [T], flags int32
-    [2] = {gates fired, hand-off faults since the last read}), one launch, no host sync
-    (include/nfdpf.h nfdpf_pass_verify)."""
+def pass_verify(parts, lw_sum, N, t0=0):
+    """[T, B, tiles, 4] step partials and [B, T] lw_sum of a one-shard speculative pass ->
+    (gates int32 [T], flags int32 [2] = {gates fired, hand-off faults since the last read},
+    obs float32 [] = the obs-likelihood), no host sync (include/nfdpf.h nfdpf_pass_verify)."""
     T, B = parts.shape[0], parts.shape[1]
     parts = parts.to(torch.float64).contiguous()
+    lw_sum = lw_sum.to(torch.float32).contiguous()
+    assert tuple(lw_sum.shape) == (B, T)
     g = torch.empty(T, device=parts.device, dtype=torch.int32)
     flags = torch.empty(2, device=parts.device, dtype=torch.int32)
-    check(lib().nfdpf_pass_verify(ptr(parts), T, B, N, int(t0), ptr(g), ptr(flags), stream_ptr(parts.device)),
-          "nfdpf_pass_verify")
-    return g, flags
+    obs = torch.empty((), device=parts.device, dtype=torch.float32)
+    check(lib().nfdpf_pass_verify(ptr(parts), ptr(lw_sum), T, B, N, int(t0), ptr(g), ptr(flags), ptr(obs),
+                                  stream_ptr(parts.device)), "nfdpf_pass_verify")
+    return g, flags, obs
 
 
 def filter_step_tiled(desc: L.FilterDesc, ws: torch.Tensor, device):

@@ -217,10 +217,13 @@ def test_pass_verify_matches_gate_batch(T, B, N):
     sq = e * e / 256 * (1 + spread)
     parts = torch.stack([m, e, sq, torch.zeros_like(m)], -1).to(DEV)
     ref = ops.ess_gate_tiled_batch(parts, N, 0, False)
-    gates, flags = ops.pass_verify(parts, N)
+    lw = (torch.randn(B, T, generator=g) * 50).to(DEV)
+    gates, flags, obs = ops.pass_verify(parts, lw, N)
     torch.cuda.synchronize()
     assert torch.equal(gates, ref)
     assert flags.tolist() == [int(ref.sum()), 0]
+    obs_ref = float((lw.double().sum(0) / (B * N)).sum())
+    assert abs(float(obs) - obs_ref) <= 1e-6 * abs(obs_ref) + 1e-6
     if T > 1:
         assert 0 < int(ref.sum()) < T, "the case should mix fired and quiet steps"
 
