@@ -1819,13 +1819,15 @@ __global__ __launch_bounds__(kTile) void tiled_norm_kernel(const nfdpf_filter_de
 }
 
 // per-row prediction / obs-likelihood sums of every step (after the last step)
-// (entries: a multiple of 8, read 8 at a time so the loads overlap; added in entry order)
+// (entries read 8 at a time so the loads overlap, the rest one by one; added in entry order:
+// `tiles` entries per (row, step) -- n_tiles for the step launches, n_tiles * 8 for the pass)
 __global__ void tiled_finalize_kernel(const double *__restrict__ fin, int BT, int tiles,
                                       float *__restrict__ pred, float *__restrict__ lw_sum) {
   const int bt = blockIdx.x * blockDim.x + threadIdx.x;
   if (bt >= BT) return;
   double px = 0, py = 0, sw = 0;
-  for (int k0 = 0; k0 < tiles; k0 += 8) {
+  int k0 = 0;
+  for (; k0 + 8 <= tiles; k0 += 8) {
     double a[8][3];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1840,6 +1842,12 @@ __global__ void tiled_finalize_kernel(const double *__restrict__ fin, int BT, in
       py += a[j][1];
       sw += a[j][2];
     }
+  }
+  for (; k0 < tiles; ++k0) {
+    const double *f = fin + ((int64_t)bt * tiles + k0) * 4;
+    px += f[1];
+    py += f[2];
+    sw += f[3];
   }
   pred[2 * bt] = (float)px;
   pred[2 * bt + 1] = (float)py;
