@@ -77,14 +77,15 @@ struct PassWs {
   uint64_t *gb;  // [2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
   uint64_t *gc;  // [2][B][tiles][8 encoder waves][kGC]      exchange C (softmax partials)
   double *fin;   // [B][T][tiles * 8][4] per encoder wave: sum p^2, sum p x0, sum p x1, sum logw
-  // forced resampling (FORCE): one granule per tile and step parity, published once the tile's
-  // slot t weights (hist_p) and particles (hist_x), written through (sc1), have drained
-  uint64_t *gp;  // [2][B][tiles]
+  // forced resampling (FORCE): slot s's unnormalised log-weights, written through (sc1) by the
+  // encoder waves before their C(s) granules, by slot parity
+  float *gu;  // [2][B][N]
 };
 
 static int64_t pass_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(2 * bt * 4 * kGA * 8) * 2 + al256(2 * bt * 8 * kGC * 8) + al256(bt * T * 8 * 32) + al256(2 * bt * 8);
+  return al256(2 * bt * 4 * kGA * 8) * 2 + al256(2 * bt * 8 * kGC * 8) + al256(bt * T * 8 * 32) +
+         al256(2 * (int64_t)B * N * 4);
 }
 
 static PassWs pass_carve(void *ws, int B, int N, int T) {
@@ -99,7 +100,7 @@ static PassWs pass_carve(void *ws, int B, int N, int T) {
   p += al256(2 * bt * 8 * kGC * 8);
   w.fin = (double *)p;
   p += al256(bt * T * 8 * 32);
-  w.gp = (uint64_t *)p;
+  w.gu = (float *)p;
   return w;
 }
 
@@ -108,12 +109,10 @@ struct PassRs {
   float pl[kPassMaxTiles * kTile];   // the row's weights of the previous slot
   float cdf[kPassMaxTiles * kTile];  // its CDF (soft_row_search)
   float wg[kPassMaxTiles * kTile];   // the gathered weights w[idx_i] of every marker i
-  float lr_l[kTile];                 // this tile's particles: resampled log-weight,
   float xr_l[kTile][2];              // source position,
   int src_l[kTile];                  // source index (N: the reference's out-of-range edge)
   double shd[16];
   float shf[16];
-  uint32_t gpw[kPassMaxTiles];
 };
 struct PassLds {
   union {
@@ -134,7 +133,9 @@ struct PassLds {
   int qf[4], rf[4];
   alignas(8) int pf[4];
   alignas(8) int ef[8];
-  int fS, fbar, pcnt;              // FORCE: resampling done, flow-wave barrier, encoder weights drained
+  float lr_l[kTile];               // FORCE: this tile's resampled log-weights (outside the union: the
+                                   // encoder waves read it while others may start their MFMA layers)
+  int fS, fbar;                    // FORCE: resampling done, flow-wave barrier
 };
 
 __device__ __forceinline__ void gran_store(uint64_t *g, uint32_t data, uint32_t tag) {
@@ -314,36 +315,33 @@ __device__ __forceinline__ void flow_barrier(int *cnt, int &round) {
 // ---- FORCE: the soft resampling of the row at the top of step t (resamplers.py:20-60, the
 // soft.hpp recipe: bit-exact indices), by the 8 flow waves (512 threads) while the encoder
 // waves wait for its log-weights (flag fS).  Input: slot t-1's normalised weights (hist_p,
-// written by the encoder waves) and particles (hist_x, by the flow waves) of the whole row,
-// written through (sc1) by the row's tiles; a tile publishes one granule once every storing
-// wave has drained (MI355X_MICROARCH.md inter-workgroup visibility, row 1: sc1 stores,
-// vmcnt(0), the storing waves' LDS counter, one lane's sc1 flag; the polling wave, then a
-// barrier, then sc1 loads) -- or the initial state at t = 0.  Every tile searches all N
-// markers (the gathered weights' renormaliser is a cascade sum over the whole row in ATen's
-// order) and keeps its own particles' source, position and log-weight in LDS.  History slots
-// are never overwritten inside the pass, so the rare read of the NEXT row's first particle
-// (the reference's out-of-range edge, src == N) only waits for that row's tile 0 to have
-// published slot t-1 or a later one.
+// normalised here from the row's unnormalised log-weights, gu) and particles (hist_x) of the
+// whole row, both written through (sc1) by the row's tiles before the C(t-1) granules that wave
+// 8 has swept when it sets fR(t-1): an encoder wave publishes its granule after its own gu
+// stores and vmcnt(0), and after its chain wave's qf(t-1), which that wave sets behind its own
+// hist_x stores and vmcnt(0) (MI355X_MICROARCH.md inter-workgroup visibility, row 1; the sweeping
+// wave, then an LDS word it sets, then sc1 loads) -- or the initial state at t = 0.  The weights
+// are pass_norm's expression on the same u and row normaliser, so bit-equal to hist_p.  Every
+// tile searches all N markers (the gathered weights' renormaliser is a cascade sum over the whole
+// row in ATen's order) and keeps its own particles' source, position and log-weight in LDS.
+// History slots are never overwritten inside the pass, so the rare read of the NEXT row's first
+// particle (the reference's out-of-range edge, src == N) only waits for that row's tile-0
+// encoder wave 0 to have published C(t-1) or a later C.
+// fR(t-1) also means that every encoder wave of this tile has finished its MFMA layers of step
+// t-1 (it publishes C(t-1) after them): the resampling scratch (PassRs) aliases their LDS.
 __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b,
                                               int tile, uint32_t tag0, int t, int &round) {
   PassRs &R = L.rs;
   const int N = d.N, tiles = n_tiles(N), tid = threadIdx.x, nth = 8 * 64;
   const int64_t grow = d.row_base + b;
-  const uint32_t tag = tag0 + (uint32_t)t;  // slot t - 1's
-  uint64_t *gp = ws.gp + ((int64_t)((t - 1) & 1) * d.B + b) * tiles;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through particle stores
-  flow_barrier(&L.fbar, round);
+  const uint32_t tag = tag0 + (uint32_t)t;  // C(t - 1)'s
   const float *xs;  // the previous slot's particles of this row
   int64_t xs_next;  // ... and the offset of the next row's
   if (t > 0) {
-    if (tid < 64) {
-      wait_flag(&L.pcnt, 8 * t);  // the encoder waves' weights of slot t - 1 have drained
-      if (tid == 0) gran_store(gp + tile, 1u, tag);
-      poll_row(gp, tiles, tag, R.gpw);
-    }
-    flow_barrier(&L.fbar, round);
-    const float *ps = d.hist_p + ((int64_t)b * d.T + t - 1) * N;
-    for (int j = tid; j < N; j += nth) R.pl[j] = load_wt(ps + j);
+    wait_flag(&L.fR, t);  // wave 8 has swept C(t - 1): slot t - 1's row normaliser in L.rn
+    const RowNorm rn = L.rn[(t - 1) & 1];
+    const float *us = ws.gu + ((int64_t)((t - 1) & 1) * d.B + b) * N;
+    for (int j = tid; j < N; j += nth) R.pl[j] = expf(load_wt(us + j) - rn.shift) / rn.Ssum + 1e-12f;  // pass_norm's p
     xs = d.hist_x + ((int64_t)b * d.T + t - 1) * N * 2;
     xs_next = (int64_t)d.T * N * 2;
   } else {
@@ -414,12 +412,12 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   flow_barrier(&L.fbar, round);
   if (tid < kTile && i0 + tid < N) {
     const int sj = R.src_l[tid];
-    R.lr_l[tid] = logf(R.wg[i0 + tid] / R.shf[8]);
+    L.lr_l[tid] = logf(R.wg[i0 + tid] / R.shf[8]);
     const float *src = xs + 2 * (sj < N ? sj : N - 1);
     if (sj >= N && b + 1 < d.B) {
       src = xs + xs_next;
-      if (t > 0) {  // row b + 1 has published slot t - 1 (or a later one): its history is final
-        const uint64_t *g = ws.gp + ((int64_t)((t - 1) & 1) * d.B + b + 1) * tiles;
+      if (t > 0) {  // row b + 1's tile-0 encoder wave 0 has published C(t - 1) (or a later C)
+        const uint64_t *g = ws.gc + ((((int64_t)((t - 1) & 1) * d.B + b + 1) * tiles) * 8) * kGC;
         Spin sp;
         for (;;) {
           const uint32_t v = (uint32_t)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
@@ -660,6 +658,8 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         S.hx[2 * i + 1] = q1;
       }
     }
+    // FORCE: drained before qf, which the encoder pair's C(t) granules then cover
+    if (FORCE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     set_flag(&L.qf[g], t + 1);
     PT(t, 5);
     x0 = q0;
@@ -761,11 +761,7 @@ __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const Pas
   float lp = 0.f;
   if (valid_e) {
     const float p = expf(u - rn.shift) / rn.Ssum + 1e-12f;
-    float *hp = d.hist_p + ((int64_t)b * d.T + s) * d.N + i_e;
-    if (FORCE)
-      store_wt(hp, p);  // the next step's resampling reads the row's weights from other tiles
-    else
-      *hp = p;
+    d.hist_p[((int64_t)b * d.T + s) * d.N + i_e] = p;
     lp = logf(p);
     sf[0] = (double)p * p;
     sf[1] = (double)p * qx0;
@@ -799,13 +795,17 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
     PT(t, 0);
     if (we == 0) {
-      // the proposal fold over step t's encoding columns (model/models.py:338-346); encfold[par]
-      // was last read by wave 0's fold of step t - 2, before qf(t - 1) this wave has waited for
-      if (lane < ncb) {
-        const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
-        L.encfold[par][lane] = fold_acc(r, O, fold_bias0(r, O), enc_t, 0, d.E);
+      // the proposal fold over the encoding columns (model/models.py:338-346) one step ahead:
+      // step t + 1's here (step 0's too at t = 0), off the path to wave 0's fold of step t + 1.
+      // encfold[(t + 1) & 1] was last read by wave 0's fold of step t - 1, before qf(t - 1),
+      // which this wave has waited for
+      for (int s = t == 0 ? 0 : t + 1; s <= t + 1 && s < d.T; ++s) {
+        if (lane < ncb) {
+          const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
+          L.encfold[s & 1][lane] = fold_acc(r, O, fold_bias0(r, O), d.enc + ((int64_t)b * d.T + s) * d.E, 0, d.E);
+        }
+        set_flag(&L.fE, s + 1);
       }
-      set_flag(&L.fE, t + 1);
       PT(t, 1);
       if (t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
       PT(t, 2);
@@ -818,12 +818,8 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
     if constexpr (FORCE) {  // the flow waves resample the row: the log-weight of the source
-      if (t > 0) {  // slot t - 1's weights (write-through) have drained: count this wave in
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if ((threadIdx.x & 63) == 0) atomicAdd(&L.pcnt, 1);
-      }
       wait_flag(&L.fS, t + 1);
-      lr = valid_e ? L.rs.lr_l[slot_e] : 0.f;
+      lr = valid_e ? L.lr_l[slot_e] : 0.f;
     }
     // cosine measurement (model/models.py:206-219) and the log-weight (DPFs.py:187)
     PT(t, 3);
@@ -850,6 +846,10 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     }
     set_flag(&L.ef[we], t + 1);  // qbuf / rbuf[par] read: the chain wave may reuse them at t + 2
     PT(t, 6);
+    if (FORCE) {  // the row's next resampling reads u from every tile: written through, drained
+      if (valid_e) store_wt(ws.gu + ((int64_t)par * d.B + b) * N + i_e, u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     // exchange C: this wave's softmax partials (wave_partials_quad's arithmetic)
     const float mw = wave_max_dpp(valid_e ? u : -INFINITY);
     const float ev = valid_e ? expf(u - mw) : 0.f;
@@ -886,7 +886,7 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
     L.pf[threadIdx.x] = 0;
   }
   if (threadIdx.x < 8) L.ef[threadIdx.x] = 0;
-  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = L.pcnt = 0;
+  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = 0;
   __syncthreads();
 #ifndef NFDPF_PRIO_CHAIN
 #define NFDPF_PRIO_CHAIN 0
