@@ -202,37 +202,33 @@ __device__ __forceinline__ void publish4(uint64_t *g, const double (&v)[4], uint
 
 // one wave sweeps granules [0, n) of a row (n <= 192) until every tag is `tag`, leaving the
 // data words in dst (LDS); false on abort
-__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst,
-                         unsigned long long *tr = nullptr) {
+// `work` (register-only arithmetic) runs once while the first sweep's loads are in flight.
+struct NoWork {
+  __device__ void operator()() const {}
+};
+template <class Work = NoWork>
+__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst, Work work = Work()) {
   const int l = threadIdx.x & 63;
   uint64_t v[3] = {0, 0, 0};
   bool ok[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) ok[c] = 64 * c + l >= n;
   Spin sp;
-#ifdef NFDPF_EXP_PTRACE
-  unsigned long long iss = 0, its = 0;
-#endif
-  for (;;) {
-#ifdef NFDPF_EXP_PTRACE
-    iss = __builtin_amdgcn_s_memrealtime();
-    ++its;
-#endif
+  auto sweep = [&]() {
 #pragma unroll
     for (int c = 0; c < 3; ++c)
       if (!ok[c]) v[c] = __hip_atomic_load(g + 64 * c + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  sweep();
+  work();
+  for (;;) {
 #pragma unroll
     for (int c = 0; c < 3; ++c)
       if (!ok[c]) ok[c] = (uint32_t)(v[c] >> 32) == tag;
     if (__all(ok[0] && ok[1] && ok[2])) break;
     if (!pass_spin(sp)) return false;
+    sweep();
   }
-#ifdef NFDPF_EXP_PTRACE
-  if (tr && l == 0) {
-    tr[0] = iss;
-    tr[1] = its;
-  }
-#endif
 #pragma unroll
   for (int c = 0; c < 3; ++c)
     if (64 * c + l < n) dst[64 * c + l] = (uint32_t)v[c];
@@ -564,7 +560,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       }
     }
     // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps; eps drawn during the
-    // previous step's B exchange (en0, en1)
+    // previous step's A exchange (en0, en1)
     float e0 = 0.f, e1 = 0.f, p0 = 0.f, p1 = 0.f;
     if (t == 0 && valid) pass_noise(d, 0, grow, i, en0, en1);
     if (valid) {
@@ -584,13 +580,17 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       publish4(ws.ga + gslot * kGA, s, tag);
     }
     PT(t, 1);
+    // the next step's motion noise, drawn while the A sweep is in flight / fA is awaited
+    auto next_noise = [&]() {
+      if (valid && t + 1 < d.T) pass_noise(d, t + 1, grow, i, en0, en1);
+    };
     if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
       // cbd[par] was last read by the prior waves at step t - 2
       if (t >= 2) {
         wait_flag2(&L.pf[0], t - 1);
         wait_flag2(&L.pf[2], t - 1);
       }
-      const bool ok = poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa);
+      const bool ok = poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, next_noise);
       PT(t, 7);
       if (ok) {
         const Ctx4 c = row_ctx(L.rowa, tiles, N);
@@ -604,6 +604,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       }
       set_flag(&L.fA, t + 1);
     } else {
+      next_noise();
       wait_flag(&L.fA, t + 1);
     }
     PT(t, 2);
@@ -620,7 +621,6 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       wave_sum_dpp_n(s);
       publish4(ws.gb + gslot * kGA, s, tag);  // exchange B
     }
-    if (valid && t + 1 < d.T) pass_noise(d, t + 1, grow, i, en0, en1);  // while the B sweep waits
     if (w == 0) {  // the proposal fold: encoding columns (from wave 8), then [mean, std] of x_dyn
       if (poll_row(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
         PT(t, 8);

@@ -54,6 +54,13 @@ last = pub.max(1)
 w0 = tr[:, 0, S].reshape(-1, 4, ch.shape[2], 12)  # (row, tile, step, k)
 print(f"A: publish spread in a row {med(pub.max(1) - pub.min(1)):.2f}; swept {med(w0[..., 7] - last[:, None, :]):.2f} after the last "
       f"publish; ctx + fold {med(w0[..., 2] - w0[..., 7]):.2f}")
+pt = ch[..., 1].reshape(-1, 4, 4, ch.shape[2])  # (row, tile, wave, step)
+rowmin = pt.min(axis=(1, 2))[:, None, None, :]
+print("A publish rel. the row's first, median per tile:", [round(med(pt[:, k] - rowmin[:, 0]), 2) for k in range(4)])
+st0 = ch[..., 0].reshape(-1, 4, 4, ch.shape[2])
+print("chain step start rel. the row's first, median per tile:", [round(med(st0[:, k] - st0.min(axis=(1, 2))[:, None, :]), 2) for k in range(4)])
+fb = tr[:, 0, S, 4].reshape(-1, 4, ch.shape[2])
+print("fB set rel. the row's first, median per tile:", [round(med(fb[:, k] - fb.min(1)), 2) for k in range(4)])
 bp = tr[:, 0:4, S, 3].reshape(-1, 16, ch.shape[2]).max(1)
 print(f"B: swept {med(w0[..., 8] - bp[:, None, :]):.2f} after the last nf_dyn inverse; fold + fB {med(w0[..., 4] - w0[..., 8]):.2f}")
 en = tr[:, 8, S]
