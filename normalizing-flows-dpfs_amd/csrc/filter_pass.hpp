@@ -62,7 +62,7 @@ __device__ unsigned long long g_ptrace[256][16][64][12];
 #define PT(t, k)                                                                                   \
   do {                                                                                             \
     const int w_ = threadIdx.x >> 6, wi_ = w_;          \
-    const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                           \
+    const int wg_ = (b) * gridDim.x + (tile); /* logical (row, tile) */                              \
     if (wi_ >= 0 && (threadIdx.x & 63) == 0 && wg_ < 256 && (t) < 64)                             \
       g_ptrace[wg_][wi_][(t)][(k)] = __builtin_amdgcn_s_memrealtime();                             \
   } while (0)
@@ -435,6 +435,17 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   if (tid < 64) set_flag(&L.fS, t + 1);  // the encoder waves may read lr_l
 }
 
+// The pass's (row, tile) of this workgroup: a row's tiles on ONE XCD where the grid allows
+// (workgroups are dealt round-robin over the 8 XCDs: ids x, x + 8, ... share one), so the
+// row's exchanges never wait on a tile that another XCD's load or clock holds back (+0.9 % at
+// C2 on one box; any bijection is correct -- placement is for speed only)
+__device__ __forceinline__ void pass_tile_row(int &b, int &tile) {
+  const int n = gridDim.x * gridDim.y, id = blockIdx.x + gridDim.x * blockIdx.y;
+  const int lin = (n & 7) == 0 ? (id & 7) * (n >> 3) + (id >> 3) : id;
+  tile = lin % gridDim.x;
+  b = lin / gridDim.x;
+}
+
 // ---- waves 0-7: the flows, one wave per particle group and stage ---------------------------
 // The t- and s-nets of one coupling half on input u from the PAIR layout core (flows.hpp ts_pair,
 // HALF = 1: one v_pk_fma_f32 advances hidden unit j of both nets), layer 3 summed the way
@@ -688,6 +699,20 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     const RowSlot S = row_slot(d, b, t);
     if constexpr (FORCE) pass_resample(d, ws, L, b, tile, tag0, t, round);
     PT(t, 0);
+    if (g == 0) {
+      // the proposal fold over the encoding columns (model/models.py:338-346) one step ahead,
+      // while this wave waits for the proposal: step t + 1's (and step 0's at t = 0), so wave
+      // 0's B fold never waits for it.  encfold[(t + 1) & 1] was last read by wave 0's fold of
+      // step t - 1, before qf[0](t - 1), which this wave has waited for
+      const int O = d.E + 4, ncb = nfl * 4 * kH;
+      for (int s = t == 0 ? 0 : t + 1; s <= t + 1 && s < d.T; ++s) {
+        if (lane < ncb) {
+          const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
+          L.encfold[s & 1][lane] = fold_acc(r, O, fold_bias0(r, O), d.enc + ((int64_t)b * d.T + s) * d.E, 0, d.E);
+        }
+        set_flag(&L.fE, s + 1);
+      }
+    }
     wait_flag(&L.qf[g], t + 1);
     PT(t, 1);
     if (valid) {
@@ -779,7 +804,7 @@ __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const Pas
 template <bool FORCE>
 __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                              uint32_t tag0) {
-  const int tiles = n_tiles(d.N), N = d.N, ncb = d.n_flows * 4 * kH;
+  const int tiles = n_tiles(d.N), N = d.N;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, we = w - 8;
   const int role = w & 1, g = (w >> 1) & 3;
   // lanes 0-31: particles [32 role, 32 role + 32) of group g (encode_dot_mfma_half)
@@ -789,53 +814,50 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   const EncFrag2 ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
-  const int O = d.E + 4;
   for (int t = 0; t < d.T; ++t) {
     const int par = t & 1;
     const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
     PT(t, 0);
-    if (we == 0) {
-      // the proposal fold over the encoding columns (model/models.py:338-346) one step ahead:
-      // step t + 1's here (step 0's too at t = 0), off the path to wave 0's fold of step t + 1.
-      // encfold[(t + 1) & 1] was last read by wave 0's fold of step t - 1, before qf(t - 1),
-      // which this wave has waited for
-      for (int s = t == 0 ? 0 : t + 1; s <= t + 1 && s < d.T; ++s) {
-        if (lane < ncb) {
-          const FoldRef r = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
-          L.encfold[s & 1][lane] = fold_acc(r, O, fold_bias0(r, O), d.enc + ((int64_t)b * d.T + s) * d.E, 0, d.E);
-        }
-        set_flag(&L.fE, s + 1);
-      }
-      PT(t, 1);
-      if (t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
-      PT(t, 2);
-    }
     // measure_row_setup (cosine), per wave into its own LDS copy
     const float ve = lane < kE ? enc_t[lane] : 0.f;
     const double vinv = 1.0 / fmax(sqrt(wave_sum((double)ve * ve)), 1e-12);
     if (lane < kE) L.encq[we][lane] = ve;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
-    if constexpr (FORCE) {  // the flow waves resample the row: the log-weight of the source
-      wait_flag(&L.fS, t + 1);
-      lr = valid_e ? L.lr_l[slot_e] : 0.f;
-    }
-    // cosine measurement (model/models.py:206-219) and the log-weight (DPFs.py:187)
-    PT(t, 3);
-    u = 0.f;
-    if (grp) {
+    // the cosine measurement (model/models.py:206-219) of step t's proposal
+    auto encode = [&]() {
+      double ss, dot;
       wait_flag(&L.qf[g], t + 1);
       PT(t, 4);
-      double ss, dot;
 #ifndef NFDPF_EXP_NOENC
       encode_dot_mfma_half<kE>(ef, role, L.qbuf[par] + g * 64, L.qbuf[par] + kTile + g * 64, L.encq[we], ss, dot,
                                L.Hws[we]);
 #else
       ss = 1.0; dot = 0.5;  // experiment only: timing without the encoder
 #endif
-      const float lk = cos_lik(ss, dot, vinv);
       PT(t, 5);
+      return cos_lik(ss, dot, vinv);
+    };
+    float lk = 0.f;
+    if constexpr (!FORCE) {
+      // the encoder first: it needs only the proposal, and it hides the C(t - 1) exchange
+      if (grp) lk = encode();
+      if (we == 0 && t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+      PT(t, 2);
+      if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+    } else {
+      // the row's resampling at the top of step t needs slot t - 1 normalised first (fR(t - 1))
+      if (we == 0 && t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+      PT(t, 2);
+      if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+      wait_flag(&L.fS, t + 1);  // the flow waves resampled the row: the log-weight of the source
+      lr = valid_e ? L.lr_l[slot_e] : 0.f;
+      if (grp) lk = encode();
+    }
+    // the log-weight (DPFs.py:187)
+    PT(t, 3);
+    u = 0.f;
+    if (grp) {
       if (valid_e) {
         d.hist_lik[((int64_t)b * d.T + t) * N + i_e] = lk;
         qx0 = L.qbuf[par][slot_e];
@@ -877,7 +899,7 @@ template <bool FORCE>
 __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_filter_desc d, PassWs ws) {
   __shared__ PassLds L;
   int b, tile;
-  tile_row(b, tile);
+  pass_tile_row(b, tile);
   const uint32_t tag0 = g_pass_epoch << 12;
   // LDS is not cleared between workgroups: zero every flag first
   if (threadIdx.x < 4) {
