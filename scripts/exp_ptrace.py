@@ -5,8 +5,8 @@ steps 4..45.
 Chain waves 0-3: 0 step start, 1 A published, 2 nf_dyn context folded (fA), 3 nf_dyn inverse
 done, 4 proposal folded (fB), 5 proposal handed over (qf); wave 0 also 7 A swept, 8 B swept.
 Prior waves 4-7: 0 step start, 1 proposal received, 2 prior done.  Encoder wave 8: 0 step
-start, 1 encoding fold (fE), 2 C(t-1) swept, 3 slot t-1 normalised, 4 proposal received,
-5 encoder done, 6 log-weight, 7 C(t) published."""
+start, 4 proposal received, 5 encoder done, 2 C(t-1) swept, 3 slot t-1 normalised, 6 log-weight,
+7 C(t) published (the gated pass's order)."""
 import ctypes
 import os
 import sys
@@ -42,11 +42,14 @@ def med(x):
     return float(np.median(x / 100.0))
 
 
-for wv, name, nph in ((0, "chain w0", 6), (3, "chain w3", 6), (4, "prior w4", 3), (7, "prior w7", 3), (8, "enc w8", 8)):
-    x = tr[:, wv, :, :nph]
+for wv, name, order in ((0, "chain w0", range(6)), (3, "chain w3", range(6)), (4, "prior w4", range(3)),
+                        (7, "prior w7", range(3)), (8, "enc w8", (0, 4, 5, 2, 3, 6, 7)), (15, "enc w15", (0, 4, 5, 3, 6, 7))):
+    order = list(order)
+    nph = len(order)
+    x = tr[:, wv][:, :, order]
     d = np.diff(x, axis=-1)[:, S]
     step = x[:, 5:47, 0] - x[:, 4:46, 0]
-    print(f"{name}: step {med(step):.2f} us |", " ".join(f"{k}->{k + 1} {med(d[..., k]):.2f}" for k in range(nph - 1)))
+    print(f"{name}: step {med(step):.2f} us |", " ".join(f"{order[k]}->{order[k + 1]} {med(d[..., k]):.2f}" for k in range(nph - 1)))
 ch = tr[:, 0:4, S]  # (wg, wave, step, k)
 print("chain step start rel. wave 0 (us):", [round(med(ch[:, k, :, 0] - ch[:, 0, :, 0]), 2) for k in range(4)])
 pub = ch[..., 1].reshape(-1, 4 * 4, ch.shape[2])  # (row, tile*wave, step)
@@ -64,5 +67,6 @@ print("fB set rel. the row's first, median per tile:", [round(med(fb[:, k] - fb.
 bp = tr[:, 0:4, S, 3].reshape(-1, 16, ch.shape[2]).max(1)
 print(f"B: swept {med(w0[..., 8] - bp[:, None, :]):.2f} after the last nf_dyn inverse; fold + fB {med(w0[..., 4] - w0[..., 8]):.2f}")
 en = tr[:, 8, S]
-print(f"fE(t) set rel. wave 0's B sweep: {med(en[..., 1] - tr[:, 0, S, 8]):.2f} (>0: the B fold waited for it)")
 print(f"prior done after qf: {med(tr[:, 4, S, 2] - tr[:, 0, S, 5]):.2f}; enc C(t) published after qf: {med(en[..., 7] - tr[:, 0, S, 5]):.2f}")
+ef = [med(tr[:, w, S, 6] - tr[:, 0, S, 5]) for w in range(8, 16)]
+print("encoder waves 8-15: log-weight (ef) after qf(t):", [round(v, 2) for v in ef])
