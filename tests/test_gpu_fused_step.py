@@ -48,6 +48,7 @@ def _setup(T=12, force=False, from_state=False, B=64, N=1000):
 
 def _run(eng, inputs, fused, monkeypatch):
     from nfdpf import _lib
+    monkeypatch.setenv("NFDPF_PASS", "0")  # the step launches (the one-launch pass would take over)
     monkeypatch.setenv("NFDPF_FUSED_STEP", "1" if fused else "0")
     res = eng.run(*inputs)
     torch.cuda.synchronize()
@@ -82,6 +83,7 @@ def test_fused_step_resampling(mode, monkeypatch):
 
 
 def test_fused_step_graph_replay(monkeypatch):
+    monkeypatch.setenv("NFDPF_PASS", "0")
     monkeypatch.setenv("NFDPF_FUSED_STEP", "1")
     eng, inp = _setup(T=8)
     eng.run(*inp)
