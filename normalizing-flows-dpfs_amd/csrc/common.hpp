@@ -358,6 +358,54 @@ __device__ float cascade_row_sum(const Get &v, int n) {
   return tot;
 }
 
+// cascade_row_sum for 8 <= n <= 1024 (n4 <= 32 per lane, so the cascade's block size is 16 and
+// no higher level ever flushes): the same additions in the same order, with each lane's up to
+// 32 values loaded before the first add (the generic loop waits for every load in turn).
+template <class Get>
+__device__ float cascade_row_sum_1k(const Get &v, int n) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int nv = n / 8, n4 = nv / 4;
+  const int k = lane / 8, j = lane - (lane / 8) * 8;
+  const bool act = lane < 32;
+  float vals[32];
+#pragma unroll
+  for (int ii = 0; ii < 32; ++ii) vals[ii] = (act && ii < n4) ? v((ii * 4 + k) * 8 + j) : 0.f;
+  float a0 = 0.f, a1 = 0.f;
+  const float a2 = 0.f, a3 = 0.f;
+  if (act) {
+    int i = 0;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      if (16 * blk + 16 <= n4) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) a0 += vals[16 * blk + jj];
+        i += 16;
+        a1 += a0;
+        a0 = 0.f;
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 32; ++ii)
+      if (ii >= i && ii < n4) a0 += vals[ii];
+    a0 += a1;
+    a0 += a2;
+    a0 += a3;
+    if (k == 0)
+      for (int r = n4 * 4; r < nv; ++r) a0 += v(r * 8 + j);
+  }
+  const float s1 = __shfl(a0, j + 8), s2 = __shfl(a0, j + 16), s3 = __shfl(a0, j + 24);
+  float ps = a0;
+  ps += s1;
+  ps += s2;
+  ps += s3;
+  float tot = 0.f;
+  for (int r = nv * 8; r < n; ++r) tot += v(r);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) tot += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ps), q));
+  return tot;
+}
+
 // ----------------------------------------------------------------------------------------
 // misc
 // ----------------------------------------------------------------------------------------

@@ -58,7 +58,7 @@ __device__ int g_pass_abort = 0;
 #ifdef NFDPF_EXP_PTRACE
 // experiment-only: per-step phase timestamps (s_memrealtime, 100 MHz) of waves 0, 1 and 8 of
 // every workgroup, steps < 64 (scripts/exp_ptrace.py)
-__device__ unsigned long long g_ptrace[256][16][64][12];
+__device__ unsigned long long g_ptrace[256][16][64][20];
 #define PT(t, k)                                                                                   \
   do {                                                                                             \
     const int w_ = threadIdx.x >> 6, wi_ = w_;          \
@@ -335,6 +335,7 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   int64_t xs_next;  // ... and the offset of the next row's
   if (t > 0) {
     wait_flag(&L.fR, t);  // wave 8 has swept C(t - 1): slot t - 1's row normaliser in L.rn
+    PT(t, 12);
     const RowNorm rn = L.rn[(t - 1) & 1];
     const float *us = ws.gu + ((int64_t)((t - 1) & 1) * d.B + b) * N;
     for (int j = tid; j < N; j += nth) R.pl[j] = expf(load_wt(us + j) - rn.shift) / rn.Ssum + 1e-12f;  // pass_norm's p
@@ -346,14 +347,16 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     xs_next = d.x_prev_rs;
   }
   flow_barrier(&L.fbar, round);
+  PT(t, 13);
   // soft_row_search's steps on 512 threads (soft.hpp)
   SoftRow row{R.pl, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
   if (row.alpha < 1.0f) {
     if (tid < 64) {
-      const float S = cascade_row_sum([&](int j) { return row.q_raw(j); }, N);
+      const float S = (N >= 8 ? cascade_row_sum_1k([&](int j) { return row.q_raw(j); }, N) : cascade_row_sum([&](int j) { return row.q_raw(j); }, N));
       if (tid == 0) R.shf[0] = S;
     }
     flow_barrier(&L.fbar, round);
+  PT(t, 14);
     row.S = R.shf[0];
   }
   // the exact f64 prefix of q: 2 consecutive j per thread (N <= 1024), wave scans, wave order
@@ -370,6 +373,7 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     }
     if (lane == 63) R.shd[w] = inc;
     flow_barrier(&L.fbar, round);
+  PT(t, 15);
     double base = 0.0;
     for (int k = 0; k < w; ++k) base += R.shd[k];
     double run = base + inc - part;
@@ -383,6 +387,7 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     }
   }
   flow_barrier(&L.fbar, round);
+  PT(t, 16);
   const float off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)t, grow, 0u).x) * (1.0f / (float)N);
   const int i0 = tile * kTile;
   for (int i = tid; i < N; i += nth) {
@@ -401,14 +406,11 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     if (i >= i0 && i < i0 + kTile) R.src_l[i - i0] = sj;
   }
   flow_barrier(&L.fbar, round);
-  if (tid < 64) {
-    const float s2 = cascade_row_sum([&](int j) { return R.wg[j]; }, N);
-    if (tid == 0) R.shf[8] = s2;
-  }
-  flow_barrier(&L.fbar, round);
+  PT(t, 17);
+  // the tile's sources' positions (their loads in flight while wave 0 sums the gathered weights),
+  // then wave 0 turns every particle of the tile into its resampled log-weight
   if (tid < kTile && i0 + tid < N) {
     const int sj = R.src_l[tid];
-    L.lr_l[tid] = logf(R.wg[i0 + tid] / R.shf[8]);
     const float *src = xs + 2 * (sj < N ? sj : N - 1);
     if (sj >= N && b + 1 < d.B) {
       src = xs + xs_next;
@@ -431,7 +433,17 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     R.xr_l[tid][0] = x0;
     R.xr_l[tid][1] = x1;
   }
+  if (tid < 64) {
+    const float s2 = (N >= 8 ? cascade_row_sum_1k([&](int j) { return R.wg[j]; }, N)
+                             : cascade_row_sum([&](int j) { return R.wg[j]; }, N));
+#pragma unroll
+    for (int k = 0; k < kTile / 64; ++k) {
+      const int s = k * 64 + tid;
+      if (i0 + s < N) L.lr_l[s] = logf(R.wg[i0 + s] / s2);
+    }
+  }
   flow_barrier(&L.fbar, round);
+  PT(t, 18);
   if (tid < 64) set_flag(&L.fS, t + 1);  // the encoder waves may read lr_l
 }
 

@@ -32,7 +32,7 @@ for _ in range(3):
     eng.run(enc, start, vel, shard=ShardInfo.from_env(B))
 torch.cuda.synchronize()
 print("pass ran as one launch:", eng.last_pass)
-buf = np.zeros((256, 16, 64, 12), dtype=np.uint64)
+buf = np.zeros((256, 16, 64, 20), dtype=np.uint64)
 assert _lib.lib().nfdpf_exp_ptrace_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 tr = buf.astype(np.int64)
 S = slice(4, 46)
@@ -66,6 +66,10 @@ fb = tr[:, 0, S, 4].reshape(-1, 4, ch.shape[2])
 print("fB set rel. the row's first, median per tile:", [round(med(fb[:, k] - fb.min(1)), 2) for k in range(4)])
 bp = tr[:, 0:4, S, 3].reshape(-1, 16, ch.shape[2]).max(1)
 print(f"B: swept {med(w0[..., 8] - bp[:, None, :]):.2f} after the last nf_dyn inverse; fold + fB {med(w0[..., 4] - w0[..., 8]):.2f}")
+if force:
+    z = tr[:, 0, S]
+    pts = [0, 12] + [k for k in range(13, 20) if np.median(z[..., k]) > 0] + [1]
+    print("forced: chain w0 resample marks", pts, "|", " ".join(f"{pts[k]}->{pts[k + 1]} {med(z[..., pts[k + 1]] - z[..., pts[k]]):.2f}" for k in range(len(pts) - 1)))
 en = tr[:, 8, S]
 print(f"prior done after qf: {med(tr[:, 4, S, 2] - tr[:, 0, S, 5]):.2f}; enc C(t) published after qf: {med(en[..., 7] - tr[:, 0, S, 5]):.2f}")
 ef = [med(tr[:, w, S, 6] - tr[:, 0, S, 5]) for w in range(8, 16)]
