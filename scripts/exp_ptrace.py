@@ -54,7 +54,7 @@ ch = tr[:, 0:4, S]  # (wg, wave, step, k)
 print("chain step start rel. wave 0 (us):", [round(med(ch[:, k, :, 0] - ch[:, 0, :, 0]), 2) for k in range(4)])
 pub = ch[..., 1].reshape(-1, 4 * 4, ch.shape[2])  # (row, tile*wave, step)
 last = pub.max(1)
-w0 = tr[:, 0, S].reshape(-1, 4, ch.shape[2], 12)  # (row, tile, step, k)
+w0 = tr[:, 0, S].reshape(-1, 4, ch.shape[2], tr.shape[-1])  # (row, tile, step, k)
 print(f"A: publish spread in a row {med(pub.max(1) - pub.min(1)):.2f}; swept {med(w0[..., 7] - last[:, None, :]):.2f} after the last "
       f"publish; ctx + fold {med(w0[..., 2] - w0[..., 7]):.2f}")
 pt = ch[..., 1].reshape(-1, 4, 4, ch.shape[2])  # (row, tile, wave, step)
