@@ -370,7 +370,10 @@ __device__ float cascade_row_sum_1k(const Get &v, int n) {
   const bool act = lane < 32;
   float vals[32];
 #pragma unroll
-  for (int ii = 0; ii < 32; ++ii) vals[ii] = (act && ii < n4) ? v((ii * 4 + k) * 8 + j) : 0.f;
+  for (int ii = 0; ii < 32; ++ii) {  // unconditional (clamped) reads: no branch per value
+    const float x = v(min((ii * 4 + k) * 8 + j, n - 1));
+    vals[ii] = (act && ii < n4) ? x : 0.f;
+  }
   float a0 = 0.f, a1 = 0.f;
   const float a2 = 0.f, a3 = 0.f;
   if (act) {
