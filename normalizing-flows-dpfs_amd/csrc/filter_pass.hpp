@@ -1,8 +1,9 @@
 // filter_pass.hpp -- the whole T-step filtering pass of DPF.filtering_pos (DPFs.py:160-214) as
-// ONE persistent launch, for the C2-shaped path (--NF-dyn RealNVP on split nets, --NF-cond, the
-// cosine measurement, N <= 1024) when every ESS gate of the pass is taken as off (the
-// speculative-gate mode: nfdpf_ess_gate_tiled_batch verifies the T gates after the pass from the
-// per-step partials this launch leaves, and a fired gate reruns the pass step by step).
+// ONE persistent launch, for the C2-shaped path (--NF-dyn RealNVP, --NF-cond, the cosine
+// measurement, N <= 1024) when every ESS gate of the pass is taken as off (the speculative-gate
+// mode: nfdpf_pass_verify / nfdpf_ess_gate_tiled_batch verify the T gates after the pass from the
+// per-step partials this launch leaves, and a fired gate reruns the pass step by step), or with
+// the soft resampler forced every step (the row's resampling inside the launch, pass_resample).
 // Included by filter_tiled.hip (same translation unit: it shares g_split_fault).
 //
 // Why: the two-launch step (tiled_fdyn_kernel + tiled_prop_quad_kernel) is a chain of
@@ -18,29 +19,34 @@
 //   C  softmax partials {max, sum e, sum e^2} -> slot t's normalisation      (DPFs.py:187-192, utils.py:39-44)
 //
 // Grid (tiles, B) of 1024-thread workgroups, one per CU, ALL resident (the host checks the grid
-// against the occupancy; a row's workgroups wait for each other).  Waves 0-7 ("flow": the t- and
-// s-nets of 4 particle groups on wave pairs, split.hpp) and waves 8-15 ("encoder": the cosine
-// measurement's particle encoder on f32 MFMA, 32 particles per wave) run two independent loops
-// over the steps and meet only through LDS flags (step-tagged, monotonic):
+// against the occupancy; a row's workgroups wait for each other; pass_tile_row puts a row's
+// tiles on one XCD).  Each of the 4 particle groups of a tile (64 particles, one per lane) has
+// one wave per stage, the stages running independent loops over the steps and meeting only
+// through LDS flags (step-tagged, monotonic):
 //
-//   flow t:  motion -> publish A -> [wave 0: poll A, nf_dyn fold -> fA] -> nf_dyn inverse ->
-//            publish B -> [wave 0: poll B, + the encoder's encoding-column fold (fE) -> fB] ->
-//            proposal inverse -> qbuf (qf) -> nf_dyn forward + densities -> rbuf (rf)
-//   enc  t:  [wave 8: poll C(t-1) -> slot t-1's row normaliser (fR), its ESS partial] ->
-//            [wave 8: the proposal fold over step t's encoding columns -> fE] ->
-//            normalise slot t-1 (hp, the prediction / obs-likelihood partials) ->
-//            encoder on qbuf -> likelihood -> log-weight -> publish C(t)
+//   chain t (waves 0-3, issue priority 3): motion -> publish A -> [wave 0: sweep A, nf_dyn
+//            fold -> fA] -> nf_dyn inverse -> publish B -> [wave 0: sweep B, proposal fold
+//            (encoding columns from prior wave 4: fE) -> fB] -> proposal inverse -> qbuf,
+//            pbuf, rbuf's propose half (qf)
+//   prior t (waves 4-7): [wave 4: the encoding-column fold of step t+1 -> fE] -> wait qf ->
+//            nf_dyn forward of the proposal + the prior density -> rbuf (rf, pf)
+//   enc  t (waves 8-15, a pair per group): encoder on qbuf (MFMA) -> [wave 8: sweep C(t-1) ->
+//            slot t-1's row normaliser (fR), its ESS partial] -> normalise slot t-1 (hp, the
+//            prediction / obs-likelihood partials) -> log-weight (ef) -> publish C(t)
+//            (forced: the C(t-1) sweep and the normalisation first, then the encoder after the
+//            row's resampling, fS)
 //
-// so the encoder of step t runs beside the flow waves' step t+1 (motion and nf_dyn inverse).
-// Every step-indexed buffer (LDS and granules) is double-buffered by step parity; the
-// dependency chains make a second reuse safe (a tile can publish exchange X of step t+2 only
-// after every tile of its row has consumed X of step t; C: an encoder poller signals fE(t)
-// only after consuming C(t-1), and no flow wave passes the proposal fold of step t without it).
+// so the prior and the encoder of step t run beside the chain's step t+1.  Every step-indexed
+// buffer (LDS and granules) is double-buffered by step parity: the exchanges are safe by the
+// dependency chains (a tile can publish exchange X of step t+2 only after every tile of its row
+// has consumed X of step t), the LDS hand-offs by explicit flags (pf before wave 0 refolds
+// cbd, ef before a chain wave refills qbuf / pbuf / rbuf, qf[0](t-1) before wave 4 refolds
+// encfold).
 //
 // Every wait is bounded (kPassWaitTicks of wall time) and a timed-out wait raises g_pass_abort so the whole grid
 // drains promptly; the host reads g_split_fault (nfdpf_split_fault) and fails loudly.
 //
-// Reductions have a fixed order (deterministic): A / B = per role-0 flow wave DPP sums, the row
+// Reductions have a fixed order (deterministic): A / B = per chain wave DPP sums, the row
 // total over (tile, wave) in order -- the order of the three-launch tiled path (tiled_front_kernel
 // -> store_sums4, block_sum_roles_store -> tiled_ctx); the tile's softmax partial = the quad
 // launch's merge over encoder waves 8..15.
