@@ -337,6 +337,12 @@ NFDPF_API int nfdpf_rqs(const float *x, const float *W, const float *H, const fl
 NFDPF_API int nfdpf_particle_init(const float *start_xy, int B, int N, float width, int true_state,
                         uint64_t seed, int64_t row_base, float *x, float *logw, void *stream);
 
+/* torch.sum(x, -1) of each row of x [B][N] in ATen's CPU cascade order (the soft resampler's
+ * q.sum() and w.sum(), resamplers.py:33-34, 56) -> out [B]: variant 0 the generic device sum,
+ * 1 the one-launch pass's load-ahead sum for 8 <= N <= 1024 (same additions, same bits).  A test
+ * probe of the bit-exact resampler's building block; no reference counterpart. */
+NFDPF_API int nfdpf_cascade_row_sum(const float *x, int B, int N, int variant, float *out, void *stream);
+
 /* One iteration of the T loop of DPF.filtering_pos (DPFs.py:160-214), fused:
  * ESS gate (batch-global, read from ess_all) -> [soft resample | OT result] -> motion ->
  * nf_dyn inverse -> NF proposal -> nf_dyn forward -> densities -> measurement ->
@@ -397,6 +403,15 @@ typedef struct nfdpf_filter_desc {
   int32_t prof_front;       /* tiled, with prof_events: 1 = prof_events is hipEvent_t[4] and events
                                [2], [3] ride in the front launch's dispatch (ESS gate + resampling +
                                motion [+ nf_dyn]: the resampler's launch) */
+  /* nfdpf_filter_pass_tiled only (NULL / 0 elsewhere): */
+  int32_t pass_gate;        /* 0 = every ESS gate taken as off (speculative; verified after the
+                               pass), 1 = the batch-global gate decided inside the launch at every
+                               step (DPFs.py:163-165; needs B_global == B) */
+  int32_t *pass_gates;      /* optional [T] out: step t's gate -- the in-launch decisions
+                               (pass_gate 1) or the verification of a speculative pass */
+  int32_t *pass_flags;      /* optional [2] out: {gates that fired, wave hand-off faults since the
+                               last read (nfdpf_split_fault's counter, read and cleared)} */
+  float *pass_obs;          /* optional [1] out: the obs-likelihood sum_t mean_{b,n} logw (DPFs.py:191) */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
@@ -430,14 +445,22 @@ NFDPF_API int64_t nfdpf_filter_desc_size(void);
  * then resamples inside the launch and there is no gate to verify), and a (tiles, B) grid of
  * 1024-thread workgroups that is resident on the current device all at once.
  * Descriptor fields as nfdpf_filter_step_tiled at t = 0, except:
+ *   dyn_params / cond_params: the PASS layout (nfdpf.pack.pass_flow_tensors: the pair layout with
+ *   the tanh algebra folded into the weights -- W1, b1 x c, W2 x -2c, b2 -> c (b2 + rowsum W2),
+ *   W3 x -2, b3 -> b3 + rowsum W3, c = 2 log2 e; no split suffix);
  *   x_prev / p_prev: the initial particles / probabilities;  vel: [T][B][2], every step's velocity;
+ *   ess_all: [B][tiles][4], the initial partials (nfdpf_filter_tiled_init; step 0's gate input);
  *   ess_out: [T][B][tiles][4], step t's softmax partials (the gates' input; the next step's
- *   partials in include/nfdpf.h's tiled layout);  gate / ess_all / scratch / defer_norm: unused;
+ *   partials in include/nfdpf.h's tiled layout);  gate / scratch / defer_norm: unused;
+ *   pass_gate / pass_gates / pass_flags / pass_obs: above (pass_gates with pass_gate 0 asks for
+ *   the verification of a speculative pass of the whole batch, B_global == B);
  *   prof_events: optional hipEvent_t[2] riding in the pass launch's own dispatch.
  * Every history slot, pred and lw_sum are written as after the T steps of the tiled path.
- * workspace: nfdpf_filter_pass_workspace_bytes(B, N, T) bytes, 256-B aligned.  A wait between
- * the row's workgroups that times out is counted in nfdpf_split_fault (the outputs are then
- * invalid).  No reference counterpart for the query / workspace functions. */
+ * workspace: nfdpf_filter_pass_workspace_bytes(B, N, T) bytes, 256-B aligned, ZEROED by the
+ * caller when it is new or its (B, N, T) changed (its first 256 bytes carry the granule tags'
+ * epoch from pass to pass).  A wait between the row's workgroups that times out is counted in
+ * nfdpf_split_fault / pass_flags[1] (the outputs are then invalid).  No reference counterpart
+ * for the query / workspace functions. */
 NFDPF_API int nfdpf_filter_pass_supported(const nfdpf_filter_desc *d);
 NFDPF_API int64_t nfdpf_filter_pass_workspace_bytes(int B, int N, int T);
 NFDPF_API int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);

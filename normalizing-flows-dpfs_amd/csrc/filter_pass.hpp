@@ -55,11 +55,21 @@ namespace nfdpf {
 
 constexpr int kPassMaxTiles = 4;   // N <= 1024: one poll sweep of <= 192 granules per exchange
 constexpr int kPassMaxT = 4000;    // tag = (epoch << 12) + t + 1
+constexpr uint32_t kPassEpochMask = (1u << 20) - 1;  // the epoch's 20 bits of the 32-bit tag
 constexpr int kGA = 8;             // granules per flow-wave publish: 4 doubles
 constexpr int kGC = 6;             // per encoder-wave publish: max (f32), sum e, sum e^2 (f64), pad
 
-__device__ uint32_t g_pass_epoch = 0;
-__device__ int g_pass_abort = 0;
+// The pass workspace's first 256 bytes (zeroed by the caller when the workspace is new or its
+// (B, N, T) layout changed, include/nfdpf.h): the granule tags' epoch -- bumped by the epilogue
+// of every pass, so consecutive passes (and graph replays) never read each other's granules --,
+// the abort word a timed-out wait raises to drain the grid (cleared by the epilogue), and the
+// epilogue's arrival counter.  Per workspace: two passes on two streams with two workspaces do
+// not interfere.
+struct PassHdr {
+  uint32_t epoch;
+  int abort;
+  uint32_t done;
+};
 
 #ifdef NFDPF_EXP_PTRACE
 // experiment-only: per-step phase timestamps (s_memrealtime, 100 MHz) of waves 0, 1 and 8 of
@@ -79,25 +89,37 @@ __device__ unsigned long long g_ptrace[256][16][64][20];
 #endif
 
 struct PassWs {
+  PassHdr *hdr;
   uint64_t *ga;  // [2][B][tiles][4 role-0 flow waves][kGA]  exchange A (x_phys sums)
   uint64_t *gb;  // [2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
   uint64_t *gc;  // [2][B][tiles][8 encoder waves][kGC]      exchange C (softmax partials)
   double *fin;   // [B][T][tiles * 8][4] per encoder wave: sum p^2, sum p x0, sum p x1, sum logw
   // forced resampling (FORCE): slot s's unnormalised log-weights, written through (sc1) by the
   // encoder waves before their C(s) granules, by slot parity
-  float *gu;  // [2][B][N]
+  float *gu;    // [2][B][N]
+  double *eq;   // [T] the epilogue's per-step obs-likelihood terms
+  int32_t *eg;  // [T] the epilogue's per-step gates
+  uint64_t wait_ticks;  // the bound of every wait (s_memrealtime ticks; kPassWaitTicks)
 };
+
+__host__ __device__ static inline int64_t pass_granule_bytes(int B, int N) {
+  const int64_t bt = (int64_t)B * n_tiles(N);
+  auto a256 = [](int64_t v) { return (v + 255) / 256 * 256; };
+  return a256(2 * bt * 4 * kGA * 8) * 2 + a256(2 * bt * 8 * kGC * 8);
+}
 
 static int64_t pass_bytes(int B, int N, int T) {
   const int64_t bt = (int64_t)B * n_tiles(N);
-  return al256(2 * bt * 4 * kGA * 8) * 2 + al256(2 * bt * 8 * kGC * 8) + al256(bt * T * 8 * 32) +
-         al256(2 * (int64_t)B * N * 4);
+  return 256 + pass_granule_bytes(B, N) + al256(bt * T * 8 * 32) + al256(2 * (int64_t)B * N * 4) +
+         al256((int64_t)T * 8) + al256((int64_t)T * 4);
 }
 
 static PassWs pass_carve(void *ws, int B, int N, int T) {
   char *p = (char *)ws;
   const int64_t bt = (int64_t)B * n_tiles(N);
   PassWs w;
+  w.hdr = (PassHdr *)p;
+  p += 256;
   w.ga = (uint64_t *)p;
   p += al256(2 * bt * 4 * kGA * 8);
   w.gb = (uint64_t *)p;
@@ -107,6 +129,10 @@ static PassWs pass_carve(void *ws, int B, int N, int T) {
   w.fin = (double *)p;
   p += al256(bt * T * 8 * 32);
   w.gu = (float *)p;
+  p += al256(2 * (int64_t)B * N * 4);
+  w.eq = (double *)p;
+  p += al256((int64_t)T * 8);
+  w.eg = (int32_t *)p;
   return w;
 }
 
@@ -148,10 +174,29 @@ __device__ __forceinline__ void gran_store(uint64_t *g, uint32_t data, uint32_t 
   __hip_atomic_store(g, ((uint64_t)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The kernel's arguments re-read from the kernarg segment where needed: LICM would otherwise
+// keep every step-invariant field and address live in SGPRs across the step loop, and the
+// nets' weight loads would then spill them through VGPR lanes (v_writelane / v_readlane around
+// every coupling)
+typedef const __attribute__((address_space(4))) nfdpf_filter_desc kdesc_t;
+typedef const __attribute__((address_space(4))) PassWs kws_t;
+__device__ __forceinline__ kdesc_t *kernarg_desc() {
+  kdesc_t *p = (kdesc_t *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ kws_t *kernarg_ws() {
+  constexpr size_t off = (sizeof(nfdpf_filter_desc) + alignof(PassWs) - 1) / alignof(PassWs) * alignof(PassWs);
+  kws_t *p = (kws_t *)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() + off);
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // A bounded spin: false once the wait has timed out (counted once, and the whole grid told to
-// drain through g_pass_abort) or another wave's has.  The bound is wall time (s_memrealtime,
-// 100 MHz): kPassWaitTicks from the wait's first miss, far above any legitimate wait (a step
-// takes ~20 us) and short enough that a grid that cannot make progress drains within a second.
+// drain through the workspace's abort word) or another wave's has.  The bound is wall time
+// (s_memrealtime, 100 MHz): kPassWaitTicks from the wait's first miss, far above any legitimate
+// wait (a step takes ~20 us) and short enough that a grid that cannot make progress drains
+// within a second.  (NFDPF_PASS_WAIT_US overrides it per call: tests force the timeout path.)
 constexpr uint64_t kPassWaitTicks = 20000000ull;  // 200 ms
 struct Spin {
   uint64_t t0 = 0;
@@ -163,14 +208,15 @@ struct Spin {
 template <int SLEEP = 1>
 __device__ __forceinline__ bool pass_spin(Spin &s) {
   if ((s.it++ & 63) == 0) {
-    if (__hip_atomic_load(&g_pass_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    int *abort_w = &kernarg_ws()->hdr->abort;
+    if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
     if (s.it == 1) {
       s.t0 = now;
-    } else if (now - s.t0 > kPassWaitTicks) {
+    } else if (now - s.t0 > kernarg_ws()->wait_ticks) {
       if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {  // first active lane
         atomicAdd(&g_split_fault, 1);
-        __hip_atomic_store(&g_pass_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
     }
@@ -465,21 +511,29 @@ __device__ __forceinline__ void pass_tile_row(int &b, int &tile) {
 }
 
 // ---- waves 0-7: the flows, one wave per particle group and stage ---------------------------
-// The t- and s-nets of one coupling half on input u from the PAIR layout core (flows.hpp ts_pair,
-// HALF = 1: one v_pk_fma_f32 advances hidden unit j of both nets), layer 3 summed the way
-// split.hpp's net_split sums it (even and odd hidden units in two chains, then (even + odd) + b3):
-// every component sees net_split's fma sequence, so the result is bit-identical to the wave-pair
-// evaluation without its LDS hand-off.  cb = the half's folded bias pairs (fold_ref order).
+// The t- and s-nets of one coupling half on input u from the PASS layout (nfdpf.pack.
+// pass_coupling_tensors: the pair layout of flows.hpp ts_pair, HALF = 1 -- one v_pk_fma_f32
+// advances hidden unit j of both nets -- with the tanh algebra folded into the weights): every
+// hidden unit is r = 1 / (1 + 2^y) of its scaled argument y (tanh = 1 - 2 r, the -2 and the next
+// layer's 2 log2(e) live in the weights), so a unit costs exp2 + add + rcp: the tanh2 of the step
+// launches' layout also multiplies by 2 log2(e) and evaluates 1 - 2 r (two packed ops per unit
+// pair more).  Layer 3 summed the way split.hpp's net_split sums it (even and odd hidden units in
+// two chains, then (even + odd) + b3).  cb = the half's folded bias pairs (fold_ref order).
 #ifndef NFDPF_PASS_SB
 #define NFDPF_PASS_SB 1
 #endif
+// {1 / (1 + 2^y.x), 1 / (1 + 2^y.y)}: 2^y = inf -> 0, 2^y = 0 -> 1 (no NaN anywhere)
+__device__ __forceinline__ f2 sig2(f2 y) {
+  const f2 d = f2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + splat(1.0f);
+  return f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
 __device__ __forceinline__ f2 ts_half(cf2 *w, float u, const f2 *cb) {
 #if NFDPF_PASS_SB
   __builtin_amdgcn_sched_barrier(0);  // no weight loads hoisted from here into the previous half
 #endif
   f2 h[kH];
 #pragma unroll
-  for (int j = 0; j < kH; ++j) h[j] = tanh2(pfma(w[j], splat(u), cb[j]));
+  for (int j = 0; j < kH; ++j) h[j] = sig2(pfma(w[j], splat(u), cb[j]));
   cf2 *w2 = w + kH;
   f2 g[kH];
 #pragma unroll
@@ -487,7 +541,7 @@ __device__ __forceinline__ f2 ts_half(cf2 *w, float u, const f2 *cb) {
     f2 a = w2[kH * kH + j];
 #pragma unroll
     for (int k = 0; k < kH; ++k) a = pfma(w2[j * kH + k], h[k], a);
-    g[j] = tanh2(a);
+    g[j] = sig2(a);
   }
   cf2 *w3 = w2 + kH * kH + kH;
   f2 e = w3[0] * g[0], o = w3[1] * g[1];
@@ -516,24 +570,6 @@ __device__ __forceinline__ float pass_forward(cf2 *fw, int ns, float &lo, float 
   ts = ts_half(fw + ns, up, cb + kH);
   lo = ts.x + lo * expf(ts.y);
   return l1 + ts.y;
-}
-
-// The kernel's arguments re-read from the kernarg segment at the top of every step: LICM would
-// otherwise keep every step-invariant field and address live in SGPRs across the step loop,
-// and the nets' weight loads would then spill them through VGPR lanes (v_writelane /
-// v_readlane around every coupling)
-typedef const __attribute__((address_space(4))) nfdpf_filter_desc kdesc_t;
-typedef const __attribute__((address_space(4))) PassWs kws_t;
-__device__ __forceinline__ kdesc_t *kernarg_desc() {
-  kdesc_t *p = (kdesc_t *)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return p;
-}
-__device__ __forceinline__ kws_t *kernarg_ws() {
-  constexpr size_t off = (sizeof(nfdpf_filter_desc) + alignof(PassWs) - 1) / alignof(PassWs) * alignof(PassWs);
-  kws_t *p = (kws_t *)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() + off);
-  asm volatile("" : "+s"(p));
-  return p;
 }
 
 // waves 0-3 ("chain", group g = w): motion -> A -> nf_dyn inverse -> B -> proposal inverse, the
@@ -918,7 +954,7 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
   __shared__ PassLds L;
   int b, tile;
   pass_tile_row(b, tile);
-  const uint32_t tag0 = g_pass_epoch << 12;
+  const uint32_t tag0 = __hip_atomic_load(&ws.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 12;
   // LDS is not cleared between workgroups: zero every flag first
   if (threadIdx.x < 4) {
     L.qf[threadIdx.x] = 0;
@@ -947,9 +983,80 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
   }
 }
 
-__global__ void tiled_pass_epoch_kernel() {
-  g_pass_epoch = g_pass_epoch + 1u;
-  g_pass_abort = 0;
+// After the pass, on its stream: one 64-lane workgroup per step k --
+//   * pred[b][k] and lw_sum[b][k] of every row (tiled_finalize_kernel's sums over the row's
+//     tiles x 8 encoder-wave entries, in order);
+//   * with `gates_from` (a speculative one-shard pass): step k's ESS gate from its input
+//     partials (k = 0: ess_all, else the pass's ess_out[k - 1]), tiled_gate_batch_kernel's
+//     arithmetic;
+//   * q_k = sum_b lw_sum[b][k] (fp64, row order) / (B N);
+// the LAST workgroup to arrive (hdr->done) adds the q_k in step order (the obs-likelihood,
+// DPFs.py:191), counts the fired gates, reads and clears the hand-off fault counter (flags, when
+// asked), clears the abort word and bumps the epoch -- the granules of the current layout are
+// cleared when its 20 bits wrap.  Replaces the epoch, finalize, gate-batch and verify launches
+// of round 4 (one 64-lane wave walked 64 steps x B rows serially there: 18 us per pass).
+__global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_filter_desc d, PassWs ws,
+                                                                 int gates_from) {
+  __shared__ float lw_l[256];
+  __shared__ int last;
+  const int k = blockIdx.x, l = threadIdx.x, T = d.T, B = d.B, tiles = n_tiles(d.N), ent = tiles * 8;
+  for (int b = l; b < B; b += 64) {
+    const int64_t bt = (int64_t)b * T + k;
+    double px = 0, py = 0, sw = 0;
+    for (int e = 0; e < ent; ++e) {
+      const double *f = ws.fin + (bt * ent + e) * 4;
+      px += f[1];
+      py += f[2];
+      sw += f[3];
+    }
+    d.pred[2 * bt] = (float)px;
+    d.pred[2 * bt + 1] = (float)py;
+    d.lw_sum[bt] = (float)sw;
+    lw_l[b] = (float)sw;
+  }
+  int fired = 0;
+  if (gates_from) {
+    const double *parts = k == 0 ? reinterpret_cast<const double *>(d.ess_all)
+                                 : reinterpret_cast<const double *>(d.ess_out) + (int64_t)(k - 1) * B * tiles * kSm;
+    const float s =
+        cascade_row_sum([&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, d.N, k > 0); }, B);
+    fired = (s / (float)B) < 0.5f * (float)d.N ? 1 : 0;
+  }
+  __syncthreads();
+  if (l == 0) {
+    double tot = 0.0;
+    for (int b = 0; b < B; ++b) tot += (double)lw_l[b];
+    ws.eq[k] = tot / ((double)B * (double)d.N);
+    ws.eg[k] = fired;
+    if (d.pass_gates && gates_from) d.pass_gates[k] = fired;
+    // release the step's terms, then count this workgroup in
+    const uint32_t n = __hip_atomic_fetch_add(&ws.hdr->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = n == (uint32_t)T - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  const uint32_t ep = __hip_atomic_load(&ws.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  if (ep > kPassEpochMask) {  // the tags' epoch wraps: no granule of this layout may keep an old tag
+    const int64_t n = pass_granule_bytes(B, d.N) / 8;
+    for (int64_t i = l; i < n; i += 64) ws.ga[i] = 0;  // ga, gb and gc are contiguous
+  }
+  if (l == 0) {
+    double acc = 0.0;
+    int nf = 0;
+    for (int t = 0; t < T; ++t) {
+      acc += __hip_atomic_load(&ws.eq[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nf += __hip_atomic_load(&ws.eg[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (d.pass_obs) d.pass_obs[0] = (float)acc;
+    if (d.pass_flags) {
+      d.pass_flags[0] = nf;
+      d.pass_flags[1] = atomicExch(&g_split_fault, 0);
+    }
+    ws.hdr->abort = 0;
+    ws.hdr->done = 0;
+    ws.hdr->epoch = ep > kPassEpochMask ? 0u : ep;
+  }
 }
 
 // The pass applies to this descriptor's configuration (the launcher also needs the speculative
@@ -963,7 +1070,7 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   // caller takes every gate as off and verifies them afterwards
   if (d.force_resample && d.resampler != NFDPF_RESAMPLE_SOFT) return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
-      d.B < 1)
+      d.B < 1 || d.B > 256)  // (the epilogue stages a step's B row sums in LDS)
     return false;
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess ||

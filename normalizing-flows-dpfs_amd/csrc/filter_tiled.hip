@@ -2091,9 +2091,16 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_pass_tiled: a forced pass needs lin and an 8-B aligned hist_x");
   NFDPF_REQUIRE(pass_config_ok(d),
                 "nfdpf_filter_pass_tiled: configuration not supported here (nfdpf_filter_pass_supported == 0)");
+  // the epilogue's gates: a speculative pass of the whole batch (a sharded one is verified by
+  // the caller over the gathered partials, nfdpf_ess_gate_tiled_batch)
+  const int verify = !d.force_resample && d.pass_gates && d.B_global == d.B && d.ess_all;
+  NFDPF_REQUIRE(!d.pass_gates || verify, "nfdpf_filter_pass_tiled: pass_gates needs a speculative pass of the whole "
+                                         "batch (B_global == B) with its initial partials in ess_all");
   hipStream_t st = as_stream(stream);
-  tiled_pass_epoch_kernel<<<1, 1, 0, st>>>();  // new granule tags for this pass
-  const PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
+  PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
+  ws.wait_ticks = kPassWaitTicks;
+  if (const char *e = getenv("NFDPF_PASS_WAIT_US"))  // read per call (tests force a timeout)
+    ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
   const dim3 g(n_tiles(d.N), d.B);
   hipEvent_t *ev = (hipEvent_t *)d.prof_events;
   const auto kern = d.force_resample ? tiled_pass_kernel<true> : tiled_pass_kernel<false>;
@@ -2101,8 +2108,7 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
     hipExtLaunchKernelGGL(kern, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
   else
     kern<<<g, 4 * kTile, 0, st>>>(d, ws);
-  const int BT = d.B * d.T;
-  tiled_finalize_kernel<<<(BT + 255) / 256, 256, 0, st>>>(ws.fin, BT, n_tiles(d.N) * 8, d.pred, d.lw_sum);
+  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, verify);
   return launch_status("nfdpf_filter_pass_tiled");
 }
 

@@ -28,9 +28,28 @@ __global__ void particle_init_kernel(const float *__restrict__ start_xy, int B, 
   logw[o] = logf(1.0f / (float)N);  // torch.log(ones / N) (:60)
 }
 
+// torch.sum(x, -1) of each row in ATen's CPU cascade order, one wave per row: variant 0 =
+// cascade_row_sum (any n), 1 = cascade_row_sum_1k (8 <= n <= 1024, the one-launch pass's forced
+// resampling) -- the same additions in the same order, so the same bits
+__global__ __launch_bounds__(64) void cascade_row_sum_kernel(const float *__restrict__ x, int N, int variant,
+                                                             float *__restrict__ out) {
+  const float *row = x + (int64_t)blockIdx.x * N;
+  const float s = variant ? cascade_row_sum_1k([&](int j) { return row[j]; }, N)
+                          : cascade_row_sum([&](int j) { return row[j]; }, N);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
 }  // namespace nfdpf
 
 using namespace nfdpf;
+
+extern "C" int nfdpf_cascade_row_sum(const float *x, int B, int N, int variant, float *out, void *stream) {
+  NFDPF_REQUIRE(x && out && B >= 0 && N >= 1, "nfdpf_cascade_row_sum: bad arguments");
+  NFDPF_REQUIRE(!variant || (N >= 8 && N <= 1024), "nfdpf_cascade_row_sum: variant 1 needs 8 <= N <= 1024");
+  if (B == 0) return NFDPF_OK;
+  cascade_row_sum_kernel<<<B, 64, 0, as_stream(stream)>>>(x, N, variant, out);
+  return launch_status("nfdpf_cascade_row_sum");
+}
 
 extern "C" int nfdpf_particle_init(const float *start_xy, int B, int N, float width, int true_state,
                                    uint64_t seed, int64_t row_base, float *x, float *logw,

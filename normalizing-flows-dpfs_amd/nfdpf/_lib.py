@@ -46,6 +46,8 @@ class FilterDesc(Structure):
         ("prof_events", c_void_p),
         ("ess_local", c_int32),
         ("prof_front", c_int32),
+        ("pass_gate", c_int32),
+        ("pass_gates", c_void_p), ("pass_flags", c_void_p), ("pass_obs", c_void_p),
     ]
 
 
@@ -115,6 +117,7 @@ SIGNATURES = {
                                   c_float, c_void_p, c_void_p]),
     "nfdpf_particle_init": (c_int, [c_void_p, c_int, c_int, c_float, c_int, c_uint64, c_int64, c_void_p, c_void_p,
                                     c_void_p]),
+    "nfdpf_cascade_row_sum": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_filter_step": (c_int, [POINTER(FilterDesc), c_void_p]),
     "nfdpf_filter_tiled_workspace_bytes": (c_int64, [c_int, c_int, c_int]),
     "nfdpf_filter_tiled_tiles": (c_int, [c_int]),

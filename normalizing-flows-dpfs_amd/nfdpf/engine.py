@@ -33,7 +33,7 @@ import torch.distributed as dist
 from . import _lib as L
 from . import ops
 from .pack import (blob, cglow_tensors, encoder_tensors, filter_flow_tensors, flows_tensors,
-                   paired_mlp_tensors, splittable)
+                   paired_mlp_tensors, pass_flow_tensors, splittable)
 
 
 @dataclass
@@ -150,12 +150,18 @@ class FilterEngine:
         self.last_pass_ok = False  # the last run's shapes allow the one-launch pass
         self.last_pass = False     # the last run's pass ran as one launch (nfdpf_filter_pass_tiled)
         self.pass_launches = 0     # one-launch passes run by this engine (verified or not)
+        # a one-launch pass whose row hand-offs timed out (its grid was not all resident: another
+        # process or kernel held CUs) turns the pass off for this engine; the step launches rerun
+        self.pass_disabled = False
+        self._shared_device = None  # per process group: does another rank use this rank's GPU?
 
     def __getstate__(self):
         # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
         # buffers / process group and the profiling events are per-process state
         st = dict(self.__dict__)
         st.pop("_pending", None)
+        st.pop("_nfdpf_pass_ws", None)
+        st["_shared_device"] = None
         st["step_events"] = None
         return st
 
@@ -204,13 +210,16 @@ class FilterEngine:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
         the configuration, and the grid resident on the current device)?"""
         c = self.cfg
-        if not (c.kernel == "tiled" and split_nets and c.rng_mode == "device"):
+        if not (c.kernel == "tiled" and split_nets and c.rng_mode == "device") or self.pass_disabled:
             return False
         if c.force_resample and c.resampler != "soft":  # a forced pass resamples inside the launch
             return False
         # every workgroup of the grid must be resident at once: never on a device shared with
-        # another rank (the one-GPU rehearsals of a sharded run), whose kernels can hold CUs
-        if shard.world > 1 and torch.cuda.device_count() < shard.world:
+        # another rank (one-GPU rehearsals of a sharded run, or ranks that all picked device 0),
+        # whose kernels can hold CUs.  (Other processes on the device are not detectable here:
+        # a pass that times out falls back to the step launches, finish_pending.)
+        # (NFDPF_PASS_SHARED_OK=1, tests only: the caller serialises the ranks' passes itself)
+        if shard.world > 1 and os.environ.get("NFDPF_PASS_SHARED_OK") != "1" and self._device_shared(shard):
             return False
         d = L.FilterDesc()
         d.B, d.N, d.T, d.E, d.B_global, d.phase = B, N, T, E, shard.B_global, 0
@@ -221,6 +230,39 @@ class FilterEngine:
         d.rng_mode, d.force_resample = L.RNG_DEVICE, int(c.force_resample)
         d.n_flows, d.hidden, d.split_nets = c.n_flows, c.hidden, int(split_nets)
         return bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
+
+    @staticmethod
+    def device_identity(dev=None) -> str:
+        """The physical GPU behind ``dev``: its UUID (or PCI location), not the process-local
+        index -- two ranks with different visible-device lists can name one GPU differently."""
+        idx = torch.cuda.current_device() if dev is None else torch.device(dev).index
+        p = torch.cuda.get_device_properties(idx)
+        uuid = getattr(p, "uuid", None)
+        if uuid is not None and str(uuid).strip("0-"):
+            return f"uuid:{uuid}"
+        pci = tuple(getattr(p, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        if any(v is not None for v in pci):
+            return f"pci:{pci}"
+        return f"index:{idx}"  # no identity exposed: same index = same device (conservative)
+
+    def _device_shared(self, shard) -> bool:
+        """Does another rank of the shard's group run on this rank's GPU?  One all-gather of the
+        device identities per engine and process group (cached)."""
+        key = id(shard.group)
+        if self._shared_device is not None and self._shared_device[0] == key:
+            return self._shared_device[1]
+        ids = [None] * shard.world
+        dist.all_gather_object(ids, self.device_identity(), group=shard.group)
+        shared = len(set(ids)) < len(ids)
+        self._shared_device = (key, shared)
+        return shared
+
+    def _pass_blobs(self, dev):
+        """The dynamic / proposal stacks in the one-launch pass's layout (nfdpf.pack.pass_flow_tensors)."""
+        m = self.m
+        dyn = blob(m, "dyn_pass", m.nf_dyn.flows, lambda: pass_flow_tensors(m.nf_dyn.flows), dev)
+        cond = blob(m, "cond_pass", m.cond_model.flows, lambda: pass_flow_tensors(m.cond_model.flows), dev)
+        return dyn, cond
 
     # -- parameters -------------------------------------------------------------------------
     def _blobs(self, dev):
@@ -390,6 +432,7 @@ class FilterEngine:
                 L.check(rc, "nfdpf_filter_step_tiled" if tiled else "nfdpf_filter_step")
 
         self.last_pass = use_pass
+        pass_out = None  # one shard: the pass epilogue's (gates, flags, obs)
         if use_pass:
             # the whole T-step pass as ONE persistent launch (nfdpf_filter_pass_tiled): every gate
             # taken as off, step t's softmax partials into ess_hist[t + 1] for the verification
@@ -397,14 +440,23 @@ class FilterEngine:
             d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = x0.data_ptr(), p0.data_ptr(), N * 2, N
             d.vel = vel_p
             d.ess_all, d.ess_out, d.gate = ess_in_p[0], ess_out_p[0], spec_gate_p
+            pdyn, pcond = self._pass_blobs(dev)  # the pass layout (tanh algebra in the weights)
+            d.dyn_params, d.cond_params = pdyn.data_ptr(), pcond.data_ptr()
+            d.pass_gate = 0
+            if shard.world == 1:  # the epilogue verifies the gates / reads the fault counter on the device
+                i32 = dict(device=dev, dtype=torch.int32)
+                pass_out = (torch.empty(T, **i32) if spec else None, torch.empty(2, **i32),
+                            torch.empty((), **f32))
+                d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
             d.prof_events, d.prof_front = None, 0
             if self.step_events is not None:
                 from .prof import EventPair
                 ev = EventPair(2)
                 self.step_events.append(ev)
                 d.prof_events = ev.ptr  # rides in the pass launch's own dispatch
-            pws = ops.pass_workspace(B, N, T, dev)
+            pws = ops.pass_workspace(B, N, T, dev, owner=self)
             L.check(L.lib().nfdpf_filter_pass_tiled(d_ref, ops._aligned_ptr(pws), stream), "nfdpf_filter_pass_tiled")
+            d.dyn_params, d.cond_params = L.ptr(dyn), L.ptr(cond)
             self.pass_launches += 1
         for t in range(0 if use_pass else T):
             if t == 0:
@@ -522,24 +574,39 @@ class FilterEngine:
         # one-chain launch does not, and then no check -- a host sync -- is paid)
         handoffs = d.split_nets or (d.measurement == L.MEAS["CRNVP"] and not d.nf_cond
                                     and os.environ.get("NFDPF_CM_TWO_CHAIN", "0") == "1")
-        check_split = tiled and handoffs and not torch.cuda.is_current_stream_capturing()
-        # one-shard speculative pass: the gates and the fault counter are verified by ONE queued
-        # launch (ops.pass_verify, capturable) and read once in finish_pending
+        capturing = torch.cuda.is_current_stream_capturing()
+        check_split = tiled and handoffs and not capturing
+        if use_pass and not spec:
+            # a forced pass: one shard's epilogue read the fault counter and reduced the
+            # obs-likelihood (one host read here, none while capturing a graph); sharded, every
+            # rank's count is summed so that all ranks fall back together
+            check_split = False
+            if not capturing:
+                faults = int(pass_out[1][1].item()) if pass_out is not None else self._faults_all(shard, dev)
+                if faults:  # the grid was not all resident: the step launches instead
+                    self._pass_fault(faults)
+                    return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, finish=finish,
+                                    speculate=speculate)
+            if pass_out is not None:
+                return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, pass_out[2], pred, fired)
+        # one-shard speculative pass: the gates and the fault counter are verified on the device
+        # (the one-launch pass's epilogue, or ops.pass_verify after the step launches -- both
+        # capturable) and read once in finish_pending
         verify_dev = spec and tiled and shard.world == 1
-        if check_split and (finish or not spec) and not verify_dev:
+        if check_split and (finish or not spec) and not verify_dev and not use_pass:
             L.check_split_fault("nfdpf_filter_step_tiled", dev)
             check_split = False
         if c.resampler == "ot" and not spec:
             self._ot_fired = self.last_ot_calls > 0
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
-        tot = None if verify_dev else lw_sum.double().sum(0)  # (pass_verify reduces it on the device)
+        tot = None if verify_dev else lw_sum.double().sum(0)  # (verified on the device: reduced there)
         if spec:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             verify = None
             if verify_dev:
-                verify = ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]
+                verify = pass_out[1:] if pass_out is not None else ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]
                 check_split = False
-            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify)
+            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass)
             if not finish:
                 return res  # the caller verifies (finish_pending, e.g. after each graph replay)
             ok = self.finish_pending()
@@ -566,18 +633,27 @@ class FilterEngine:
         evaluate all T gates (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the
         obs-likelihood into the result.  False: some gate fired -- the pass is not the
         reference's and must be rerun without speculation (run(..., speculate=False))."""
-        parts, tot, shard, N, res, split_dev, verify = self._pending
-        if verify is not None:  # ops.pass_verify's flags: the one host synchronisation
+        parts, tot, shard, N, res, split_dev, verify, was_pass = self._pending
+        if verify is not None:  # the device verification's flags: the one host synchronisation
             fired, faults = verify[0].tolist()
             if faults:
-                raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "
-                                   f"(outputs invalid)")
+                if not was_pass:
+                    raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "
+                                       f"(outputs invalid)")
+                self._pass_fault(faults)  # the one-launch pass's grid was not resident: rerun step by step
+                return False
             if fired:
                 return False
             res.obs_likelihood = verify[1]
             return True
         if split_dev is not None:
-            L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
+            if was_pass:
+                faults = self._faults_all(shard, split_dev)
+                if faults:
+                    self._pass_fault(faults)
+                    return False
+            else:
+                L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
         tot = tot.clone()
         parts = self._gather_steps(parts, shard)
         if shard.world > 1:
@@ -589,6 +665,28 @@ class FilterEngine:
         return True
 
     # -- helpers ----------------------------------------------------------------------------
+    def _pass_fault(self, faults: int):
+        """A one-launch pass timed out waiting for its own workgroups (its grid was not all
+        resident: another process or stream held CUs, or a CU mask): warn, turn the pass off
+        for this engine; the caller reruns the pass with the step launches."""
+        import warnings
+        warnings.warn(f"nfdpf_filter_pass_tiled: {faults} row hand-off wait(s) timed out (the pass's grid was not "
+                      f"resident); rerunning with the step launches, the one-launch pass is off for this engine",
+                      RuntimeWarning, stacklevel=3)
+        self.pass_disabled = True
+
+    @staticmethod
+    def _faults_all(shard: ShardInfo, dev) -> int:
+        """The hand-off fault counter (read and cleared), summed over the shard's ranks."""
+        n = int(L.lib().nfdpf_split_fault(1, L.stream_ptr(dev)))
+        if n < 0:
+            raise L.NfdpfError("could not read the device fault counter")
+        if shard.world > 1:
+            t = torch.tensor([n], device=dev, dtype=torch.int64)
+            dist.all_reduce(t, group=shard.group)
+            n = int(t.item())
+        return n
+
     @staticmethod
     def _global(t: torch.Tensor, shard: ShardInfo) -> torch.Tensor:
         """Host copy of a per-row tensor over the whole (sharded) batch."""

@@ -532,10 +532,22 @@ def tiled_workspace(B: int, N: int, T: int, device) -> torch.Tensor:
     return workspace(int(lib().nfdpf_filter_tiled_workspace_bytes(B, N, T)), device, tag="tiled")
 
 
-def pass_workspace(B: int, N: int, T: int, device) -> torch.Tensor:
-    """Workspace of the one-launch pass (nfdpf_filter_pass_tiled): the row exchanges' granules
-    and the per-wave prediction / obs-likelihood partials."""
-    return workspace(int(lib().nfdpf_filter_pass_workspace_bytes(B, N, T)), device, tag="pass")
+def pass_workspace(B: int, N: int, T: int, device, owner=None) -> torch.Tensor:
+    """Workspace of the one-launch pass (nfdpf_filter_pass_tiled): a header (the granule tags'
+    epoch, the abort word), the row exchanges' granules and the per-wave prediction /
+    obs-likelihood partials.  Kept on ``owner`` (one per FilterEngine: passes of two engines --
+    e.g. on two streams -- never share granules or an abort word; module-level without one) and
+    zeroed, stream-ordered, when it is new or its (B, N, T) layout changed (include/nfdpf.h):
+    stale granules of another layout must not carry a live tag."""
+    store = owner.__dict__ if owner is not None else _ws
+    nbytes = int(lib().nfdpf_filter_pass_workspace_bytes(B, N, T))
+    t, layout = store.get("_nfdpf_pass_ws", (None, None))
+    if t is None or t.device != torch.device(device) or t.numel() < nbytes + 256:
+        t = torch.zeros(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)
+    elif layout != (B, N, T):
+        t.zero_()
+    store["_nfdpf_pass_ws"] = (t, (B, N, T))
+    return t
 
 
 def tiled_init(p0: torch.Tensor, out: torch.Tensor):

@@ -223,6 +223,42 @@ def filter_flow_tensors(flows):
     return flows_tensors(flows) + (split_flow_tensors(flows) if splittable(flows) else [])
 
 
+# 2 log2(e): tanh(a) = 1 - 2 / (1 + 2^(c a))
+TANH_C = 2.0 / 0.6931471805599453
+
+
+def pass_coupling_tensors(t_net: nn.Module, s_net: nn.Module, half: int):
+    """One coupling half of the one-launch pass (csrc/filter_pass.hpp ts_half) in the pair
+    layout of coupling_pair_tensors with the tanh algebra folded into the weights: with
+    r = 1 / (1 + 2^y) a hidden unit's tanh is 1 - 2 r, so a layer that reads tanh outputs h
+    reads r instead as W h + b = (b + sum_k W[:, k]) - 2 W r, and the next tanh's scale c =
+    2 log2(e) goes into the layer producing its argument:
+      W1' = c W1 (core and context columns), b1' = c b1,
+      W2' = -2 c W2, b2' = c (b2 + rowsum W2),  W3' = -2 W3, b3' = b3 + rowsum W3
+    (computed in float64, rounded once).  Each hidden unit then costs exp2 + add + rcp:
+    the multiply by c and the 1 - 2 r fma of the plain layout are gone (nf/flows.py:101-114
+    computes the same function; the rounding differs at the 1e-7 level)."""
+    c = TANH_C
+    nets = []
+    for net in (t_net, s_net):
+        (w1, b1), (w2, b2), (w3, b3) = [(m.weight.detach().double(), m.bias.detach().double())
+                                        for m in _linears(net.network)]
+        nets.append(dict(w1=c * w1[:, :half], w2=-2.0 * c * w2, b2=c * (b2 + w2.sum(1)), w3=-2.0 * w3,
+                         b3=b3 + w3.sum(1), w1c=c * w1[:, half:], b1=c * b1))
+    t, s = nets
+    return [pair(t[k], s[k]).float() for k in ("w1", "w2", "b2", "w3", "b3", "w1c", "b1")]
+
+
+def pass_flow_tensors(flows):
+    """The one-launch pass's dynamic / proposal stack (nfdpf_filter_pass_tiled, include/nfdpf.h):
+    per RealNVP(_cond) flow the halves (t1, s1), (t2, s2) as pass_coupling_tensors."""
+    out = []
+    for f in flows:
+        half = f.dim // 2
+        out += pass_coupling_tensors(f.t1, f.s1, half) + pass_coupling_tensors(f.t2, f.s2, half)
+    return out
+
+
 class BlobCache:
     """Flat fp32 copy of a parameter set on one device in a kernel layout, rebuilt only when
     a source parameter changes (storage, version counter)."""

@@ -105,3 +105,110 @@ def test_sharded_engine_matches_unsharded(case, tmp_path):
     fired = int((full["index"] != ident[:, None, :]).any(-1).any(0).sum())
     print(f"\n{case}: B={B} over {world} ranks, resampling fired in {fired} steps, OT calls {full['ot_calls']}")
     assert fired > 0 or full["ot_calls"] > 0
+
+
+# ---- the one-launch pass, sharded (nfdpf_filter_pass_tiled + finish_pending's all-gather and
+# batch gate): "quiet" = the bench's model at its init weights on N(0,1) encodings (no gate
+# fires: the sharded passes ARE the result), "firing" = the c2_full workload (aligned encodings:
+# the gathered verification catches the fired gate and every rank reruns with the per-step
+# exchange)
+PASS_CASES = {"quiet": (8, 1000, 12), "firing": (8, 1000, 12)}
+
+
+def _pass_inputs(kind, rows):
+    """-> (models on DEV, enc, start, vel) of the case's rows."""
+    B, N, T = PASS_CASES[kind]
+    sl = slice(*rows)
+    if kind == "quiet":
+        import bench
+        from DPFs import DPF
+        flags = bench.CONFIGS["c2"][0]
+        torch.manual_seed(2)
+        models = DPF(bench.make_args(flags, B, N, T, {})).to(DEV).eval()
+        g = torch.Generator().manual_seed(31)
+        enc, start, vel = torch.randn(B, T, 32, generator=g), torch.randn(B, 4, generator=g) * 10, \
+            torch.randn(B, T, 2, generator=g) * 3
+    else:
+        import _fullsize as F
+        wl = F.workload("c2_full", B=B, N=N, T=T)
+        models, enc, start, vel = wl["models"].to(DEV), wl["enc"], wl["start"], wl["vel"]
+    return models, enc[sl].to(DEV), start[sl].to(DEV), vel[sl].to(DEV)
+
+
+def _pass_run(kind, rows, shard=None, rank=0, world=1):
+    """The auto-mode engine on the case's rows: a speculative one-launch pass (run(finish=False);
+    sharded, the ranks' passes run one after the other -- they share the one GPU, and each grid
+    must be resident by itself), then finish_pending (sharded: one all-gather of all steps'
+    partials and the batch gate) and, if a gate fired, the per-step rerun."""
+    import torch.distributed as dist
+    from nfdpf.engine import FilterConfig, FilterEngine
+    B, N, T = PASS_CASES[kind]
+    models, enc, start, vel = _pass_inputs(kind, rows)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321, kernel="tiled")
+    eng = FilterEngine(cfg, models)
+    for r in range(world):
+        if r == rank:
+            res = eng.run(enc, start, vel, shard=shard, finish=False)
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+    launched = eng.last_pass
+    verified = eng.finish_pending()
+    eng._pending = None
+    if not verified:
+        res = eng.run(enc, start, vel, shard=shard, speculate=False)
+    torch.cuda.synchronize()
+    out = {f: getattr(res, f).cpu() for f in FIELDS if getattr(res, f) is not None}
+    out["obs_likelihood"] = res.obs_likelihood.cpu()
+    out["launched"], out["verified"] = launched, verified
+    return out
+
+
+def _worker_pass(rank, world, port, kind, path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root, os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NFDPF_PASS_SHARED_OK="1")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf import _lib
+        from nfdpf.engine import ShardInfo
+        _lib.load()
+        B = PASS_CASES[kind][0] // world
+        out = _pass_run(kind, (rank * B, (rank + 1) * B), ShardInfo.from_env(B), rank, world)
+        torch.save(out, f"{path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("kind", list(PASS_CASES))
+def test_sharded_pass_matches_unsharded(kind, tmp_path):
+    """The one-launch pass on two ranks (rows [0, 4) and [4, 8), device RNG keyed on the global
+    row) == the unsharded pass, bit for bit: every history; the obs-likelihood to 1e-6 (an fp64
+    sum reduced per rank, then across ranks).  quiet: the sharded passes verify and are the
+    result; firing: the gathered verification catches the fired gate on both ranks alike and the
+    per-step rerun is returned.  (The test-only NFDPF_PASS_SHARED_OK lets ranks that share the one
+    GPU run the pass, serialised by barriers.)"""
+    import torch.multiprocessing as mp
+    from nfdpf import _lib
+    _lib.load()
+    B = PASS_CASES[kind][0]
+    full = _pass_run(kind, (0, B))
+    assert full["launched"], "the unsharded one-launch pass did not run"
+    assert full["verified"] == (kind == "quiet")
+    world = 2
+    path = str(tmp_path / "pass")
+    mp.start_processes(_worker_pass, args=(world, _free_port(), kind, path), nprocs=world, start_method="spawn")
+    parts = [torch.load(f"{path}.{r}", weights_only=True) for r in range(world)]
+    h = B // world
+    for r, part in enumerate(parts):
+        assert part["launched"], f"rank {r}: the sharded one-launch pass did not run"
+        assert part["verified"] == full["verified"], (r, part["verified"])
+        for f in FIELDS:
+            if f in full:
+                assert torch.equal(part[f], full[f][r * h:(r + 1) * h]), (kind, f, r)
+        a, b = float(part["obs_likelihood"]), float(full["obs_likelihood"])
+        assert abs(a - b) <= 1e-6 * abs(b), (a, b)

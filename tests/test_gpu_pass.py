@@ -8,6 +8,8 @@ Within a step the pass differs from the step launches only in the order of ONE r
 row's x_phys sums: per tile here, per row there), so (a) is a rounding-level comparison; (b)
 is the reference-parity check: every history within the reference's own float32 envelope.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -120,30 +122,50 @@ class _Replay:
         return v
 
 
-@pytest.mark.parametrize("fixture", ["bench", "e2e_c2.npz"])
-@pytest.mark.parametrize("B,N,T", [(4, 1000, 10), (3, 257, 6), (2, 1024, 8)])
+def _fractions(what, ours, r32, r64, rtol, atol):
+    """north_star's 1e-5 bar: the fraction of elements within rtol |ref64| + atol of the float64
+    oracle, ours next to the reference's own float32 run (printed for the round's record)."""
+    ours, r32, r64 = (np.asarray(a, dtype=np.float64) for a in (ours, r32, r64))
+    bar = rtol * np.abs(r64) + atol
+    f_ours, f_ref = float(np.mean(np.abs(ours - r64) <= bar)), float(np.mean(np.abs(r32 - r64) <= bar))
+    print(f"  {what}: within {rtol:g} rel + {atol:g}: ours {100 * f_ours:.3f} %, reference float32 "
+          f"{100 * f_ref:.3f} %; max err ours {np.abs(ours - r64).max():.3e} vs float32 {np.abs(r32 - r64).max():.3e}")
+
+
+PASS_ORACLE_CASES = [(4, 1000, 10, "bench"), (3, 257, 6, "bench"), (2, 1024, 8, "bench"), (4, 1000, 10, "e2e_c2.npz"),
+                     (3, 257, 6, "e2e_c2.npz"), (2, 1024, 8, "e2e_c2.npz"),
+                     # the BASELINE C2 shape itself, the bench's model (DPF(args) at its init weights)
+                     (64, 1000, 50, "bench")]
+
+
+@pytest.mark.parametrize("B,N,T,fixture", PASS_ORACLE_CASES)
 def test_pass_vs_oracle(B, N, T, fixture):
     """The pass against the oracle run on the same initial particles and motion noise: ours vs
     the oracle in float64 within 4x (max) / 2.5x (mean) of the oracle float32's own error
     (test_gpu_parity._check_envelope, the one-step tests' bar), free-running over T steps (no
-    resampling: nothing discrete can diverge)."""
+    resampling: nothing discrete can diverge).  Includes the headline shape, 64 x 1000 x 50.
+    The e2e_c2 flows (std 0.05) degenerate the weights on some draws and the gate then fires
+    (the pass is rerun step by step, compared elsewhere): the first of a fixed list of input
+    seeds whose gates all stay off is used -- deterministic, and never a skip."""
     from nfdpf import ops
     c = e2e_cfg(load("e2e_c2.npz"))  # the C2 flags
     c["N"] = N
     models = _models(fixture)
     w = {k: v.detach().cpu() for k, v in models.state_dict().items()}
-    enc, start, vel = _inputs(B, T, seed=7 * N + B)
     from nfdpf.engine import FilterConfig, FilterEngine
     cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=5,
                        kernel="tiled", speculate_gate=True)
-    x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 5, 0, DEV)
-    eng = FilterEngine(cfg, models)
-    res = eng.run(enc, start, vel, init=(x0, logw0))
-    torch.cuda.synchronize()
-    if fixture != "bench" and not eng.last_pass:
-        pytest.skip("the ESS gate fired on these draws (the step-by-step rerun is pinned elsewhere)")
-    assert eng.last_pass, "a gate fired: the one-launch pass was rerun step by step"
+    for k in range(8 if fixture != "bench" else 1):
+        enc, start, vel = _inputs(B, T, seed=7 * N + B + 1000 * k)
+        x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 5, 0, DEV)
+        eng = FilterEngine(cfg, models)
+        res = eng.run(enc, start, vel, init=(x0, logw0))
+        torch.cuda.synchronize()
+        if eng.last_pass:
+            break
+    assert eng.last_pass, "a gate fired on every input seed: the one-launch pass was rerun step by step"
     outs = {}
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     for dt in (torch.float32, torch.float64):
         with O.precision(dt):
             wd = O.cast_params(w, dt)
@@ -152,11 +174,12 @@ def test_pass_vs_oracle(B, N, T, fixture):
         outs[dt] = [a.double().numpy() if torch.is_tensor(a) else a for a in r]
     r32, r64 = outs[torch.float32], outs[torch.float64]
     np.testing.assert_array_equal(res.index.cpu().numpy(), r32[5])
-    _check_envelope(res.particles.cpu(), r32[0], r64[0], 1e-5, 1e-4, "particles")
-    _check_envelope(res.probs.cpu(), r32[1], r64[1], 1e-5, 1e-9, "weights")
-    _check_envelope(res.lik.cpu(), r32[3], r64[3], 1e-5, 2e-5, "likelihood")
-    _check_envelope(res.jac.cpu(), r32[6], r64[6], 1e-5, 1e-6, "jac")
-    _check_envelope(res.prior.cpu(), r32[7], r64[7], 1e-5, 1e-5, "prior")
+    print(f"\npass vs oracle, B={B} N={N} T={T} ({fixture}):")
+    for i, what, rtol, atol in ((0, "particles", 1e-5, 1e-4), (1, "weights", 1e-5, 1e-9), (3, "likelihood", 1e-5, 2e-5),
+                                (6, "jac", 1e-5, 1e-6), (7, "prior", 1e-5, 1e-5)):
+        ours = getattr(res, ("particles", "probs", None, "lik", None, None, "jac", "prior")[i]).cpu()
+        _check_envelope(ours, r32[i], r64[i], rtol, atol, what)
+        _fractions(what, ours, r32[i], r64[i], 1e-5, 0.0 if what != "jac" else 1e-6)
     obs64 = float(r64[8])
     assert abs(float(res.obs_likelihood) - obs64) <= 4 * abs(float(r32[8]) - obs64) + 1e-5 * abs(obs64) + 1e-4
 
@@ -302,3 +325,143 @@ def test_forced_pass_resampling_bit_exact(B, N, T):
     assert torch.isfinite(a.probs).all()
     s = a.probs.sum(-1)
     assert torch.allclose(s, torch.ones_like(s) + N * 1e-12, atol=1e-5)
+
+
+class _StepDraws:
+    """One step's device draws replayed into the oracle: the soft-resampling offsets and the
+    motion noise (the HostRNG interface of oracle.filter_step)."""
+
+    def __init__(self, off, noise):
+        self.off, self.nz = off, noise
+
+    def offsets(self, B, N):
+        return self.off.clone()
+
+    def noise(self, B, N, std):
+        return self.nz.clone()
+
+
+def _soft_indices32(soft32):
+    """The float64 oracle's soft resampler with the reference's own (float32) indices: the
+    marker search is the one discrete step, and float64 arithmetic can move a marker across a
+    CDF step -- the envelope then measures the continuous arithmetic around the same indices
+    (test_gpu_parity._oracle64_one_step does the same)."""
+    def soft64(x, p, alpha, offsets=None, gen=None):
+        with O.precision(torch.float32):
+            _, _, idx = soft32(x.float(), p.float(), alpha, offsets.float())
+        B, N = p.shape
+        q = alpha * p + (1 - alpha) / N
+        q = q / q.sum(-1, keepdim=True)
+        w = (p / q).reshape(B * N)[idx]
+        return x.reshape(B * N, -1)[idx], w / w.sum(-1, keepdim=True), idx
+    return soft64
+
+
+@pytest.mark.parametrize("B,N,T", [(6, 1000, 8), (4, 257, 6), (3, 100, 5), (64, 1000, 50)])
+def test_forced_pass_every_step_vs_oracle(B, N, T, monkeypatch):
+    """--force-resample inside the one-launch pass, every step against the oracle's step
+    (oracle.filter_step = DPFs.py:160-192 with resamplers.py:20-60) started from the PASS's own
+    slot t-1 (particles, normalised weights) with the pass's device offsets and motion noise:
+    the indices bit for bit against the float32 oracle, and the resampled weights' consequence --
+    the normalised weights p -- with the particles, likelihood, jac and prior of every slot within
+    the reference's own float32 envelope against the float64 oracle (_check_envelope).  Teacher
+    forcing from our own state: a marker within rounding of a CDF step cannot make the two runs
+    follow different particles, so every step of a 64 x 1000 x 50 forced pass is pinned."""
+    from nfdpf import ops
+    from nfdpf.engine import FilterConfig, FilterEngine
+    models = _models("e2e_c2.npz")
+    w = {k: v.detach().cpu() for k, v in models.state_dict().items()}
+    c = e2e_cfg(load("e2e_c2.npz"))
+    c["N"] = N
+    enc, start, vel = _inputs(B, T, seed=B * 31 + N)
+    x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 77, 0, DEV)
+    p0, _ = ops.normalize_log_probs(logw0)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=77,
+                       kernel="tiled", force_resample=True)
+    eng = FilterEngine(cfg, models)
+    res = eng.run(enc, start, vel, init=(x0, logw0))
+    torch.cuda.synchronize()
+    assert eng.last_pass, "the forced pass did not run as one launch"
+    off = torch.from_numpy(_philox_offsets(77, T, B, N))
+    xs, ps, nz = res.particles.cpu(), res.probs.cpu(), res.noise.cpu()
+    x0c, p0c, encc, startc, velc = x0.cpu(), p0.cpu(), enc.cpu(), start.cpu(), vel.cpu()
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    keys = ("x", "p", "lik", "jac", "prior")
+    outs = {}
+    soft32 = O.soft_resample
+    for dt in (torch.float32, torch.float64):
+        if dt == torch.float64:
+            monkeypatch.setattr(O, "soft_resample", _soft_indices32(soft32))
+        acc = {k: [] for k in keys + ("idx",)}
+        with O.precision(dt):
+            wd = O.cast_params(w, dt)
+            meas = O.make_measurement(c, wd)
+            for t_ in range(T):
+                xp = (x0c if t_ == 0 else xs[:, t_ - 1]).to(dt)
+                pp = (p0c if t_ == 0 else ps[:, t_ - 1]).to(dt)
+                v = (startc[:, 2:] if t_ == 0 else velc[:, t_ - 1]).to(dt)
+                r = O.filter_step(c, wd, meas, xp, pp, v, encc[:, t_].to(dt), _StepDraws(off[t_], nz[:, t_].to(dt)),
+                                  force_resample=True)
+                for k in keys + ("idx",):
+                    acc[k].append(r[k])
+        outs[dt] = {k: torch.stack(v, 1).double().numpy() for k, v in acc.items()}
+    r32, r64 = outs[torch.float32], outs[torch.float64]
+    np.testing.assert_array_equal(res.index.cpu().numpy(), r32["idx"].astype(np.int64))
+    print(f"\nforced pass vs oracle step by step, B={B} N={N} T={T}:")
+    for k, ours, rtol, atol in (("x", xs, 1e-5, 1e-4), ("p", ps, 1e-5, 1e-9), ("lik", res.lik.cpu(), 1e-5, 2e-5),
+                                ("jac", res.jac.cpu(), 1e-5, 1e-6), ("prior", res.prior.cpu(), 1e-5, 1e-5)):
+        _check_envelope(ours, r32[k], r64[k], rtol, atol, k)
+        _fractions(k, ours, r32[k], r64[k], 1e-5, 0.0 if k != "jac" else 1e-6)
+
+
+@pytest.mark.parametrize("N", [8, 100, 257, 1000, 1024])
+def test_cascade_row_sum_1k_equals_generic(N):
+    """The forced pass's load-ahead cascade sum (cascade_row_sum_1k) == the generic device
+    cascade sum == ATen's CPU order restated (oracle/cascade.py), bit for bit, on rows of mixed
+    magnitudes (the resampler's q and gathered weights)."""
+    from nfdpf import _lib
+    from oracle.cascade import torch_cpu_row_sum
+    g = torch.Generator().manual_seed(N)
+    B = 33
+    x = torch.rand(B, N, generator=g) * torch.exp(torch.randn(B, N, generator=g) * 3)
+    x[0] = 1.0 / N
+    xd = x.to(DEV).contiguous()
+    out = [torch.empty(B, device=DEV) for _ in range(2)]
+    for v in range(2):
+        _lib.check(_lib.lib().nfdpf_cascade_row_sum(xd.data_ptr(), B, N, v, out[v].data_ptr(),
+                                                    torch.cuda.current_stream().cuda_stream), "cascade_row_sum")
+    torch.cuda.synchronize()
+    ref = np.array([torch_cpu_row_sum(r) for r in x.numpy()], dtype=np.float32)
+    np.testing.assert_array_equal(out[0].cpu().numpy(), ref)
+    np.testing.assert_array_equal(out[1].cpu().numpy(), ref)
+    assert torch.equal(x.sum(-1), torch.from_numpy(ref))  # the restatement is torch's own order here
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_pass_timeout_falls_back(force, monkeypatch):
+    """A one-launch pass whose row hand-off waits time out (NFDPF_PASS_WAIT_US=1: a 1 us bound,
+    standing in for a grid that is not all resident) drains, counts its faults, warns, turns the
+    pass off for the engine and reruns the step launches: the returned result is the step
+    launches' own, bit for bit, and the next run does not try the pass again."""
+    models = _models("e2e_c2.npz")
+    B, N, T = 4, 1000, 6
+    enc, start, vel = _inputs(B, T, seed=5)
+    from nfdpf.engine import FilterConfig, FilterEngine
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=9, kernel="tiled",
+                       speculate_gate=None if force else True, force_resample=force)
+    monkeypatch.setenv("NFDPF_PASS_WAIT_US", "1")
+    eng = FilterEngine(cfg, models)
+    with pytest.warns(RuntimeWarning, match="timed out"):
+        a = eng.run(enc, start, vel)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("NFDPF_PASS_WAIT_US")
+    assert eng.pass_disabled and eng.pass_launches == 1 and not eng.last_pass
+    eng.run(enc, start, vel)
+    assert eng.pass_launches == 1, "the pass ran again after a fault"
+    monkeypatch.setenv("NFDPF_PASS", "0")
+    b = FilterEngine(cfg, models).run(enc, start, vel)
+    torch.cuda.synchronize()
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    from nfdpf import _lib
+    assert _lib.lib().nfdpf_split_fault(1, torch.cuda.current_stream().cuda_stream) == 0
