@@ -423,6 +423,9 @@ def main():
     ap.add_argument("--no-forced", action="store_true",
                     help="skip the line's `forced` object (the same workload with --force-resample, timed "
                          "in a second loop; on by default for the configurations whose pass takes < 30 ms)")
+    ap.add_argument("--no-informative", action="store_true",
+                    help="skip the line's `informative` object (the same workload on informative frame encodings, "
+                         "where the ESS gate fires on most steps, timed in its own loop; on by default for c1-c3)")
     ap.add_argument("--batch", type=int, default=None, help="override B per GPU (exploration only)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: capture the whole T-step pass (all launches of filtering_pos) in a hipGraph and "
@@ -487,7 +490,7 @@ def main():
     # positions, what a trained frame encoder approximates): the timed passes' N(0,1) encodings
     # carry no information, so their RMSE is not a filtering-quality number.  One untimed pass
     # on its own engine (the timed engine's speculation state is left alone).
-    rmse_inf = None
+    rmse_inf, enc_inf = None, None
     if not args.enc_from_state:
         with torch.no_grad():
             enc_inf = dpf.particle_encoder(state[:, :, :2].float()).contiguous()
@@ -544,6 +547,32 @@ def main():
                   "execution": "hipGraph replay of the pass" if run_f["graph"] is not None else "Python launches",
                   "roofline": roof_f}
 
+    # the same workload on INFORMATIVE frame encodings (the particle encoder at the true
+    # positions: the likelihood peaks near the truth, the weights degenerate and the ESS gate
+    # fires on most steps, as with a trained model), timed in its own loop: the gated pass
+    # decides and resamples inside the launch there
+    informative = None
+    if not args.force_resample and not args.enc_from_state and not args.no_informative and cheap and \
+            flags["measurement"] in ("cos", "CRNVP"):
+        run_i = timed_passes(fcfg, dpf, enc_inf, start, vel_in, shard, args, world, dev)
+        res_i = run_i["res"]
+        ident = (torch.arange(N, device=dev) + N * (shard.row_base + torch.arange(B, device=dev))[:, None])
+        fired_i = run_i["eng"].last_ot_calls if flags["resampler_type"] == "ot" else \
+            int((res_i.index != ident[:, None, :]).flatten(2).any(-1).any(0).sum())
+        se_i = ((res_i.pred - state[:, :, :2]) ** 2).sum().double()
+        if world > 1:
+            dist.all_reduce(se_i)
+        eng_i = run_i["eng"]
+        informative = {"value": B * world * N * T * args.steps / run_i["elapsed"], "unit": "particle-steps/s",
+                       "ms_per_step": run_i["elapsed"] / args.steps * 1e3, "steps": args.steps,
+                       "resampled_steps": fired_i, "of_steps": T, "rmse": float(torch.sqrt(se_i / cnt)),
+                       "encodings": "particle encoder at the true positions (--enc-from-state)",
+                       "execution": ("hipGraph replay of the pass" if run_i["graph"] is not None else "Python launches")
+                                    + (", the whole pass as one launch" if eng_i.last_pass else "")
+                                    + (", ESS gate decided inside the launch" if eng_i.last_gate_pass else "")
+                                    + (", speculative ESS gate" if run_i["spec"] else ""),
+                       "pass_kernel_avg_ms_live": run_i["kernel_ms"] if eng_i.last_pass else None}
+
     if rank == 0:
         units = B * world * N * T * args.steps
         value = units / elapsed
@@ -557,6 +586,7 @@ def main():
                          f"{'forced' if args.force_resample else 'ESS-gated'} resampling, device RNG, "
                          f"{'hipGraph replay of the pass' if graph is not None else 'Python launches'}"
                          + (", the whole pass as one launch" if eng.last_pass else "")
+                         + (", ESS gate decided inside the launch" if eng.last_gate_pass else "")
                          + (", speculative ESS gate verified once per pass" if spec else "")
                          + (", frame encodings = particle encoder(true positions)" if args.enc_from_state else ""),
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
@@ -569,6 +599,8 @@ def main():
         }
         if forced is not None:
             out["forced"] = forced
+        if informative is not None:
+            out["informative"] = informative
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.config, force=args.force_resample)
         print(json.dumps(out))

@@ -88,11 +88,20 @@ __device__ unsigned long long g_ptrace[256][16][64][20];
   } while (0)
 #endif
 
+// pass modes (tiled_pass_kernel<MODE>)
+constexpr int kModeSpec = 0;   // every ESS gate taken as off (verified after the pass)
+constexpr int kModeForce = 1;  // --force-resample: the row resampled at the top of every step
+constexpr int kModeGate = 2;   // the batch-global ESS gate decided inside the launch, every step
+
 struct PassWs {
   PassHdr *hdr;
-  uint64_t *ga;  // [2][B][tiles][4 role-0 flow waves][kGA]  exchange A (x_phys sums)
-  uint64_t *gb;  // [2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
-  uint64_t *gc;  // [2][B][tiles][8 encoder waves][kGC]      exchange C (softmax partials)
+  // exchanges A and B by [variant][step parity]: variant 0 = the step without resampling, 1 = the
+  // step after the row's resampling (kModeGate: a step speculated as not resampling and then
+  // redone leaves variant 0 granules behind that nobody waits for any more)
+  uint64_t *ga;  // [2][2][B][tiles][4 role-0 flow waves][kGA]  exchange A (x_phys sums)
+  uint64_t *gb;  // [2][2][B][tiles][4][kGA]                   exchange B (x_dyn sums)
+  uint64_t *gc;  // [2][B][tiles][8 encoder waves][kGC]         exchange C (softmax partials)
+  uint64_t *ge;  // [2][B] kModeGate: each row's 1 / sum p^2 of slot s (by the parity of s)
   double *fin;   // [B][T][tiles * 8][4] per encoder wave: sum p^2, sum p x0, sum p x1, sum logw
   // forced resampling (FORCE): slot s's unnormalised log-weights, written through (sc1) by the
   // encoder waves before their C(s) granules, by slot parity
@@ -105,7 +114,7 @@ struct PassWs {
 __host__ __device__ static inline int64_t pass_granule_bytes(int B, int N) {
   const int64_t bt = (int64_t)B * n_tiles(N);
   auto a256 = [](int64_t v) { return (v + 255) / 256 * 256; };
-  return a256(2 * bt * 4 * kGA * 8) * 2 + a256(2 * bt * 8 * kGC * 8);
+  return a256(4 * bt * 4 * kGA * 8) * 2 + a256(2 * bt * 8 * kGC * 8) + a256(2 * (int64_t)B * 8);
 }
 
 static int64_t pass_bytes(int B, int N, int T) {
@@ -121,11 +130,13 @@ static PassWs pass_carve(void *ws, int B, int N, int T) {
   w.hdr = (PassHdr *)p;
   p += 256;
   w.ga = (uint64_t *)p;
-  p += al256(2 * bt * 4 * kGA * 8);
+  p += al256(4 * bt * 4 * kGA * 8);
   w.gb = (uint64_t *)p;
-  p += al256(2 * bt * 4 * kGA * 8);
+  p += al256(4 * bt * 4 * kGA * 8);
   w.gc = (uint64_t *)p;
   p += al256(2 * bt * 8 * kGC * 8);
+  w.ge = (uint64_t *)p;
+  p += al256(2 * (int64_t)B * 8);
   w.fin = (double *)p;
   p += al256(bt * T * 8 * 32);
   w.gu = (float *)p;
@@ -161,13 +172,20 @@ struct PassLds {
   uint32_t rowa[kPassMaxTiles * 4 * kGA];  // wave 0's A / B sweep
   uint32_t rowc[kPassMaxTiles * 8 * kGC];  // wave 8's C sweep
   RowNorm rn[2];                   // slot s's row normaliser, by parity of s
-  int fA, fB, fE, fR;              // step-tagged flags (see the header comment)
+  int fA, fB, fE, fR;              // step-tagged flags (see the header comment; fA / fB: 4 (t + 1) + code)
   int qf[4], rf[4];
   alignas(8) int pf[4];
   alignas(8) int ef[8];
-  float lr_l[kTile];               // FORCE: this tile's resampled log-weights (outside the union: the
-                                   // encoder waves read it while others may start their MFMA layers)
+  float lr_l[kTile];               // FORCE / GATE: this tile's resampled log-weights (outside the union:
+                                   // the encoder waves read it while others may start their MFMA layers)
   int fS, fbar;                    // FORCE: resampling done, flow-wave barrier
+  // kModeGate: the decisions (dec[t & 1] of step t, valid once fD >= t + 1; wave 8), the chain's
+  // redo request to the prior waves (rq = t + 1: join the row's resampling of step t), each chain
+  // wave's "slot t - 1's hist_x stores have landed" (hxf[g] = t), wave 8's batch sweep
+  int fD, rq;
+  int dec[2];
+  int hxf[4];
+  uint32_t rowe[256];
 };
 
 __device__ __forceinline__ void gran_store(uint64_t *g, uint32_t data, uint32_t tag) {
@@ -252,41 +270,57 @@ __device__ __forceinline__ void publish4(uint64_t *g, const double (&v)[4], uint
   }
 }
 
-// one wave sweeps granules [0, n) of a row (n <= 192) until every tag is `tag`, leaving the
-// data words in dst (LDS); false on abort
+// one wave sweeps granules [0, n) of a row (n <= 64 NC) until every tag is `tag`, leaving the
+// data words in dst (LDS): 0; 1 on abort; 2 when `stop()` (an LDS read, checked between sweeps)
+// became true first (kModeGate: the step being speculated must be redone).
 // `work` (register-only arithmetic) runs once while the first sweep's loads are in flight.
 struct NoWork {
   __device__ void operator()() const {}
 };
-template <class Work = NoWork>
-__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst, Work work = Work()) {
+struct NoStop {
+  __device__ bool operator()() const { return false; }
+};
+template <int NC = 3, class Work = NoWork, class Stop = NoStop>
+__device__ int poll_rowx(const uint64_t *g, int n, uint32_t tag, uint32_t *dst, Work work = Work(),
+                         Stop stop = Stop()) {
   const int l = threadIdx.x & 63;
-  uint64_t v[3] = {0, 0, 0};
-  bool ok[3];
+  uint64_t v[NC];
+  bool ok[NC];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) ok[c] = 64 * c + l >= n;
+  for (int c = 0; c < NC; ++c) {
+    v[c] = 0;
+    ok[c] = 64 * c + l >= n;
+  }
   Spin sp;
   auto sweep = [&]() {
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < NC; ++c)
       if (!ok[c]) v[c] = __hip_atomic_load(g + 64 * c + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   sweep();
   work();
   for (;;) {
+    bool all = true;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < NC; ++c) {
       if (!ok[c]) ok[c] = (uint32_t)(v[c] >> 32) == tag;
-    if (__all(ok[0] && ok[1] && ok[2])) break;
-    if (!pass_spin(sp)) return false;
+      all = all && ok[c];
+    }
+    if (__all(all)) break;
+    if (stop()) return 2;
+    if (!pass_spin(sp)) return 1;
     sweep();
   }
 #pragma unroll
-  for (int c = 0; c < 3; ++c)
+  for (int c = 0; c < NC; ++c)
     if (64 * c + l < n) dst[64 * c + l] = (uint32_t)v[c];
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  return true;
+  return 0;
+}
+template <class Work = NoWork>
+__device__ bool poll_row(const uint64_t *g, int n, uint32_t tag, uint32_t *dst, Work work = Work()) {
+  return poll_rowx<3>(g, n, tag, dst, work) == 0;
 }
 
 __device__ __forceinline__ double lds_double(const uint32_t *w, int q) {
@@ -572,12 +606,34 @@ __device__ __forceinline__ float pass_forward(cf2 *fw, int ns, float &lo, float 
   return l1 + ts.y;
 }
 
+// kModeGate: step t's decision once wave 8 has taken it (fD >= t + 1): 1 = the batch-global ESS
+// gate fired (DPFs.py:163-165); the same value in every workgroup of the grid
+__device__ __forceinline__ int wait_dec(PassLds &L, int t) {
+  wait_flag(&L.fD, t + 1);
+  return __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[t & 1]);
+}
+__device__ __forceinline__ bool dec_fired(PassLds &L, int t) {
+  return __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.fD) >= t + 1 &&
+         __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[t & 1]) != 0;
+}
+
 // waves 0-3 ("chain", group g = w): motion -> A -> nf_dyn inverse -> B -> proposal inverse, the
 // path from one step's particles to the next's; the proposal goes to the group's prior wave and
-// encoder pair through LDS (qbuf, pbuf, rbuf's propose half; flag qf[g])
-template <bool FORCE>
+// encoder pair through LDS (qbuf, pbuf, rbuf's propose half; flag qf[g]).
+// kModeGate: the step's gate is decided by wave 8 from slot t - 1 (after the C(t - 1) sweep, one
+// batch-wide granule sweep); the chain PREDICTS it from step t - 1's decision:
+//   * predicted to fire: the row is resampled first (as kModeForce, the 8 flow waves), then the
+//     decision -- known by then -- picks the resampled or the own particles;
+//   * predicted not to fire: the step runs on the own particles at once (variant 0) and the
+//     decision is checked while wave 0 waits for A / B and before anything is committed; if the
+//     gate fired after all, the attempt is dropped, the prior waves are called in (rq) and the
+//     step is redone after the row's resampling (variant 1: its own exchange buffers).
+// Nothing of step t leaves the chain (histories, qbuf, qf) before its decision is known, so the
+// prior and encoder waves only ever see the committed step.
+template <int MODE>
 __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                            uint32_t tag0) {
+  constexpr bool FORCE = MODE == kModeForce, GATE = MODE == kModeGate;
   const int tiles = n_tiles(d.N), N = d.N, nfl = d.n_flows, ncb = nfl * 4 * kH;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = w, slot = g * 64 + lane;
@@ -603,111 +659,167 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + d.E + c) + rc.w];
   }
   constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
-  int round = 0;  // flow_barrier rounds (FORCE)
+  int round = 0;  // flow_barrier rounds (FORCE / GATE)
+  int prev_dec = 0;  // GATE: the decision of step t - 1 (the prediction for step t)
   float en0 = 0.f, en1 = 0.f;  // the next step's motion noise
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
-    cf2 *dyn = wptr2(d.dyn_params), *cond = wptr2(d.cond_params);
     const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const uint32_t tag = tag0 + (uint32_t)t + 1u;
-    const RowSlot S = row_slot(d, b, t);
     const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
-    int src = i;
     PT(t, 0);
-    if constexpr (FORCE) {  // soft resampling of the row every step (--force-resample)
-      pass_resample(d, ws, L, b, tile, tag0, t, round);
+    if (t == 0 && valid) pass_noise(d, 0, grow, i, en0, en1);
+    // the step's input particles: own (x0, x1) or the row's resampling's
+    float xs0 = x0, xs1 = x1;
+    int src = i, variant = 0, fire = FORCE ? 1 : 0;
+    const int pred = GATE ? (t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
+    bool known = !GATE || t == 0;  // the step's decision is in hand (GATE: else speculated)
+    auto take_resampled = [&]() {
       if (valid) {
-        x0 = L.rs.xr_l[slot][0];
-        x1 = L.rs.xr_l[slot][1];
+        xs0 = L.rs.xr_l[slot][0];
+        xs1 = L.rs.xr_l[slot][1];
         src = L.rs.src_l[slot];
       }
+    };
+    if (FORCE || (GATE && pred)) {  // soft resampling of the row (--force-resample / predicted)
+      if (GATE && t > 0) {  // slot t - 1's hist_x stores landed: this tile's C(t - 1) may go out
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        set_flag(&L.hxf[g], t);
+      }
+      pass_resample(d, ws, L, b, tile, tag0, t, round);
+      if (GATE) {
+        fire = wait_dec(L, t);
+        known = true;
+      }
+      if (fire) take_resampled();
+      variant = GATE && fire ? 1 : 0;
     }
-    // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps; eps drawn during the
-    // previous step's A exchange (en0, en1)
-    float e0 = 0.f, e1 = 0.f, p0 = 0.f, p1 = 0.f;
-    if (t == 0 && valid) pass_noise(d, 0, grow, i, en0, en1);
+    float e0 = 0.f, e1 = 0.f, p0 = 0.f, p1 = 0.f, jac = 0.f, q0 = 0.f, q1 = 0.f, ldp = 0.f;
+    // one attempt at step t from (xs0, xs1): 0 done; 2 dropped (GATE: the gate fired while the
+    // attempt speculated that it would not; `spec` enables the checks)
+    auto attempt = [&](bool first, bool spec) -> int {
+      // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps; eps drawn during the
+      // previous step's A exchange (en0, en1)
+      e0 = e1 = p0 = p1 = 0.f;
+      if (valid) {
+        e0 = en0;
+        e1 = en1;
+        p0 = (xs0 + v0) + e0;
+        p1 = (xs1 + v1) + e1;
+      }
+      const int64_t vb = (int64_t)(variant * 2 + par) * d.B;
+      const int64_t gslot = ((vb + b) * tiles + tile) * 4 + g;
+      const int64_t grow0 = (vb + b) * tiles * 4;
+      {  // exchange A: this wave's sums of x_phys
+        double s[4] = {p0, p1, (double)p0 * p0, (double)p1 * p1};
+        wave_sum_dpp_n(s);
+        publish4(ws.ga + gslot * kGA, s, tag);
+      }
+      PT(t, 1);
+      // the next step's motion noise, drawn while the A sweep is in flight / fA is awaited
+      auto next_noise = [&]() {
+        if (first && valid && t + 1 < d.T) pass_noise(d, t + 1, grow, i, en0, en1);
+      };
+      auto stop = [&]() { return spec && dec_fired(L, t); };
+      const int fa = 4 * (t + 1) + 2 * variant;
+      if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
+        // cbd[par] was last read by the prior waves at step t - 2
+        if (t >= 2) {
+          wait_flag2(&L.pf[0], t - 1);
+          wait_flag2(&L.pf[2], t - 1);
+        }
+        const int st = poll_rowx<3>(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, next_noise, stop);
+        if (GATE && first) {  // (the poll's loads drained this wave's slot t - 1 stores too)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          set_flag(&L.hxf[g], t);
+        }
+        PT(t, 7);
+        if (st == 0) {
+          const Ctx4 c = row_ctx(L.rowa, tiles, N);
+          if (fold_lane) {
+            const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
+            float v = fwd[0];
+#pragma unroll
+            for (int q = 0; q < kOctxDyn; ++q) v = fmaf(fwd[1 + q], cv[q], v);
+            reinterpret_cast<float *>(L.cbd[par])[lane] = v;
+          }
+        }
+        set_flag(&L.fA, st == 2 ? fa + 1 : fa);
+        if (st == 2) return 2;
+      } else {
+        if (GATE && first) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          set_flag(&L.hxf[g], t);
+        }
+        next_noise();
+        wait_flag(&L.fA, fa);
+        if (spec && __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.fA) == fa + 1) return 2;
+      }
+      PT(t, 2);
+      // nf_dyn inverse (model/models.py:305-332)
+      cf2 *dyn = wptr2(d.dyn_params), *cond = wptr2(d.cond_params);
+      float xd0 = p0, xd1 = p1, ld = 0.f;
+      if (valid)
+        for (int f = nfl - 1; f >= 0; --f) ld += pass_inverse(dyn + f * 2 * nsd, nsd, xd0, xd1, L.cbd[par] + f * 2 * kH);
+      jac = -ld;
+      PT(t, 3);
+      {
+        double s[4] = {valid ? xd0 : 0.0, valid ? xd1 : 0.0, valid ? (double)xd0 * xd0 : 0.0,
+                       valid ? (double)xd1 * xd1 : 0.0};
+        wave_sum_dpp_n(s);
+        publish4(ws.gb + gslot * kGA, s, tag);  // exchange B
+      }
+      if (w == 0) {  // the proposal fold: encoding columns (from prior wave 4), then [mean, std] of x_dyn
+        const int st = poll_rowx<3>(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, NoWork(), stop);
+        if (st == 0) {
+          PT(t, 8);
+          const Ctx4 c = row_ctx(L.rowa, tiles, N);
+          wait_flag(&L.fE, t + 1);
+          if (fold_lane) {
+            const float c4[4] = {c.m0, c.m1, c.s0, c.s1};
+            float a = L.encfold[par][lane];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a = fmaf(fwc[q], c4[q], a);
+            reinterpret_cast<float *>(L.cbc[par])[lane] = a;
+          }
+        }
+        set_flag(&L.fB, st == 2 ? fa + 1 : fa);
+        if (st == 2) return 2;
+      } else {
+        wait_flag(&L.fB, fa);
+        if (spec && __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.fB) == fa + 1) return 2;
+      }
+      PT(t, 4);
+      // NF proposal inverse (model/models.py:334-356)
+      q0 = xd0;
+      q1 = xd1;
+      ldp = 0.f;
+      if (valid)
+        for (int f = nfl - 1; f >= 0; --f) ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
+      return 0;
+    };
+    for (int a = 0;; ++a) {  // (one copy of the attempt's code: a loop, not two calls)
+      attempt(a == 0, GATE && !known);
+      if (!GATE || known) break;
+      // the speculated step's decision: commit, or drop the attempt and redo after resampling
+      fire = wait_dec(L, t);
+      known = true;
+      if (!fire) break;
+      if (w == 0) set_flag(&L.rq, t + 1);  // the prior waves join the row's resampling
+      pass_resample(d, ws, L, b, tile, tag0, t, round);
+      take_resampled();
+      variant = 1;
+    }
+    // commit step t: the histories, and the proposal to the prior wave and the encoder pair
+    const RowSlot S = row_slot(d, b, t);
     if (valid) {
-      e0 = en0;
-      e1 = en1;
-      p0 = (x0 + v0) + e0;
-      p1 = (x1 + v1) + e1;
       S.hnoise[2 * i] = e0;
       S.hnoise[2 * i + 1] = e1;
       S.hidx[i] = (int64_t)N * grow + src;
+      if (S.hjac) S.hjac[i] = jac;
     }
-    const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 4 + g;
-    const int64_t grow0 = ((int64_t)par * d.B + b) * tiles * 4;
-    {  // exchange A: this wave's sums of x_phys
-      double s[4] = {p0, p1, (double)p0 * p0, (double)p1 * p1};
-      wave_sum_dpp_n(s);
-      publish4(ws.ga + gslot * kGA, s, tag);
-    }
-    PT(t, 1);
-    // the next step's motion noise, drawn while the A sweep is in flight / fA is awaited
-    auto next_noise = [&]() {
-      if (valid && t + 1 < d.T) pass_noise(d, t + 1, grow, i, en0, en1);
-    };
-    if (w == 0) {  // the row's nf_dyn context and fold (fold_one's fma sequence)
-      // cbd[par] was last read by the prior waves at step t - 2
-      if (t >= 2) {
-        wait_flag2(&L.pf[0], t - 1);
-        wait_flag2(&L.pf[2], t - 1);
-      }
-      const bool ok = poll_row(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, next_noise);
-      PT(t, 7);
-      if (ok) {
-        const Ctx4 c = row_ctx(L.rowa, tiles, N);
-        if (fold_lane) {
-          const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
-          float v = fwd[0];
-#pragma unroll
-          for (int q = 0; q < kOctxDyn; ++q) v = fmaf(fwd[1 + q], cv[q], v);
-          reinterpret_cast<float *>(L.cbd[par])[lane] = v;
-        }
-      }
-      set_flag(&L.fA, t + 1);
-    } else {
-      next_noise();
-      wait_flag(&L.fA, t + 1);
-    }
-    PT(t, 2);
-    // nf_dyn inverse (model/models.py:305-332)
-    float xd0 = p0, xd1 = p1, ld = 0.f;
-    if (valid)
-      for (int f = nfl - 1; f >= 0; --f) ld += pass_inverse(dyn + f * 2 * nsd, nsd, xd0, xd1, L.cbd[par] + f * 2 * kH);
-    const float jac = -ld;
-    PT(t, 3);
-    if (valid && S.hjac) S.hjac[i] = jac;
-    {
-      double s[4] = {valid ? xd0 : 0.0, valid ? xd1 : 0.0, valid ? (double)xd0 * xd0 : 0.0,
-                     valid ? (double)xd1 * xd1 : 0.0};
-      wave_sum_dpp_n(s);
-      publish4(ws.gb + gslot * kGA, s, tag);  // exchange B
-    }
-    if (w == 0) {  // the proposal fold: encoding columns (from wave 8), then [mean, std] of x_dyn
-      if (poll_row(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa)) {
-        PT(t, 8);
-        const Ctx4 c = row_ctx(L.rowa, tiles, N);
-        wait_flag(&L.fE, t + 1);
-        if (fold_lane) {
-          const float c4[4] = {c.m0, c.m1, c.s0, c.s1};
-          float a = L.encfold[par][lane];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) a = fmaf(fwc[q], c4[q], a);
-          reinterpret_cast<float *>(L.cbc[par])[lane] = a;
-        }
-      }
-      set_flag(&L.fB, t + 1);
-    } else {
-      wait_flag(&L.fB, t + 1);
-    }
-    PT(t, 4);
-    // NF proposal inverse (model/models.py:334-356)
-    float q0 = xd0, q1 = xd1, ldp = 0.f;
-    if (valid)
-      for (int f = nfl - 1; f >= 0; --f) ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
     // the group's encoder pair has read qbuf / rbuf[par] of step t - 2
     if (t >= 2) wait_flag2(&L.ef[2 * g], t - 1);
     if (valid) {  // to the prior wave and the encoder pair
@@ -716,27 +828,37 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       L.pbuf[par][slot] = p0 - e0;
       L.pbuf[par][kTile + slot] = p1 - e1;
       L.rbuf[par][kTile + slot] = (density(e0, e1, K, two_var) + jac) + (-ldp);  // propose
-      if (FORCE) {  // the next step's resampling reads the row's particles from other tiles
+      if (FORCE || GATE) {  // a later step's resampling reads the row's particles from other tiles
         store_wt2(S.hx + 2 * i, q0, q1);
       } else {
         S.hx[2 * i] = q0;
         S.hx[2 * i + 1] = q1;
       }
     }
-    // FORCE: drained before qf, which the encoder pair's C(t) granules then cover
+    // FORCE: drained before qf, which the encoder pair's C(t) granules then cover (GATE: drained
+    // by the next step's A sweep / resampling, hxf)
     if (FORCE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     set_flag(&L.qf[g], t + 1);
     PT(t, 5);
     x0 = q0;
     x1 = q1;
+    prev_dec = fire;
+  }
+  if (GATE) {  // the last slot's stores (the encoder pair's C(T - 1) waits for them)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    set_flag(&L.hxf[g], d.T);
   }
 }
 
 // waves 4-7 ("prior", group g = w - 4): the nf_dyn forward of the proposal and the prior density
-// (model/models.py:358-377, stage_prior_split) off the chain, into rbuf's prior half (flag rf[g])
-template <bool FORCE>
+// (model/models.py:358-377, stage_prior_split) off the chain, into rbuf's prior half (flag rf[g]).
+// They are half of the 8 flow waves that resample the row (pass_resample): every step (FORCE),
+// or (GATE) at the top of a step predicted to fire, or when the chain drops a step it had
+// speculated not to fire (rq) -- the same steps as the chain waves, so their barriers match.
+template <int MODE>
 __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                            uint32_t tag0) {
+  constexpr bool FORCE = MODE == kModeForce, GATE = MODE == kModeGate;
   const int N = d.N, nfl = d.n_flows;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = w - 4, slot = g * 64 + lane;
@@ -744,6 +866,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
   const bool valid = i < N;
   constexpr int nsd = kNsDyn;
   int round = 0;
+  int prev_dec = 0;
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
@@ -751,7 +874,8 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const RowSlot S = row_slot(d, b, t);
-    if constexpr (FORCE) pass_resample(d, ws, L, b, tile, tag0, t, round);
+    const int pred = GATE ? (t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
+    if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round);
     PT(t, 0);
     if (g == 0) {
       // the proposal fold over the encoding columns (model/models.py:338-346) one step ahead,
@@ -766,6 +890,18 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
         }
         set_flag(&L.fE, s + 1);
       }
+    }
+    if (GATE && !pred && t > 0) {
+      // the proposal, or the chain's call to resample the row after all (a dropped speculation;
+      // rq is only ever raised before qf of the same step)
+      Spin sp;
+      for (;;) {
+        const int q = __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.qf[g]);
+        const int r = __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq);
+        if (q >= t + 1 || r >= t + 1 || !pass_spin<NFDPF_PASS_FLAG_SLEEP>(sp)) break;
+      }
+      asm volatile("" ::: "memory");
+      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1) pass_resample(d, ws, L, b, tile, tag0, t, round);
     }
     wait_flag(&L.qf[g], t + 1);
     PT(t, 1);
@@ -784,6 +920,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     }
     set_flag(&L.rf[g], t + 1);
     set_flag(&L.pf[g], t + 1);
+    if (GATE) prev_dec = __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]);  // committed: known
     PT(t, 2);
   }
 }
@@ -791,10 +928,11 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
 // ---- waves 8-15 -----------------------------------------------------------------------------
 // wave 8: sweep C(s) of the row, leave its tile's merged ESS partial (the quad launch's merge,
 // include/nfdpf.h) at ess_out[s] and the row normaliser of slot s (row_norm) in L.rn
-__device__ __forceinline__ void pass_poll_c(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
-                                            uint32_t tag0, int s) {
+__device__ __forceinline__ float pass_poll_c(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b,
+                                             int tile, uint32_t tag0, int s) {
   const int tiles = n_tiles(d.N), lane = threadIdx.x & 63;
   const int64_t row0 = (((int64_t)(s & 1) * d.B + b) * tiles) * 8;
+  float inv = 0.f;
   if (poll_row(ws.gc + row0 * kGC, tiles * 8 * kGC, tag0 + (uint32_t)s + 1u, L.rowc)) {
     // lane k < tiles: tile k's {max, sum e, sum e^2} over its encoder waves in order
     const int k = lane < tiles ? lane : 0;
@@ -825,13 +963,58 @@ __device__ __forceinline__ void pass_poll_c(const nfdpf_filter_desc &d, const Pa
     double Sd = 0.0;
     for (int kk = 0; kk < tiles; ++kk) Sd += readlane_d(sum, kk) * (double)expf(readlane_f(m, kk) - M);
     if (lane == 0) L.rn[s & 1] = RowNorm{M, (float)Sd, 0.f};
+    // the row's 1 / sum p^2 of slot s (the next step's gate term): row_inv_ess's arithmetic on
+    // the same per-tile partials it would read from ess_out (filter_tiled.hip), + 1e-12 terms
+    double Mx = -INFINITY;
+    for (int kk = 0; kk < tiles; ++kk) {
+      const double mk = (double)readlane_f(m, kk);
+      Mx = mk > Mx ? mk : Mx;
+    }
+    double Sg = 0.0, Q = 0.0;
+    for (int kk = 0; kk < tiles; ++kk) {
+      const float f = expf((float)((double)readlane_f(m, kk) - Mx));
+      Sg += readlane_d(sum, kk) * (double)f;
+      Q += readlane_d(sq, kk) * ((double)f * (double)f);
+    }
+    const double sp2 = Q / (Sg * Sg) + (2e-12 + (double)d.N * 1e-24);
+    inv = 1.0f / (float)sp2;
   }
   set_flag(&L.fR, s + 1);
+  return inv;
+}
+
+// kModeGate, wave 8 of every workgroup: the batch-global ESS gate of step t (DPFs.py:163-165:
+// torch.mean over the rows of 1 / sum p^2 of slot t - 1, < 0.5 N), tiled_gate_batch_kernel's
+// arithmetic.  t = 0: from the initial partials (ess_all).  t > 0: this row's term `inv` (from the
+// C(t - 1) sweep) goes out as one granule from its tile 0, the B rows' granules are swept, and
+// the mean follows ATen's cascade order over them.  Every workgroup decides alike, from the same
+// words.  The decision goes to dec[t & 1] / fD; workgroup (0, 0) also records it (pass_gates,
+// the epilogue's count).
+__device__ __forceinline__ void pass_gate(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
+                                          uint32_t tag0, int t, float inv) {
+  const int tiles = n_tiles(d.N), lane = threadIdx.x & 63, B = d.B;
+  float s;
+  if (t == 0) {
+    const double *parts = reinterpret_cast<const double *>(d.ess_all);
+    s = cascade_row_sum([&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, d.N, false); }, B);
+  } else {
+    uint64_t *ge = ws.ge + (int64_t)((t - 1) & 1) * B;
+    const uint32_t tag = tag0 + (uint32_t)t;  // slot t - 1's
+    if (tile == 0 && lane == 0) gran_store(ge + b, __float_as_uint(inv), tag);
+    poll_rowx<4>(ge, B, tag, L.rowe);
+    s = cascade_row_sum([&](int r) { return __uint_as_float(L.rowe[r]); }, B);
+  }
+  const int fire = (s / (float)B) < 0.5f * (float)d.N ? 1 : 0;
+  if (lane == 0) L.dec[t & 1] = fire;
+  set_flag(&L.fD, t + 1);
+  if (b == 0 && tile == 0 && lane == 0) {
+    ws.eg[t] = fire;
+    if (d.pass_gates) d.pass_gates[t] = fire;
+  }
 }
 
 // normalise slot s of this wave's particles (finish_prev's arithmetic, the cosine measurement:
 // unshifted): hp, and the wave's prediction / obs-likelihood partials; returns log p
-template <bool FORCE>
 __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                            int s, int i_e, bool valid_e, float u, float qx0, float qx1) {
   wait_flag(&L.fR, s + 1);
@@ -855,9 +1038,14 @@ __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const Pas
   return lp;
 }
 
-template <bool FORCE>
+// waves 8-15 (a pair per group): the cosine measurement on the MFMA encoder, the log-weights,
+// exchange C and (wave 8) its sweep, slot t's normalisation; kModeGate: wave 8 also decides the
+// next step's gate right after the C sweep (pass_gate), and a step whose gate fired takes the
+// resampled log-weight of its particle's source (lr_l) instead of its own log p
+template <int MODE>
 __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                              uint32_t tag0) {
+  constexpr bool FORCE = MODE == kModeForce, GATE = MODE == kModeGate;
   const int tiles = n_tiles(d.N), N = d.N;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, we = w - 8;
   const int role = w & 1, g = (w >> 1) & 3;
@@ -868,6 +1056,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   const EncFrag2 ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
+  if (GATE && we == 0) pass_gate(d, ws, L, b, tile, tag0, 0, 0.f);
   for (int t = 0; t < d.T; ++t) {
     const int par = t & 1;
     const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
@@ -893,20 +1082,33 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       return cos_lik(ss, dot, vinv);
     };
     float lk = 0.f;
-    if constexpr (!FORCE) {
+    if constexpr (MODE == kModeSpec) {
       // the encoder first: it needs only the proposal, and it hides the C(t - 1) exchange
       if (grp) lk = encode();
       if (we == 0 && t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
       PT(t, 2);
-      if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
-    } else {
+      if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+    } else if constexpr (FORCE) {
       // the row's resampling at the top of step t needs slot t - 1 normalised first (fR(t - 1))
       if (we == 0 && t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
       PT(t, 2);
-      if (t > 0) lr = pass_norm<FORCE>(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+      if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
       wait_flag(&L.fS, t + 1);  // the flow waves resampled the row: the log-weight of the source
       lr = valid_e ? L.lr_l[slot_e] : 0.f;
       if (grp) lk = encode();
+    } else {
+      // GATE: slot t - 1's exchange, its normaliser and step t's decision first (the chain's
+      // speculation of step t waits for it), then the measurement
+      if (we == 0 && t > 0) {
+        const float inv = pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+        pass_gate(d, ws, L, b, tile, tag0, t, inv);
+      }
+      PT(t, 2);
+      if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
+      if (grp) lk = encode();
+      // step t is committed (qf): its decision is known; a fired gate resampled the row and
+      // this particle's log-weight is its source's (the chain's resampling left it in lr_l)
+      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0) lr = valid_e ? L.lr_l[slot_e] : 0.f;
     }
     // the log-weight (DPFs.py:187)
     PT(t, 3);
@@ -922,10 +1124,11 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     }
     set_flag(&L.ef[we], t + 1);  // qbuf / rbuf[par] read: the chain wave may reuse them at t + 2
     PT(t, 6);
-    if (FORCE) {  // the row's next resampling reads u from every tile: written through, drained
+    if (FORCE || GATE) {  // the row's next resampling reads u from every tile: written through, drained
       if (valid_e) store_wt(ws.gu + ((int64_t)par * d.B + b) * N + i_e, u);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if (GATE) wait_flag(&L.hxf[g], t + 1);  // ... and the particles (the chain's slot-t stores)
     // exchange C: this wave's softmax partials (wave_partials_quad's arithmetic)
     const float mw = wave_max_dpp(valid_e ? u : -INFINITY);
     const float ev = valid_e ? expf(u - mw) : 0.f;
@@ -946,10 +1149,10 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   }
   // the last slot's normalisation
   if (we == 0) pass_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
-  pass_norm<FORCE>(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
+  pass_norm(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
 }
 
-template <bool FORCE>
+template <int MODE>
 __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_filter_desc d, PassWs ws) {
   __shared__ PassLds L;
   int b, tile;
@@ -960,9 +1163,10 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
     L.qf[threadIdx.x] = 0;
     L.rf[threadIdx.x] = 0;
     L.pf[threadIdx.x] = 0;
+    L.hxf[threadIdx.x] = 0;
   }
   if (threadIdx.x < 8) L.ef[threadIdx.x] = 0;
-  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = 0;
+  if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = L.fD = L.rq = 0;
   __syncthreads();
 // issue priority: the chain waves carry the pass's critical path (chain 3 / others 0: +0.8 %
 // at C2 over equal priorities, two A/B rounds on one box)
@@ -973,13 +1177,13 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
 #endif
   if (threadIdx.x < 4 * 64) {
     __builtin_amdgcn_s_setprio(NFDPF_PRIO_CHAIN);
-    pass_chain<FORCE>(d, ws, L, b, tile, tag0);
+    pass_chain<MODE>(d, ws, L, b, tile, tag0);
   } else if (threadIdx.x < 8 * 64) {
     __builtin_amdgcn_s_setprio(NFDPF_PRIO_PRIOR);
-    pass_prior<FORCE>(d, ws, L, b, tile, tag0);
+    pass_prior<MODE>(d, ws, L, b, tile, tag0);
   } else {
     __builtin_amdgcn_s_setprio(NFDPF_PRIO_ENC);
-    pass_encoder<FORCE>(d, ws, L, b, tile, tag0);
+    pass_encoder<MODE>(d, ws, L, b, tile, tag0);
   }
 }
 
@@ -995,8 +1199,9 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
 // asked), clears the abort word and bumps the epoch -- the granules of the current layout are
 // cleared when its 20 bits wrap.  Replaces the epoch, finalize, gate-batch and verify launches
 // of round 4 (one 64-lane wave walked 64 steps x B rows serially there: 18 us per pass).
-__global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_filter_desc d, PassWs ws,
-                                                                 int gates_from) {
+// gates: 0 none, 1 verify (the speculative pass's gates from its partials), 2 the pass decided
+// them itself (kModeGate: ws.eg already holds them; only counted here)
+__global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_filter_desc d, PassWs ws, int gates) {
   __shared__ float lw_l[256];
   __shared__ int last;
   const int k = blockIdx.x, l = threadIdx.x, T = d.T, B = d.B, tiles = n_tiles(d.N), ent = tiles * 8;
@@ -1015,7 +1220,7 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     lw_l[b] = (float)sw;
   }
   int fired = 0;
-  if (gates_from) {
+  if (gates == 1) {
     const double *parts = k == 0 ? reinterpret_cast<const double *>(d.ess_all)
                                  : reinterpret_cast<const double *>(d.ess_out) + (int64_t)(k - 1) * B * tiles * kSm;
     const float s =
@@ -1027,8 +1232,8 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     double tot = 0.0;
     for (int b = 0; b < B; ++b) tot += (double)lw_l[b];
     ws.eq[k] = tot / ((double)B * (double)d.N);
-    ws.eg[k] = fired;
-    if (d.pass_gates && gates_from) d.pass_gates[k] = fired;
+    if (gates != 2) ws.eg[k] = fired;
+    if (d.pass_gates && gates == 1) d.pass_gates[k] = fired;
     // release the step's terms, then count this workgroup in
     const uint32_t n = __hip_atomic_fetch_add(&ws.hdr->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = n == (uint32_t)T - 1;
@@ -1059,6 +1264,16 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
   }
 }
 
+static int pass_mode_of(const nfdpf_filter_desc &d) {
+  return d.force_resample ? kModeForce : d.pass_gate ? kModeGate : kModeSpec;
+}
+typedef void (*pass_kernel_t)(const nfdpf_filter_desc, PassWs);
+static pass_kernel_t pass_kernel_of(const nfdpf_filter_desc &d) {
+  const int m = pass_mode_of(d);
+  return m == kModeForce ? tiled_pass_kernel<kModeForce> : m == kModeGate ? tiled_pass_kernel<kModeGate>
+                                                                          : tiled_pass_kernel<kModeSpec>;
+}
+
 // The pass applies to this descriptor's configuration (the launcher also needs the speculative
 // gate: d.gate given, ess_local) and every workgroup of its grid can be resident at once.
 static bool pass_config_ok(const nfdpf_filter_desc &d) {
@@ -1069,6 +1284,8 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   // a forced pass resamples every step inside the launch (soft resampler only); otherwise the
   // caller takes every gate as off and verifies them afterwards
   if (d.force_resample && d.resampler != NFDPF_RESAMPLE_SOFT) return false;
+  // the in-launch gate: the whole batch in this launch, the soft resampler (its lin markers)
+  if (d.pass_gate && !d.force_resample && (d.B_global != d.B || d.resampler != NFDPF_RESAMPLE_SOFT)) return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
       d.B < 1 || d.B > 256)  // (the epilogue stages a step's B row sums in LDS)
     return false;
@@ -1076,7 +1293,7 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &occ, d.force_resample ? tiled_pass_kernel<true> : tiled_pass_kernel<false>, 4 * kTile, 0) != hipSuccess ||
+          &occ, pass_kernel_of(d), 4 * kTile, 0) != hipSuccess ||
       occ < 1)
     return false;
   return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;

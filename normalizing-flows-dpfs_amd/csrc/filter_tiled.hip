@@ -2091,11 +2091,14 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_pass_tiled: a forced pass needs lin and an 8-B aligned hist_x");
   NFDPF_REQUIRE(pass_config_ok(d),
                 "nfdpf_filter_pass_tiled: configuration not supported here (nfdpf_filter_pass_supported == 0)");
-  // the epilogue's gates: a speculative pass of the whole batch (a sharded one is verified by
-  // the caller over the gathered partials, nfdpf_ess_gate_tiled_batch)
-  const int verify = !d.force_resample && d.pass_gates && d.B_global == d.B && d.ess_all;
-  NFDPF_REQUIRE(!d.pass_gates || verify, "nfdpf_filter_pass_tiled: pass_gates needs a speculative pass of the whole "
-                                         "batch (B_global == B) with its initial partials in ess_all");
+  const int mode = pass_mode_of(d);
+  NFDPF_REQUIRE(d.ess_all || mode == kModeForce, "nfdpf_filter_pass_tiled: ess_all (the initial partials) missing");
+  // the epilogue's gates: those of a speculative pass of the whole batch (a sharded one is
+  // verified by the caller over the gathered partials, nfdpf_ess_gate_tiled_batch), or the
+  // decisions the gated pass took itself
+  const int verify = mode == kModeSpec && d.pass_gates && d.B_global == d.B;
+  NFDPF_REQUIRE(!d.pass_gates || verify || mode == kModeGate,
+                "nfdpf_filter_pass_tiled: pass_gates needs a pass of the whole batch (B_global == B) that is not forced");
   hipStream_t st = as_stream(stream);
   PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
   ws.wait_ticks = kPassWaitTicks;
@@ -2103,12 +2106,12 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
     ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
   const dim3 g(n_tiles(d.N), d.B);
   hipEvent_t *ev = (hipEvent_t *)d.prof_events;
-  const auto kern = d.force_resample ? tiled_pass_kernel<true> : tiled_pass_kernel<false>;
+  const auto kern = pass_kernel_of(d);
   if (ev)
     hipExtLaunchKernelGGL(kern, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
   else
     kern<<<g, 4 * kTile, 0, st>>>(d, ws);
-  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, verify);
+  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate ? 2 : verify);
   return launch_status("nfdpf_filter_pass_tiled");
 }
 

@@ -65,6 +65,10 @@ class FilterConfig:
     # exchange, then gather all steps' softmax partials once and verify the gates (a fired
     # gate reruns the pass with the per-step exchange); None = on when the batch is sharded
     speculate_gate: Optional[bool] = None
+    # the one-launch pass with the ESS gate decided INSIDE the launch at every step (one GPU, soft
+    # resampler: nfdpf_filter_pass_tiled with pass_gate = 1); None / True = wherever it applies
+    # and the pass is not speculated explicitly, False = never
+    pass_gate: Optional[bool] = None
 
 
 @dataclass
@@ -154,6 +158,8 @@ class FilterEngine:
         # process or kernel held CUs) turns the pass off for this engine; the step launches rerun
         self.pass_disabled = False
         self._shared_device = None  # per process group: does another rank use this rank's GPU?
+        self.last_gate_pass = False  # the last run was the gated one-launch pass (gates decided in the launch)
+        self.last_gates = None       # one shard's one-launch pass: its T gates (decided, or verified) [T] int32
 
     def __getstate__(self):
         # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
@@ -161,12 +167,13 @@ class FilterEngine:
         st = dict(self.__dict__)
         st.pop("_pending", None)
         st.pop("_nfdpf_pass_ws", None)
+        st["last_gates"] = None
         st["_shared_device"] = None
         st["step_events"] = None
         return st
 
     def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False,
-                     finish=True, pass_ok=False) -> bool:
+                     finish=True, pass_ok=False, gate_ok=False) -> bool:
         """Does the next pass run with the speculative ESS gate (every gate taken as off, the T
         gates verified once after the pass from all steps' partials, a fired gate rerunning the
         pass step by step)?  Auto mode (``speculate`` and cfg.speculate_gate None): yes for the
@@ -174,7 +181,9 @@ class FilterEngine:
         for OT at any world size (its gate is read on the host before every Sinkhorn call,
         DPFs.py:165: a device->host sync per step), and wherever the whole pass runs as ONE
         persistent launch (``pass_ok``: nfdpf_filter_pass_tiled, the C2 shape; it needs every
-        gate of the pass known in advance) -- unless the previous pass resampled (OT: its gates
+        gate of the pass known in advance) and the gate cannot be decided inside that launch
+        (``gate_ok``: one GPU, soft resampler -- the gated pass decides every gate itself, so
+        nothing is speculated there) -- unless the previous pass resampled (OT: its gates
         are then read step by step) or a recent miss is backing off (a miss costs a whole second
         pass; the next 1, 2, 4 ... 64 passes run step by step).  Not for the step-by-step soft
         resampler on one GPU: its per-step gate is device-side already, and speculating saved
@@ -188,7 +197,7 @@ class FilterEngine:
         auto = speculate is None and c.speculate_gate is None
         if speculate is None:
             speculate = c.speculate_gate if c.speculate_gate is not None else \
-                (tiled and (shard.world > 1 or c.resampler == "ot" or pass_ok))
+                (tiled and (shard.world > 1 or c.resampler == "ot" or (pass_ok and not gate_ok)))
             if auto and finish and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 speculate = False
         if auto and tiled and c.resampler == "ot" and self._ot_fired:
@@ -203,8 +212,16 @@ class FilterEngine:
     def speculates(self, shard=None, finish=True) -> bool:
         """Whether run() (auto arguments, device RNG) will speculate the gates of its next pass
         (same shapes as the last run: whether the one-launch pass applies is taken from it)."""
-        return self._decide_spec(shard or ShardInfo(), None, self.cfg.rng_mode == "host", finish=finish,
-                                 pass_ok=self.last_pass_ok)
+        shard = shard or ShardInfo()
+        return self._decide_spec(shard, None, self.cfg.rng_mode == "host", finish=finish,
+                                 pass_ok=self.last_pass_ok, gate_ok=self._gate_ok(shard, self.last_pass_ok))
+
+    def _gate_ok(self, shard, pass_ok) -> bool:
+        """Can the one-launch pass decide the ESS gate inside the launch (the whole batch on this
+        GPU, the soft resampler)?"""
+        c = self.cfg
+        return bool(pass_ok and shard.world == 1 and c.resampler == "soft" and not c.force_resample
+                    and c.pass_gate is not False)
 
     def _pass_supported(self, B, N, T, E, split_nets, shard) -> bool:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
@@ -339,11 +356,15 @@ class FilterEngine:
         pass_ok = (not external and teacher is None and not host_mode
                    and self._pass_supported(B, N, T, E, split_nets, shard))
         self.last_pass_ok = pass_ok
+        gate_ok = self._gate_ok(shard, pass_ok)
         spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish,
-                                 pass_ok=pass_ok)
-        # the one-launch pass: gates speculated (verified after it), or every step resampling
-        # (--force-resample: no gate to decide, the row's resampling runs inside the launch)
-        use_pass = pass_ok and (spec or c.force_resample)
+                                 pass_ok=pass_ok, gate_ok=gate_ok)
+        # the one-launch pass: gates speculated (verified after it), decided inside the launch
+        # (one GPU, soft resampler), or every step resampling (--force-resample: no gate to
+        # decide, the row's resampling runs inside the launch)
+        gate_pass = gate_ok and not spec
+        use_pass = pass_ok and (spec or c.force_resample or gate_pass)
+        self.last_gate_pass = gate_pass
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)
@@ -442,11 +463,12 @@ class FilterEngine:
             d.ess_all, d.ess_out, d.gate = ess_in_p[0], ess_out_p[0], spec_gate_p
             pdyn, pcond = self._pass_blobs(dev)  # the pass layout (tanh algebra in the weights)
             d.dyn_params, d.cond_params = pdyn.data_ptr(), pcond.data_ptr()
-            d.pass_gate = 0
+            d.pass_gate = int(gate_pass)
             if shard.world == 1:  # the epilogue verifies the gates / reads the fault counter on the device
                 i32 = dict(device=dev, dtype=torch.int32)
-                pass_out = (torch.empty(T, **i32) if spec else None, torch.empty(2, **i32),
+                pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(2, **i32),
                             torch.empty((), **f32))
+                self.last_gates = pass_out[0]  # the T gates: decided in the launch, or verified
                 d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
             d.prof_events, d.prof_front = None, 0
             if self.step_events is not None:
@@ -577,7 +599,7 @@ class FilterEngine:
         capturing = torch.cuda.is_current_stream_capturing()
         check_split = tiled and handoffs and not capturing
         if use_pass and not spec:
-            # a forced pass: one shard's epilogue read the fault counter and reduced the
+            # a forced or gated pass: one shard's epilogue read the fault counter and reduced the
             # obs-likelihood (one host read here, none while capturing a graph); sharded, every
             # rank's count is summed so that all ranks fall back together
             check_split = False

@@ -47,9 +47,11 @@ def _run(case, rows, shard=None):
     name, B, N, T = CASES[case]
     wl = F.workload(name, B=B, N=N, T=T)
     c = F.cfg_dict(wl["flags"], N)
+    # (pass_gate off: the unsharded run's rerun after a fired gate is then the step launches, as the
+    # sharded ranks' -- the gated one-launch pass needs the whole batch on one GPU)
     cfg = FilterConfig(N=N, NF_dyn=c["NF_dyn"], NF_cond=c["NF_cond"], measurement=c["measurement"],
                        resampler=c["resampler"], dyn_flow=c["dyn_flow"], force_resample=wl["force"], seed=123,
-                       kernel="tiled")
+                       kernel="tiled", pass_gate=False)
     eng = FilterEngine(cfg, wl["models"].to(DEV))
     sl = slice(*rows)
     res = eng.run(wl["enc"][sl].to(DEV), wl["start"][sl].to(DEV), wl["vel"][sl].to(DEV), shard=shard)
@@ -144,11 +146,12 @@ def _pass_run(kind, rows, shard=None, rank=0, world=1):
     from nfdpf.engine import FilterConfig, FilterEngine
     B, N, T = PASS_CASES[kind]
     models, enc, start, vel = _pass_inputs(kind, rows)
-    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321, kernel="tiled")
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321, kernel="tiled",
+                       pass_gate=False)  # (the unsharded rerun: the step launches, as the sharded ranks')
     eng = FilterEngine(cfg, models)
     for r in range(world):
         if r == rank:
-            res = eng.run(enc, start, vel, shard=shard, finish=False)
+            res = eng.run(enc, start, vel, shard=shard, finish=False, speculate=True)
             torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

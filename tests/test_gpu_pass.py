@@ -2,11 +2,13 @@
 against (a) the step-by-step tiled launches on the same device-RNG draws and (b) the oracle
 (the reference's algorithm, float32 and float64) replaying those draws.  GPU box only.
 
-The pass runs every ESS gate as off (DPFs.py:163-165 speculated) and the engine verifies the T
-gates afterwards; a fired gate reruns the pass step by step (test_pass_gate_fired_reruns).
-Within a step the pass differs from the step launches only in the order of ONE reduction (the
-row's x_phys sums: per tile here, per row there), so (a) is a rounding-level comparison; (b)
-is the reference-parity check: every history within the reference's own float32 envelope.
+Three modes: speculative (every ESS gate, DPFs.py:163-165, taken as off and verified after the
+pass; a fired gate reruns the pass), forced (the row resampled at the top of every step) and
+gated (the batch-global gate decided inside the launch at every step -- the default on one GPU).
+Against the step launches the pass differs in the order of the row's x_phys sums and in the
+coupling nets' rounding (the tanh algebra is folded into the pass layout's weights), so (a) is
+a rounding-level comparison; (b) is the reference-parity check: every history within the
+reference's own float32 envelope, the gate decisions and resampling indices exact.
 """
 import os
 
@@ -85,12 +87,17 @@ def test_pass_matches_step_launches(B, N, T, fixture, monkeypatch):
     models = _models(fixture)
     enc, start, vel = _inputs(B, T, seed=B * 1000 + N)
     eng, a = _run(models, N, enc, start, vel, spec=True)
-    assert eng.pass_launches == 1, "the one-launch pass did not run"
-    _, b = _run(models, N, enc, start, vel, spec=False)
-    if fixture == "e2e_c2w.npz" and not eng.last_pass:  # a gate fired: the rerun is the result
-        for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
-            assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert eng.pass_launches >= 1, "the one-launch pass did not run"
+    if fixture == "e2e_c2w.npz" and not eng.last_gates.eq(0).all():
+        # a gate fired: the verification caught it and the rerun -- the gated one-launch pass --
+        # is the result, bit for bit the gated pass run directly
+        assert eng.pass_launches == 2 and eng.last_gate_pass
+        eng_g, g = _run(models, N, enc, start, vel, spec=False)
+        assert eng_g.last_gate_pass and eng_g.pass_launches == 1
+        for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred", "obs_likelihood"):
+            assert torch.equal(getattr(a, f), getattr(g, f)), f
         return
+    _, b = _run(models, N, enc, start, vel, spec=False, env="0", monkeypatch=monkeypatch)  # the step launches
     assert eng.last_pass, f"a gate fired on the {fixture} flows"
     assert torch.equal(a.noise, b.noise)
     assert torch.equal(a.index, b.index)
@@ -185,21 +192,30 @@ def test_pass_vs_oracle(B, N, T, fixture):
 
 
 def test_pass_gate_fired_reruns(monkeypatch):
-    """Encodings aligned with the true state: the ESS gate fires, the verification catches it
-    and the pass reruns step by step -- the result is the step-by-step pass, bit for bit."""
+    """Encodings aligned with the true state: the ESS gate fires.  The speculative pass's
+    verification catches it and reruns -- as the gated one-launch pass, which decides every gate
+    inside the launch: the result is that pass run directly, bit for bit (histories, decisions,
+    obs-likelihood).  (The gated pass against the reference at every step, decisions and indices
+    exact: test_gated_pass_every_step_vs_oracle.)"""
     fx = load("e2e_c2.npz")
     models = _Models(weights(fx), e2e_cfg(fx))
     enc, start, vel = t(fx["enc"]).to(DEV), t(fx["start"]).to(DEV), t(fx["vel"]).to(DEV)
     N = int(fx["N"])
     eng_a, a = _run(models, N, enc, start, vel, spec=True)
-    _, b = _run(models, N, enc, start, vel, spec=False)
+    assert eng_a.pass_launches == 2 and eng_a.last_gate_pass, "the fired speculation was not rerun as the gated pass"
+    ga = eng_a.last_gates.clone()
+    eng_b, b = _run(models, N, enc, start, vel, spec=False)
+    assert eng_b.pass_launches == 1 and eng_b.last_gate_pass
     for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred"):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     assert torch.equal(a.obs_likelihood, b.obs_likelihood)
+    assert torch.equal(ga, eng_b.last_gates)
     B, T = enc.shape[0], enc.shape[1]
     ident = torch.arange(N, device=DEV) + N * torch.arange(B, device=DEV)[:, None]
-    assert int((a.index != ident[:, None, :]).any(-1).any(0).sum()) > 0, "the gate never fired"
-    assert not eng_a.last_pass  # the returned pass is the rerun
+    fired_rows = (a.index != ident[:, None, :]).any(-1).any(0).int()
+    assert int(fired_rows.sum()) > 0, "the gate never fired"
+    # a fired step resamples (almost surely moves some index), a quiet one leaves the identity
+    assert torch.equal(fired_rows, ga.int()), (fired_rows.tolist(), ga.tolist())
 
 
 def test_pass_deterministic_and_graph_replay():
@@ -465,3 +481,120 @@ def test_pass_timeout_falls_back(force, monkeypatch):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     from nfdpf import _lib
     assert _lib.lib().nfdpf_split_fault(1, torch.cuda.current_stream().cuda_stream) == 0
+
+
+@pytest.mark.parametrize("B,N,T", [(64, 1000, 50), (6, 777, 12), (3, 100, 8)])
+def test_gated_pass_every_step_vs_oracle(B, N, T, monkeypatch):
+    """The gated one-launch pass (the ESS gate decided INSIDE the launch at every step,
+    DPFs.py:163-170) on the c2_full workload -- the C2 flags and size with frame encodings aligned
+    with the true state, so the gate fires on a mix of steps -- against the oracle's step
+    (oracle.filter_step, DPFs.py:160-192) started from the PASS's own slot t-1 with its device
+    offsets and motion noise: every step's gate decision equals the reference's
+    torch.mean(1 / sum p^2) < 0.5 N on the same weights, the indices are bit-exact, and the
+    particles, weights, likelihood, jac and prior of every slot lie within the reference's own
+    float32 envelope against the float64 oracle.  Both fired and quiet steps must occur."""
+    import _fullsize as F
+    from nfdpf import ops
+    from nfdpf.engine import FilterConfig, FilterEngine
+    wl = F.workload("c2_full", B=B, N=N, T=T)
+    models = wl["models"].to(DEV)
+    w = {k: v.detach().cpu() for k, v in models.state_dict().items()}
+    c = F.cfg_dict(wl["flags"], N)
+    enc, start, vel = wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV)
+    x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 4242, 0, DEV)
+    p0, _ = ops.normalize_log_probs(logw0)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=4242, kernel="tiled")
+    eng = FilterEngine(cfg, models)
+    res = eng.run(enc, start, vel, init=(x0, logw0))
+    torch.cuda.synchronize()
+    assert eng.last_pass and eng.last_gate_pass, "the gated one-launch pass did not run"
+    gates = eng.last_gates.cpu()
+    off = torch.from_numpy(_philox_offsets(4242, T, B, N))
+    xs, ps, nz = res.particles.cpu(), res.probs.cpu(), res.noise.cpu()
+    x0c, p0c, encc, startc, velc = x0.cpu(), p0.cpu(), enc.cpu(), start.cpu(), vel.cpu()
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    keys = ("x", "p", "lik", "jac", "prior", "idx", "lw_mean")
+    outs, fired = {}, {}
+    soft32 = O.soft_resample
+    for dt in (torch.float32, torch.float64):
+        if dt == torch.float64:
+            monkeypatch.setattr(O, "soft_resample", _soft_indices32(soft32))
+        acc = {k: [] for k in keys}
+        fired[dt] = []
+        with O.precision(dt):
+            wd = O.cast_params(w, dt)
+            meas = O.make_measurement(c, wd)
+            for t_ in range(T):
+                xp = (x0c if t_ == 0 else xs[:, t_ - 1]).to(dt)
+                pp = (p0c if t_ == 0 else ps[:, t_ - 1]).to(dt)
+                v = (startc[:, 2:] if t_ == 0 else velc[:, t_ - 1]).to(dt)
+                # float64: the reference's own (float32) decision, as its indices
+                r = O.filter_step(c, wd, meas, xp, pp, v, encc[:, t_].to(dt), _StepDraws(off[t_], nz[:, t_].to(dt)),
+                                  force_resample=bool(gates[t_]) if dt == torch.float64 else False)
+                fired[dt].append(bool(r["fired"]))
+                for k in keys:
+                    acc[k].append(r[k] if k != "lw_mean" else r[k].reshape(1))
+        outs[dt] = {k: torch.stack(v, 1 if k != "lw_mean" else 0).double().numpy() for k, v in acc.items()}
+    dec = [bool(g) for g in gates.tolist()]
+    assert dec == fired[torch.float32], f"gate decisions differ from the reference's: {dec} vs {fired[torch.float32]}"
+    n_fired = sum(dec)
+    print(f"\ngated pass vs oracle step by step, B={B} N={N} T={T}: the gate fired in {n_fired} of {T} steps")
+    assert 0 < n_fired < T, "the case should mix fired and quiet steps"
+    r32, r64 = outs[torch.float32], outs[torch.float64]
+    np.testing.assert_array_equal(res.index.cpu().numpy(), r32["idx"].astype(np.int64))
+    for k, ours, rtol, atol in (("x", xs, 1e-5, 1e-4), ("p", ps, 1e-5, 1e-9), ("lik", res.lik.cpu(), 1e-5, 2e-5),
+                                ("jac", res.jac.cpu(), 1e-5, 1e-6), ("prior", res.prior.cpu(), 1e-5, 1e-5)):
+        _check_envelope(ours, r32[k], r64[k], rtol, atol, k)
+        _fractions(k, ours, r32[k], r64[k], 1e-5, 0.0 if k != "jac" else 1e-6)
+    obs32, obs64 = r32["lw_mean"].sum(), r64["lw_mean"].sum()
+    assert abs(float(res.obs_likelihood) - obs64) <= 4 * abs(obs32 - obs64) + 1e-5 * abs(obs64) + 1e-4
+
+
+def test_gated_pass_quiet_equals_speculative():
+    """On a workload whose gate never fires (the bench's model at its init weights, N(0,1)
+    encodings) the gated pass takes the speculative pass's path at every step: identical bits,
+    obs-likelihood included, and no decision fired."""
+    models = _models("bench")
+    B, N, T = 16, 1000, 20
+    enc, start, vel = _inputs(B, T, seed=77)
+    eng_s, s_ = _run(models, N, enc, start, vel, spec=True)
+    eng_g, g_ = _run(models, N, enc, start, vel, spec=None)
+    assert eng_s.last_pass and not eng_s.last_gate_pass and eng_s.pass_launches == 1
+    assert eng_g.last_pass and eng_g.last_gate_pass
+    assert int(eng_g.last_gates.sum()) == 0
+    for f in ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred", "obs_likelihood"):
+        assert torch.equal(getattr(s_, f), getattr(g_, f)), f
+
+
+def test_gated_pass_decisions_match_gate_kernel():
+    """The in-launch decisions (from registers, after each step's row exchange) equal the batch
+    gate kernel (nfdpf_ess_gate_tiled_batch) on the same pass's own per-step partials -- the two
+    evaluate one arithmetic."""
+    from nfdpf import ops
+    import _fullsize as F
+    B, N, T = 8, 1000, 16
+    wl = F.workload("c2_full", B=B, N=N, T=T)
+    models = wl["models"].to(DEV)
+    from nfdpf.engine import FilterConfig, FilterEngine
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=99, kernel="tiled")
+    eng = FilterEngine(cfg, models)
+    captured = {}
+    orig = ops.tiled_init
+
+    def keep(p0, out):  # the engine's [T + 1, B, tiles, 4] partials: slot 0 is the initial one
+        captured["base"] = out
+        return orig(p0, out)
+    ops.tiled_init = keep
+    try:
+        eng.run(wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+    finally:
+        ops.tiled_init = orig
+    torch.cuda.synchronize()
+    assert eng.last_gate_pass
+    tiles = ops.tiled_tiles(N)
+    base = captured["base"]
+    hist = torch.as_strided(base, (T, B, tiles, 4), base.stride() if base.dim() == 4 else
+                            (B * tiles * 4, tiles * 4, 4, 1))
+    ref = ops.ess_gate_tiled_batch(hist.contiguous(), N, 0, False)
+    assert torch.equal(ref.cpu(), eng.last_gates.cpu()), (ref.tolist(), eng.last_gates.tolist())
+    assert 0 < int(ref.sum()) < T
