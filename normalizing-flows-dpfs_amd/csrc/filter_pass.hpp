@@ -496,7 +496,9 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   // the tile's sources' positions (their loads in flight while wave 0 sums the gathered weights),
   // then wave 0 turns every particle of the tile into its resampled log-weight
   if (tid < kTile && i0 + tid < N) {
-    const int sj = R.src_l[tid];
+    // (clamped: after an abort the barriers no longer order anything and src_l may hold stale
+    // LDS words -- an address must never come from them)
+    const int sj = min(max(R.src_l[tid], 0), N);
     const float *src = xs + 2 * (sj < N ? sj : N - 1);
     if (sj >= N && b + 1 < d.B) {
       src = xs + xs_next;
@@ -680,7 +682,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       if (valid) {
         xs0 = L.rs.xr_l[slot][0];
         xs1 = L.rs.xr_l[slot][1];
-        src = L.rs.src_l[slot];
+        src = min(max(L.rs.src_l[slot], 0), N);  // (a value, never an address; clamped all the same)
       }
     };
     if (FORCE || (GATE && pred)) {  // soft resampling of the row (--force-resample / predicted)
@@ -805,6 +807,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       if (!GATE || known) break;
       // the speculated step's decision: commit, or drop the attempt and redo after resampling
       fire = wait_dec(L, t);
+      PT(t, 9);
       known = true;
       if (!fire) break;
       if (w == 0) set_flag(&L.rq, t + 1);  // the prior waves join the row's resampling
@@ -1042,10 +1045,41 @@ __device__ __forceinline__ float pass_norm(const nfdpf_filter_desc &d, const Pas
 // exchange C and (wave 8) its sweep, slot t's normalisation; kModeGate: wave 8 also decides the
 // next step's gate right after the C sweep (pass_gate), and a step whose gate fired takes the
 // resampled log-weight of its particle's source (lr_l) instead of its own log p
+// issue priority: the chain waves carry the pass's critical path (chain 3 / others 0: +0.8 %
+// at C2 over equal priorities, two A/B rounds on one box)
+#ifndef NFDPF_PRIO_CHAIN
+#define NFDPF_PRIO_CHAIN 3
+#define NFDPF_PRIO_PRIOR 0
+#define NFDPF_PRIO_ENC 0
+#endif
+#ifndef NFDPF_GPRIO_PRIOR
+#define NFDPF_GPRIO_PRIOR 0
+#endif
+// Which encoder wave sweeps exchange C (and, GATE, decides the gate), and the issue priority it
+// takes meanwhile: in the gated and forced passes that sweep is on the step's critical path
+// (the decision / the row's resampling wait for it), while its SIMD also carries a chain wave
+// at priority 3.
+#ifndef NFDPF_SWEEP_WE
+#define NFDPF_SWEEP_WE 0
+#endif
+#ifndef NFDPF_SWEEP_PRIO
+#define NFDPF_SWEEP_PRIO 0
+#endif
+template <int MODE>
+__device__ __forceinline__ void sweep_prio(bool on) {
+  if constexpr (MODE != kModeSpec && NFDPF_SWEEP_PRIO != 0) {
+    if (on)
+      __builtin_amdgcn_s_setprio(NFDPF_SWEEP_PRIO);
+    else
+      __builtin_amdgcn_s_setprio(NFDPF_PRIO_ENC);
+  }
+}
+
 template <int MODE>
 __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                              uint32_t tag0) {
   constexpr bool FORCE = MODE == kModeForce, GATE = MODE == kModeGate;
+  const int sweeper = MODE == kModeSpec ? 0 : NFDPF_SWEEP_WE;  // (encoder-wave index, 0..7)
   const int tiles = n_tiles(d.N), N = d.N;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, we = w - 8;
   const int role = w & 1, g = (w >> 1) & 3;
@@ -1056,7 +1090,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   const EncFrag2 ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
-  if (GATE && we == 0) pass_gate(d, ws, L, b, tile, tag0, 0, 0.f);
+  if (GATE && we == sweeper) pass_gate(d, ws, L, b, tile, tag0, 0, 0.f);
   for (int t = 0; t < d.T; ++t) {
     const int par = t & 1;
     const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
@@ -1090,7 +1124,11 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
     } else if constexpr (FORCE) {
       // the row's resampling at the top of step t needs slot t - 1 normalised first (fR(t - 1))
-      if (we == 0 && t > 0) pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+      if (we == sweeper && t > 0) {
+        sweep_prio<MODE>(true);
+        pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+        sweep_prio<MODE>(false);
+      }
       PT(t, 2);
       if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
       wait_flag(&L.fS, t + 1);  // the flow waves resampled the row: the log-weight of the source
@@ -1099,9 +1137,12 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     } else {
       // GATE: slot t - 1's exchange, its normaliser and step t's decision first (the chain's
       // speculation of step t waits for it), then the measurement
-      if (we == 0 && t > 0) {
+      if (we == sweeper && t > 0) {
+        sweep_prio<MODE>(true);
         const float inv = pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
+        PT(t, 10);
         pass_gate(d, ws, L, b, tile, tag0, t, inv);
+        sweep_prio<MODE>(false);
       }
       PT(t, 2);
       if (t > 0) lr = pass_norm(d, ws, L, b, tile, t - 1, i_e, valid_e, u, qx0, qx1);
@@ -1148,7 +1189,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     PT(t, 7);
   }
   // the last slot's normalisation
-  if (we == 0) pass_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
+  if (we == sweeper) pass_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
   pass_norm(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
 }
 
@@ -1168,18 +1209,14 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
   if (threadIdx.x < 8) L.ef[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.fA = L.fB = L.fE = L.fR = L.fS = L.fbar = L.fD = L.rq = 0;
   __syncthreads();
-// issue priority: the chain waves carry the pass's critical path (chain 3 / others 0: +0.8 %
-// at C2 over equal priorities, two A/B rounds on one box)
-#ifndef NFDPF_PRIO_CHAIN
-#define NFDPF_PRIO_CHAIN 3
-#define NFDPF_PRIO_PRIOR 0
-#define NFDPF_PRIO_ENC 0
-#endif
   if (threadIdx.x < 4 * 64) {
     __builtin_amdgcn_s_setprio(NFDPF_PRIO_CHAIN);
     pass_chain<MODE>(d, ws, L, b, tile, tag0);
   } else if (threadIdx.x < 8 * 64) {
-    __builtin_amdgcn_s_setprio(NFDPF_PRIO_PRIOR);
+    if constexpr (MODE == kModeSpec)
+      __builtin_amdgcn_s_setprio(NFDPF_PRIO_PRIOR);
+    else  // the prior's nf_dyn forward feeds the weights every decision / resampling waits for
+      __builtin_amdgcn_s_setprio(NFDPF_GPRIO_PRIOR);
     pass_prior<MODE>(d, ws, L, b, tile, tag0);
   } else {
     __builtin_amdgcn_s_setprio(NFDPF_PRIO_ENC);

@@ -152,8 +152,9 @@ def test_pass_vs_oracle(B, N, T, fixture):
     (test_gpu_parity._check_envelope, the one-step tests' bar), free-running over T steps (no
     resampling: nothing discrete can diverge).  Includes the headline shape, 64 x 1000 x 50.
     The e2e_c2 flows (std 0.05) degenerate the weights on some draws and the gate then fires
-    (the pass is rerun step by step, compared elsewhere): the first of a fixed list of input
-    seeds whose gates all stay off is used -- deterministic, and never a skip."""
+    (compared elsewhere): the first of a fixed list of input seeds whose gates all stay off by a
+    margin (every step's ESS above 0.6 N, so that the oracle's own rounding cannot tip one) is
+    used -- deterministic, and never a skip."""
     from nfdpf import ops
     c = e2e_cfg(load("e2e_c2.npz"))  # the C2 flags
     c["N"] = N
@@ -162,15 +163,17 @@ def test_pass_vs_oracle(B, N, T, fixture):
     from nfdpf.engine import FilterConfig, FilterEngine
     cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=5,
                        kernel="tiled", speculate_gate=True)
-    for k in range(8 if fixture != "bench" else 1):
+    for k in range(12 if fixture != "bench" else 1):
         enc, start, vel = _inputs(B, T, seed=7 * N + B + 1000 * k)
         x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 5, 0, DEV)
         eng = FilterEngine(cfg, models)
         res = eng.run(enc, start, vel, init=(x0, logw0))
         torch.cuda.synchronize()
-        if eng.last_pass:
+        ess = (1.0 / (res.probs[:, :-1].double() ** 2).sum(-1)).mean(0)  # the gates of steps 1 .. T-1
+        if eng.last_pass and (T == 1 or float(ess.min()) > 0.6 * N):
             break
-    assert eng.last_pass, "a gate fired on every input seed: the one-launch pass was rerun step by step"
+    assert eng.last_pass and (T == 1 or float(ess.min()) > 0.6 * N), \
+        "no input seed kept the gate off by a margin: the one-launch pass was rerun step by step"
     outs = {}
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     for dt in (torch.float32, torch.float64):
