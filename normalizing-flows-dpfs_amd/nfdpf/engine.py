@@ -148,6 +148,13 @@ class FilterEngine:
         self.step_events = None  # list -> nfdpf.prof.EventPair around the dominant launch of step T//2 of every pass
         self._spec_backoff = 0  # auto speculative gate: passes to run per-step after the next miss / 2
         self._spec_skip = 0     # per-step passes left before speculating again
+        # auto, where the gated one-launch pass applies: after a speculative pass missed (a gate
+        # fired) the next passes run gated -- the gates decided inside the launch, nothing wasted
+        # when they fire -- until two gated passes in a row fired none; then speculation again
+        # (the speculative pass is the faster one when no gate fires: no batch-wide decision in
+        # each step's critical path)
+        self._gate_mode = False
+        self._gate_quiet = 0
         # OT, auto mode: did the last pass resample?  Then the next one reads its gates step by
         # step (as the reference: one host sync per step); otherwise it speculates
         self._ot_fired = False
@@ -183,7 +190,8 @@ class FilterEngine:
         persistent launch (``pass_ok``: nfdpf_filter_pass_tiled, the C2 shape; it needs every
         gate of the pass known in advance) and the gate cannot be decided inside that launch
         (``gate_ok``: one GPU, soft resampler -- the gated pass decides every gate itself, so
-        nothing is speculated there) -- unless the previous pass resampled (OT: its gates
+        nothing is speculated while the recent passes' gates fire: the engine's gate mode) -- unless
+        the previous pass resampled (OT: its gates
         are then read step by step) or a recent miss is backing off (a miss costs a whole second
         pass; the next 1, 2, 4 ... 64 passes run step by step).  Not for the step-by-step soft
         resampler on one GPU: its per-step gate is device-side already, and speculating saved
@@ -197,7 +205,7 @@ class FilterEngine:
         auto = speculate is None and c.speculate_gate is None
         if speculate is None:
             speculate = c.speculate_gate if c.speculate_gate is not None else \
-                (tiled and (shard.world > 1 or c.resampler == "ot" or (pass_ok and not gate_ok)))
+                (tiled and (shard.world > 1 or c.resampler == "ot" or (pass_ok and not (gate_ok and self._gate_mode))))
             if auto and finish and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 speculate = False
         if auto and tiled and c.resampler == "ot" and self._ot_fired:
@@ -604,11 +612,18 @@ class FilterEngine:
             # rank's count is summed so that all ranks fall back together
             check_split = False
             if not capturing:
-                faults = int(pass_out[1][1].item()) if pass_out is not None else self._faults_all(shard, dev)
+                if pass_out is not None:
+                    n_fired, faults = pass_out[1].tolist()
+                else:
+                    n_fired, faults = 0, self._faults_all(shard, dev)
                 if faults:  # the grid was not all resident: the step launches instead
                     self._pass_fault(faults)
                     return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, finish=finish,
                                     speculate=speculate)
+                if gate_pass and auto:  # back to speculation after two gated passes without a fired gate
+                    self._gate_quiet = 0 if n_fired else self._gate_quiet + 1
+                    if self._gate_quiet >= 2:
+                        self._gate_mode, self._gate_quiet = False, 0
             if pass_out is not None:
                 return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, pass_out[2], pred, fired)
         # one-shard speculative pass: the gates and the fault counter are verified on the device
@@ -637,9 +652,13 @@ class FilterEngine:
             if ok:
                 self._spec_backoff = 0
                 return res
-            # a gate fired: the pass again, with the per-step exchange
+            # a gate fired: the pass again, gated (one GPU, the one-launch pass: the gates decided in
+            # the launch; the next passes stay gated while gates keep firing) or with the per-step
+            # exchange
             if ot_auto:
                 self._ot_fired = True  # the rerun below sets it from its own OT calls
+            elif auto and gate_ok and not self.pass_disabled:
+                self._gate_mode, self._gate_quiet = True, 0
             elif auto:
                 self._spec_backoff = min(2 * self._spec_backoff or 1, 64)
                 self._spec_skip = self._spec_backoff

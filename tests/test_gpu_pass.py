@@ -506,7 +506,8 @@ def test_gated_pass_every_step_vs_oracle(B, N, T, monkeypatch):
     enc, start, vel = wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV)
     x0, logw0 = ops.particle_init(start[:, :2], B, N, 128.0, False, 4242, 0, DEV)
     p0, _ = ops.normalize_log_probs(logw0)
-    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=4242, kernel="tiled")
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=4242, kernel="tiled",
+                       speculate_gate=False)  # the gated pass from the first pass on
     eng = FilterEngine(cfg, models)
     res = eng.run(enc, start, vel, init=(x0, logw0))
     torch.cuda.synchronize()
@@ -561,7 +562,7 @@ def test_gated_pass_quiet_equals_speculative():
     B, N, T = 16, 1000, 20
     enc, start, vel = _inputs(B, T, seed=77)
     eng_s, s_ = _run(models, N, enc, start, vel, spec=True)
-    eng_g, g_ = _run(models, N, enc, start, vel, spec=None)
+    eng_g, g_ = _run(models, N, enc, start, vel, spec=False)  # (no speculation: the gated pass)
     assert eng_s.last_pass and not eng_s.last_gate_pass and eng_s.pass_launches == 1
     assert eng_g.last_pass and eng_g.last_gate_pass
     assert int(eng_g.last_gates.sum()) == 0
@@ -579,7 +580,8 @@ def test_gated_pass_decisions_match_gate_kernel():
     wl = F.workload("c2_full", B=B, N=N, T=T)
     models = wl["models"].to(DEV)
     from nfdpf.engine import FilterConfig, FilterEngine
-    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=99, kernel="tiled")
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=99, kernel="tiled",
+                       speculate_gate=False)
     eng = FilterEngine(cfg, models)
     captured = {}
     orig = ops.tiled_init
@@ -601,3 +603,28 @@ def test_gated_pass_decisions_match_gate_kernel():
     ref = ops.ess_gate_tiled_batch(hist.contiguous(), N, 0, False)
     assert torch.equal(ref.cpu(), eng.last_gates.cpu()), (ref.tolist(), eng.last_gates.tolist())
     assert 0 < int(ref.sum()) < T
+
+
+def test_auto_mode_switches_between_speculative_and_gated():
+    """Auto mode on one GPU: a quiet workload keeps the speculative pass (verified, no gate fired);
+    when a speculative pass misses, the rerun is the gated pass and the engine stays gated while
+    gates keep firing; after two gated passes without a fired gate it speculates again."""
+    import _fullsize as F
+    from nfdpf.engine import FilterConfig, FilterEngine
+    B, N, T = 8, 1000, 12
+    wl = F.workload("c2_full", B=B, N=N, T=T)
+    models = wl["models"].to(DEV)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=5, kernel="tiled")
+    eng = FilterEngine(cfg, models)
+    fire = (wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+    g = torch.Generator().manual_seed(1)
+    quiet = (torch.randn(B, T, 32, generator=g).to(DEV) * 0.0, wl["start"].to(DEV), wl["vel"].to(DEV))
+    eng.run(*fire)
+    assert eng.pass_launches == 2 and eng.last_gate_pass and int(eng.last_gates.sum()) > 0  # missed, rerun gated
+    eng.run(*fire)
+    assert eng.pass_launches == 3 and eng.last_gate_pass  # stays gated while gates fire
+    for k in range(2):
+        eng.run(*quiet)
+        assert eng.last_gate_pass and int(eng.last_gates.sum()) == 0
+    eng.run(*quiet)
+    assert eng.last_pass and not eng.last_gate_pass, "two quiet gated passes: speculation again"
