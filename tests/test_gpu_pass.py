@@ -139,7 +139,7 @@ def _fractions(what, ours, r32, r64, rtol, atol):
           f"{100 * f_ref:.3f} %; max err ours {np.abs(ours - r64).max():.3e} vs float32 {np.abs(r32 - r64).max():.3e}")
 
 
-PASS_ORACLE_CASES = [(4, 1000, 10, "bench"), (3, 257, 6, "bench"), (2, 1024, 8, "bench"), (4, 1000, 10, "e2e_c2.npz"),
+PASS_ORACLE_CASES = [(4, 1000, 10, "bench"), (3, 257, 6, "bench"), (2, 1024, 8, "bench"), (4, 1000, 6, "e2e_c2.npz"),
                      (3, 257, 6, "e2e_c2.npz"), (2, 1024, 8, "e2e_c2.npz"),
                      # the BASELINE C2 shape itself, the bench's model (DPF(args) at its init weights)
                      (64, 1000, 50, "bench")]
@@ -170,10 +170,11 @@ def test_pass_vs_oracle(B, N, T, fixture):
         res = eng.run(enc, start, vel, init=(x0, logw0))
         torch.cuda.synchronize()
         ess = (1.0 / (res.probs[:, :-1].double() ** 2).sum(-1)).mean(0)  # the gates of steps 1 .. T-1
-        if eng.last_pass and (T == 1 or float(ess.min()) > 0.6 * N):
+        quiet = eng.last_pass and not eng.last_gate_pass and eng.pass_launches == 1  # the speculative pass verified
+        if quiet and (T == 1 or float(ess.min()) > 0.6 * N):
             break
-    assert eng.last_pass and (T == 1 or float(ess.min()) > 0.6 * N), \
-        "no input seed kept the gate off by a margin: the one-launch pass was rerun step by step"
+    assert quiet and (T == 1 or float(ess.min()) > 0.6 * N), \
+        "no input seed kept the gate off by a margin (a fired gate reruns the pass gated)"
     outs = {}
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     for dt in (torch.float32, torch.float64):
