@@ -1245,7 +1245,24 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
   for (int b = l; b < B; b += 64) {
     const int64_t bt = (int64_t)b * T + k;
     double px = 0, py = 0, sw = 0;
-    for (int e = 0; e < ent; ++e) {
+    int e = 0;
+    for (; e + 8 <= ent; e += 8) {  // 8 entries' loads in flight, then the adds in entry order
+      double a[8][3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const double *f = ws.fin + (bt * ent + e + j) * 4;
+        a[j][0] = f[1];
+        a[j][1] = f[2];
+        a[j][2] = f[3];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        px += a[j][0];
+        py += a[j][1];
+        sw += a[j][2];
+      }
+    }
+    for (; e < ent; ++e) {
       const double *f = ws.fin + (bt * ent + e) * 4;
       px += f[1];
       py += f[2];
@@ -1283,12 +1300,20 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     const int64_t n = pass_granule_bytes(B, d.N) / 8;
     for (int64_t i = l; i < n; i += 64) ws.ga[i] = 0;  // ga, gb and gc are contiguous
   }
+  // every step's terms in flight at once (lane t: steps t, t + 64, ...), then added in step order
+  __shared__ double eq_l[kPassMaxT];
+  __shared__ int eg_l[kPassMaxT];
+  for (int t = l; t < T; t += 64) {
+    eq_l[t] = __hip_atomic_load(&ws.eq[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    eg_l[t] = __hip_atomic_load(&ws.eg[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
   if (l == 0) {
     double acc = 0.0;
     int nf = 0;
     for (int t = 0; t < T; ++t) {
-      acc += __hip_atomic_load(&ws.eq[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      nf += __hip_atomic_load(&ws.eg[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      acc += eq_l[t];
+      nf += eg_l[t];
     }
     if (d.pass_obs) d.pass_obs[0] = (float)acc;
     if (d.pass_flags) {
