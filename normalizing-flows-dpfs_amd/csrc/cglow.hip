@@ -27,6 +27,9 @@
 
 namespace nfdpf {
 namespace cg {
+#ifdef NFDPF_EXP_CGDUMP
+__device__ float g_cgdump[256];
+#endif
 
 constexpr int kTileP = 16;    // particles per workgroup tile
 constexpr int kThreads = 256;
@@ -43,6 +46,9 @@ struct Lds {
   float an[kTileP][2 * kC + 1];        // actnorm (logs | bias)
   float wm[kTileP][kC * kC + 4];       // 1x1 conv weight, row-major [out][in] (rows 16-B aligned)
   float ld[kTileP];                    // per-particle log-det of actnorm + 1x1 conv
+#ifdef NFDPF_EXP_CGDUMP
+  float ldw_dbg[kTileP];
+#endif
   int row[kTileP];
   float escale[2 * kYH + kC];          // exp of the coupling net's log-scales (once per launch)
   float zrow[kC + 1];                  // zeros: the 3x3 convolutions' out-of-grid neighbour
@@ -337,6 +343,9 @@ __device__ __forceinline__ void phase_y(float (&y)[kC], int p, int q) {
   // the pivot rows go through this particle's S.ex[p][0] (free until phase_resize writes it)
   const float ldw = logabsdet12(wr, q, &S.ex[p][0][0]);
   if (q == 0) S.ld[p] = 16.0f * sl + 16.0f * ldw;  // dimensions (4x4) x (sum logs, log|det W|)
+#ifdef NFDPF_EXP_CGDUMP
+  if (q == 0) S.ldw_dbg[p] = ldw;
+#endif
 }
 
 // resize_x = conv3x3(3->16, pad 1) ReLU, conv2x2/2(16->6) ReLU, fused per 4x4 position (the
@@ -805,6 +814,18 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
     CGTRACE(8)
     const int64_t gi = g0 + p;
     const float part = phase_f(gw, p, q, zout && gi < total ? zout + gi * kE : nullptr);
+#ifdef NFDPF_EXP_CGDUMP
+    // experiment only: one particle's 1x1-conv W, its log|det W| (the LU's), actnorm outputs
+    if (gi == (int64_t)NFDPF_CG_TARGET && q < 16) {
+      for (int k = q; k < kC * kC; k += 16) g_cgdump[k] = S.wm[p][k];
+      for (int k = q; k < 2 * kC; k += 16) g_cgdump[160 + k] = S.an[p][k];
+      if (q == 0) {
+        g_cgdump[200] = S.ldw_dbg[p];
+        g_cgdump[201] = S.ld[p];
+        g_cgdump[202] = part;
+      }
+    }
+#endif
     if (q == 0 && gi < total) {
       // logdet0 = -log(256) * 192, plus actnorm / 1x1-conv log-dets, plus this particle's sum
       const float obj = (-5.545177444479562f * (float)kE + S.ld[p]) + part;
@@ -821,6 +842,11 @@ __global__ __launch_bounds__(kThreads, NFDPF_CG_WGS) void cglow_kernel(const flo
 
 using namespace nfdpf;
 
+#ifdef NFDPF_EXP_CGDUMP
+extern "C" NFDPF_API int nfdpf_exp_cgdump_read(void *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cgdump), sizeof(g_cgdump)) == hipSuccess ? 0 : 1;
+}
+#endif
 #ifdef NFDPF_EXP_CGTRACE
 extern "C" NFDPF_API int nfdpf_exp_cgtrace_read(void *host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cgtrace), sizeof(g_cgtrace)) == hipSuccess ? 0 : 1;

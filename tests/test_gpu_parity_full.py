@@ -184,16 +184,32 @@ def test_fullsize_teacher_forced(name):
                f"(reference float32 {e_r.max():.3e}, ratio {e_k.max() / max(e_r.max(), 1e-30):.2f}), mean "
                f"{e_k.mean():.3e} (reference {e_r.mean():.3e})")
         # The kernel alone, on the reference's own particles: mean <= 2.5x and the 99.9th
-        # percentile <= 4x the reference float32's.  The case MAXIMUM is one element of the
-        # 240 000 where the likelihood is steepest: 4.6-4.8x in round 4 (fp64 elimination for
-        # log|det W| measured no better, so it is not the 1x1 conv's LU); it is capped at 6x
-        # here and printed, not held to 4x -- DESIGN.md §4 records it as open.
+        # percentile <= 4x the reference float32's, and every element within 4x the reference's
+        # case maximum PLUS its own float32 floor: 4 sigma_i, sigma_i = the likelihood's
+        # first-order response to rounding the 12x12 1x1-conv matrix W_i to float32 (iid errors
+        # of half an ulp of max|W_i|: sigma = hw / (ln2 dims) 2^-24 max|W_i| ||W_i^-1||_F).  The
+        # round-4 outlier (b 6, step 2, n 8339; 4.6-6x the reference's max) is such an element:
+        # W has cond 5.9e6, our W is within 1.2 ulp of the float64 W (rms error 9.2e-9, the
+        # reference float32's 8.5e-9) and our LU's log|det| within 7e-3 of float64 slogdet of OUR
+        # W, yet log|det W| moves 0.18 -- random W errors of that rms move it 0.044 median, 0.155
+        # at p99 (scripts/r05_cglow_w.py).  No layer is worse than the
+        # reference's float32; the element is the tail of the conditioning amplification.
         qk, qr = np.quantile(e_k, 0.999), np.quantile(e_r, 0.999)
+        sig = _cglow_w_sigma(w, ref[0])
+        bar = 4 * e_r.max() + 2e-5 + 4 * sig
+        n_floor = int((4 * sig > 4 * e_r.max() + 2e-5).sum())
+        worst = np.unravel_index(np.argmax(e_k - bar), e_k.shape)
         _table(f"  likelihood, kernel alone: 99.9th percentile err {qk:.3e} (reference {qr:.3e}, ratio "
-               f"{qk / max(qr, 1e-30):.2f}); max ratio {e_k.max() / max(e_r.max(), 1e-30):.2f} (cap 6)")
+               f"{qk / max(qr, 1e-30):.2f}); max ratio {e_k.max() / max(e_r.max(), 1e-30):.2f}; elements whose "
+               f"float32 W floor exceeds 4x the reference max: {n_floor}; tightest element {tuple(map(int, worst))} "
+               f"err {e_k[worst]:.3e} bar {bar[worst]:.3e} (sigma {sig[worst]:.3e})")
+        ill = sig > 1e-4  # the ill-conditioned W: error in units of the element's float32 floor
+        if ill.any():
+            _table(f"  likelihood at the {int(ill.sum())} elements with sigma > 1e-4: max err / sigma ours "
+                   f"{(e_k[ill] / sig[ill]).max():.2f}, reference float32 {(e_r[ill] / sig[ill]).max():.2f}")
         assert qk <= 4 * qr + 2e-5, (qk, qr)
         assert e_k.mean() <= 2.5 * e_r.mean() + 2e-5, (e_k.mean(), e_r.mean())
-        assert e_k.max() <= 6 * e_r.max() + 2e-5, (e_k.max(), e_r.max())
+        assert (e_k <= bar).all(), (tuple(map(int, worst)), e_k[worst], bar[worst], sig[worst], e_r.max())
     fails = []
     for what, i, k, atol in QUANTITIES:
         if ref[i] is None:
@@ -323,6 +339,31 @@ def _cglow_lik64_at(w, x):
     """The float64 CGLOW likelihood (row-max shifted, model/models.py:280-303) of a case's
     frame encodings at the particles x (B, T, N, 2), step by step."""
     out = [_cglow_oracle(w["params"], w["enc"][:, t], x[:, t].float(), torch.float64) for t in range(x.shape[1])]
+    return np.stack(out, 1)
+
+
+def _cglow_w_sigma(w, x, rows=8):
+    """Per element (B, T, N): the std of the likelihood's first-order response to rounding the
+    1x1-conv matrix W (O.cglow_step's invconv, float64) to float32 with iid errors of half an ulp
+    of max|W|: d lik / d log|det W| = hw / (ln2 dims) and d log|det W| = tr(W^-1 dW), whose std
+    for iid dW of std s is s ||W^-1||_F.  One flow step (K = 1, as the cases)."""
+    p = O.cast_params(w["params"], torch.float64)
+    pe = O.sub(p, "particle_encoder")
+    inv = O.sub(O.sub(O.sub(p, "cglow_measurement"), "flow.layers.1"), "invconv")
+    assert not any(k.startswith("cglow_measurement.flow.layers.2.") for k in p)
+    hw, dims = 16.0, 192.0
+    out = []
+    with O.precision(torch.float64), torch.no_grad():
+        for t in range(x.shape[1]):
+            per = []
+            for b in range(0, x.shape[0], rows):
+                xb = x[b:b + rows, t].double()
+                Bc, N = xb.shape[:2]
+                es = O.particle_encode(pe, xb.reshape(-1, 2)).reshape(Bc * N, 3, 8, 8)
+                W = O._cond_net(inv, es, Bc * N).reshape(-1, 12, 12)
+                s = torch.linalg.inv(W).pow(2).sum((1, 2)).sqrt() * W.abs().amax((1, 2)) * 2.0 ** -24
+                per.append((s * hw / (np.log(2.0) * dims)).reshape(Bc, N))
+            out.append(torch.cat(per).numpy())
     return np.stack(out, 1)
 
 
