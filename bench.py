@@ -289,25 +289,61 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
         # after each replay finish_pending() gathers all steps' partials once (sharded),
         # verifies the T gates and reduces the obs-likelihood -- a fired gate (never at the
         # bench's init weights) reruns the pass step by step, inside the timing.
+        # One GPU, speculative: TWO graphs (two sets of pass outputs) replayed alternately, and
+        # pass k's verification -- its epilogue's flags, copied to pinned host memory right after
+        # the replay -- read once an event behind that copy completes, while pass k + 1 already
+        # runs: the host round trip no longer leaves the GPU idle between passes.  A fired gate
+        # reruns pass k (gated) before the next replay; the last pass is verified inside the
+        # timing.
+        pipelined = spec and world == 1
+        graphs, caps, pends = [], [], []
         try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                res = eng.run(enc, start, vel_in, shard=shard, finish=not spec)
-            graph.replay()
+            for _ in range(2 if pipelined else 1):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    res = eng.run(enc, start, vel_in, shard=shard, finish=not spec)
+                graphs.append(g)
+                caps.append(res)
+                pends.append(eng.take_pending() if spec else None)
+            for g in graphs:
+                g.replay()
             torch.cuda.synchronize()
+            graph = graphs[0]
         except RuntimeError as e:  # capture refused: keep the Python launch path
             print(f"bench: hipGraph capture failed ({e}); timing Python launches", file=sys.stderr)
             graph = None
             torch.cuda.synchronize()
-        cap = res
 
         def step_graph():
             graph.replay()
-            if spec and not eng.finish_pending():
+            if spec and not eng.finish_pending(pends[0]):
                 return eng.run(enc, start, vel_in, shard=shard, speculate=False)
-            return cap
+            return caps[0]
+
+        evs_done = [torch.cuda.Event(), torch.cuda.Event()]
+        pipe = {"k": 0, "prev": None}
+
+        def verify_prev():
+            j = pipe["prev"]
+            if j is None:
+                return None
+            pipe["prev"] = None
+            evs_done[j].synchronize()
+            if not eng.finish_pending(pends[j], synced=True):
+                return eng.run(enc, start, vel_in, shard=shard, speculate=False)
+            return caps[j]
+
+        def step_pipe():
+            i = pipe["k"] & 1
+            graphs[i].replay()
+            eng.stage_flags(pends[i])
+            evs_done[i].record()
+            out = verify_prev()
+            pipe["prev"], pipe["k"] = i, pipe["k"] + 1
+            return out if out is not None else caps[i]
+        step_pipe.drain = verify_prev
         if graph is not None:
-            step = step_graph  # noqa: F811
+            step = step_pipe if pipelined else step_graph  # noqa: F811
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -315,6 +351,8 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
+    if getattr(step, "drain", None) is not None:  # the last pipelined pass's verification
+        res = step.drain() or res
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -467,6 +467,16 @@ NFDPF_API int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *d, void *workspac
 /* the t = 0 gate input from p0 [B,N] -> ess_parts [B][tiles][4] */
 NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess_parts,
                             void *stream);
+/* nfdpf_particle_init + nfdpf_normalize_log_probs (add 0) + nfdpf_filter_tiled_init in ONE launch
+ * (one workgroup per row, N <= 1024), bit-identical to the three: particle_initialization
+ * (utils.py:46-62, device RNG; start: [B][start_rs >= 4] rows of the start state, x, y, vx, vy)
+ * -> x [B,N,2], logw [B,N]; p0 = normalize_log_probs(logw) (DPFs.py:153) -> p [B,N], inv_ess [B]
+ * (nullable); the t = 0 gate input -> ess_parts [B][tiles][4]; and (vel nullable) every step's
+ * velocity in the descriptor's [T][B][2] layout: the start velocity, then vel_in[b][t - 1][2]
+ * (rows of vel_rs floats; DPFs.py:158, 173). */
+NFDPF_API int nfdpf_filter_init(const float *start, int start_rs, const float *vel_in, int vel_rs, int T, int B,
+                                int N, float width, int true_state, uint64_t seed, int64_t row_base, float *x,
+                                float *logw, float *p, float *inv_ess, double *ess_parts, float *vel, void *stream);
 NFDPF_API int nfdpf_filter_step_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);
 /* the ESS gate (DPFs.py:163-165) of step t from the [B][tiles][4] partials of step t-1
  * -> int32 [1] (OT path) */

@@ -1878,6 +1878,80 @@ __global__ __launch_bounds__(kTile) void tiled_ess_init_kernel(const float *__re
   }
 }
 
+// particle_initialization (utils.py:46-62, device RNG) + p0 = normalize_log_probs (DPFs.py:153) +
+// the t = 0 gate's per-tile partials, one workgroup per row (N <= 1024, one particle per thread):
+// particle_init_kernel's, normalize_kernel's and tiled_ess_init_kernel's arithmetic in their
+// orders (the same bits) in one launch instead of three.  The tile sums reuse the wave sums of
+// normalize's sum p^2 (a tile is waves 4k..4k+3, summed in order as block_sum sums a tile's).
+// Also every step's velocity in the [T][B][2] layout the step and pass launches read: the start
+// velocity, then vel_in[:, t - 1] (DPFs.py:158, 173).
+__global__ __launch_bounds__(1024) void filter_init_kernel(const float *__restrict__ start, int start_rs,
+                                                           const float *__restrict__ vel_in, int vel_rs, int T,
+                                                           int N, float width, int true_state, uint64_t seed,
+                                                           int64_t row_base, float *__restrict__ x,
+                                                           float *__restrict__ logw, float *__restrict__ p,
+                                                           float *__restrict__ inv_ess, double *__restrict__ parts,
+                                                           float *__restrict__ vel) {
+  __shared__ float shf[16];
+  __shared__ double shd[16];
+  const int b = blockIdx.x, i = threadIdx.x;
+  if (vel)
+    for (int k = i; k < 2 * T; k += blockDim.x) {
+      const int t = k >> 1, c = k & 1;
+      vel[((int64_t)t * gridDim.x + b) * 2 + c] =
+          t == 0 ? start[(int64_t)b * start_rs + 2 + c] : vel_in[(int64_t)b * vel_rs + 2 * (t - 1) + c];
+    }
+  const bool valid = i < N;
+  const int64_t o = (int64_t)b * N + i;
+  float lw = -INFINITY;
+  if (valid) {
+    const int64_t grow = row_base + b;
+    float a0, a1;
+    if (true_state) {
+      const U4 r = rng_draw(seed, kTagInitNormal, 0u, grow, (uint32_t)i);
+      box_muller(r.x, r.y, a0, a1);
+      a0 += start[(int64_t)b * start_rs];
+      a1 += start[(int64_t)b * start_rs + 1];
+    } else {
+      const U4 r = rng_draw(seed, kTagInitPos, 0u, grow, (uint32_t)i);
+      const float hi = width / 2.0f, lo = -width / 2.0f;
+      a0 = (hi - lo) * u01(r.x) + lo;
+      a1 = (hi - lo) * u01(r.y) + lo;
+    }
+    x[2 * o] = a0;
+    x[2 * o + 1] = a1;
+    lw = logf(1.0f / (float)N);
+    logw[o] = lw;
+  }
+  const float m = block_max(lw, shf);
+  const float S = (float)block_sum(valid ? (double)expf(lw - m) : 0.0, shd);
+  float v = 0.f;
+  if (valid) {
+    v = expf(lw - m) / S + 0.0f;
+    p[o] = v;
+  }
+  const double w2 = wave_sum(valid ? (double)v * (double)v : 0.0);
+  __syncthreads();
+  if ((i & 63) == 0) shd[i >> 6] = w2;
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6, tiles = n_tiles(N);
+  if (i == 0 && inv_ess) {
+    double r = shd[0];
+    for (int k = 1; k < nw; ++k) r += shd[k];
+    inv_ess[b] = 1.0f / (float)r;
+  }
+  if (i < tiles) {
+    const int w0 = 4 * i;
+    double r = shd[w0];
+    for (int k = w0 + 1; k < w0 + 4 && k < nw; ++k) r += shd[k];
+    double *sm = parts + ((int64_t)b * tiles + i) * kSm;
+    sm[0] = 0.0;
+    sm[1] = i == 0 ? 1.0 : 0.0;
+    sm[2] = r;
+    sm[3] = 0.0;
+  }
+}
+
 __global__ void tiled_gate_kernel(const double *__restrict__ parts, int B, int tiles, int N, int t, int force,
                                   int32_t *gate) {
   const float s = cascade_row_sum([&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, N, t > 0); },
@@ -2155,6 +2229,21 @@ extern "C" int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *es
   if (B == 0) return NFDPF_OK;
   tiled_ess_init_kernel<<<dim3(n_tiles(N), B), kTile, 0, as_stream(stream)>>>(p0, N, ess_parts);
   return launch_status("nfdpf_filter_tiled_init");
+}
+
+extern "C" int nfdpf_filter_init(const float *start, int start_rs, const float *vel_in, int vel_rs, int T, int B,
+                                 int N, float width, int true_state, uint64_t seed, int64_t row_base, float *x,
+                                 float *logw, float *p, float *inv_ess, double *ess_parts, float *vel, void *stream) {
+  NFDPF_REQUIRE(x && logw && p && ess_parts && (!true_state || start) && (!vel || (start && (T <= 1 || vel_in))),
+                "nfdpf_filter_init: null pointer");
+  NFDPF_REQUIRE(B >= 0 && N >= 1 && N <= 1024 && T >= 0 && start_rs >= 4 && vel_rs >= 2 * (T > 1 ? T - 1 : 0),
+                "nfdpf_filter_init: bad sizes (need 1 <= N <= 1024, start rows >= 4, vel rows >= 2 (T - 1); got N=%d)",
+                N);
+  if (B == 0) return NFDPF_OK;
+  filter_init_kernel<<<B, row_threads(N), 0, as_stream(stream)>>>(start, start_rs, vel_in, vel_rs, T, N, width,
+                                                                  true_state, seed, row_base, x, logw, p, inv_ess,
+                                                                  ess_parts, vel);
+  return launch_status("nfdpf_filter_init");
 }
 
 extern "C" int nfdpf_split_fault(int reset, void *stream) {

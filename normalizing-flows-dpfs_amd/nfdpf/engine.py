@@ -345,17 +345,6 @@ class FilterEngine:
         start_state = start_state.float()
         vel_input = vel_input.float()
 
-        # initial particles / weights (utils.py:46-62) and p0 = normalize_log_probs (DPFs.py:153)
-        if init is not None:
-            x0, logw0 = (t.to(dev).float().contiguous() for t in init)
-        elif host_mode:
-            xg = host.init(self._global(start_state[:, :2], shard), N, c.width, c.init_with_true_state)
-            x0 = xg[shard.row_base:shard.row_base + B].to(dev).contiguous()
-            logw0 = torch.log(torch.ones([B, N], device=dev) / N)
-        else:
-            x0, logw0 = ops.particle_init(start_state[:, :2].to(dev), B, N, c.width, c.init_with_true_state,
-                                          c.seed, shard.row_base, dev)
-        p0, ie0 = ops.normalize_log_probs(logw0)
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
         ot_auto = auto and tiled and c.resampler == "ot"
@@ -393,10 +382,32 @@ class FilterEngine:
             if spec or use_pass:  # every step's partials kept for the verification
                 ess_hist = torch.empty((T + 1, B, tiles, 4), device=dev, dtype=torch.float64)
                 ess_bufs = [ess_hist[t] for t in range(1, T + 1)]
-                ess0 = ops.tiled_init(p0, ess_hist[0])
+                ess0 = ess_hist[0]
             else:
                 ess_bufs = [torch.empty((B, tiles, 4), device=dev, dtype=torch.float64) for _ in range(2)]
-                ess0 = ops.tiled_init(p0, torch.empty((B, tiles, 4), device=dev, dtype=torch.float64))
+                ess0 = torch.empty((B, tiles, 4), device=dev, dtype=torch.float64)
+        # initial particles / weights (utils.py:46-62) and p0 = normalize_log_probs (DPFs.py:153)
+        # (device RNG, tiled, N <= 1024: the three and the t = 0 gate partials in one launch)
+        vel_steps = None
+        if init is None and not host_mode and tiled and N <= 1024:
+            # (+ every step's velocity in the [T][B][2] layout: no cat / transpose launches)
+            x0, logw0, p0, ie0, vel_steps = ops.filter_init(start_state.to(dev), B, N, c.width, c.init_with_true_state,
+                                                            c.seed, shard.row_base, dev, ess0,
+                                                            vel_input=vel_input.to(dev), T=T)
+        else:
+            if init is not None:
+                x0, logw0 = (t.to(dev).float().contiguous() for t in init)
+            elif host_mode:
+                xg = host.init(self._global(start_state[:, :2], shard), N, c.width, c.init_with_true_state)
+                x0 = xg[shard.row_base:shard.row_base + B].to(dev).contiguous()
+                logw0 = torch.log(torch.ones([B, N], device=dev) / N)
+            else:
+                x0, logw0 = ops.particle_init(start_state[:, :2].to(dev), B, N, c.width, c.init_with_true_state,
+                                              c.seed, shard.row_base, dev)
+            p0, ie0 = ops.normalize_log_probs(logw0)
+            if tiled:
+                ops.tiled_init(p0, ess0)
+        if tiled:
             ws = ops.tiled_workspace(B, N, T, dev)
             gather_buf = torch.empty((shard.B_global, tiles, 4), device=dev, dtype=torch.float64) \
                 if shard.world > 1 and not spec else None
@@ -408,8 +419,9 @@ class FilterEngine:
         gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
         spec_gate = torch.zeros(1, device=dev, dtype=torch.int32) if spec else None
         # velocity used by each step's motion: start velocity, then vel_input[:, t-1] (DPFs.py:158,173)
-        vel_steps = torch.cat([start_state[:, None, 2:4].to(dev), vel_input[:, :T - 1].to(dev)], 1)
-        vel_steps = vel_steps.transpose(0, 1).contiguous()  # (T, B, 2)
+        if vel_steps is None:
+            vel_steps = torch.cat([start_state[:, None, 2:4].to(dev), vel_input[:, :T - 1].to(dev)], 1)
+            vel_steps = vel_steps.transpose(0, 1).contiguous()  # (T, B, 2)
         dyn, cond, pe, meas = self._blobs(dev)
         lin = ops.linspace_markers(N, dev) if c.resampler == "soft" else None
 
@@ -476,6 +488,7 @@ class FilterEngine:
                 i32 = dict(device=dev, dtype=torch.int32)
                 pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(2, **i32),
                             torch.empty((), **f32))
+
                 self.last_gates = pass_out[0]  # the T gates: decided in the launch, or verified
                 d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
             d.prof_events, d.prof_front = None, 0
@@ -641,7 +654,8 @@ class FilterEngine:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             verify = None
             if verify_dev:
-                verify = pass_out[1:] if pass_out is not None else ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]
+                verify = [pass_out[1], pass_out[2], None] if pass_out is not None else \
+                    list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None]
                 check_split = False
             self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass)
             if not finish:
@@ -668,15 +682,42 @@ class FilterEngine:
         obs = (tot / (shard.B_global * N)).sum().float()
         return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, obs, pred, fired)
 
-    def finish_pending(self) -> bool:
-        """Verify the speculative pass of the last ``run`` (its buffers, so also after a graph
-        replay of it): gather every step's softmax partials over the shards (one all-gather),
-        evaluate all T gates (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the
-        obs-likelihood into the result.  False: some gate fired -- the pass is not the
-        reference's and must be rerun without speculation (run(..., speculate=False))."""
-        parts, tot, shard, N, res, split_dev, verify, was_pass = self._pending
+    @staticmethod
+    def stage_flags(pending):
+        """Enqueue (current stream) the copy of a one-shard speculative pass's device flags
+        {fired, faults} into pinned host memory; after an event recorded behind it has completed,
+        ``finish_pending(pending, synced=True)`` reads them with no stream operation -- so a
+        later pass already queued keeps running (pipelined passes, bench.py).  Not while
+        capturing a graph (the pinned allocation is not capturable): after the replay."""
+        verify = pending[6]
+        if verify is None:
+            return
+        if verify[2] is None:
+            verify[2] = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        verify[2].copy_(verify[0], non_blocking=True)
+
+    def take_pending(self):
+        """The verification state of the last ``run(finish=False)``, handed to the caller (e.g.
+        one per captured graph when passes are pipelined): ``finish_pending(pending)`` later."""
+        p, self._pending = self._pending, None
+        return p
+
+    def finish_pending(self, pending=None, synced: bool = False) -> bool:
+        """Verify the speculative pass of the last ``run`` (or the given ``take_pending()``
+        state; its buffers, so also after a graph replay of it): gather every step's softmax
+        partials over the shards (one all-gather), evaluate all T gates
+        (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the obs-likelihood into the
+        result.  False: some gate fired -- the pass is not the reference's and must be rerun
+        without speculation (run(..., speculate=False)).
+        ``synced``: the pass's flags were staged (stage_flags) and an event recorded after that
+        copy has completed: they are read from pinned host memory with no stream operation, so a
+        later pass already queued behind it keeps running (pipelined passes, bench.py)."""
+        parts, tot, shard, N, res, split_dev, verify, was_pass = pending if pending is not None else self._pending
         if verify is not None:  # the device verification's flags: the one host synchronisation
-            fired, faults = verify[0].tolist()
+            if synced and verify[2] is not None:  # staged (stage_flags) and known complete
+                fired, faults = verify[2].tolist()
+            else:
+                fired, faults = verify[0].tolist()
             if faults:
                 if not was_pass:
                     raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "

@@ -550,6 +550,28 @@ def pass_workspace(B: int, N: int, T: int, device, owner=None) -> torch.Tensor:
     return t
 
 
+def filter_init(start_state, B, N, width, true_state, seed, row_base, device, ess_out, vel_input=None, T=0):
+    """particle_init + normalize_log_probs + tiled_init in one launch (nfdpf_filter_init, N <= 1024)
+    -> (x [B,N,2], logw [B,N], p0 [B,N], inv_ess [B], vel_steps [T,B,2] or None); the t = 0 gate
+    partials into ``ess_out`` ([B, tiles, 4] float64).  ``start_state`` [B, >= 4] (x, y, vx, vy);
+    with ``vel_input`` [B, >= T - 1, 2] also every step's velocity (the start velocity, then
+    vel_input[:, t - 1]) in the descriptor's [T][B][2] layout."""
+    x = torch.empty((B, N, 2), device=device, dtype=f32)
+    lw = torch.empty((B, N), device=device, dtype=f32)
+    p = torch.empty((B, N), device=device, dtype=f32)
+    ie = torch.empty(B, device=device, dtype=f32)
+    st = _c(start_state)
+    vel = vi = None
+    if vel_input is not None:
+        vi = _c(vel_input)
+        vel = torch.empty((T, B, 2), device=device, dtype=f32)
+    check(lib().nfdpf_filter_init(ptr(st), st.shape[1], ptr(vi), vi.shape[1] * 2 if vi is not None else 2, int(T), B,
+                                  N, float(width), int(bool(true_state)), int(seed) & (2**64 - 1), int(row_base),
+                                  ptr(x), ptr(lw), ptr(p), ptr(ie), ptr(ess_out), ptr(vel), stream_ptr(device)),
+          "nfdpf_filter_init")
+    return x, lw, p, ie, vel
+
+
 def tiled_init(p0: torch.Tensor, out: torch.Tensor):
     B, N = p0.shape
     check(lib().nfdpf_filter_tiled_init(ptr(p0), B, N, ptr(out), stream_ptr(p0.device)), "nfdpf_filter_tiled_init")

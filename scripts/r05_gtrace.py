@@ -1,4 +1,5 @@
-"""Experiment: where a step of the GATED one-launch pass (kModeGate) waits -- per-step phase
+"""Experiment: where a step of the GATED one-launch pass (kModeGate; --spec: the speculative pass,
+--force: the forced pass) waits -- per-step phase
 timestamps (lib built with -DNFDPF_EXP_PTRACE: scripts/exp_build.sh PTRACE -DNFDPF_EXP_PTRACE,
 loaded through NFDPF_LIB).  C2 bench workload ([--informative]: frame encodings = the particle
 encoder at the true positions, the gate fires), the last of 3 passes; medians over the 256
@@ -16,7 +17,7 @@ from nfdpf import _lib  # noqa: E402
 
 flags, B, N, T, _, _ = bench.CONFIGS["c2"]
 torch.manual_seed(2)
-a = bench.make_args(flags, B, N, T, {})
+a = bench.make_args(flags, B, N, T, {"force_resample": "--force" in sys.argv})
 from DPFs import DPF  # noqa: E402
 from nfdpf.engine import FilterEngine, ShardInfo  # noqa: E402
 dev = torch.device("cuda", 0)

@@ -434,6 +434,29 @@ def test_forced_pass_every_step_vs_oracle(B, N, T, monkeypatch):
         _fractions(k, ours, r32[k], r64[k], 1e-5, 0.0 if k != "jac" else 1e-6)
 
 
+@pytest.mark.parametrize("N,true_state", [(1000, False), (1000, True), (900, False), (1024, True), (65, False),
+                                          (1, False)])
+def test_filter_init_equals_three_launches(N, true_state):
+    """nfdpf_filter_init (one launch) == nfdpf_particle_init + nfdpf_normalize_log_probs +
+    nfdpf_filter_tiled_init bit for bit: particles, log-weights, p0, 1 / sum p0^2 and the t = 0
+    gate partials, on ragged N (a last tile of fewer waves) and both init modes."""
+    from nfdpf import ops
+    B = 5
+    start = (torch.randn(B, 4) * 30).to(DEV)
+    T = 7
+    vel_in = (torch.randn(B, T + 2, 2) * 3).to(DEV)
+    x, lw, p, ie, vel = ops.filter_init(start, B, N, 128.0, true_state, 11, 3, DEV,
+                                        ess := torch.full((B, ops.tiled_tiles(N), 4), float("nan"), device=DEV,
+                                                          dtype=torch.float64), vel_input=vel_in, T=T)
+    x3, lw3 = ops.particle_init(start[:, :2], B, N, 128.0, true_state, 11, 3, DEV)
+    p3, ie3 = ops.normalize_log_probs(lw3)
+    ess3 = ops.tiled_init(p3, torch.empty_like(ess))
+    torch.cuda.synchronize()
+    vel3 = torch.cat([start[:, None, 2:4], vel_in[:, :T - 1]], 1).transpose(0, 1).contiguous()
+    for a, b in ((x, x3), (lw, lw3), (p, p3), (ie, ie3), (ess, ess3), (vel, vel3)):
+        assert torch.equal(a.cpu(), b.cpu())
+
+
 @pytest.mark.parametrize("N", [8, 100, 257, 1000, 1024])
 def test_cascade_row_sum_1k_equals_generic(N):
     """The forced pass's load-ahead cascade sum (cascade_row_sum_1k) == the generic device
@@ -585,16 +608,16 @@ def test_gated_pass_decisions_match_gate_kernel():
                        speculate_gate=False)
     eng = FilterEngine(cfg, models)
     captured = {}
-    orig = ops.tiled_init
+    orig = ops.filter_init
 
-    def keep(p0, out):  # the engine's [T + 1, B, tiles, 4] partials: slot 0 is the initial one
-        captured["base"] = out
-        return orig(p0, out)
-    ops.tiled_init = keep
+    def keep(*a, **k):  # the engine's [T + 1, B, tiles, 4] partials: slot 0 is the initial one
+        captured["base"] = a[8] if len(a) > 8 else k["ess_out"]
+        return orig(*a, **k)
+    ops.filter_init = keep
     try:
         eng.run(wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
     finally:
-        ops.tiled_init = orig
+        ops.filter_init = orig
     torch.cuda.synchronize()
     assert eng.last_gate_pass
     tiles = ops.tiled_tiles(N)
