@@ -477,6 +477,12 @@ NFDPF_API int nfdpf_filter_tiled_init(const float *p0, int B, int N, double *ess
 NFDPF_API int nfdpf_filter_init(const float *start, int start_rs, const float *vel_in, int vel_rs, int T, int B,
                                 int N, float width, int true_state, uint64_t seed, int64_t row_base, float *x,
                                 float *logw, float *p, float *inv_ess, double *ess_parts, float *vel, void *stream);
+/* Pinned, device-mapped, coherent host memory (hipHostMalloc Mapped | Coherent, zeroed): *host for
+ * the caller, *dev for kernel arguments -- e.g. pass_flags, written by the pass epilogue with
+ * system-scope stores and read on the host once an event behind the pass has completed (no copy
+ * launch).  No reference counterpart. */
+NFDPF_API int nfdpf_host_mapped_alloc(int64_t bytes, void **host, void **dev);
+NFDPF_API int nfdpf_host_mapped_free(void *host);
 NFDPF_API int nfdpf_filter_step_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);
 /* the ESS gate (DPFs.py:163-165) of step t from the [B][tiles][4] partials of step t-1
  * -> int32 [1] (OT path) */

@@ -88,6 +88,12 @@ __device__ unsigned long long g_ptrace[256][16][64][20];
   } while (0)
 #endif
 
+// SPEC: the prior wave, not the chain, stores the step's histories (hist_x, noise, index, jac):
+// five vector stores per step off the chain's critical path (experiment knob)
+#ifndef NFDPF_PASS_HSTORE
+#define NFDPF_PASS_HSTORE 1
+#endif
+
 // pass modes (tiled_pass_kernel<MODE>)
 constexpr int kModeSpec = 0;   // every ESS gate taken as off (verified after the pass)
 constexpr int kModeForce = 1;  // --force-resample: the row resampled at the top of every step
@@ -176,6 +182,9 @@ struct PassLds {
   int qf[4], rf[4];
   alignas(8) int pf[4];
   alignas(8) int ef[8];
+#if NFDPF_PASS_HSTORE
+  float ebuf[2][3 * kTile];        // SPEC: the chain's motion noise and log|det J|, to the prior wave
+#endif
   float lr_l[kTile];               // FORCE / GATE: this tile's resampled log-weights (outside the union:
                                    // the encoder waves read it while others may start their MFMA layers)
   int fS, fbar;                    // FORCE: resampling done, flow-wave barrier
@@ -329,7 +338,7 @@ __device__ __forceinline__ double lds_double(const uint32_t *w, int q) {
 
 // the row context from an A / B sweep: lanes c < 4 add component c over (tile, wave) in order
 // (block_sum_roles_store, then tiled_ctx), every lane gets the context
-__device__ __forceinline__ Ctx4 row_ctx(const uint32_t *rw, int tiles, int N) {
+__device__ __forceinline__ Ctx4 row_ctx(const uint32_t *rw, int tiles, double inv_n, double inv_n1) {
   const int c = threadIdx.x & 3;
   double a = 0.0;
   for (int k = 0; k < tiles; ++k) {
@@ -339,11 +348,12 @@ __device__ __forceinline__ Ctx4 row_ctx(const uint32_t *rw, int tiles, int N) {
     a += tk;
   }
   // ctx_from_sums's arithmetic with its two components on two lanes (lane k: mean and std of
-  // component k), one division chain per lane instead of both in sequence
+  // component k); the selects branch-free (both readlanes uniform, then one v_cndmask per half)
   const int k = threadIdx.x & 1;
-  const double s = k ? readlane_d(a, 1) : readlane_d(a, 0), q = k ? readlane_d(a, 3) : readlane_d(a, 2);
-  const double m = s / N;
-  const float sd = (float)sqrt((q - s * m) / (N - 1));
+  const double s0 = readlane_d(a, 0), s1 = readlane_d(a, 1), q0 = readlane_d(a, 2), q1 = readlane_d(a, 3);
+  const double s = k ? s1 : s0, q = k ? q1 : q0;
+  const double m = ctx_mean(s, inv_n);
+  const float sd = (float)sqrt(ctx_var(s, q, m, inv_n1));
   const float mf = (float)m;
   return Ctx4{readlane_f(mf, 0), readlane_f(mf, 1), readlane_f(sd, 0), readlane_f(sd, 1)};
 }
@@ -661,16 +671,20 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + d.E + c) + rc.w];
   }
   constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
+  const double inv_n = 1.0 / N, inv_n1 = 1.0 / (N - 1);  // the row contexts' (ctx_from_sums)
   int round = 0;  // flow_barrier rounds (FORCE / GATE)
   int prev_dec = 0;  // GATE: the decision of step t - 1 (the prediction for step t)
   float en0 = 0.f, en1 = 0.f;  // the next step's motion noise
+  // the step's velocity, loaded one step ahead (beside the next step's noise): no scalar-load
+  // latency at the head of the step
+  float nv0 = d.vel[2 * (int64_t)b], nv1 = d.vel[2 * (int64_t)b + 1];
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
     const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const uint32_t tag = tag0 + (uint32_t)t + 1u;
-    const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
+    const float v0 = nv0, v1 = nv1;
     PT(t, 0);
     if (t == 0 && valid) pass_noise(d, 0, grow, i, en0, en1);
     // the step's input particles: own (x0, x1) or the row's resampling's
@@ -722,7 +736,11 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       PT(t, 1);
       // the next step's motion noise, drawn while the A sweep is in flight / fA is awaited
       auto next_noise = [&]() {
-        if (first && valid && t + 1 < d.T) pass_noise(d, t + 1, grow, i, en0, en1);
+        if (first && t + 1 < d.T) {
+          if (valid) pass_noise(d, t + 1, grow, i, en0, en1);
+          nv0 = d.vel[2 * ((int64_t)(t + 1) * d.B + b)];
+          nv1 = d.vel[2 * ((int64_t)(t + 1) * d.B + b) + 1];
+        }
       };
       auto stop = [&]() { return spec && dec_fired(L, t); };
       const int fa = 4 * (t + 1) + 2 * variant;
@@ -739,7 +757,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         }
         PT(t, 7);
         if (st == 0) {
-          const Ctx4 c = row_ctx(L.rowa, tiles, N);
+          const Ctx4 c = row_ctx(L.rowa, tiles, inv_n, inv_n1);
           if (fold_lane) {
             const float cv[4] = {c.m0, c.m1, c.s0, c.s1};
             float v = fwd[0];
@@ -777,7 +795,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         const int st = poll_rowx<3>(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, NoWork(), stop);
         if (st == 0) {
           PT(t, 8);
-          const Ctx4 c = row_ctx(L.rowa, tiles, N);
+          const Ctx4 c = row_ctx(L.rowa, tiles, inv_n, inv_n1);
           wait_flag(&L.fE, t + 1);
           if (fold_lane) {
             const float c4[4] = {c.m0, c.m1, c.s0, c.s1};
@@ -816,24 +834,35 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       variant = 1;
     }
     // commit step t: the histories, and the proposal to the prior wave and the encoder pair
+    constexpr bool HS = NFDPF_PASS_HSTORE && MODE == kModeSpec;  // the prior wave stores them
     const RowSlot S = row_slot(d, b, t);
-    if (valid) {
+    if (valid && !HS) {
       S.hnoise[2 * i] = e0;
       S.hnoise[2 * i + 1] = e1;
       S.hidx[i] = (int64_t)N * grow + src;
       if (S.hjac) S.hjac[i] = jac;
     }
-    // the group's encoder pair has read qbuf / rbuf[par] of step t - 2
+    // the group's encoder pair has read qbuf / rbuf[par] of step t - 2 (HS: its prior wave ebuf)
     if (t >= 2) wait_flag2(&L.ef[2 * g], t - 1);
+#if NFDPF_PASS_HSTORE
+    if (HS && t >= 2) wait_flag(&L.pf[g], t - 1);
+#endif
     if (valid) {  // to the prior wave and the encoder pair
       L.qbuf[par][slot] = q0;
       L.qbuf[par][kTile + slot] = q1;
       L.pbuf[par][slot] = p0 - e0;
       L.pbuf[par][kTile + slot] = p1 - e1;
       L.rbuf[par][kTile + slot] = (density(e0, e1, K, two_var) + jac) + (-ldp);  // propose
+#if NFDPF_PASS_HSTORE
+      if (HS) {
+        L.ebuf[par][slot] = e0;
+        L.ebuf[par][kTile + slot] = e1;
+        L.ebuf[par][2 * kTile + slot] = jac;
+      }
+#endif
       if (FORCE || GATE) {  // a later step's resampling reads the row's particles from other tiles
         store_wt2(S.hx + 2 * i, q0, q1);
-      } else {
+      } else if (!HS) {
         S.hx[2 * i] = q0;
         S.hx[2 * i + 1] = q1;
       }
@@ -911,6 +940,16 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     if (valid) {
       float lo = L.qbuf[par][slot], up = L.qbuf[par][kTile + slot], ld2 = 0.f;
       const float r0 = L.pbuf[par][slot], r1 = L.pbuf[par][kTile + slot];
+#if NFDPF_PASS_HSTORE
+      if constexpr (MODE == kModeSpec) {  // the chain's histories of step t (pass_chain's commit)
+        S.hx[2 * i] = lo;
+        S.hx[2 * i + 1] = up;
+        S.hnoise[2 * i] = L.ebuf[par][slot];
+        S.hnoise[2 * i + 1] = L.ebuf[par][kTile + slot];
+        S.hidx[i] = (int64_t)N * (d.row_base + b) + i;
+        if (S.hjac) S.hjac[i] = L.ebuf[par][2 * kTile + slot];
+      }
+#endif
 #ifndef NFDPF_EXP_NOFWD
       for (int f = 0; f < nfl; ++f)
 #else
@@ -1238,10 +1277,13 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
 // of round 4 (one 64-lane wave walked 64 steps x B rows serially there: 18 us per pass).
 // gates: 0 none, 1 verify (the speculative pass's gates from its partials), 2 the pass decided
 // them itself (kModeGate: ws.eg already holds them; only counted here)
-__global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_filter_desc d, PassWs ws, int gates) {
+// ept: fin entries per tile (8 encoder waves in tiled_pass_kernel, 4 particle groups in
+// tiled_pass_cm_kernel)
+__global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_filter_desc d, PassWs ws, int gates,
+                                                                 int ept) {
   __shared__ float lw_l[256];
   __shared__ int last;
-  const int k = blockIdx.x, l = threadIdx.x, T = d.T, B = d.B, tiles = n_tiles(d.N), ent = tiles * 8;
+  const int k = blockIdx.x, l = threadIdx.x, T = d.T, B = d.B, tiles = n_tiles(d.N), ent = tiles * ept;
   for (int b = l; b < B; b += 64) {
     const int64_t bt = (int64_t)b * T + k;
     double px = 0, py = 0, sw = 0;
@@ -1316,9 +1358,9 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
       nf += eg_l[t];
     }
     if (d.pass_obs) d.pass_obs[0] = (float)acc;
-    if (d.pass_flags) {
-      d.pass_flags[0] = nf;
-      d.pass_flags[1] = atomicExch(&g_split_fault, 0);
+    if (d.pass_flags) {  // (system scope: the caller may map them from pinned host memory)
+      __hip_atomic_store(&d.pass_flags[0], nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&d.pass_flags[1], atomicExch(&g_split_fault, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     ws.hdr->abort = 0;
     ws.hdr->done = 0;

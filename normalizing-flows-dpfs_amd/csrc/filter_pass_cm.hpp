@@ -1,0 +1,239 @@
+// filter_pass_cm.hpp -- the whole T-step filtering pass of DPF.filtering_pos (DPFs.py:160-214) as
+// ONE persistent launch for the C3 shape: no dynamic flow, no conditional proposal (the bootstrap
+// proposal x_t = (x_{t-1} + vel) + eps), the conditional-RealNVP measurement (model/models.py:
+// 256-278, shifted by the row max of the raw likelihood), every ESS gate taken as off (the
+// speculative mode: the caller verifies the T gates afterwards from the per-step partials this
+// launch leaves, and a fired gate reruns the pass step by step -- OT or soft resampling there).
+// Included by filter_tiled.hip after filter_pass.hpp (its workspace, granules and epilogue).
+//
+// Why this shape pipelines: without resampling a particle never leaves its lane and its path
+// x_0, x_1, ... needs nothing from the row (the bootstrap proposal has no context exchange), so
+// the measurement of every step -- all the arithmetic (12.7 k FLOP per particle-step) -- is
+// independent of the weights.  Only the log-weights form a chain across steps: step t's
+// u_t = ((log p_{t-1} + lik_t) + prior) - propose needs slot t - 1 normalised, i.e. the row's
+// softmax partials of u_{t-1} (exchange C, the granules of filter_pass.hpp) and the row max of
+// the raw likelihood (the CRNVP shift, model/models.py:276).  That chain is short (a sweep and a
+// few VALU ops per particle); the likelihoods run ahead of it.
+//
+// Grid (tiles, B) of 512-thread workgroups, all resident (pass_cm_config_ok).  Wave w handles
+// particle group g = w & 3 (64 particles of the tile, one per lane; waves w and w + 4 share a
+// SIMD) on the steps of parity k = w >> 2: two steps of a group in flight per SIMD, each wave
+// with 256 VGPRs for the measurement's registers.  Per step t, wave (g, t & 1):
+//   1. x_t from x_{t-1} (LDS xr, from the group's other wave; flag xf[g]) + vel_t + eps_t ->
+//      xr, hist_x / noise / index;
+//   2. lik_t = crnvp_lik(x_t) (raw), the step's frame encoding in the wave's own LDS copy;
+//   3. [group 0's wave: sweep C(t - 1) -> slot t - 1's row normaliser rn (LDS, flag fR) and
+//      the tile's merged partial -> ess_out[t - 1]] -> normalise slot t - 1 of the group from
+//      the other wave's hand-over nb (finish_prev's arithmetic: hist_p, hist_lik shifted, the
+//      fin partials) -> log p_{t-1};
+//   4. u_t, the group's partials {max u, sum e, sum e^2, max lik} -> C(t) granules.
+// The waves of parity T & 1 normalise the last slot after their loop.
+//
+// Every wait is bounded (pass_spin: 200 ms, the workspace's abort word), as in filter_pass.hpp.
+
+namespace nfdpf {
+
+constexpr int kCmWaves = 8;  // 512 threads: two waves (two steps in flight) per particle group
+
+struct PassCmLds {
+  float xr[2][4][64][2];     // x_t by parity of t: the group's other wave reads it for step t + 1
+  float nb[2][5][kTile];     // slot t's hand-over by parity: lr, raw lik, prior, x0, x1
+  float encq[kCmWaves][kE];  // each wave's copy of its step's frame encoding (crnvp_lik's encv)
+  uint32_t rowc[kPassMaxTiles * 4 * kGC];
+  RowNorm rn[2];
+  int xf[4];                 // x_t of group g written (t + 1)
+  int fR;                    // slot t's row normaliser in rn[t & 1] (t + 1)
+};
+
+// the row normaliser of slot s from its C(s) granules (tiles x 4 groups, each {max u, sum e,
+// sum e^2, max raw lik}): the tile's merge over its groups in order (ess_out[s], the gate's
+// input), then row_norm's arithmetic over the tiles in order with the CRNVP shift.  One wave.
+__device__ __forceinline__ void pass_cm_poll_c(const nfdpf_filter_desc &d, const PassWs &ws, PassCmLds &L, int b,
+                                               int tile, uint32_t tag0, int s) {
+  const int tiles = n_tiles(d.N), lane = threadIdx.x & 63;
+  const int64_t row0 = (((int64_t)(s & 1) * d.B + b) * tiles) * 4;
+  if (poll_row(ws.gc + row0 * kGC, tiles * 4 * kGC, tag0 + (uint32_t)s + 1u, L.rowc)) {
+    const int k = lane < tiles ? lane : 0;
+    float m = -INFINITY, lm = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      m = fmaxf(m, __uint_as_float(L.rowc[(k * 4 + v) * kGC]));
+      lm = fmaxf(lm, __uint_as_float(L.rowc[(k * 4 + v) * kGC + 5]));
+    }
+    double sum = 0.0, sq = 0.0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int q = (k * 4 + v) * kGC;
+      const float mv = __uint_as_float(L.rowc[q]);
+      if (mv > -INFINITY) {
+        const double f = (double)expf(mv - m);
+        sum += lds_double(L.rowc, q + 1) * f;
+        sq += lds_double(L.rowc, q + 3) * f * f;
+      }
+    }
+    if (lane == tile) {
+      double *sm = reinterpret_cast<double *>(d.ess_out) + (((int64_t)s * d.B + b) * tiles + tile) * kSm;
+      sm[0] = m;
+      sm[1] = sum;
+      sm[2] = sq;
+      sm[3] = lm;
+    }
+    // row_norm (filter_tiled.hip) over the tiles in order, shifted by the row max raw likelihood
+    float M = -INFINITY, Lmax = -INFINITY;
+    for (int kk = 0; kk < tiles; ++kk) {
+      M = fmaxf(M, (float)(double)readlane_f(m, kk));
+      Lmax = fmaxf(Lmax, readlane_f(lm, kk));
+    }
+    double Sd = 0.0;
+    for (int kk = 0; kk < tiles; ++kk) Sd += readlane_d(sum, kk) * (double)expf(readlane_f(m, kk) - M);
+    if (lane == 0) L.rn[s & 1] = RowNorm{M - Lmax, (float)Sd, Lmax};
+  }
+  set_flag(&L.fR, s + 1);
+}
+
+// normalise slot s of this wave's group from the hand-over nb[s & 1] (finish_prev / prev_p_of's
+// arithmetic, shifted): hist_p, hist_lik (the shifted likelihood), the group's fin partials
+// (entry g of the tile); returns log p
+__device__ __forceinline__ float pass_cm_norm(const nfdpf_filter_desc &d, const PassWs &ws, PassCmLds &L, int b,
+                                              int tile, int g, int s, int slot, int i, bool valid) {
+  wait_flag(&L.fR, s + 1);
+  const RowNorm rn = L.rn[s & 1];
+  double sf[4] = {0.0, 0.0, 0.0, 0.0};
+  float lp = 0.f;
+  if (valid) {
+    const int par = s & 1;
+    const float lr = L.nb[par][0][slot], raw = L.nb[par][1][slot], pr = L.nb[par][2][slot];
+    const float lk = raw - rn.Lmax;
+    const float lw = ((lr + lk) + pr) - pr;
+    const float p = expf(lw - rn.shift) / rn.Ssum + 1e-12f;
+    const int64_t o = ((int64_t)b * d.T + s) * d.N + i;
+    d.hist_p[o] = p;
+    d.hist_lik[o] = lk;
+    lp = logf(p);
+    sf[0] = (double)p * p;
+    sf[1] = (double)p * L.nb[par][3][slot];
+    sf[2] = (double)p * L.nb[par][4][slot];
+    sf[3] = lw;
+  }
+  wave_sum_dpp_n(sf);
+  const int lane = threadIdx.x & 63, tiles = n_tiles(d.N);
+  if (lane < 4)
+    ws.fin[((((int64_t)b * d.T + s) * tiles + tile) * 4 + g) * 4 + lane] =
+        lane == 0 ? sf[0] : lane == 1 ? sf[1] : lane == 2 ? sf[2] : sf[3];
+  return lp;
+}
+
+template <int MEAS>
+__global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const nfdpf_filter_desc d, PassWs ws) {
+  static_assert(MEAS == NFDPF_MEAS_CRNVP, "the C3-shaped pass: the conditional-RealNVP measurement");
+  __shared__ PassCmLds L;
+  int b, tile;
+  pass_tile_row(b, tile);
+  const uint32_t tag0 = __hip_atomic_load(&ws.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 12;
+  if (threadIdx.x < 4) L.xf[threadIdx.x] = 0;
+  if (threadIdx.x == 0) L.fR = 0;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int g = w & 3, k = w >> 2, slot = g * 64 + lane, N = d.N, tiles = n_tiles(N);
+  const int i = tile * kTile + slot;
+  const bool valid = i < N;
+  const int64_t grow = d.row_base + b;
+  __syncthreads();
+  float lr = 0.f;  // log p of this wave's particle in the slot before its next step
+  if (k == 0) {  // x_0 = the initial particles (step 0 is parity 0's)
+    if (valid) {
+      L.xr[1][g][lane][0] = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i];
+      L.xr[1][g][lane][1] = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i + 1];
+      lr = logf(d.p_prev[(int64_t)b * d.p_prev_rs + i]);
+    }
+  }
+  for (int t = k; t < d.T; t += 2) {
+    const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
+    const PassWs &ws = *(const PassWs *)kernarg_ws();
+    const int par = t & 1;
+    const RowSlot S = row_slot(d, b, t);
+    // 1. motion (model/models.py:191-204): the bootstrap proposal, prior = propose = density(eps)
+    float e0 = 0.f, e1 = 0.f;
+    if (valid) pass_noise(d, t, grow, i, e0, e1);
+    const float v0 = d.vel[2 * ((int64_t)t * d.B + b)], v1 = d.vel[2 * ((int64_t)t * d.B + b) + 1];
+    if (lane < kE) L.encq[w][lane] = d.enc[((int64_t)b * d.T + t) * d.E + lane];
+    wait_flag(&L.xf[g], t);  // x_{t-1} of the group
+    float x0 = 0.f, x1 = 0.f, de = 0.f;
+    if (valid) {
+      x0 = (L.xr[par ^ 1][g][lane][0] + v0) + e0;
+      x1 = (L.xr[par ^ 1][g][lane][1] + v1) + e1;
+      L.xr[par][g][lane][0] = x0;
+      L.xr[par][g][lane][1] = x1;
+    }
+    set_flag(&L.xf[g], t + 1);
+    if (valid) {
+      S.hx[2 * i] = x0;
+      S.hx[2 * i + 1] = x1;
+      S.hnoise[2 * i] = e0;
+      S.hnoise[2 * i + 1] = e1;
+      S.hidx[i] = (int64_t)N * grow + i;
+      de = density(e0, e1, d.dens_const, 2.0f * (d.pos_noise * d.pos_noise)) + 0.0f;
+    }
+    // 2. the measurement of x_t (model/models.py:256-278), unshifted
+    float raw = -INFINITY;
+    if (valid)
+      raw = crnvp_lik(wptr(d.pe_params), wptr(d.meas_params), d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
+    // 3. slot t - 1: its row normaliser (group 0's wave sweeps C(t - 1)), its normalisation
+    if (t > 0) {
+      if (g == 0) pass_cm_poll_c(d, ws, L, b, tile, tag0, t - 1);
+      lr = pass_cm_norm(d, ws, L, b, tile, g, t - 1, slot, i, valid);
+    }
+    // 4. the log-weight (DPFs.py:187) and exchange C(t): this group's softmax partials
+    float u = -INFINITY;
+    if (valid) {
+      u = ((lr + raw) + de) - de;
+      L.nb[par][0][slot] = lr;
+      L.nb[par][1][slot] = raw;
+      L.nb[par][2][slot] = de;
+      L.nb[par][3][slot] = x0;
+      L.nb[par][4][slot] = x1;
+    }
+    const float mw = wave_max_dpp(u), lmw = wave_max_dpp(raw);
+    const float ev = valid ? expf(u - mw) : 0.f;
+    double r[2] = {(double)ev, (double)ev * ev};
+    wave_sum_dpp_n(r);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // nb written before C(t) can be swept
+    if (lane < kGC) {
+      const uint64_t eb = (uint64_t)__double_as_longlong(r[0]), qb = (uint64_t)__double_as_longlong(r[1]);
+      const uint32_t word = lane == 0 ? __float_as_uint(mw)
+                            : lane == 1 ? (uint32_t)eb
+                            : lane == 2 ? (uint32_t)(eb >> 32)
+                            : lane == 3 ? (uint32_t)qb
+                            : lane == 4 ? (uint32_t)(qb >> 32)
+                                        : __float_as_uint(lmw);
+      const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 4 + g;
+      gran_store(ws.gc + gslot * kGC + lane, word, tag0 + (uint32_t)t + 1u);
+    }
+  }
+  // the last slot's normalisation: the waves of parity T & 1 (they would have run step T)
+  if (k == (d.T & 1)) {
+    if (g == 0) pass_cm_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
+    pass_cm_norm(d, ws, L, b, tile, g, d.T - 1, slot, i, valid);
+  }
+}
+
+// The C3-shaped pass applies: the configuration, the speculative gate (not forced, not gated in
+// the launch), and every workgroup of its grid resident at once.
+static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_PASS");  // read per call: NFDPF_PASS=0 keeps the step-by-step launches
+  if (e && e[0] == '0') return false;
+  if (d.nf_dyn != NFDPF_DYN_NONE || d.nf_cond || d.measurement != NFDPF_MEAS_CRNVP) return false;
+  if (d.rng_mode != NFDPF_RNG_DEVICE || d.phase != 0 || d.E != kE || d.force_resample || d.pass_gate) return false;
+  if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 0 || d.n_flows > kMaxFlows || d.T < 1 ||
+      d.T > kPassMaxT || d.B < 1 || d.B > 256)
+    return false;
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>, kCmWaves * 64, 0) !=
+          hipSuccess ||
+      occ < 1)
+    return false;
+  return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;
+}
+
+}  // namespace nfdpf

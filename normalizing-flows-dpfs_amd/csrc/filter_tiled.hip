@@ -2142,11 +2142,14 @@ static void dispatch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStr
 
 }  // namespace nfdpf
 
-#include "filter_pass.hpp"  // the whole pass as one persistent launch (C2 shape, speculative gate)
+#include "filter_pass.hpp"     // the whole pass as one persistent launch (C2 shape)
+#include "filter_pass_cm.hpp"  // ... the C3 shape (bootstrap proposal, CRNVP measurement, speculative gate)
 
 using namespace nfdpf;
 
-extern "C" int nfdpf_filter_pass_supported(const nfdpf_filter_desc *d) { return d && pass_config_ok(*d) ? 1 : 0; }
+extern "C" int nfdpf_filter_pass_supported(const nfdpf_filter_desc *d) {
+  return d && (pass_config_ok(*d) || pass_cm_config_ok(*d)) ? 1 : 0;
+}
 
 extern "C" int64_t nfdpf_filter_pass_workspace_bytes(int B, int N, int T) {
   return (B <= 0 || N <= 0 || T <= 0) ? 256 : pass_bytes(B, N, T);
@@ -2157,9 +2160,29 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   const nfdpf_filter_desc &d = *dp;
   NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, "nfdpf_filter_pass_tiled: workspace not 256-B aligned");
   NFDPF_REQUIRE(d.t == 0, "nfdpf_filter_pass_tiled: a pass starts at t = 0 (got t=%d)", d.t);
-  NFDPF_REQUIRE(d.hist_x && d.hist_p && d.hist_noise && d.hist_lik && d.hist_idx && d.hist_jac && d.hist_prior &&
-                    d.ess_out && d.enc && d.vel && d.x_prev && d.p_prev && d.lw_sum && d.pred,
+  NFDPF_REQUIRE(d.hist_x && d.hist_p && d.hist_noise && d.hist_lik && d.hist_idx && d.ess_out && d.enc && d.vel &&
+                    d.x_prev && d.p_prev && d.lw_sum && d.pred,
                 "nfdpf_filter_pass_tiled: null input/output pointer");
+  if (pass_cm_config_ok(d)) {  // the C3 shape: no flows on the particle path, the CRNVP measurement
+    NFDPF_REQUIRE(d.pe_params && d.meas_params && d.ess_all, "nfdpf_filter_pass_tiled: parameters / ess_all missing");
+    const int verify_cm = d.pass_gates && d.B_global == d.B;
+    NFDPF_REQUIRE(!d.pass_gates || verify_cm, "nfdpf_filter_pass_tiled: pass_gates needs a pass of the whole batch");
+    hipStream_t st = as_stream(stream);
+    PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
+    ws.wait_ticks = kPassWaitTicks;
+    if (const char *e = getenv("NFDPF_PASS_WAIT_US"))  // read per call (tests force a timeout)
+      ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
+    const dim3 g(n_tiles(d.N), d.B);
+    hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+    if (ev)
+      hipExtLaunchKernelGGL(tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>, g, dim3(kCmWaves * 64), 0, st, ev[0], ev[1], 0, d,
+                            ws);
+    else
+      tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP><<<g, kCmWaves * 64, 0, st>>>(d, ws);
+    tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, verify_cm, 4);
+    return launch_status("nfdpf_filter_pass_tiled");
+  }
+  NFDPF_REQUIRE(d.hist_jac && d.hist_prior, "nfdpf_filter_pass_tiled: null input/output pointer");
   NFDPF_REQUIRE(d.dyn_params && d.cond_params && d.pe_params, "nfdpf_filter_pass_tiled: parameters missing");
   NFDPF_REQUIRE(!d.force_resample || (d.lin && ((uintptr_t)d.hist_x & 7) == 0),
                 "nfdpf_filter_pass_tiled: a forced pass needs lin and an 8-B aligned hist_x");
@@ -2185,7 +2208,7 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
     hipExtLaunchKernelGGL(kern, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
   else
     kern<<<g, 4 * kTile, 0, st>>>(d, ws);
-  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate ? 2 : verify);
+  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate ? 2 : verify, 8);
   return launch_status("nfdpf_filter_pass_tiled");
 }
 

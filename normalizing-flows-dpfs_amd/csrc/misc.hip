@@ -1,4 +1,6 @@
 // misc.hip -- particle_initialization (utils.py:46-62) in DEVICE rng mode.
+#include <cstring>
+
 #include "common.hpp"
 
 namespace nfdpf {
@@ -62,3 +64,28 @@ extern "C" int nfdpf_particle_init(const float *start_xy, int B, int N, float wi
       start_xy, B, N, width, true_state, seed, row_base, x, logw);
   return launch_status("nfdpf_particle_init");
 }
+
+// Pinned, device-mapped, coherent host memory (the zero-copy path of hipHostMalloc): a kernel's
+// small result words (the one-launch pass's flags) land in host memory with the kernel, and the
+// host reads them once an event behind the kernel has completed -- no copy launch.
+extern "C" int nfdpf_host_mapped_alloc(int64_t bytes, void **host, void **dev) {
+  NFDPF_REQUIRE(bytes > 0 && host && dev, "nfdpf_host_mapped_alloc: bad arguments");
+  *host = *dev = nullptr;
+  if (hipHostMalloc(host, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    *host = nullptr;
+    return launch_status("nfdpf_host_mapped_alloc (hipHostMalloc)");
+  }
+  memset(*host, 0, (size_t)bytes);
+  if (hipHostGetDevicePointer(dev, *host, 0) != hipSuccess) {
+    (void)hipHostFree(*host);
+    *host = *dev = nullptr;
+    return launch_status("nfdpf_host_mapped_alloc (hipHostGetDevicePointer)");
+  }
+  return NFDPF_OK;
+}
+
+extern "C" int nfdpf_host_mapped_free(void *host) {
+  if (host) NFDPF_REQUIRE(hipHostFree(host) == hipSuccess, "nfdpf_host_mapped_free: hipHostFree failed");
+  return NFDPF_OK;
+}
+

@@ -35,11 +35,15 @@ __device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b, i
 }
 __device__ __forceinline__ RowSlot row_slot(const nfdpf_filter_desc &d, int b) { return row_slot(d, b, d.t); }
 
-// context from (sum x, sum y, sum x^2, sum y^2) over N particles
+// context from (sum x, sum y, sum x^2, sum y^2) over N particles: mean = s / N and std =
+// sqrt((q - s mean) / (N - 1)) as products with the fp64 reciprocals 1 / N, 1 / (N - 1) (the
+// one-launch pass's chain takes them from registers: no fp64 division on its critical path)
+__device__ __forceinline__ double ctx_mean(double s, double inv_n) { return s * inv_n; }
+__device__ __forceinline__ double ctx_var(double s, double q, double m, double inv_n1) { return (q - s * m) * inv_n1; }
 __device__ __forceinline__ Ctx4 ctx_from_sums(double a0, double a1, double b0, double b1, int N) {
-  const double m0 = a0 / N, m1 = a1 / N;
-  return Ctx4{(float)m0, (float)m1, (float)sqrt((b0 - a0 * m0) / (N - 1)),
-              (float)sqrt((b1 - a1 * m1) / (N - 1))};
+  const double inv_n = 1.0 / N, inv_n1 = 1.0 / (N - 1);
+  const double m0 = ctx_mean(a0, inv_n), m1 = ctx_mean(a1, inv_n);
+  return Ctx4{(float)m0, (float)m1, (float)sqrt(ctx_var(a0, b0, m0, inv_n1)), (float)sqrt(ctx_var(a1, b1, m1, inv_n1))};
 }
 
 // source of the particle before motion

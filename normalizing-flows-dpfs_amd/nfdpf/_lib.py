@@ -124,6 +124,8 @@ SIGNATURES = {
     "nfdpf_filter_tiled_fused": (c_int, [POINTER(FilterDesc)]),
     "nfdpf_filter_desc_size": (c_int64, []),
     "nfdpf_filter_tiled_init": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_host_mapped_alloc": (c_int, [c_int64, c_void_p, c_void_p]),
+    "nfdpf_host_mapped_free": (c_int, [c_void_p]),
     "nfdpf_filter_init": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_uint64,
                                   c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_filter_pass_supported": (c_int, [POINTER(FilterDesc)]),

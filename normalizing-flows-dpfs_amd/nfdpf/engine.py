@@ -164,6 +164,7 @@ class FilterEngine:
         # a one-launch pass whose row hand-offs timed out (its grid was not all resident: another
         # process or kernel held CUs) turns the pass off for this engine; the step launches rerun
         self.pass_disabled = False
+        self._hmapped = None  # ops.HostMapped slots for the speculative pass's flags (lazy)
         self._shared_device = None  # per process group: does another rank use this rank's GPU?
         self.last_gate_pass = False  # the last run was the gated one-launch pass (gates decided in the launch)
         self.last_gates = None       # one shard's one-launch pass: its T gates (decided, or verified) [T] int32
@@ -177,6 +178,7 @@ class FilterEngine:
         st["last_gates"] = None
         st["_shared_device"] = None
         st["step_events"] = None
+        st["_hmapped"] = None  # (pinned host memory of this process)
         return st
 
     def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False,
@@ -235,7 +237,10 @@ class FilterEngine:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
         the configuration, and the grid resident on the current device)?"""
         c = self.cfg
-        if not (c.kernel == "tiled" and split_nets and c.rng_mode == "device") or self.pass_disabled:
+        # the C2 shape (split RealNVP flows on the particle path) or the C3 shape (none: the
+        # bootstrap proposal, tiled_pass_cm_kernel)
+        flows_ok = split_nets or (not c.NF_dyn and not c.NF_cond)
+        if not (c.kernel == "tiled" and flows_ok and c.rng_mode == "device") or self.pass_disabled:
             return False
         if c.force_resample and c.resampler != "soft":  # a forced pass resamples inside the launch
             return False
@@ -417,7 +422,8 @@ class FilterEngine:
             gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
         ess_all = ess0 if spec else self._gather(ess0, shard, gather_buf)
         gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
-        spec_gate = torch.zeros(1, device=dev, dtype=torch.int32) if spec else None
+        # (the step launches' speculative gate word; the one-launch pass reads none)
+        spec_gate = torch.zeros(1, device=dev, dtype=torch.int32) if spec and not use_pass else None
         # velocity used by each step's motion: start velocity, then vel_input[:, t-1] (DPFs.py:158,173)
         if vel_steps is None:
             vel_steps = torch.cat([start_state[:, None, 2:4].to(dev), vel_input[:, :T - 1].to(dev)], 1)
@@ -461,7 +467,7 @@ class FilterEngine:
         hx_p, hp_p, vel_p = hx.data_ptr(), hp.data_ptr(), vel_steps.data_ptr()
         ess_out_p = [b.data_ptr() for b in ess_bufs]
         ess_in_p = [ess0.data_ptr()] + ess_out_p[:-1] if (spec or use_pass) else None
-        spec_gate_p = spec_gate.data_ptr() if spec else None
+        spec_gate_p = spec_gate.data_ptr() if spec_gate is not None else None
         stream = ops.stream_ptr(dev)
         launch = L.lib().nfdpf_filter_step_tiled if tiled else L.lib().nfdpf_filter_step
         ws_p = ops._aligned_ptr(ws) if tiled else None
@@ -474,6 +480,7 @@ class FilterEngine:
 
         self.last_pass = use_pass
         pass_out = None  # one shard: the pass epilogue's (gates, flags, obs)
+        flags_host = None  # ... the flags mapped from host memory (speculative pass)
         if use_pass:
             # the whole T-step pass as ONE persistent launch (nfdpf_filter_pass_tiled): every gate
             # taken as off, step t's softmax partials into ess_hist[t + 1] for the verification
@@ -481,16 +488,25 @@ class FilterEngine:
             d.x_prev, d.p_prev, d.x_prev_rs, d.p_prev_rs = x0.data_ptr(), p0.data_ptr(), N * 2, N
             d.vel = vel_p
             d.ess_all, d.ess_out, d.gate = ess_in_p[0], ess_out_p[0], spec_gate_p
-            pdyn, pcond = self._pass_blobs(dev)  # the pass layout (tanh algebra in the weights)
-            d.dyn_params, d.cond_params = pdyn.data_ptr(), pcond.data_ptr()
+            if c.NF_dyn:  # the pass layout (tanh algebra in the weights); the C3 shape has no flows here
+                pdyn, pcond = self._pass_blobs(dev)
+                d.dyn_params, d.cond_params = pdyn.data_ptr(), pcond.data_ptr()
             d.pass_gate = int(gate_pass)
             if shard.world == 1:  # the epilogue verifies the gates / reads the fault counter on the device
                 i32 = dict(device=dev, dtype=torch.int32)
                 pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(2, **i32),
                             torch.empty((), **f32))
-
                 self.last_gates = pass_out[0]  # the T gates: decided in the launch, or verified
                 d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
+                if spec:
+                    # the speculative pass's {fired, faults} straight into pinned, device-mapped host
+                    # memory (ops.HostMapped): read without a copy launch once the pass is complete
+                    capturing = torch.cuda.is_current_stream_capturing()
+                    if self._hmapped is None and not capturing:
+                        self._hmapped = ops.HostMapped()
+                    if self._hmapped is not None:
+                        fdev, flags_host = self._hmapped.take(reserve=capturing)
+                        d.pass_flags = fdev
             d.prof_events, d.prof_front = None, 0
             if self.step_events is not None:
                 from .prof import EventPair
@@ -654,8 +670,8 @@ class FilterEngine:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             verify = None
             if verify_dev:
-                verify = [pass_out[1], pass_out[2], None] if pass_out is not None else \
-                    list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None]
+                verify = [pass_out[1] if flags_host is None else None, pass_out[2], flags_host] \
+                    if pass_out is not None else list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None]
                 check_split = False
             self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass)
             if not finish:
@@ -690,7 +706,7 @@ class FilterEngine:
         later pass already queued keeps running (pipelined passes, bench.py).  Not while
         capturing a graph (the pinned allocation is not capturable): after the replay."""
         verify = pending[6]
-        if verify is None:
+        if verify is None or verify[0] is None:  # (flags already mapped from host memory)
             return
         if verify[2] is None:
             verify[2] = torch.empty(2, dtype=torch.int32, pin_memory=True)
@@ -714,7 +730,11 @@ class FilterEngine:
         later pass already queued behind it keeps running (pipelined passes, bench.py)."""
         parts, tot, shard, N, res, split_dev, verify, was_pass = pending if pending is not None else self._pending
         if verify is not None:  # the device verification's flags: the one host synchronisation
-            if synced and verify[2] is not None:  # staged (stage_flags) and known complete
+            if verify[0] is None:  # mapped from host memory: complete once the stream is
+                if not synced:
+                    torch.cuda.current_stream().synchronize()
+                fired, faults = (int(v) for v in verify[2][:2])
+            elif synced and verify[2] is not None:  # staged (stage_flags) and known complete
                 fired, faults = verify[2].tolist()
             else:
                 fired, faults = verify[0].tolist()

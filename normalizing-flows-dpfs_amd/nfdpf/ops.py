@@ -572,6 +572,46 @@ def filter_init(start_state, B, N, width, true_state, seed, row_base, device, es
     return x, lw, p, ie, vel
 
 
+class HostMapped:
+    """Slots of pinned, device-mapped, coherent host memory (nfdpf_host_mapped_alloc): a kernel
+    writes a slot through its device address, the host reads it (numpy view) once an event
+    behind that kernel has completed -- no copy launch.  ``take()`` hands out slots round robin;
+    ``take(reserve=True)`` (a slot baked into a captured graph) is never handed out again.
+    Allocated on construction: not while a stream is being captured."""
+
+    def __init__(self, slots: int = 64, slot_bytes: int = 64):
+        import ctypes
+        import numpy as np
+        self.slot_bytes, self.slots = slot_bytes, slots
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().nfdpf_host_mapped_alloc(slots * slot_bytes, ctypes.byref(h), ctypes.byref(d)),
+              "nfdpf_host_mapped_alloc")
+        self._host, self._dev = h.value, d.value
+        buf = (ctypes.c_int32 * (slots * slot_bytes // 4)).from_address(self._host)
+        self._view = np.frombuffer(buf, dtype=np.int32).reshape(slots, slot_bytes // 4)
+        self._free = list(range(slots))
+        self._next = 0
+
+    def take(self, reserve: bool = False):
+        """-> (device address, int32 numpy view of the slot)."""
+        if not self._free:
+            raise L.NfdpfError("HostMapped: every slot is reserved by a captured graph")
+        k = self._free[self._next % len(self._free)]
+        if reserve:
+            self._free.remove(k)
+        else:
+            self._next += 1
+        return self._dev + k * self.slot_bytes, self._view[k]
+
+    def __del__(self):
+        try:
+            if getattr(self, "_host", None):
+                lib().nfdpf_host_mapped_free(self._host)
+                self._host = None
+        except Exception:  # interpreter shutdown
+            pass
+
+
 def tiled_init(p0: torch.Tensor, out: torch.Tensor):
     B, N = p0.shape
     check(lib().nfdpf_filter_tiled_init(ptr(p0), B, N, ptr(out), stream_ptr(p0.device)), "nfdpf_filter_tiled_init")
