@@ -328,16 +328,19 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
             if j is None:
                 return None
             pipe["prev"] = None
-            evs_done[j].synchronize()
+            if not eng.wait_flags(pends[j]):  # (flags not host-mapped: an event behind the copy)
+                evs_done[j].synchronize()
             if not eng.finish_pending(pends[j], synced=True):
                 return eng.run(enc, start, vel_in, shard=shard, speculate=False)
             return caps[j]
 
         def step_pipe():
             i = pipe["k"] & 1
+            eng.arm_flags(pends[i])
             graphs[i].replay()
-            eng.stage_flags(pends[i])
-            evs_done[i].record()
+            if pends[i][6] is not None and pends[i][6][0] is not None:  # flags on the device: stage a copy
+                eng.stage_flags(pends[i])
+                evs_done[i].record()
             out = verify_prev()
             pipe["prev"], pipe["k"] = i, pipe["k"] + 1
             return out if out is not None else caps[i]

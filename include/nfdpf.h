@@ -409,8 +409,10 @@ typedef struct nfdpf_filter_desc {
                                step (DPFs.py:163-165; needs B_global == B) */
   int32_t *pass_gates;      /* optional [T] out: step t's gate -- the in-launch decisions
                                (pass_gate 1) or the verification of a speculative pass */
-  int32_t *pass_flags;      /* optional [2] out: {gates that fired, wave hand-off faults since the
-                               last read (nfdpf_split_fault's counter, read and cleared)} */
+  int32_t *pass_flags;      /* optional [3] out: {gates that fired, wave hand-off faults since the
+                               last read (nfdpf_split_fault's counter, read and cleared), 1 written
+                               last with a system-scope release (a completion word: host-mapped
+                               flags can be waited on without a stream operation)} */
   float *pass_obs;          /* optional [1] out: the obs-likelihood sum_t mean_{b,n} logw (DPFs.py:191) */
 } nfdpf_filter_desc;
 

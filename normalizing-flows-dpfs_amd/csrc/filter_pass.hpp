@@ -1287,28 +1287,25 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
   for (int b = l; b < B; b += 64) {
     const int64_t bt = (int64_t)b * T + k;
     double px = 0, py = 0, sw = 0;
-    int e = 0;
-    for (; e + 8 <= ent; e += 8) {  // 8 entries' loads in flight, then the adds in entry order
-      double a[8][3];
+    // every entry's loads in flight at once (ent <= kPassMaxTiles * 8 = 32), then the adds in
+    // entry order: one memory round trip per row instead of one per 8 entries
+    double a[kPassMaxTiles * 8][3];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const double *f = ws.fin + (bt * ent + e + j) * 4;
+    for (int j = 0; j < kPassMaxTiles * 8; ++j) {
+      if (j < ent) {
+        const double *f = ws.fin + (bt * ent + j) * 4;
         a[j][0] = f[1];
         a[j][1] = f[2];
         a[j][2] = f[3];
       }
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kPassMaxTiles * 8; ++j) {
+      if (j < ent) {
         px += a[j][0];
         py += a[j][1];
         sw += a[j][2];
       }
-    }
-    for (; e < ent; ++e) {
-      const double *f = ws.fin + (bt * ent + e) * 4;
-      px += f[1];
-      py += f[2];
-      sw += f[3];
     }
     d.pred[2 * bt] = (float)px;
     d.pred[2 * bt + 1] = (float)py;
@@ -1361,6 +1358,7 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     if (d.pass_flags) {  // (system scope: the caller may map them from pinned host memory)
       __hip_atomic_store(&d.pass_flags[0], nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&d.pass_flags[1], atomicExch(&g_split_fault, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&d.pass_flags[2], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // written, last
     }
     ws.hdr->abort = 0;
     ws.hdr->done = 0;

@@ -34,6 +34,11 @@
 namespace nfdpf {
 
 constexpr int kCmWaves = 8;  // 512 threads: two waves (two steps in flight) per particle group
+// experiment knob: the measurement's weights staged in LDS once per launch (ds_read broadcasts)
+// instead of streamed through the scalar cache every step
+#ifndef NFDPF_CM_STAGE
+#define NFDPF_CM_STAGE 0
+#endif
 
 struct PassCmLds {
   float xr[2][4][64][2];     // x_t by parity of t: the group's other wave reads it for step t + 1
@@ -43,6 +48,9 @@ struct PassCmLds {
   RowNorm rn[2];
   int xf[4];                 // x_t of group g written (t + 1)
   int fR;                    // slot t's row normaliser in rn[t & 1] (t + 1)
+#if NFDPF_CM_STAGE
+  alignas(16) float wst[kCrnvpPe + kMaxFlows * kCrnvpFlow];  // [encoder | flows]
+#endif
 };
 
 // the row normaliser of slot s from its C(s) granules (tiles x 4 groups, each {max u, sum e,
@@ -132,6 +140,10 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
   const uint32_t tag0 = __hip_atomic_load(&ws.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 12;
   if (threadIdx.x < 4) L.xf[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.fR = 0;
+#if NFDPF_CM_STAGE
+  for (int q = threadIdx.x; q < kCrnvpPe; q += blockDim.x) L.wst[q] = d.pe_params[q];
+  for (int q = threadIdx.x; q < d.n_flows * kCrnvpFlow; q += blockDim.x) L.wst[kCrnvpPe + q] = d.meas_params[q];
+#endif
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = w & 3, k = w >> 2, slot = g * 64 + lane, N = d.N, tiles = n_tiles(N);
   const int i = tile * kTile + slot;
@@ -175,8 +187,14 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
     }
     // 2. the measurement of x_t (model/models.py:256-278), unshifted
     float raw = -INFINITY;
-    if (valid)
+    if (valid) {
+#if NFDPF_CM_STAGE
+      const float *wl = L.wst;
+      raw = crnvp_lik(wl, wl + kCrnvpPe, d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
+#else
       raw = crnvp_lik(wptr(d.pe_params), wptr(d.meas_params), d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
+#endif
+    }
     // 3. slot t - 1: its row normaliser (group 0's wave sweeps C(t - 1)), its normalisation
     if (t > 0) {
       if (g == 0) pass_cm_poll_c(d, ws, L, b, tile, tag0, t - 1);

@@ -23,6 +23,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import time
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -494,7 +495,7 @@ class FilterEngine:
             d.pass_gate = int(gate_pass)
             if shard.world == 1:  # the epilogue verifies the gates / reads the fault counter on the device
                 i32 = dict(device=dev, dtype=torch.int32)
-                pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(2, **i32),
+                pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(3, **i32),
                             torch.empty((), **f32))
                 self.last_gates = pass_out[0]  # the T gates: decided in the launch, or verified
                 d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
@@ -506,6 +507,7 @@ class FilterEngine:
                         self._hmapped = ops.HostMapped()
                     if self._hmapped is not None:
                         fdev, flags_host = self._hmapped.take(reserve=capturing)
+                        flags_host[2] = 0  # armed: the epilogue sets it last (arm_flags before a replay)
                         d.pass_flags = fdev
             d.prof_events, d.prof_front = None, 0
             if self.step_events is not None:
@@ -642,7 +644,7 @@ class FilterEngine:
             check_split = False
             if not capturing:
                 if pass_out is not None:
-                    n_fired, faults = pass_out[1].tolist()
+                    n_fired, faults = pass_out[1].tolist()[:2]
                 else:
                     n_fired, faults = 0, self._faults_all(shard, dev)
                 if faults:  # the grid was not all resident: the step launches instead
@@ -712,6 +714,28 @@ class FilterEngine:
             verify[2] = torch.empty(2, dtype=torch.int32, pin_memory=True)
         verify[2].copy_(verify[0], non_blocking=True)
 
+    @staticmethod
+    def arm_flags(pending):
+        """Before replaying a captured speculative pass whose flags are mapped from host memory:
+        clear its completion word (the epilogue sets it, last, with a system-scope release)."""
+        verify = pending[6]
+        if verify is not None and verify[0] is None:
+            verify[2][2] = 0
+
+    @staticmethod
+    def wait_flags(pending, timeout_s: float = 60.0) -> bool:
+        """Wait on the host, with no stream operation, until the pass's epilogue has written its
+        flags into host memory (their completion word); False where the flags are not mapped."""
+        verify = pending[6]
+        if verify is None or verify[0] is not None:
+            return False
+        view = verify[2]
+        t0 = time.perf_counter()
+        while int(view[2]) == 0:
+            if time.perf_counter() - t0 > timeout_s:
+                raise L.NfdpfError(f"the one-launch pass's flags did not arrive within {timeout_s} s")
+        return True
+
     def take_pending(self):
         """The verification state of the last ``run(finish=False)``, handed to the caller (e.g.
         one per captured graph when passes are pipelined): ``finish_pending(pending)`` later."""
@@ -735,9 +759,9 @@ class FilterEngine:
                     torch.cuda.current_stream().synchronize()
                 fired, faults = (int(v) for v in verify[2][:2])
             elif synced and verify[2] is not None:  # staged (stage_flags) and known complete
-                fired, faults = verify[2].tolist()
+                fired, faults = verify[2].tolist()[:2]
             else:
-                fired, faults = verify[0].tolist()
+                fired, faults = verify[0].tolist()[:2]
             if faults:
                 if not was_pass:
                     raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "
