@@ -374,26 +374,20 @@ __device__ float cascade_row_sum_1k(const Get &v, int n) {
     const float x = v(min((ii * 4 + k) * 8 + j, n - 1));
     vals[ii] = (act && ii < n4) ? x : 0.f;
   }
-  float a0 = 0.f, a1 = 0.f;
-  const float a2 = 0.f, a3 = 0.f;
+  // The cascade's slots, with the values past n4 zeroed (x + 0 = x exactly, the sums are of
+  // non-negative terms): a full first block of 16 leaves a1 = S0 and the rest sums into a0 = S1
+  // (or, n4 = 32, a second full block makes a1 = S0 + S1 and a0 = 0); with n4 < 16 a0 = S0 and
+  // S1 = 0.  In every case the slot is S1 + S0 (IEEE addition commutes): two independent chains
+  // of 16 adds instead of one predicated chain of 32.
+  float a0 = 0.f;
   if (act) {
-    int i = 0;
+    float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      if (16 * blk + 16 <= n4) {
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) a0 += vals[16 * blk + jj];
-        i += 16;
-        a1 += a0;
-        a0 = 0.f;
-      }
+    for (int jj = 0; jj < 16; ++jj) {
+      s0 += vals[jj];
+      s1 += vals[16 + jj];
     }
-#pragma unroll
-    for (int ii = 0; ii < 32; ++ii)
-      if (ii >= i && ii < n4) a0 += vals[ii];
-    a0 += a1;
-    a0 += a2;
-    a0 += a3;
+    a0 = s1 + s0;
     if (k == 0)
       for (int r = n4 * 4; r < nv; ++r) a0 += v(r * 8 + j);
   }

@@ -401,6 +401,9 @@ __device__ __forceinline__ void flow_barrier(int *cnt, int &round) {
   round += 8;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if ((threadIdx.x & 63) == 0) atomicAdd(cnt, 1);
+#ifdef NFDPF_PASS_WAKE
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_wakeup" ::: "memory");
+#endif
   wait_flag(cnt, round);
 }
 
@@ -448,8 +451,10 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   SoftRow row{R.pl, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
   if (row.alpha < 1.0f) {
     if (tid < 64) {
+      PT(t, 19);
       const float S = (N >= 8 ? cascade_row_sum_1k([&](int j) { return row.q_raw(j); }, N) : cascade_row_sum([&](int j) { return row.q_raw(j); }, N));
       if (tid == 0) R.shf[0] = S;
+      PT(t, 11);
     }
     flow_barrier(&L.fbar, round);
   PT(t, 14);
@@ -486,21 +491,41 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   PT(t, 16);
   const float off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)t, grow, 0u).x) * (1.0f / (float)N);
   const int i0 = tile * kTile;
-  for (int i = tid; i < N; i += nth) {
-    const float m = off + d.lin[i];
-    int lo = 0, hi = N - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (R.cdf[mid] < m)
-        lo = mid + 1;
-      else
-        hi = mid;
+  {  // markers tid and tid + 512 (N <= 1024), their two binary searches interleaved (two LDS
+     // probes in flight per step instead of one search after the other); the same lower bound
+    const int ia = tid, ib = tid + nth;
+    const bool va = ia < N, vb = ib < N;
+    const float ma = va ? off + d.lin[ia] : 0.f, mb = vb ? off + d.lin[ib] : 0.f;
+    int loa = 0, hia = N - 1, lob = 0, hib = N - 1;
+    while (loa < hia || lob < hib) {
+      const int mida = (loa + hia) >> 1, midb = (lob + hib) >> 1;
+      const float ca = R.cdf[mida], cb = R.cdf[midb];
+      if (loa < hia) {
+        if (ca < ma)
+          loa = mida + 1;
+        else
+          hia = mida;
+      }
+      if (lob < hib) {
+        if (cb < mb)
+          lob = midb + 1;
+        else
+          hib = midb;
+      }
     }
-    const int sj = lo + (1.0f < m ? 1 : 0);
     // sj == N: the reference's out-of-range edge (next row's first particle, weight 0)
-    R.wg[i] = sj < N ? row.w(sj) : 0.f;
-    if (i >= i0 && i < i0 + kTile) R.src_l[i - i0] = sj;
+    if (va) {
+      const int sj = loa + (1.0f < ma ? 1 : 0);
+      R.wg[ia] = sj < N ? row.w(sj) : 0.f;
+      if (ia >= i0 && ia < i0 + kTile) R.src_l[ia - i0] = sj;
+    }
+    if (vb) {
+      const int sj = lob + (1.0f < mb ? 1 : 0);
+      R.wg[ib] = sj < N ? row.w(sj) : 0.f;
+      if (ib >= i0 && ib < i0 + kTile) R.src_l[ib - i0] = sj;
+    }
   }
+  PT(t, 6);
   flow_barrier(&L.fbar, round);
   PT(t, 17);
   // the tile's sources' positions (their loads in flight while wave 0 sums the gathered weights),
@@ -531,9 +556,11 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     R.xr_l[tid][0] = x0;
     R.xr_l[tid][1] = x1;
   }
+  PT(t, 10);
   if (tid < 64) {
     const float s2 = (N >= 8 ? cascade_row_sum_1k([&](int j) { return R.wg[j]; }, N)
                              : cascade_row_sum([&](int j) { return R.wg[j]; }, N));
+    PT(t, 9);
 #pragma unroll
     for (int k = 0; k < kTile / 64; ++k) {
       const int s = k * 64 + tid;
