@@ -347,6 +347,32 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
         step_pipe.drain = verify_prev
         if graph is not None:
             step = step_pipe if pipelined else step_graph  # noqa: F811
+    elif spec and world == 1 and eng.last_pass:
+        # --graph 0, one GPU, a speculative one-launch pass: the same pipelining with Python
+        # launches -- pass k + 1 is launched (run(finish=False)) before pass k's flags are waited
+        # for, so the host's launch path overlaps the GPU (fresh outputs per pass)
+        pp = {"prev": None}
+
+        def verify_prev_py():
+            prev = pp["prev"]
+            if prev is None:
+                return None
+            pp["prev"] = None
+            pend, out = prev
+            if not eng.wait_flags(pend):
+                torch.cuda.current_stream().synchronize()
+            if not eng.finish_pending(pend, synced=True):
+                return eng.run(enc, start, vel_in, shard=shard, speculate=False)
+            return out
+
+        def step_py_pipe():
+            out = eng.run(enc, start, vel_in, shard=shard, finish=False)
+            pend = eng.take_pending()
+            done = verify_prev_py()
+            pp["prev"] = (pend, out)
+            return done if done is not None else out
+        step_py_pipe.drain = verify_prev_py
+        step = step_py_pipe  # noqa: F811
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -114,17 +114,17 @@ def test_sharded_engine_matches_unsharded(case, tmp_path):
 # fires: the sharded passes ARE the result), "firing" = the c2_full workload (aligned encodings:
 # the gathered verification catches the fired gate and every rank reruns with the per-step
 # exchange)
-PASS_CASES = {"quiet": (8, 1000, 12), "firing": (8, 1000, 12)}
+PASS_CASES = {"quiet": (8, 1000, 12), "firing": (8, 1000, 12), "quiet_c3": (8, 1000, 12)}
 
 
 def _pass_inputs(kind, rows):
     """-> (models on DEV, enc, start, vel) of the case's rows."""
     B, N, T = PASS_CASES[kind]
     sl = slice(*rows)
-    if kind == "quiet":
+    if kind in ("quiet", "quiet_c3"):  # (quiet_c3: the C3 shape, tiled_pass_cm_kernel, OT resampler)
         import bench
         from DPFs import DPF
-        flags = bench.CONFIGS["c2"][0]
+        flags = bench.CONFIGS["c2" if kind == "quiet" else "c3"][0]
         torch.manual_seed(2)
         models = DPF(bench.make_args(flags, B, N, T, {})).to(DEV).eval()
         g = torch.Generator().manual_seed(31)
@@ -146,8 +146,12 @@ def _pass_run(kind, rows, shard=None, rank=0, world=1):
     from nfdpf.engine import FilterConfig, FilterEngine
     B, N, T = PASS_CASES[kind]
     models, enc, start, vel = _pass_inputs(kind, rows)
-    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321, kernel="tiled",
-                       pass_gate=False)  # (the unsharded rerun: the step launches, as the sharded ranks')
+    if kind == "quiet_c3":
+        cfg = FilterConfig(N=N, NF_dyn=False, NF_cond=False, measurement="CRNVP", resampler="ot", seed=321,
+                           kernel="tiled")
+    else:
+        cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321,
+                           kernel="tiled", pass_gate=False)  # (the unsharded rerun: the step launches, as the ranks')
     eng = FilterEngine(cfg, models)
     for r in range(world):
         if r == rank:
@@ -201,7 +205,7 @@ def test_sharded_pass_matches_unsharded(kind, tmp_path):
     B = PASS_CASES[kind][0]
     full = _pass_run(kind, (0, B))
     assert full["launched"], "the unsharded one-launch pass did not run"
-    assert full["verified"] == (kind == "quiet")
+    assert full["verified"] == (kind != "firing")
     world = 2
     path = str(tmp_path / "pass")
     mp.start_processes(_worker_pass, args=(world, _free_port(), kind, path), nprocs=world, start_method="spawn")
