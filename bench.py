@@ -430,8 +430,8 @@ def dominant(cfg_name, flags, kernel, B, N, T, fcfg, run, force):
     F_EX = F_EXEC.get(cfg_name, F_ALG) if kname.startswith("tiled_prop") else F_ALG
     bound = "mfma" if kname == "cglow_kernel" else "valu"
     if kernel == "tiled" and eng.last_pass:  # the whole pass in one launch: every step's FLOP
-        # (the C3 shape -- no flows on the particle path, CRNVP -- is tiled_pass_cm_kernel)
-        c3_shape = not flags["NF_dyn"] and not flags["NF_cond"] and flags["measurement"] == "CRNVP"
+        # (no flows on the particle path -- C3's CRNVP, C1's cosine -- is tiled_pass_cm_kernel)
+        c3_shape = not flags["NF_dyn"] and not flags["NF_cond"]  # (C1 too: the cosine measurement)
         kname, F_ALG = ("tiled_pass_cm_kernel" if c3_shape else "tiled_pass_kernel"), F_STEP
         F_EX = F_EXEC_STEP.get(cfg_name, F_ALG)
         units, nbytes = B * N * T, B_ALG * B * N * T

@@ -56,6 +56,7 @@ struct PassCmLds {
 // the row normaliser of slot s from its C(s) granules (tiles x 4 groups, each {max u, sum e,
 // sum e^2, max raw lik}): the tile's merge over its groups in order (ess_out[s], the gate's
 // input), then row_norm's arithmetic over the tiles in order with the CRNVP shift.  One wave.
+template <bool SHIFT>
 __device__ __forceinline__ void pass_cm_poll_c(const nfdpf_filter_desc &d, const PassWs &ws, PassCmLds &L, int b,
                                                int tile, uint32_t tag0, int s) {
   const int tiles = n_tiles(d.N), lane = threadIdx.x & 63;
@@ -94,7 +95,7 @@ __device__ __forceinline__ void pass_cm_poll_c(const nfdpf_filter_desc &d, const
     }
     double Sd = 0.0;
     for (int kk = 0; kk < tiles; ++kk) Sd += readlane_d(sum, kk) * (double)expf(readlane_f(m, kk) - M);
-    if (lane == 0) L.rn[s & 1] = RowNorm{M - Lmax, (float)Sd, Lmax};
+    if (lane == 0) L.rn[s & 1] = SHIFT ? RowNorm{M - Lmax, (float)Sd, Lmax} : RowNorm{M, (float)Sd, 0.f};
   }
   set_flag(&L.fR, s + 1);
 }
@@ -102,6 +103,7 @@ __device__ __forceinline__ void pass_cm_poll_c(const nfdpf_filter_desc &d, const
 // normalise slot s of this wave's group from the hand-over nb[s & 1] (finish_prev / prev_p_of's
 // arithmetic, shifted): hist_p, hist_lik (the shifted likelihood), the group's fin partials
 // (entry g of the tile); returns log p
+template <bool SHIFT>
 __device__ __forceinline__ float pass_cm_norm(const nfdpf_filter_desc &d, const PassWs &ws, PassCmLds &L, int b,
                                               int tile, int g, int s, int slot, int i, bool valid) {
   wait_flag(&L.fR, s + 1);
@@ -111,7 +113,7 @@ __device__ __forceinline__ float pass_cm_norm(const nfdpf_filter_desc &d, const 
   if (valid) {
     const int par = s & 1;
     const float lr = L.nb[par][0][slot], raw = L.nb[par][1][slot], pr = L.nb[par][2][slot];
-    const float lk = raw - rn.Lmax;
+    const float lk = SHIFT ? raw - rn.Lmax : raw;
     const float lw = ((lr + lk) + pr) - pr;
     const float p = expf(lw - rn.shift) / rn.Ssum + 1e-12f;
     const int64_t o = ((int64_t)b * d.T + s) * d.N + i;
@@ -133,7 +135,9 @@ __device__ __forceinline__ float pass_cm_norm(const nfdpf_filter_desc &d, const 
 
 template <int MEAS>
 __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const nfdpf_filter_desc d, PassWs ws) {
-  static_assert(MEAS == NFDPF_MEAS_CRNVP, "the C3-shaped pass: the conditional-RealNVP measurement");
+  static_assert(MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_COS || MEAS == NFDPF_MEAS_GAUSSIAN,
+                "the no-flow pass: the CRNVP, cosine or gaussian measurement");
+  constexpr bool SHIFT = meas_shifted<MEAS>();  // CRNVP / gaussian: lik - the row max (model/models.py:276)
   __shared__ PassCmLds L;
   int b, tile;
   pass_tile_row(b, tile);
@@ -187,18 +191,39 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
     }
     // 2. the measurement of x_t (model/models.py:256-278), unshifted
     float raw = -INFINITY;
+    double vinv = 0.0;
+    if constexpr (MEAS == NFDPF_MEAS_COS) {  // measure_row_setup's 1 / max(|v|, 1e-12), per wave
+      const float ve = lane < kE ? d.enc[((int64_t)b * d.T + t) * d.E + lane] : 0.f;
+      vinv = 1.0 / fmax(sqrt(wave_sum((double)ve * ve)), 1e-12);
+    }
     if (valid) {
+      if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
 #if NFDPF_CM_STAGE
-      const float *wl = L.wst;
-      raw = crnvp_lik(wl, wl + kCrnvpPe, d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
+        const float *wl = L.wst;
+        raw = crnvp_lik(wl, wl + kCrnvpPe, d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
 #else
-      raw = crnvp_lik(wptr(d.pe_params), wptr(d.meas_params), d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
+        raw = crnvp_lik(wptr(d.pe_params), wptr(d.meas_params), d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
 #endif
+      } else if constexpr (MEAS == NFDPF_MEAS_COS) {  // model/models.py:206-219 (measure<COS>'s arithmetic)
+        double ss, dot;
+        encode_dot<kE>(wptr(d.pe_params), x0, x1, L.encq[w], ss, dot);
+        raw = cos_lik(ss, dot, vinv);
+      } else {  // the gaussian measurement, model/models.py:237-254 (measure<GAUSSIAN>'s arithmetic)
+        float e[kE];
+        particle_encode<kE>(wptr(d.pe_params), x0, x1, e);
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < kE; ++j) {
+          const float vv = (L.encq[w][j] - e[j] - 1.0f) * 0.1f;
+          m = fmaf(vv, vv, m);
+        }
+        raw = -0.5f * (kE * 1.8378770664093453f + m) - kE * 2.302585092994046f;
+      }
     }
     // 3. slot t - 1: its row normaliser (group 0's wave sweeps C(t - 1)), its normalisation
     if (t > 0) {
-      if (g == 0) pass_cm_poll_c(d, ws, L, b, tile, tag0, t - 1);
-      lr = pass_cm_norm(d, ws, L, b, tile, g, t - 1, slot, i, valid);
+      if (g == 0) pass_cm_poll_c<SHIFT>(d, ws, L, b, tile, tag0, t - 1);
+      lr = pass_cm_norm<SHIFT>(d, ws, L, b, tile, g, t - 1, slot, i, valid);
     }
     // 4. the log-weight (DPFs.py:187) and exchange C(t): this group's softmax partials
     float u = -INFINITY;
@@ -229,9 +254,16 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
   }
   // the last slot's normalisation: the waves of parity T & 1 (they would have run step T)
   if (k == (d.T & 1)) {
-    if (g == 0) pass_cm_poll_c(d, ws, L, b, tile, tag0, d.T - 1);
-    pass_cm_norm(d, ws, L, b, tile, g, d.T - 1, slot, i, valid);
+    if (g == 0) pass_cm_poll_c<SHIFT>(d, ws, L, b, tile, tag0, d.T - 1);
+    pass_cm_norm<SHIFT>(d, ws, L, b, tile, g, d.T - 1, slot, i, valid);
   }
+}
+
+typedef void (*pass_cm_kernel_t)(const nfdpf_filter_desc, PassWs);
+static pass_cm_kernel_t pass_cm_kernel_of(const nfdpf_filter_desc &d) {
+  return d.measurement == NFDPF_MEAS_COS        ? tiled_pass_cm_kernel<NFDPF_MEAS_COS>
+         : d.measurement == NFDPF_MEAS_GAUSSIAN ? tiled_pass_cm_kernel<NFDPF_MEAS_GAUSSIAN>
+                                                : tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>;
 }
 
 // The C3-shaped pass applies: the configuration, the speculative gate (not forced, not gated in
@@ -239,7 +271,9 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
 static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
   const char *e = getenv("NFDPF_PASS");  // read per call: NFDPF_PASS=0 keeps the step-by-step launches
   if (e && e[0] == '0') return false;
-  if (d.nf_dyn != NFDPF_DYN_NONE || d.nf_cond || d.measurement != NFDPF_MEAS_CRNVP) return false;
+  if (d.nf_dyn != NFDPF_DYN_NONE || d.nf_cond ||
+      (d.measurement != NFDPF_MEAS_CRNVP && d.measurement != NFDPF_MEAS_COS && d.measurement != NFDPF_MEAS_GAUSSIAN))
+    return false;
   if (d.rng_mode != NFDPF_RNG_DEVICE || d.phase != 0 || d.E != kE || d.force_resample || d.pass_gate) return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 0 || d.n_flows > kMaxFlows || d.T < 1 ||
       d.T > kPassMaxT || d.B < 1 || d.B > 256)
@@ -247,7 +281,7 @@ static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>, kCmWaves * 64, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pass_cm_kernel_of(d), kCmWaves * 64, 0) !=
           hipSuccess ||
       occ < 1)
     return false;

@@ -2163,8 +2163,9 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   NFDPF_REQUIRE(d.hist_x && d.hist_p && d.hist_noise && d.hist_lik && d.hist_idx && d.ess_out && d.enc && d.vel &&
                     d.x_prev && d.p_prev && d.lw_sum && d.pred,
                 "nfdpf_filter_pass_tiled: null input/output pointer");
-  if (pass_cm_config_ok(d)) {  // the C3 shape: no flows on the particle path, the CRNVP measurement
-    NFDPF_REQUIRE(d.pe_params && d.meas_params && d.ess_all, "nfdpf_filter_pass_tiled: parameters / ess_all missing");
+  if (pass_cm_config_ok(d)) {  // the C3 / C1 shape: no flows on the particle path (CRNVP, cosine, gaussian)
+    NFDPF_REQUIRE(d.pe_params && (d.meas_params || d.measurement != NFDPF_MEAS_CRNVP) && d.ess_all,
+                  "nfdpf_filter_pass_tiled: parameters / ess_all missing");
     const int verify_cm = d.pass_gates && d.B_global == d.B;
     NFDPF_REQUIRE(!d.pass_gates || verify_cm, "nfdpf_filter_pass_tiled: pass_gates needs a pass of the whole batch");
     hipStream_t st = as_stream(stream);
@@ -2174,11 +2175,11 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
       ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
     const dim3 g(n_tiles(d.N), d.B);
     hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+    const auto kern = pass_cm_kernel_of(d);
     if (ev)
-      hipExtLaunchKernelGGL(tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>, g, dim3(kCmWaves * 64), 0, st, ev[0], ev[1], 0, d,
-                            ws);
+      hipExtLaunchKernelGGL(kern, g, dim3(kCmWaves * 64), 0, st, ev[0], ev[1], 0, d, ws);
     else
-      tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP><<<g, kCmWaves * 64, 0, st>>>(d, ws);
+      kern<<<g, kCmWaves * 64, 0, st>>>(d, ws);
     tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, verify_cm, 4);
     return launch_status("nfdpf_filter_pass_tiled");
   }

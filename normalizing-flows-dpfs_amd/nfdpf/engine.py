@@ -231,8 +231,10 @@ class FilterEngine:
         """Can the one-launch pass decide the ESS gate inside the launch (the whole batch on this
         GPU, the soft resampler)?"""
         c = self.cfg
+        # (the gated mode is the C2-shaped pass's, tiled_pass_kernel; the no-flow pass -- C1 / C3
+        # shapes -- only speculates)
         return bool(pass_ok and shard.world == 1 and c.resampler == "soft" and not c.force_resample
-                    and c.pass_gate is not False)
+                    and c.pass_gate is not False and c.NF_dyn and c.NF_cond)
 
     def _pass_supported(self, B, N, T, E, split_nets, shard) -> bool:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
