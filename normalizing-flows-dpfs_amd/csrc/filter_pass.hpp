@@ -93,6 +93,11 @@ __device__ unsigned long long g_ptrace[256][16][64][20];
 #ifndef NFDPF_PASS_HSTORE
 #define NFDPF_PASS_HSTORE 1
 #endif
+// SPEC: the next step's motion and exchange A published at the end of the step, before its
+// commit (A/B: pass 0.595-0.614 vs 0.621-0.630 ms, three pairs on one box)
+#ifndef NFDPF_PASS_PRE
+#define NFDPF_PASS_PRE 1
+#endif
 
 // pass modes (tiled_pass_kernel<MODE>)
 constexpr int kModeSpec = 0;   // every ESS gate taken as off (verified after the pass)
@@ -705,6 +710,10 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
   // the step's velocity, loaded one step ahead (beside the next step's noise): no scalar-load
   // latency at the head of the step
   float nv0 = d.vel[2 * (int64_t)b], nv1 = d.vel[2 * (int64_t)b + 1];
+  // SPEC (NFDPF_PASS_PRE): the next step's x_phys / noise, its A already published (pre)
+  constexpr bool PRE = NFDPF_PASS_PRE && MODE == kModeSpec;
+  float pp0 = 0.f, pp1 = 0.f, pe0 = 0.f, pe1 = 0.f;
+  bool pre = false;
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
@@ -745,20 +754,27 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     auto attempt = [&](bool first, bool spec) -> int {
       // motion (model/models.py:191-204): x_phys = (x_src + vel) + eps; eps drawn during the
       // previous step's A exchange (en0, en1)
-      e0 = e1 = p0 = p1 = 0.f;
-      if (valid) {
-        e0 = en0;
-        e1 = en1;
-        p0 = (xs0 + v0) + e0;
-        p1 = (xs1 + v1) + e1;
-      }
       const int64_t vb = (int64_t)(variant * 2 + par) * d.B;
       const int64_t gslot = ((vb + b) * tiles + tile) * 4 + g;
       const int64_t grow0 = (vb + b) * tiles * 4;
-      {  // exchange A: this wave's sums of x_phys
-        double s[4] = {p0, p1, (double)p0 * p0, (double)p1 * p1};
-        wave_sum_dpp_n(s);
-        publish4(ws.ga + gslot * kGA, s, tag);
+      if (PRE && pre) {  // SPEC: step t's motion and A were done at the end of step t - 1
+        e0 = pe0;
+        e1 = pe1;
+        p0 = pp0;
+        p1 = pp1;
+      } else {
+        e0 = e1 = p0 = p1 = 0.f;
+        if (valid) {
+          e0 = en0;
+          e1 = en1;
+          p0 = (xs0 + v0) + e0;
+          p1 = (xs1 + v1) + e1;
+        }
+        {  // exchange A: this wave's sums of x_phys
+          double s[4] = {p0, p1, (double)p0 * p0, (double)p1 * p1};
+          wave_sum_dpp_n(s);
+          publish4(ws.ga + gslot * kGA, s, tag);
+        }
       }
       PT(t, 1);
       // the next step's motion noise, drawn while the A sweep is in flight / fA is awaited
@@ -845,6 +861,23 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       ldp = 0.f;
       if (valid)
         for (int f = nfl - 1; f >= 0; --f) ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
+      if (PRE && t + 1 < d.T) {
+        // SPEC: step t + 1's motion (its noise and velocity are in hand) and its exchange A go
+        // out now, before step t's commit, whose LDS hand-offs then overlap A's visibility.  (A
+        // of step t + 1 reuses the parity of step t - 1's, which every tile of the row consumed
+        // before publishing B(t), swept above.)
+        pe0 = pe1 = pp0 = pp1 = 0.f;
+        if (valid) {
+          pe0 = en0;
+          pe1 = en1;
+          pp0 = (q0 + nv0) + pe0;
+          pp1 = (q1 + nv1) + pe1;
+        }
+        const int64_t gslot1 = (((int64_t)(par ^ 1) * d.B + b) * tiles + tile) * 4 + g;
+        double s[4] = {pp0, pp1, (double)pp0 * pp0, (double)pp1 * pp1};
+        wave_sum_dpp_n(s);
+        publish4(ws.ga + gslot1 * kGA, s, tag + 1u);
+      }
       return 0;
     };
     for (int a = 0;; ++a) {  // (one copy of the attempt's code: a loop, not two calls)
@@ -902,6 +935,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     x0 = q0;
     x1 = q1;
     prev_dec = fire;
+    pre = PRE;
   }
   if (GATE) {  // the last slot's stores (the encoder pair's C(T - 1) waits for them)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
