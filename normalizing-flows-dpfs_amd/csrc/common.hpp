@@ -364,7 +364,11 @@ __device__ float cascade_row_sum(const Get &v, int n) {
 template <class Get>
 __device__ float cascade_row_sum_1k(const Get &v, int n) {
 #pragma clang fp contract(off)
-  const int lane = threadIdx.x & 63;
+  // (an opaque lane: inside a persistent step loop the compiler would otherwise hoist the 32
+  // loads' lane addresses out of the loop and, out of VGPRs, spill them to scratch -- 32 scratch
+  // reloads per call on the forced pass's critical path)
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
   const int nv = n / 8, n4 = nv / 4;
   const int k = lane / 8, j = lane - (lane / 8) * 8;
   const bool act = lane < 32;

@@ -202,6 +202,14 @@ struct PassLds {
   uint32_t rowe[256];
 };
 
+// A loop-invariant lane value made opaque inside a persistent step loop: the compiler would
+// otherwise hoist the 64-bit addresses derived from it out of the loop and, short of VGPRs,
+// spill them to scratch (reloaded every step on the critical path)
+__device__ __forceinline__ int opaque_int(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ void gran_store(uint64_t *g, uint32_t data, uint32_t tag) {
   __hip_atomic_store(g, ((uint64_t)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -691,16 +699,26 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
   }
   // wave 0 folds both contexts: the weights of the context columns, once per launch
   const bool fold_lane = w == 0 && lane < ncb;
+  // the fold weights: held in registers for the whole pass (SPEC), or loaded per step under the
+  // exchange's poll (FORCE / GATE: their VGPR pressure spilled the held copies to scratch, whose
+  // reloads sat on the fold)
+  constexpr bool HOLD = MODE == kModeSpec;
   float fwd[1 + kOctxDyn] = {}, fwc[4] = {};
-  if (fold_lane) {
-    const FoldRef r = fold_ref(d.dyn_params, kNsDyn, lane);
+  auto load_fwd = [&](const nfdpf_filter_desc &dd) {
+    const FoldRef r = fold_ref(dd.dyn_params, kNsDyn, lane);
     fwd[0] = fold_bias0(r, kOctxDyn);
 #pragma unroll
     for (int c = 0; c < kOctxDyn; ++c) fwd[1 + c] = r.w1c[2 * (r.j * kOctxDyn + c) + r.w];
-    const int O = d.E + 4;
-    const FoldRef rc = fold_ref(d.cond_params, net_size<1, kH>(O), lane);
+  };
+  auto load_fwc = [&](const nfdpf_filter_desc &dd) {
+    const int O = dd.E + 4;
+    const FoldRef rc = fold_ref(dd.cond_params, net_size<1, kH>(O), lane);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + d.E + c) + rc.w];
+    for (int c = 0; c < 4; ++c) fwc[c] = rc.w1c[2 * (rc.j * O + dd.E + c) + rc.w];
+  };
+  if (HOLD && fold_lane) {
+    load_fwd(d);
+    load_fwc(d);
   }
   constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
   const double inv_n = 1.0 / N, inv_n1 = 1.0 / (N - 1);  // the row contexts' (ctx_from_sums)
@@ -714,9 +732,11 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
   constexpr bool PRE = NFDPF_PASS_PRE && MODE == kModeSpec;
   float pp0 = 0.f, pp1 = 0.f, pe0 = 0.f, pe1 = 0.f;
   bool pre = false;
+  const int i_ = i, slot_ = slot;
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
+    const int i = opaque_int(i_), slot = opaque_int(slot_);
     const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const uint32_t tag = tag0 + (uint32_t)t + 1u;
@@ -793,6 +813,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
           wait_flag2(&L.pf[0], t - 1);
           wait_flag2(&L.pf[2], t - 1);
         }
+        if (!HOLD && fold_lane) load_fwd(d);
         const int st = poll_rowx<3>(ws.ga + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, next_noise, stop);
         if (GATE && first) {  // (the poll's loads drained this wave's slot t - 1 stores too)
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -835,6 +856,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         publish4(ws.gb + gslot * kGA, s, tag);  // exchange B
       }
       if (w == 0) {  // the proposal fold: encoding columns (from prior wave 4), then [mean, std] of x_dyn
+        if (!HOLD && fold_lane) load_fwc(d);
         const int st = poll_rowx<3>(ws.gb + grow0 * kGA, tiles * 4 * kGA, tag, L.rowa, NoWork(), stop);
         if (st == 0) {
           PT(t, 8);
@@ -960,9 +982,11 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
   constexpr int nsd = kNsDyn;
   int round = 0;
   int prev_dec = 0;
+  const int i_ = i, slot_ = slot;
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
+    const int i = opaque_int(i_), slot = opaque_int(slot_);
     cf2 *dyn = wptr2(d.dyn_params);
     const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
@@ -1191,7 +1215,11 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
   if (GATE && we == sweeper) pass_gate(d, ws, L, b, tile, tag0, 0, 0.f);
+  const int slot_e_ = slot_e, i_e_ = i_e;
   for (int t = 0; t < d.T; ++t) {
+    // (opaque_int where the VGPR pressure spilled their addresses: FORCE / GATE)
+    const int slot_e = MODE == kModeSpec ? slot_e_ : opaque_int(slot_e_);
+    const int i_e = MODE == kModeSpec ? i_e_ : opaque_int(i_e_);
     const int par = t & 1;
     const float *enc_t = d.enc + ((int64_t)b * d.T + t) * d.E;
     PT(t, 0);
