@@ -125,6 +125,28 @@ __device__ __forceinline__ double dpp_d(double v) {
 }
 constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
 
+// a double moved by DPP with 0 where the source lane is out of the row (or the row masked off)
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp_d0(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, ROWMASK, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// Inclusive prefix sum over the wave's 64 lanes on DPP (row_shr 1, 2, 4, 8 inside each 16-lane
+// row, then row_bcast15 / row_bcast31 across rows): six steps without an LDS permute.  Its
+// addition order differs from a shfl_up scan: callers rely on it only where every partial sum
+// is exact (e.g. f64 sums of ~1e3 fp32 terms of a bounded exponent range).
+__device__ __forceinline__ double wave_incl_scan_dpp_d(double v) {
+  v += dpp_d0<0x111>(v);
+  v += dpp_d0<0x112>(v);
+  v += dpp_d0<0x114>(v);
+  v += dpp_d0<0x118>(v);
+  v += dpp_d0<0x142, 0xa>(v);
+  v += dpp_d0<0x143, 0xc>(v);
+  return v;
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }

@@ -445,6 +445,12 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   const uint32_t tag = tag0 + (uint32_t)t;  // C(t - 1)'s
   const float *xs;  // the previous slot's particles of this row
   int64_t xs_next;  // ... and the offset of the next row's
+  // the marker phase's inputs, in flight before the wait for the row's weights: markers tid and
+  // tid + 512 (N <= 1024) of the fixed linspace, the step's offset draw
+  const int ia = tid, ib = tid + nth;
+  const bool va = ia < N, vb = ib < N;
+  const float lin_a = va ? d.lin[ia] : 0.f, lin_b = vb ? d.lin[ib] : 0.f;
+  const float off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)t, grow, 0u).x) * (1.0f / (float)N);
   if (t > 0) {
     wait_flag(&L.fR, t);  // wave 8 has swept C(t - 1): slot t - 1's row normaliser in L.rn
     PT(t, 12);
@@ -479,11 +485,18 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     const double a = j0 < N ? (double)row.q(j0) : 0.0, c = j0 + 1 < N ? (double)row.q(j0 + 1) : 0.0;
     const double part = a + c;
     const int lane = tid & 63, w = tid >> 6;
+    // f64 sums of fp32 q terms: with the uniform mixture every q >= (1 - alpha) / (N S) and the
+    // partial sums stay below ~1, so when that floor is >= 2^-19 every partial sum is exact and the
+    // DPP scan's addition order gives the bits of any order; otherwise the shfl_up scan
     double inc = part;
+    if ((1.0f - row.alpha) * row.u >= 0x1p-18f) {
+      inc = wave_incl_scan_dpp_d(part);
+    } else {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double u = __shfl_up(inc, o);
-      if (lane >= o) inc += u;
+      for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(inc, o);
+        if (lane >= o) inc += u;
+      }
     }
     if (lane == 63) R.shd[w] = inc;
     flow_barrier(&L.fbar, round);
@@ -502,13 +515,10 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   }
   flow_barrier(&L.fbar, round);
   PT(t, 16);
-  const float off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)t, grow, 0u).x) * (1.0f / (float)N);
   const int i0 = tile * kTile;
   {  // markers tid and tid + 512 (N <= 1024), their two binary searches interleaved (two LDS
      // probes in flight per step instead of one search after the other); the same lower bound
-    const int ia = tid, ib = tid + nth;
-    const bool va = ia < N, vb = ib < N;
-    const float ma = va ? off + d.lin[ia] : 0.f, mb = vb ? off + d.lin[ib] : 0.f;
+    const float ma = va ? off + lin_a : 0.f, mb = vb ? off + lin_b : 0.f;
     int loa = 0, hia = N - 1, lob = 0, hib = N - 1;
     while (loa < hia || lob < hib) {
       const int mida = (loa + hia) >> 1, midb = (lob + hib) >> 1;
