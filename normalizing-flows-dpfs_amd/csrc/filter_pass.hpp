@@ -516,26 +516,21 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   flow_barrier(&L.fbar, round);
   PT(t, 16);
   const int i0 = tile * kTile;
-  {  // markers tid and tid + 512 (N <= 1024), their two binary searches interleaved (two LDS
-     // probes in flight per step instead of one search after the other); the same lower bound
+  {  // markers tid and tid + 512 (N <= 1024), their two searches interleaved (two LDS probes in
+     // flight per step instead of one search after the other); the same lower bound
     const float ma = va ? off + lin_a : 0.f, mb = vb ? off + lin_b : 0.f;
-    int loa = 0, hia = N - 1, lob = 0, hib = N - 1;
-    while (loa < hia || lob < hib) {
-      const int mida = (loa + hia) >> 1, midb = (lob + hib) >> 1;
-      const float ca = R.cdf[mida], cb = R.cdf[midb];
-      if (loa < hia) {
-        if (ca < ma)
-          loa = mida + 1;
-        else
-          hia = mida;
-      }
-      if (lob < hib) {
-        if (cb < mb)
-          lob = midb + 1;
-        else
-          hib = midb;
-      }
+    // branch-free lower bound (the first j with cdf[j] >= m, N if none) in fixed halving steps,
+    // clamped to N - 1: the binary search's result, without divergent loop exits
+    int loa = 0, lob = 0;
+#pragma unroll
+    for (int step = kPassMaxTiles * kTile / 2; step >= 1; step >>= 1) {
+      const int ja = loa + step - 1, jb = lob + step - 1;
+      const float ca = R.cdf[min(ja, N - 1)], cb = R.cdf[min(jb, N - 1)];
+      loa += (ja < N && ca < ma) ? step : 0;
+      lob += (jb < N && cb < mb) ? step : 0;
     }
+    loa = min(loa, N - 1);
+    lob = min(lob, N - 1);
     // sj == N: the reference's out-of-range edge (next row's first particle, weight 0)
     if (va) {
       const int sj = loa + (1.0f < ma ? 1 : 0);
