@@ -383,7 +383,9 @@ __device__ float cascade_row_sum(const Get &v, int n) {
 // cascade_row_sum for 8 <= n <= 1024 (n4 <= 32 per lane, so the cascade's block size is 16 and
 // no higher level ever flushes): the same additions in the same order, with each lane's up to
 // 32 values loaded before the first add (the generic loop waits for every load in turn).
-template <class Get>
+// CAP >= 1024: v(j) may be read for any j < 1024 (an LDS array of that size; the values past n are
+// loaded and discarded -- selected away, never added), so no index needs the clamp to n - 1
+template <int CAP = 0, class Get>
 __device__ float cascade_row_sum_1k(const Get &v, int n) {
 #pragma clang fp contract(off)
   // (an opaque lane: inside a persistent step loop the compiler would otherwise hoist the 32
@@ -397,7 +399,7 @@ __device__ float cascade_row_sum_1k(const Get &v, int n) {
   float vals[32];
 #pragma unroll
   for (int ii = 0; ii < 32; ++ii) {  // unconditional (clamped) reads: no branch per value
-    const float x = v(min((ii * 4 + k) * 8 + j, n - 1));
+    const float x = v(CAP >= 1024 ? (ii * 4 + k) * 8 + j : min((ii * 4 + k) * 8 + j, n - 1));
     vals[ii] = (act && ii < n4) ? x : 0.f;
   }
   // The cascade's slots, with the values past n4 zeroed (x + 0 = x exactly, the sums are of

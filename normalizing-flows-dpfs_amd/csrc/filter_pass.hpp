@@ -437,8 +437,13 @@ __device__ __forceinline__ void flow_barrier(int *cnt, int &round) {
 // encoder wave 0 to have published C(t-1) or a later C.
 // fR(t-1) also means that every encoder wave of this tile has finished its MFMA layers of step
 // t-1 (it publishes C(t-1) after them): the resampling scratch (PassRs) aliases their LDS.
+// FORCE (late = true): the tail needs no barrier -- each chain wave gathers its own slots' sources
+// (slot == tid) and reads them back itself, and wave 7, a prior wave idle until the proposal, sums
+// the gathered weights and writes lr_l, then raises fS: the encoder waves wait for fS before their
+// MFMA layers reuse this scratch.  (GATE: wave 0 and a closing barrier; its encoder waves read
+// lr_l only after the chain's commit, which that barrier orders.)
 __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b,
-                                              int tile, uint32_t tag0, int t, int &round) {
+                                              int tile, uint32_t tag0, int t, int &round, bool late) {
   PassRs &R = L.rs;
   const int N = d.N, tiles = n_tiles(N), tid = threadIdx.x, nth = 8 * 64;
   const int64_t grow = d.row_base + b;
@@ -471,7 +476,7 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   if (row.alpha < 1.0f) {
     if (tid < 64) {
       PT(t, 19);
-      const float S = (N >= 8 ? cascade_row_sum_1k([&](int j) { return row.q_raw(j); }, N) : cascade_row_sum([&](int j) { return row.q_raw(j); }, N));
+      const float S = (N >= 8 ? cascade_row_sum_1k<kPassMaxTiles * kTile>([&](int j) { return row.q_raw(j); }, N) : cascade_row_sum([&](int j) { return row.q_raw(j); }, N));
       if (tid == 0) R.shf[0] = S;
       PT(t, 11);
     }
@@ -575,19 +580,20 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     R.xr_l[tid][1] = x1;
   }
   PT(t, 10);
-  if (tid < 64) {
-    const float s2 = (N >= 8 ? cascade_row_sum_1k([&](int j) { return R.wg[j]; }, N)
+  const int sw = late ? nth - 64 : 0;  // the wave that sums the gathered weights
+  if (tid >= sw && tid < sw + 64) {
+    const float s2 = (N >= 8 ? cascade_row_sum_1k<kPassMaxTiles * kTile>([&](int j) { return R.wg[j]; }, N)
                              : cascade_row_sum([&](int j) { return R.wg[j]; }, N));
     PT(t, 9);
 #pragma unroll
     for (int k = 0; k < kTile / 64; ++k) {
-      const int s = k * 64 + tid;
+      const int s = k * 64 + tid - sw;
       if (i0 + s < N) L.lr_l[s] = logf(R.wg[i0 + s] / s2);
     }
   }
-  flow_barrier(&L.fbar, round);
+  if (!late) flow_barrier(&L.fbar, round);
   PT(t, 18);
-  if (tid < 64) set_flag(&L.fS, t + 1);  // the encoder waves may read lr_l
+  if (tid >= sw && tid < sw + 64) set_flag(&L.fS, t + 1);  // the encoder waves may read lr_l
 }
 
 // The pass's (row, tile) of this workgroup: a row's tiles on ONE XCD where the grid allows
@@ -765,7 +771,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         set_flag(&L.hxf[g], t);
       }
-      pass_resample(d, ws, L, b, tile, tag0, t, round);
+      pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
       if (GATE) {
         fire = wait_dec(L, t);
         known = true;
@@ -916,7 +922,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       known = true;
       if (!fire) break;
       if (w == 0) set_flag(&L.rq, t + 1);  // the prior waves join the row's resampling
-      pass_resample(d, ws, L, b, tile, tag0, t, round);
+      pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
       take_resampled();
       variant = 1;
     }
@@ -997,7 +1003,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     const int par = t & 1;
     const RowSlot S = row_slot(d, b, t);
     const int pred = GATE ? (t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
-    if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round);
+    if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
     PT(t, 0);
     if (g == 0) {
       // the proposal fold over the encoding columns (model/models.py:338-346) one step ahead,
@@ -1023,7 +1029,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
         if (q >= t + 1 || r >= t + 1 || !pass_spin<NFDPF_PASS_FLAG_SLEEP>(sp)) break;
       }
       asm volatile("" ::: "memory");
-      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1) pass_resample(d, ws, L, b, tile, tag0, t, round);
+      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
     }
     wait_flag(&L.qf[g], t + 1);
     PT(t, 1);
