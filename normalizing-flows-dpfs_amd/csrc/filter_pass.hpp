@@ -437,11 +437,14 @@ __device__ __forceinline__ void flow_barrier(int *cnt, int &round) {
 // encoder wave 0 to have published C(t-1) or a later C.
 // fR(t-1) also means that every encoder wave of this tile has finished its MFMA layers of step
 // t-1 (it publishes C(t-1) after them): the resampling scratch (PassRs) aliases their LDS.
-// FORCE (late = true): the tail needs no barrier -- each chain wave gathers its own slots' sources
-// (slot == tid) and reads them back itself, and wave 7, a prior wave idle until the proposal, sums
-// the gathered weights and writes lr_l, then raises fS: the encoder waves wait for fS before their
-// MFMA layers reuse this scratch.  (GATE: wave 0 and a closing barrier; its encoder waves read
-// lr_l only after the chain's commit, which that barrier orders.)
+#ifndef NFDPF_GATE_LATE
+#define NFDPF_GATE_LATE 1
+#endif
+// late = true (FORCE; GATE unless NFDPF_GATE_LATE=0): the tail needs no barrier -- each chain
+// wave gathers its own slots' sources (slot == tid) and reads them back itself, and wave 7, a
+// prior wave idle until the proposal, sums the gathered weights and writes lr_l, then raises fS:
+// the encoder waves wait for fS before their MFMA layers reuse this scratch (GATE: after the
+// chain's commit, when step t or t - 1 fired).
 __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b,
                                               int tile, uint32_t tag0, int t, int &round, bool late) {
   PassRs &R = L.rs;
@@ -771,7 +774,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         set_flag(&L.hxf[g], t);
       }
-      pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
+      pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
       if (GATE) {
         fire = wait_dec(L, t);
         known = true;
@@ -922,7 +925,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       known = true;
       if (!fire) break;
       if (w == 0) set_flag(&L.rq, t + 1);  // the prior waves join the row's resampling
-      pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
+      pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
       take_resampled();
       variant = 1;
     }
@@ -1003,7 +1006,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     const int par = t & 1;
     const RowSlot S = row_slot(d, b, t);
     const int pred = GATE ? (t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
-    if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
+    if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
     PT(t, 0);
     if (g == 0) {
       // the proposal fold over the encoding columns (model/models.py:338-346) one step ahead,
@@ -1029,7 +1032,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
         if (q >= t + 1 || r >= t + 1 || !pass_spin<NFDPF_PASS_FLAG_SLEEP>(sp)) break;
       }
       asm volatile("" ::: "memory");
-      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE);
+      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
     }
     wait_flag(&L.qf[g], t + 1);
     PT(t, 1);
@@ -1225,6 +1228,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   const EncFrag2 ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
+  int pdec = 0;  // GATE: step t - 1's decision (the flow waves resampled at step t iff it or step t's fired)
   if (GATE && we == sweeper) pass_gate(d, ws, L, b, tile, tag0, 0, 0.f);
   const int slot_e_ = slot_e, i_e_ = i_e;
   for (int t = 0; t < d.T; ++t) {
@@ -1244,6 +1248,9 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
     auto encode = [&]() {
       double ss, dot;
       wait_flag(&L.qf[g], t + 1);
+      // GATE: a resampling at step t (predicted, or the chain's redo) may still be summing its
+      // gathered weights in the scratch the MFMA layers reuse -- until fS (qf implies fD >= t + 1)
+      if (GATE && (pdec || __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0)) wait_flag(&L.fS, t + 1);
       PT(t, 4);
 #ifndef NFDPF_EXP_NOENC
       encode_dot_mfma_half<kE>(ef, role, L.qbuf[par] + g * 64, L.qbuf[par] + kTile + g * 64, L.encq[we], ss, dot,
@@ -1288,7 +1295,8 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       if (grp) lk = encode();
       // step t is committed (qf): its decision is known; a fired gate resampled the row and
       // this particle's log-weight is its source's (the chain's resampling left it in lr_l)
-      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0) lr = valid_e ? L.lr_l[slot_e] : 0.f;
+      pdec = __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]);
+      if (pdec != 0) lr = valid_e ? L.lr_l[slot_e] : 0.f;
     }
     // the log-weight (DPFs.py:187)
     PT(t, 3);
