@@ -161,6 +161,7 @@ static PassWs pass_carve(void *ws, int B, int N, int T) {
 // forced resampling of the row (FORCE), at the top of a step while no wave is encoding
 struct PassRs {
   float pl[kPassMaxTiles * kTile];   // the row's weights of the previous slot
+  float qr[kPassMaxTiles * kTile];   // their mixture q_raw (SoftRow::q_raw, written beside pl)
   float cdf[kPassMaxTiles * kTile];  // its CDF (soft_row_search)
   float wg[kPassMaxTiles * kTile];   // the gathered weights w[idx_i] of every marker i
   float xr_l[kTile][2];              // source position,
@@ -459,27 +460,36 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   const bool va = ia < N, vb = ib < N;
   const float lin_a = va ? d.lin[ia] : 0.f, lin_b = vb ? d.lin[ib] : 0.f;
   const float off = u01(rng_draw(d.seed, kTagOffset, (uint32_t)t, grow, 0u).x) * (1.0f / (float)N);
+  // soft_row_search's steps on 512 threads (soft.hpp); q_raw of every weight kept beside it
+  SoftRow row{R.pl, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
+  const bool mix = row.alpha < 1.0f;
+  auto put = [&](int j, float pj) {
+    R.pl[j] = pj;
+    R.qr[j] = row.q_raw_of(pj);
+  };
   if (t > 0) {
     wait_flag(&L.fR, t);  // wave 8 has swept C(t - 1): slot t - 1's row normaliser in L.rn
     PT(t, 12);
     const RowNorm rn = L.rn[(t - 1) & 1];
     const float *us = ws.gu + ((int64_t)((t - 1) & 1) * d.B + b) * N;
-    for (int j = tid; j < N; j += nth) R.pl[j] = expf(load_wt(us + j) - rn.shift) / rn.Ssum + 1e-12f;  // pass_norm's p
+    for (int j = tid; j < N; j += nth) put(j, expf(load_wt(us + j) - rn.shift) / rn.Ssum + 1e-12f);  // pass_norm's p
     xs = d.hist_x + ((int64_t)b * d.T + t - 1) * N * 2;
     xs_next = (int64_t)d.T * N * 2;
   } else {
-    for (int j = tid; j < N; j += nth) R.pl[j] = d.p_prev[(int64_t)b * d.p_prev_rs + j];
+    for (int j = tid; j < N; j += nth) put(j, d.p_prev[(int64_t)b * d.p_prev_rs + j]);
     xs = d.x_prev + (int64_t)b * d.x_prev_rs;
     xs_next = d.x_prev_rs;
   }
   flow_barrier(&L.fbar, round);
   PT(t, 13);
-  // soft_row_search's steps on 512 threads (soft.hpp)
-  SoftRow row{R.pl, N, d.alpha, 1.0f / (float)N, (float)(1.0 - (double)d.alpha), 1.0f};
-  if (row.alpha < 1.0f) {
+  // SoftRow's q and w on the stored q_raw (the same values, not recomputed)
+  auto qv = [&](int j) { return mix ? R.qr[j] / row.S : R.pl[j]; };
+  auto wv = [&](int j) { return mix ? R.pl[j] / qv(j) : row.u; };
+  if (mix) {
     if (tid < 64) {
       PT(t, 19);
-      const float S = (N >= 8 ? cascade_row_sum_1k<kPassMaxTiles * kTile>([&](int j) { return row.q_raw(j); }, N) : cascade_row_sum([&](int j) { return row.q_raw(j); }, N));
+      const float S = (N >= 8 ? cascade_row_sum_1k<kPassMaxTiles * kTile>([&](int j) { return R.qr[j]; }, N)
+                              : cascade_row_sum([&](int j) { return R.qr[j]; }, N));
       if (tid == 0) R.shf[0] = S;
       PT(t, 11);
     }
@@ -490,7 +500,7 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
   // the exact f64 prefix of q: 2 consecutive j per thread (N <= 1024), wave scans, wave order
   {
     const int j0 = 2 * tid;
-    const double a = j0 < N ? (double)row.q(j0) : 0.0, c = j0 + 1 < N ? (double)row.q(j0 + 1) : 0.0;
+    const double a = j0 < N ? (double)qv(j0) : 0.0, c = j0 + 1 < N ? (double)qv(j0 + 1) : 0.0;
     const double part = a + c;
     const int lane = tid & 63, w = tid >> 6;
     // f64 sums of fp32 q terms: with the uniform mixture every q >= (1 - alpha) / (N S) and the
@@ -509,8 +519,12 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     if (lane == 63) R.shd[w] = inc;
     flow_barrier(&L.fbar, round);
   PT(t, 15);
-    double base = 0.0;
-    for (int k = 0; k < w; ++k) base += R.shd[k];
+    double base = 0.0, sh[8];  // (the 8 wave totals loaded at once, then added in wave order)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[k] = R.shd[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < w) base += sh[k];
     double run = base + inc - part;
     if (j0 < N) {
       run += a;
@@ -542,12 +556,12 @@ __device__ __forceinline__ void pass_resample(const nfdpf_filter_desc &d, const 
     // sj == N: the reference's out-of-range edge (next row's first particle, weight 0)
     if (va) {
       const int sj = loa + (1.0f < ma ? 1 : 0);
-      R.wg[ia] = sj < N ? row.w(sj) : 0.f;
+      R.wg[ia] = sj < N ? wv(sj) : 0.f;
       if (ia >= i0 && ia < i0 + kTile) R.src_l[ia - i0] = sj;
     }
     if (vb) {
       const int sj = lob + (1.0f < mb ? 1 : 0);
-      R.wg[ib] = sj < N ? row.w(sj) : 0.f;
+      R.wg[ib] = sj < N ? wv(sj) : 0.f;
       if (ib >= i0 && ib < i0 + kTile) R.src_l[ib - i0] = sj;
     }
   }

@@ -21,9 +21,10 @@ struct SoftRow {
   int N;
   float alpha, u, one_minus_alpha;
   float S;         // cascade sum of q_raw
-  __device__ __forceinline__ float q_raw(int j) const {
+  __device__ __forceinline__ float q_raw(int j) const { return q_raw_of(p[j]); }
+  __device__ __forceinline__ float q_raw_of(float pj) const {
 #pragma clang fp contract(off)
-    return alpha < 1.0f ? p[j] * alpha + u * one_minus_alpha : p[j];
+    return alpha < 1.0f ? pj * alpha + u * one_minus_alpha : pj;
   }
   __device__ __forceinline__ float q(int j) const { return alpha < 1.0f ? q_raw(j) / S : p[j]; }
   __device__ __forceinline__ float w(int j) const { return alpha < 1.0f ? p[j] / q(j) : u; }
