@@ -404,7 +404,8 @@ __device__ __forceinline__ float load_wt(const float *p) {
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
 __device__ __forceinline__ void load_wt2(const float *p, float &a, float &b) {
-  const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t v =
+      __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   a = __uint_as_float((uint32_t)v);
   b = __uint_as_float((uint32_t)(v >> 32));
 }
@@ -874,7 +875,8 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       cf2 *dyn = wptr2(d.dyn_params), *cond = wptr2(d.cond_params);
       float xd0 = p0, xd1 = p1, ld = 0.f;
       if (valid)
-        for (int f = nfl - 1; f >= 0; --f) ld += pass_inverse(dyn + f * 2 * nsd, nsd, xd0, xd1, L.cbd[par] + f * 2 * kH);
+        for (int f = nfl - 1; f >= 0; --f)
+          ld += pass_inverse(dyn + f * 2 * nsd, nsd, xd0, xd1, L.cbd[par] + f * 2 * kH);
       jac = -ld;
       PT(t, 3);
       {
@@ -910,7 +912,8 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       q1 = xd1;
       ldp = 0.f;
       if (valid)
-        for (int f = nfl - 1; f >= 0; --f) ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
+        for (int f = nfl - 1; f >= 0; --f)
+          ldp += pass_inverse(cond + f * 2 * nsc, nsc, q0, q1, L.cbc[par] + f * 2 * kH);
       if (PRE && t + 1 < d.T) {
         // SPEC: step t + 1's motion (its noise and velocity are in hand) and its exchange A go
         // out now, before step t's commit, whose LDS hand-offs then overlap A's visibility.  (A
@@ -1046,7 +1049,8 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
         if (q >= t + 1 || r >= t + 1 || !pass_spin<NFDPF_PASS_FLAG_SLEEP>(sp)) break;
       }
       asm volatile("" ::: "memory");
-      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
+      if (__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.rq) >= t + 1)
+        pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
     }
     wait_flag(&L.qf[g], t + 1);
     PT(t, 1);
