@@ -165,6 +165,11 @@ class FilterEngine:
         # a one-launch pass whose row hand-offs timed out (its grid was not all resident: another
         # process or kernel held CUs) turns the pass off for this engine; the step launches rerun
         self.pass_disabled = False
+        # why the last run's shapes kept a pass-family configuration off the one-launch pass
+        # (N above 1024, more (row, tile) workgroups than the device holds at once), else None;
+        # warned once per engine
+        self.pass_fallback_reason = None
+        self._fallback_warned = False
         self._hmapped = None  # ops.HostMapped slots for the speculative pass's flags (lazy)
         self._shared_device = None  # per process group: does another rank use this rank's GPU?
         self.last_gate_pass = False  # the last run was the gated one-launch pass (gates decided in the launch)
@@ -262,7 +267,31 @@ class FilterEngine:
         d.resampler = L.RESAMPLE[c.resampler]
         d.rng_mode, d.force_resample = L.RNG_DEVICE, int(c.force_resample)
         d.n_flows, d.hidden, d.split_nets = c.n_flows, c.hidden, int(split_nets)
-        return bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
+        ok = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
+        self.pass_fallback_reason = None if ok else self._shape_limit(B, N)
+        if self.pass_fallback_reason and not self._fallback_warned and os.environ.get("NFDPF_PASS") != "0":
+            import warnings
+            warnings.warn(f"nfdpf: the one-launch pass does not cover this shape ({self.pass_fallback_reason}); "
+                          f"running the step launches (about half the speed)", RuntimeWarning, stacklevel=3)
+            self._fallback_warned = True
+        return ok
+
+    @staticmethod
+    def _shape_limit(B, N):
+        """The one-launch pass's shape limits (csrc/filter_pass.hpp pass_config_ok,
+        filter_pass_cm.hpp pass_cm_config_ok): N <= 1024 (4 tiles of 256 per row), every
+        (row, tile) workgroup resident at once (one per CU), at most 256 rows per launch."""
+        if not torch.cuda.is_available():
+            return None
+        tiles = -(-N // 256)
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        if N > 1024:
+            return f"N={N} > 1024 particles per row"
+        if B > 256:
+            return f"B={B} > 256 rows per launch"
+        if B * tiles > cus:
+            return f"B={B} rows x {tiles} tiles = {B * tiles} workgroups, more than the {cus} CUs hold at once"
+        return None
 
     @staticmethod
     def device_identity(dev=None) -> str:

@@ -281,6 +281,27 @@ def test_pass_disabled_by_env(monkeypatch):
     assert not eng.last_pass
 
 
+def test_pass_shape_fallback_is_reported(monkeypatch):
+    """A C2-shaped run beyond the pass's shape limits (here more (row, tile) workgroups than the
+    device's CUs hold at once) runs the step launches and says so: one RuntimeWarning per engine
+    and ``pass_fallback_reason``; NFDPF_PASS=0 (chosen, not a limit) stays quiet."""
+    fx = load("e2e_c2.npz")
+    models = _Models(weights(fx), e2e_cfg(fx))
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    B = cus // 4 + 1  # N = 1000: 4 tiles per row
+    enc, start, vel = _inputs(B, 2, seed=5)
+    with pytest.warns(RuntimeWarning, match="one-launch pass does not cover"):
+        eng, _ = _run(models, 1000, enc, start, vel, spec=True)
+    assert not eng.last_pass and eng.pass_launches == 0
+    assert "workgroups" in eng.pass_fallback_reason
+    monkeypatch.setenv("NFDPF_PASS", "0")
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        eng2, _ = _run(models, 1000, enc[:2], start[:2], vel[:2], spec=True)
+    assert not eng2.last_pass
+
+
 def _philox_offsets(seed, T, B, N, row_base=0):
     """The device RNG's soft-resampling offsets (csrc/common.hpp rng_draw(seed, kTagOffset = 1,
     t, row, 0) -> u01 / N), restated on the host: offsets [T, B] float32."""
