@@ -120,6 +120,10 @@ struct PassWs {
   double *eq;   // [T] the epilogue's per-step obs-likelihood terms
   int32_t *eg;  // [T] the epilogue's per-step gates
   uint64_t wait_ticks;  // the bound of every wait (s_memrealtime ticks; kPassWaitTicks)
+  // the first row of this launch: a speculative pass of more rows than the device holds at once
+  // runs as several launches of resident rows (the rows of a speculative pass never wait for
+  // each other), every table indexed by the batch row row0 + the grid's row
+  int row0;
 };
 
 __host__ __device__ static inline int64_t pass_granule_bytes(int B, int N) {
@@ -138,6 +142,7 @@ static PassWs pass_carve(void *ws, int B, int N, int T) {
   char *p = (char *)ws;
   const int64_t bt = (int64_t)B * n_tiles(N);
   PassWs w;
+  w.row0 = 0;
   w.hdr = (PassHdr *)p;
   p += 256;
   w.ga = (uint64_t *)p;
@@ -622,7 +627,37 @@ __device__ __forceinline__ void pass_tile_row(int &b, int &tile) {
   const int n = gridDim.x * gridDim.y, id = blockIdx.x + gridDim.x * blockIdx.y;
   const int lin = (n & 7) == 0 ? (id & 7) * (n >> 3) + (id >> 3) : id;
   tile = lin % gridDim.x;
-  b = lin / gridDim.x;
+  b = lin / gridDim.x + kernarg_ws()->row0;
+}
+
+// Rows of (tiles) workgroups of `kern` the device holds at once (0: not even one row, or the
+// query failed)
+template <class K>
+static int pass_resident_rows(K kern, int threads, int tiles) {
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, threads, 0) != hipSuccess || occ < 1)
+    return 0;
+  return (int)((int64_t)cus * occ / tiles);
+}
+
+// Launch `kern` over the pass's rows in chunks of `rows` resident rows (one launch when all fit);
+// the profiling events (if any) bracket the first and the last launch
+template <class K>
+static void pass_launch_rows(K kern, const nfdpf_filter_desc &d, PassWs ws, int threads, int rows,
+                             hipStream_t st) {
+  hipEvent_t *ev = (hipEvent_t *)d.prof_events;
+  const int tiles = n_tiles(d.N);
+  for (int r0 = 0; r0 < d.B; r0 += rows) {
+    ws.row0 = r0;
+    const dim3 g(tiles, std::min(rows, d.B - r0));
+    hipEvent_t e0 = ev && r0 == 0 ? ev[0] : nullptr, e1 = ev && r0 + rows >= d.B ? ev[1] : nullptr;
+    if (e0 || e1)
+      hipExtLaunchKernelGGL(kern, g, dim3(threads), 0, st, e0, e1, 0, d, ws);
+    else
+      kern<<<g, threads, 0, st>>>(d, ws);
+  }
 }
 
 // ---- waves 0-7: the flows, one wave per particle group and stage ---------------------------
@@ -1517,14 +1552,10 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
       d.B < 1 || d.B > 256)  // (the epilogue stages a step's B row sums in LDS)
     return false;
-  int dev = 0, cus = 0, occ = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &occ, pass_kernel_of(d), 4 * kTile, 0) != hipSuccess ||
-      occ < 1)
-    return false;
-  return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;
+  // every workgroup resident at once; a speculative pass (no row waits for another) may also
+  // run its rows in resident chunks (pass_launch_rows)
+  const int rows = pass_resident_rows(pass_kernel_of(d), 4 * kTile, n_tiles(d.N));
+  return rows >= d.B || (rows >= 1 && pass_mode_of(d) == kModeSpec);
 }
 
 }  // namespace nfdpf

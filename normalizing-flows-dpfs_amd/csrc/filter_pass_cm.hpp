@@ -267,7 +267,7 @@ static pass_cm_kernel_t pass_cm_kernel_of(const nfdpf_filter_desc &d) {
 }
 
 // The C3-shaped pass applies: the configuration, the speculative gate (not forced, not gated in
-// the launch), and every workgroup of its grid resident at once.
+// the launch), and at least one row's workgroups resident at once.
 static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
   const char *e = getenv("NFDPF_PASS");  // read per call: NFDPF_PASS=0 keeps the step-by-step launches
   if (e && e[0] == '0') return false;
@@ -278,14 +278,8 @@ static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 0 || d.n_flows > kMaxFlows || d.T < 1 ||
       d.T > kPassMaxT || d.B < 1 || d.B > 256)
     return false;
-  int dev = 0, cus = 0, occ = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pass_cm_kernel_of(d), kCmWaves * 64, 0) !=
-          hipSuccess ||
-      occ < 1)
-    return false;
-  return (int64_t)n_tiles(d.N) * d.B <= (int64_t)cus * occ;
+  // (speculative only: its rows may run in resident chunks, pass_launch_rows)
+  return pass_resident_rows(pass_cm_kernel_of(d), kCmWaves * 64, n_tiles(d.N)) >= 1;
 }
 
 }  // namespace nfdpf

@@ -2173,13 +2173,10 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
     ws.wait_ticks = kPassWaitTicks;
     if (const char *e = getenv("NFDPF_PASS_WAIT_US"))  // read per call (tests force a timeout)
       ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
-    const dim3 g(n_tiles(d.N), d.B);
-    hipEvent_t *ev = (hipEvent_t *)d.prof_events;
     const auto kern = pass_cm_kernel_of(d);
-    if (ev)
-      hipExtLaunchKernelGGL(kern, g, dim3(kCmWaves * 64), 0, st, ev[0], ev[1], 0, d, ws);
-    else
-      kern<<<g, kCmWaves * 64, 0, st>>>(d, ws);
+    const int rows = pass_resident_rows(kern, kCmWaves * 64, n_tiles(d.N));
+    NFDPF_REQUIRE(rows >= 1, "nfdpf_filter_pass_tiled: no row of the pass fits on the device");
+    pass_launch_rows(kern, d, ws, kCmWaves * 64, std::min(rows, d.B), st);
     tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, verify_cm, 4);
     return launch_status("nfdpf_filter_pass_tiled");
   }
@@ -2202,13 +2199,12 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   ws.wait_ticks = kPassWaitTicks;
   if (const char *e = getenv("NFDPF_PASS_WAIT_US"))  // read per call (tests force a timeout)
     ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
-  const dim3 g(n_tiles(d.N), d.B);
-  hipEvent_t *ev = (hipEvent_t *)d.prof_events;
   const auto kern = pass_kernel_of(d);
-  if (ev)
-    hipExtLaunchKernelGGL(kern, g, dim3(4 * kTile), 0, st, ev[0], ev[1], 0, d, ws);
-  else
-    kern<<<g, 4 * kTile, 0, st>>>(d, ws);
+  const int rows = pass_resident_rows(kern, 4 * kTile, n_tiles(d.N));
+  // (pass_config_ok: the forced and gated passes have all their rows resident in one launch)
+  NFDPF_REQUIRE(rows >= d.B || (rows >= 1 && mode == kModeSpec),
+                "nfdpf_filter_pass_tiled: the pass's rows do not fit on the device");
+  pass_launch_rows(kern, d, ws, 4 * kTile, std::min(rows, d.B), st);
   tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate ? 2 : verify, 8);
   return launch_status("nfdpf_filter_pass_tiled");
 }

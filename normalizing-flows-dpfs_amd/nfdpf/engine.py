@@ -170,6 +170,7 @@ class FilterEngine:
         # warned once per engine
         self.pass_fallback_reason = None
         self._fallback_warned = False
+        self._gate_resident = False  # the last run's shapes fit the gated pass (all rows resident)
         self._hmapped = None  # ops.HostMapped slots for the speculative pass's flags (lazy)
         self._shared_device = None  # per process group: does another rank use this rank's GPU?
         self.last_gate_pass = False  # the last run was the gated one-launch pass (gates decided in the launch)
@@ -238,8 +239,10 @@ class FilterEngine:
         c = self.cfg
         # (the gated mode is the C2-shaped pass's, tiled_pass_kernel; the no-flow pass -- C1 / C3
         # shapes -- only speculates)
+        # (and every row resident at once: the gated pass's rows wait for the batch's decision;
+        # a speculative pass of more rows runs them in resident chunks)
         return bool(pass_ok and shard.world == 1 and c.resampler == "soft" and not c.force_resample
-                    and c.pass_gate is not False and c.NF_dyn and c.NF_cond)
+                    and c.pass_gate is not False and c.NF_dyn and c.NF_cond and getattr(self, "_gate_resident", False))
 
     def _pass_supported(self, B, N, T, E, split_nets, shard) -> bool:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
@@ -268,8 +271,12 @@ class FilterEngine:
         d.rng_mode, d.force_resample = L.RNG_DEVICE, int(c.force_resample)
         d.n_flows, d.hidden, d.split_nets = c.n_flows, c.hidden, int(split_nets)
         ok = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
-        self.pass_fallback_reason = None if ok else self._shape_limit(B, N)
-        if self.pass_fallback_reason and not self._fallback_warned and os.environ.get("NFDPF_PASS") != "0":
+        self._gate_resident = False
+        if ok and c.NF_dyn and c.NF_cond and not c.force_resample and shard.world == 1:
+            d.pass_gate = 1
+            self._gate_resident = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
+        self.pass_fallback_reason = None if ok else self._shape_limit(B, N, c.force_resample)
+        if self.pass_fallback_reason and not getattr(self, "_fallback_warned", False) and os.environ.get("NFDPF_PASS") != "0":
             import warnings
             warnings.warn(f"nfdpf: the one-launch pass does not cover this shape ({self.pass_fallback_reason}); "
                           f"running the step launches (about half the speed)", RuntimeWarning, stacklevel=3)
@@ -277,10 +284,12 @@ class FilterEngine:
         return ok
 
     @staticmethod
-    def _shape_limit(B, N):
+    def _shape_limit(B, N, all_resident):
         """The one-launch pass's shape limits (csrc/filter_pass.hpp pass_config_ok,
-        filter_pass_cm.hpp pass_cm_config_ok): N <= 1024 (4 tiles of 256 per row), every
-        (row, tile) workgroup resident at once (one per CU), at most 256 rows per launch."""
+        filter_pass_cm.hpp pass_cm_config_ok): N <= 1024 (4 tiles of 256 per row), at most 256
+        rows per pass, and -- for the forced pass (``all_resident``: its rows read each other's
+        particles) -- every (row, tile) workgroup resident at once (one per CU); a speculative
+        pass of more rows runs them in resident chunks."""
         if not torch.cuda.is_available():
             return None
         tiles = -(-N // 256)
@@ -289,7 +298,7 @@ class FilterEngine:
             return f"N={N} > 1024 particles per row"
         if B > 256:
             return f"B={B} > 256 rows per launch"
-        if B * tiles > cus:
+        if all_resident and B * tiles > cus:
             return f"B={B} rows x {tiles} tiles = {B * tiles} workgroups, more than the {cus} CUs hold at once"
         return None
 

@@ -73,7 +73,10 @@ def _run(models, N, enc, start, vel, spec, seed=41, env=None, monkeypatch=None):
 CASES = [(6, 1000, 8, "e2e_c2.npz"), (6, 1000, 8, "e2e_c2w.npz"), (5, 777, 6, "e2e_c2.npz"),
          (5, 777, 6, "e2e_c2w.npz"), (3, 100, 5, "e2e_c2.npz"), (4, 257, 7, "e2e_c2.npz"),
          (4, 257, 7, "e2e_c2w.npz"), (2, 1024, 4, "e2e_c2.npz"), (64, 1000, 50, "bench"),
-         (64, 1000, 50, "e2e_c2w.npz")]
+         (64, 1000, 50, "e2e_c2w.npz"),
+         # more rows than the device holds at once (MI355X: 256 CUs, 64 rows of 4 tiles): the
+         # speculative pass runs them in resident chunks of rows, one launch each
+         (96, 1000, 6, "bench"), (80, 777, 5, "e2e_c2.npz")]
 
 
 @pytest.mark.parametrize("B,N,T,fixture", CASES)
@@ -282,24 +285,29 @@ def test_pass_disabled_by_env(monkeypatch):
 
 
 def test_pass_shape_fallback_is_reported(monkeypatch):
-    """A C2-shaped run beyond the pass's shape limits (here more (row, tile) workgroups than the
-    device's CUs hold at once) runs the step launches and says so: one RuntimeWarning per engine
-    and ``pass_fallback_reason``; NFDPF_PASS=0 (chosen, not a limit) stays quiet."""
+    """A C2-shaped run beyond the pass's shape limits (here N > 1024 particles per row) runs the
+    step launches and says so: one RuntimeWarning per engine and ``pass_fallback_reason``;
+    NFDPF_PASS=0 (chosen, not a limit) stays quiet.  A speculative pass of more rows than the
+    device holds at once is NOT such a limit: its rows run in resident chunks."""
     fx = load("e2e_c2.npz")
     models = _Models(weights(fx), e2e_cfg(fx))
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    B = cus // 4 + 1  # N = 1000: 4 tiles per row
-    enc, start, vel = _inputs(B, 2, seed=5)
+    enc, start, vel = _inputs(2, 2, seed=5)
     with pytest.warns(RuntimeWarning, match="one-launch pass does not cover"):
-        eng, _ = _run(models, 1000, enc, start, vel, spec=True)
+        eng, _ = _run(models, 1100, enc, start, vel, spec=True)
     assert not eng.last_pass and eng.pass_launches == 0
-    assert "workgroups" in eng.pass_fallback_reason
-    monkeypatch.setenv("NFDPF_PASS", "0")
+    assert "1024" in eng.pass_fallback_reason
     import warnings
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    B = cus // 4 + 1  # N = 1000: 4 tiles per row, one row more than resident at once
+    enc, start, vel = _inputs(B, 2, seed=5)
     with warnings.catch_warnings():
         warnings.simplefilter("error", RuntimeWarning)
-        eng2, _ = _run(models, 1000, enc[:2], start[:2], vel[:2], spec=True)
-    assert not eng2.last_pass
+        eng2, _ = _run(models, 1000, enc, start, vel, spec=True)
+        assert eng2.pass_launches >= 1 and eng2.pass_fallback_reason is None
+        assert not eng2._gate_resident  # (the gated pass needs every row resident: not here)
+        monkeypatch.setenv("NFDPF_PASS", "0")
+        eng3, _ = _run(models, 1000, enc[:2], start[:2], vel[:2], spec=True)
+    assert not eng3.last_pass
 
 
 def _philox_offsets(seed, T, B, N, row_base=0):
