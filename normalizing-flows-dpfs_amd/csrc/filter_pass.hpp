@@ -120,9 +120,9 @@ struct PassWs {
   double *eq;   // [T] the epilogue's per-step obs-likelihood terms
   int32_t *eg;  // [T] the epilogue's per-step gates
   uint64_t wait_ticks;  // the bound of every wait (s_memrealtime ticks; kPassWaitTicks)
-  // the first row of this launch: a speculative pass of more rows than the device holds at once
-  // runs as several launches of resident rows (the rows of a speculative pass never wait for
-  // each other), every table indexed by the batch row row0 + the grid's row
+  // the first row of this launch: a speculative or forced pass of more rows than the device
+  // holds at once runs as several launches of resident rows (pass_launch_rows), every table
+  // indexed by the batch row row0 + the grid's row
   int row0;
 };
 
@@ -642,17 +642,22 @@ static int pass_resident_rows(K kern, int threads, int tiles) {
   return (int)((int64_t)cus * occ / tiles);
 }
 
-// Launch `kern` over the pass's rows in chunks of `rows` resident rows (one launch when all fit);
-// the profiling events (if any) bracket the first and the last launch
+// Launch `kern` over the pass's rows in chunks of `rows` resident rows (one launch when all fit),
+// the LAST chunk first: a row reads nothing of another row except, in the forced pass, the next
+// row's slot t - 1 particles at the reference's out-of-range edge (pass_resample) -- which a
+// later chunk has then written in full, every granule tag of it at or past the one waited for.
+// (The gated pass's rows wait for the batch's decision: it is never chunked.)  The profiling
+// events (if any) bracket the first launch and the last.
 template <class K>
 static void pass_launch_rows(K kern, const nfdpf_filter_desc &d, PassWs ws, int threads, int rows,
                              hipStream_t st) {
   hipEvent_t *ev = (hipEvent_t *)d.prof_events;
-  const int tiles = n_tiles(d.N);
-  for (int r0 = 0; r0 < d.B; r0 += rows) {
+  const int tiles = n_tiles(d.N), nch = (d.B + rows - 1) / rows;
+  for (int c = nch - 1; c >= 0; --c) {
+    const int r0 = c * rows;
     ws.row0 = r0;
     const dim3 g(tiles, std::min(rows, d.B - r0));
-    hipEvent_t e0 = ev && r0 == 0 ? ev[0] : nullptr, e1 = ev && r0 + rows >= d.B ? ev[1] : nullptr;
+    hipEvent_t e0 = ev && c == nch - 1 ? ev[0] : nullptr, e1 = ev && c == 0 ? ev[1] : nullptr;
     if (e0 || e1)
       hipExtLaunchKernelGGL(kern, g, dim3(threads), 0, st, e0, e1, 0, d, ws);
     else
@@ -1552,10 +1557,10 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
       d.B < 1 || d.B > 256)  // (the epilogue stages a step's B row sums in LDS)
     return false;
-  // every workgroup resident at once; a speculative pass (no row waits for another) may also
-  // run its rows in resident chunks (pass_launch_rows)
+  // every workgroup resident at once; a speculative or forced pass may also run its rows in
+  // resident chunks (pass_launch_rows), the gated one not (its rows wait for the batch decision)
   const int rows = pass_resident_rows(pass_kernel_of(d), 4 * kTile, n_tiles(d.N));
-  return rows >= d.B || (rows >= 1 && pass_mode_of(d) == kModeSpec);
+  return rows >= d.B || (rows >= 1 && pass_mode_of(d) != kModeGate);
 }
 
 }  // namespace nfdpf

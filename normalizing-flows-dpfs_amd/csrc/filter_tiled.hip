@@ -2201,8 +2201,8 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
     ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
   const auto kern = pass_kernel_of(d);
   const int rows = pass_resident_rows(kern, 4 * kTile, n_tiles(d.N));
-  // (pass_config_ok: the forced and gated passes have all their rows resident in one launch)
-  NFDPF_REQUIRE(rows >= d.B || (rows >= 1 && mode == kModeSpec),
+  // (pass_config_ok: the gated pass has all its rows resident in one launch)
+  NFDPF_REQUIRE(rows >= d.B || (rows >= 1 && mode != kModeGate),
                 "nfdpf_filter_pass_tiled: the pass's rows do not fit on the device");
   pass_launch_rows(kern, d, ws, 4 * kTile, std::min(rows, d.B), st);
   tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate ? 2 : verify, 8);

@@ -275,7 +275,7 @@ class FilterEngine:
         if ok and c.NF_dyn and c.NF_cond and not c.force_resample and shard.world == 1:
             d.pass_gate = 1
             self._gate_resident = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
-        self.pass_fallback_reason = None if ok else self._shape_limit(B, N, c.force_resample)
+        self.pass_fallback_reason = None if ok else self._shape_limit(B, N)
         if self.pass_fallback_reason and not getattr(self, "_fallback_warned", False) and os.environ.get("NFDPF_PASS") != "0":
             import warnings
             warnings.warn(f"nfdpf: the one-launch pass does not cover this shape ({self.pass_fallback_reason}); "
@@ -284,12 +284,11 @@ class FilterEngine:
         return ok
 
     @staticmethod
-    def _shape_limit(B, N, all_resident):
+    def _shape_limit(B, N):
         """The one-launch pass's shape limits (csrc/filter_pass.hpp pass_config_ok,
         filter_pass_cm.hpp pass_cm_config_ok): N <= 1024 (4 tiles of 256 per row), at most 256
-        rows per pass, and -- for the forced pass (``all_resident``: its rows read each other's
-        particles) -- every (row, tile) workgroup resident at once (one per CU); a speculative
-        pass of more rows runs them in resident chunks."""
+        rows per pass (a speculative or forced pass of more rows than the device holds at once
+        runs them in resident chunks; the gated pass is then not used)."""
         if not torch.cuda.is_available():
             return None
         tiles = -(-N // 256)
@@ -298,8 +297,8 @@ class FilterEngine:
             return f"N={N} > 1024 particles per row"
         if B > 256:
             return f"B={B} > 256 rows per launch"
-        if all_resident and B * tiles > cus:
-            return f"B={B} rows x {tiles} tiles = {B * tiles} workgroups, more than the {cus} CUs hold at once"
+        if tiles > cus:
+            return f"one row's {tiles} workgroups exceed the {cus} CUs"
         return None
 
     @staticmethod

@@ -406,7 +406,8 @@ def _soft_indices32(soft32):
     return soft64
 
 
-@pytest.mark.parametrize("B,N,T", [(6, 1000, 8), (4, 257, 6), (3, 100, 5), (64, 1000, 50)])
+# (80 rows of N = 1000: more than the device holds at once -- resident chunks, the last first)
+@pytest.mark.parametrize("B,N,T", [(6, 1000, 8), (4, 257, 6), (3, 100, 5), (64, 1000, 50), (80, 1000, 6)])
 def test_forced_pass_every_step_vs_oracle(B, N, T, monkeypatch):
     """--force-resample inside the one-launch pass, every step against the oracle's step
     (oracle.filter_step = DPFs.py:160-192 with resamplers.py:20-60) started from the PASS's own
