@@ -446,8 +446,9 @@ NFDPF_API int64_t nfdpf_filter_desc_size(void);
  * measurement, device RNG, N <= 1024, n_flows <= 2, the soft resampler when forced (every step
  * then resamples inside the launch and there is no gate to verify), B <= 256, and a (tiles, B)
  * grid of 1024-thread workgroups that is resident on the current device all at once -- except a
- * speculative or forced pass, which runs more rows than fit as consecutive launches of resident
- * rows, the last rows first (e.g. 96 rows of N = 1000 on 256 CUs: rows 64-95, then 0-63).
+ * speculative or forced C2-shaped pass, which runs more rows than fit as consecutive launches
+ * of resident rows, the last rows first (e.g. 96 rows of N = 1000 on 256 CUs: rows 64-95, then
+ * 0-63); the C3-shaped pass needs all its rows resident (above that its step launches are faster).
  * Descriptor fields as nfdpf_filter_step_tiled at t = 0, except:
  *   dyn_params / cond_params: the PASS layout (nfdpf.pack.pass_flow_tensors: the pair layout with
  *   the tanh algebra folded into the weights -- W1, b1 x c, W2 x -2c, b2 -> c (b2 + rowsum W2),
