@@ -166,8 +166,7 @@ class FilterEngine:
         # process or kernel held CUs) turns the pass off for this engine; the step launches rerun
         self.pass_disabled = False
         # why the last run's shapes kept a pass-family configuration off the one-launch pass
-        # (N above 1024, more (row, tile) workgroups than the device holds at once), else None;
-        # warned once per engine
+        # (N above 1024, more than 256 rows), else None; warned once per engine
         self.pass_fallback_reason = None
         self._fallback_warned = False
         self._gate_resident = False  # the last run's shapes fit the gated pass (all rows resident)
@@ -242,7 +241,8 @@ class FilterEngine:
         # (and every row resident at once: the gated pass's rows wait for the batch's decision;
         # a speculative pass of more rows runs them in resident chunks)
         return bool(pass_ok and shard.world == 1 and c.resampler == "soft" and not c.force_resample
-                    and c.pass_gate is not False and c.NF_dyn and c.NF_cond and getattr(self, "_gate_resident", False))
+                    and c.pass_gate is not False and c.NF_dyn and c.NF_cond
+                    and getattr(self, "_gate_resident", False))
 
     def _pass_supported(self, B, N, T, E, split_nets, shard) -> bool:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
@@ -276,7 +276,8 @@ class FilterEngine:
             d.pass_gate = 1
             self._gate_resident = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
         self.pass_fallback_reason = None if ok else self._shape_limit(B, N)
-        if self.pass_fallback_reason and not getattr(self, "_fallback_warned", False) and os.environ.get("NFDPF_PASS") != "0":
+        warn = self.pass_fallback_reason and not getattr(self, "_fallback_warned", False)
+        if warn and os.environ.get("NFDPF_PASS") != "0":
             import warnings
             warnings.warn(f"nfdpf: the one-launch pass does not cover this shape ({self.pass_fallback_reason}); "
                           f"running the step launches (about half the speed)", RuntimeWarning, stacklevel=3)
