@@ -1447,12 +1447,23 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
 // tiled_pass_cm_kernel)
 __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_filter_desc d, PassWs ws, int gates,
                                                                  int ept) {
-  __shared__ float lw_l[256];
+  __shared__ float lw_l[256], inv_l[256];
   __shared__ int last;
   const int k = blockIdx.x, l = threadIdx.x, T = d.T, B = d.B, tiles = n_tiles(d.N), ent = tiles * ept;
+  // gates == 1: step k's gate input (k = 0: ess_all, else the pass's ess_out[k - 1]), each row's
+  // partials loaded beside its fin entries (one memory round trip for both)
+  const double *parts = gates != 1 ? nullptr
+                        : k == 0   ? reinterpret_cast<const double *>(d.ess_all)
+                                   : reinterpret_cast<const double *>(d.ess_out) + (int64_t)(k - 1) * B * tiles * kSm;
   for (int b = l; b < B; b += 64) {
     const int64_t bt = (int64_t)b * T + k;
     double px = 0, py = 0, sw = 0;
+    double gp[kPassMaxTiles * kSm];
+    if (gates == 1) {
+#pragma unroll
+      for (int q = 0; q < kPassMaxTiles * kSm; ++q)
+        if (q < tiles * kSm) gp[q] = parts[(int64_t)b * tiles * kSm + q];
+    }
     // every entry's loads in flight at once (ent <= kPassMaxTiles * 8 = 32), then the adds in
     // entry order: one memory round trip per row instead of one per 8 entries
     double a[kPassMaxTiles * 8][3];
@@ -1477,16 +1488,15 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     d.pred[2 * bt + 1] = (float)py;
     d.lw_sum[bt] = (float)sw;
     lw_l[b] = (float)sw;
-  }
-  int fired = 0;
-  if (gates == 1) {
-    const double *parts = k == 0 ? reinterpret_cast<const double *>(d.ess_all)
-                                 : reinterpret_cast<const double *>(d.ess_out) + (int64_t)(k - 1) * B * tiles * kSm;
-    const float s =
-        cascade_row_sum([&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, d.N, k > 0); }, B);
-    fired = (s / (float)B) < 0.5f * (float)d.N ? 1 : 0;
+    // the row's 1 / sum p^2 (row_inv_ess's arithmetic, row_inv_ess_t)
+    if (gates == 1) inv_l[b] = row_inv_ess_t<kPassMaxTiles>([&](int q) { return gp[q]; }, tiles, d.N, k > 0);
   }
   __syncthreads();
+  int fired = 0;
+  if (gates == 1) {  // tiled_gate_batch_kernel's cascade over the rows' terms
+    const float s = cascade_row_sum([&](int r) { return inv_l[r]; }, B);
+    fired = (s / (float)B) < 0.5f * (float)d.N ? 1 : 0;
+  }
   if (l == 0) {
     double tot = 0.0;
     for (int b = 0; b < B; ++b) tot += (double)lw_l[b];
