@@ -99,12 +99,42 @@ def synthetic_disk(B, T, seed, E):
             torch.from_numpy(enc))
 
 
+def cgroup_cpus():
+    """CPUs this process's cgroup may use (cgroup v2 cpu.max / v1 cfs quota), None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads():
+    """The CPU baseline's thread count: NFDPF_CPU_THREADS if set, else every CPU of the process's
+    affinity mask that its cgroup quota lets run at once (on the GPU box the mask lists the whole
+    machine while the quota is the box's share: threads beyond the quota only time-slice)."""
+    env = os.environ.get("NFDPF_CPU_THREADS")
+    if env:
+        return int(env)
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpus()
+    return min(n, q) if q else n
+
+
 def cpu_baseline(cfg_name, seconds_budget=25.0, force=False):
     """The oracle (PyTorch-CPU restatement, timing-faithful: O(N^2) marker matching, FP64
     Sinkhorn, torch.cat history) on the host cores, on a bounded sample of the workload."""
     from oracle import dpf_oracle as O
     flags, B, N, T, _, _ = CONFIGS[cfg_name]
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = cpu_threads()
     torch.set_num_threads(cores)
     torch.manual_seed(2)
     a = make_args(flags, B, N, T, {})
@@ -152,7 +182,9 @@ def cpu_baseline(cfg_name, seconds_budget=25.0, force=False):
     ot_note = ""
     if flags["resampler_type"] == "ot":
         ot_note = f", OT resampling in {len(ot_calls) // (reps + 1)} of {Ts} steps"
+    q = cgroup_cpus()
     return {"value": Bs * N * Ts / med, "unit": "particle-steps/s", "cores": cores, "kind": "port",
+            "cpu_affinity": len(os.sched_getaffinity(0)), "cgroup_cpus": q,
             "sample": f"oracle filtering B={Bs} N={N} T={Ts} ({'forced' if force else 'ESS-gated'} resampling"
                       f"{ot_note}), median of {reps} after 1 "
                       f"warm-up; host {platform.processor() or platform.machine()}"}
@@ -282,6 +314,10 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
     # auto (engine.FilterEngine.run): speculative gates when sharded, for OT at any world size
     # unless the previous pass resampled, and wherever the whole pass runs as one launch
     spec = eng.speculates(shard)  # the engine's own decision for the next pass (engine._decide_spec)
+    # one GPU, a gated or forced one-launch pass (gates decided inside the launch): captured with
+    # finish=False too, so that each replay's fault flags are checked (finish_pending) -- a replay
+    # whose row hand-offs timed out is rerun, never taken for a result
+    decided = world == 1 and eng.last_pass and not spec
     if args.graph and ((fcfg.resampler == "soft" and world == 1) or spec):
         # the pass has no host synchronisation in this mode: capture it once, replay per step
         # (every launch of every time step runs on each replay; only the Python launch path goes).
@@ -295,16 +331,16 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
         # runs: the host round trip no longer leaves the GPU idle between passes.  A fired gate
         # reruns pass k (gated) before the next replay; the last pass is verified inside the
         # timing.
-        pipelined = spec and world == 1
+        pipelined = (spec or decided) and world == 1
         graphs, caps, pends = [], [], []
         try:
             for _ in range(2 if pipelined else 1):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    res = eng.run(enc, start, vel_in, shard=shard, finish=not spec)
+                    res = eng.run(enc, start, vel_in, shard=shard, finish=not (spec or decided))
                 graphs.append(g)
                 caps.append(res)
-                pends.append(eng.take_pending() if spec else None)
+                pends.append(eng.take_pending() if (spec or decided) else None)
             for g in graphs:
                 g.replay()
             torch.cuda.synchronize()
@@ -316,7 +352,7 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
 
         def step_graph():
             graph.replay()
-            if spec and not eng.finish_pending(pends[0]):
+            if pends[0] is not None and not eng.finish_pending(pends[0]):
                 return eng.run(enc, start, vel_in, shard=shard, speculate=False)
             return caps[0]
 

@@ -174,6 +174,7 @@ class FilterEngine:
         self._shared_device = None  # per process group: does another rank use this rank's GPU?
         self.last_gate_pass = False  # the last run was the gated one-launch pass (gates decided in the launch)
         self.last_gates = None       # one shard's one-launch pass: its T gates (decided, or verified) [T] int32
+        self.last_verify = None      # finish_pending's outcome: "ok", "fired" (a gate miss) or "fault"
 
     def __getstate__(self):
         # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
@@ -207,7 +208,9 @@ class FilterEngine:
         3: 2.09e9 vs 2.13e9 particle-steps/s).  ``consume``: count this pass
         against the back-off (run() only).  A pass captured into a graph (``finish`` with a
         capturing stream) cannot verify its gates on the host: auto mode does not speculate
-        there (run(finish=False) does, leaving finish_pending to the caller)."""
+        there (run(finish=False) does, leaving finish_pending to the caller); a gated or forced
+        one-launch pass captured there leaves its fault flags in the pending state instead
+        (take_pending / finish_pending after each replay)."""
         c = self.cfg
         tiled = c.kernel == "tiled"
         auto = speculate is None and c.speculate_gate is None
@@ -408,6 +411,7 @@ class FilterEngine:
         gate_pass = gate_ok and not spec
         use_pass = pass_ok and (spec or c.force_resample or gate_pass)
         self.last_gate_pass = gate_pass
+        self.last_gates = None  # (set below by a one-shard one-launch pass; never a previous run's)
 
         f32 = dict(device=dev, dtype=torch.float32)
         hx = torch.empty((B, T, N, 2), **f32)
@@ -521,7 +525,8 @@ class FilterEngine:
 
         self.last_pass = use_pass
         pass_out = None  # one shard: the pass epilogue's (gates, flags, obs)
-        flags_host = None  # ... the flags mapped from host memory (speculative pass)
+        flags_host = None  # ... the flags mapped from host memory
+        flags_lease = None  # ... and the lease of their slot when a captured graph holds it
         if use_pass:
             # the whole T-step pass as ONE persistent launch (nfdpf_filter_pass_tiled): every gate
             # taken as off, step t's softmax partials into ess_hist[t + 1] for the verification
@@ -539,14 +544,17 @@ class FilterEngine:
                             torch.empty((), **f32))
                 self.last_gates = pass_out[0]  # the T gates: decided in the launch, or verified
                 d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
-                if spec:
-                    # the speculative pass's {fired, faults} straight into pinned, device-mapped host
-                    # memory (ops.HostMapped): read without a copy launch once the pass is complete
-                    capturing = torch.cuda.is_current_stream_capturing()
+                capturing = torch.cuda.is_current_stream_capturing()
+                if spec or capturing or not finish:
+                    # the pass's {fired, faults, done} straight into pinned, device-mapped host memory
+                    # (ops.HostMapped): read without a copy launch once the pass is complete -- the
+                    # speculative pass's verification, and the fault check of a gated / forced pass
+                    # that is captured (checked after each replay: finish_pending) or pipelined
                     if self._hmapped is None and not capturing:
                         self._hmapped = ops.HostMapped()
-                    if self._hmapped is not None:
-                        fdev, flags_host = self._hmapped.take(reserve=capturing)
+                    got = self._hmapped.take(reserve=capturing) if self._hmapped is not None else None
+                    if got is not None:  # (None: every slot reserved -- the flags stay in device memory)
+                        fdev, flags_host, flags_lease = got
                         flags_host[2] = 0  # armed: the epilogue sets it last (arm_flags before a replay)
                         d.pass_flags = fdev
             d.prof_events, d.prof_front = None, 0
@@ -679,9 +687,16 @@ class FilterEngine:
         check_split = tiled and handoffs and not capturing
         if use_pass and not spec:
             # a forced or gated pass: one shard's epilogue read the fault counter and reduced the
-            # obs-likelihood (one host read here, none while capturing a graph); sharded, every
-            # rank's count is summed so that all ranks fall back together
+            # obs-likelihood (one host read here); sharded, every rank's count is summed so that all
+            # ranks fall back together.  Captured in a graph, or run(finish=False): the flags are
+            # left in the pending state (take_pending / finish_pending after each replay: a replay
+            # whose hand-offs timed out must not pass for a result), nothing is read here.
             check_split = False
+            if pass_out is not None and (capturing or not finish):
+                res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, pass_out[2], pred, fired)
+                verify = [pass_out[1] if flags_host is None else None, pass_out[2], flags_host, flags_lease]
+                self._pending = (None, None, shard, N, res, None, verify, True, True)
+                return res
             if not capturing:
                 if pass_out is not None:
                     n_fired, faults = pass_out[1].tolist()[:2]
@@ -712,10 +727,10 @@ class FilterEngine:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             verify = None
             if verify_dev:
-                verify = [pass_out[1] if flags_host is None else None, pass_out[2], flags_host] \
-                    if pass_out is not None else list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None]
+                verify = [pass_out[1] if flags_host is None else None, pass_out[2], flags_host, flags_lease] \
+                    if pass_out is not None else list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None, None]
                 check_split = False
-            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass)
+            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass, False)
             if not finish:
                 return res  # the caller verifies (finish_pending, e.g. after each graph replay)
             ok = self.finish_pending()
@@ -724,6 +739,10 @@ class FilterEngine:
             if ok:
                 self._spec_backoff = 0
                 return res
+            if self.last_verify == "fault":
+                # the pass's grid was not resident (not a gate miss): the one-launch pass is now off
+                # for this engine and the step launches rerun it; the speculation state is left alone
+                return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, speculate=speculate)
             # a gate fired: the pass again, gated (one GPU, the one-launch pass: the gates decided in
             # the launch; the next passes stay gated while gates keep firing) or with the per-step
             # exchange
@@ -751,7 +770,7 @@ class FilterEngine:
         if verify is None or verify[0] is None:  # (flags already mapped from host memory)
             return
         if verify[2] is None:
-            verify[2] = torch.empty(2, dtype=torch.int32, pin_memory=True)
+            verify[2] = torch.empty(verify[0].shape, dtype=verify[0].dtype, pin_memory=True)
         verify[2].copy_(verify[0], non_blocking=True)
 
     @staticmethod
@@ -765,15 +784,29 @@ class FilterEngine:
     @staticmethod
     def wait_flags(pending, timeout_s: float = 60.0) -> bool:
         """Wait on the host, with no stream operation, until the pass's epilogue has written its
-        flags into host memory (their completion word); False where the flags are not mapped."""
+        flags into host memory (their completion word); False where the flags are not mapped.
+        Spins with a yield for the first millisecond, then sleeps 50 us between reads; every 10 ms
+        it asks whether the current stream is idle -- an idle stream with the word still unset
+        means the pass never ran (a launch or stream error): raised at once, not after the bound."""
         verify = pending[6]
         if verify is None or verify[0] is not None:
             return False
         view = verify[2]
         t0 = time.perf_counter()
+        last_q = t0
         while int(view[2]) == 0:
-            if time.perf_counter() - t0 > timeout_s:
+            now = time.perf_counter()
+            if now - t0 > timeout_s:
                 raise L.NfdpfError(f"the one-launch pass's flags did not arrive within {timeout_s} s")
+            if now - t0 < 1e-3:
+                os.sched_yield()
+                continue
+            time.sleep(50e-6)
+            if now - last_q > 10e-3:
+                last_q = now
+                if torch.cuda.current_stream().query() and int(view[2]) == 0:
+                    raise L.NfdpfError("the one-launch pass's stream is idle but its flags were never written "
+                                       "(the pass or its epilogue did not run)")
         return True
 
     def take_pending(self):
@@ -788,11 +821,18 @@ class FilterEngine:
         partials over the shards (one all-gather), evaluate all T gates
         (nfdpf_ess_gate_tiled_batch) and, if none fired, reduce the obs-likelihood into the
         result.  False: some gate fired -- the pass is not the reference's and must be rerun
-        without speculation (run(..., speculate=False)).
+        without speculation (run(..., speculate=False)) -- or the pass's row hand-offs timed out
+        (its grid was not resident; the one-launch pass is then off for this engine and a rerun
+        takes the step launches).  ``self.last_verify`` tells the two apart: "ok", "fired" or
+        "fault".  A gated or forced one-launch pass (its gates decided inside the launch) that was
+        captured or run with finish=False only has its fault flags checked here: "ok" or "fault".
         ``synced``: the pass's flags were staged (stage_flags) and an event recorded after that
         copy has completed: they are read from pinned host memory with no stream operation, so a
         later pass already queued behind it keeps running (pipelined passes, bench.py)."""
-        parts, tot, shard, N, res, split_dev, verify, was_pass = pending if pending is not None else self._pending
+        pend = pending if pending is not None else self._pending
+        parts, tot, shard, N, res, split_dev, verify, was_pass = pend[:8]
+        decided = len(pend) > 8 and pend[8]  # the gates were decided inside the launch
+        self.last_verify = "ok"
         if verify is not None:  # the device verification's flags: the one host synchronisation
             if verify[0] is None:  # mapped from host memory: complete once the stream is
                 if not synced:
@@ -807,8 +847,10 @@ class FilterEngine:
                     raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "
                                        f"(outputs invalid)")
                 self._pass_fault(faults)  # the one-launch pass's grid was not resident: rerun step by step
+                self.last_verify = "fault"
                 return False
-            if fired:
+            if fired and not decided:
+                self.last_verify = "fired"
                 return False
             res.obs_likelihood = verify[1]
             return True
@@ -817,6 +859,7 @@ class FilterEngine:
                 faults = self._faults_all(shard, split_dev)
                 if faults:
                     self._pass_fault(faults)
+                    self.last_verify = "fault"
                     return False
             else:
                 L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
@@ -826,6 +869,7 @@ class FilterEngine:
             dist.all_reduce(tot, group=shard.group)
         gates = ops.ess_gate_tiled_batch(parts, N, 0, False)
         if bool(gates.any()):
+            self.last_verify = "fired"
             return False
         res.obs_likelihood = (tot / (shard.B_global * N)).sum().float()
         return True

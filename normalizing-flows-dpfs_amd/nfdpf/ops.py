@@ -593,21 +593,49 @@ class HostMapped:
         self._next = 0
 
     def take(self, reserve: bool = False):
-        """-> (device address, int32 numpy view of the slot)."""
+        """-> (device address, int32 numpy view of the slot, lease).  ``reserve``: the slot stays
+        out of the round robin until the returned lease is released (``lease.release()``, or
+        when the lease object is dropped -- e.g. with the pending state of the captured pass that
+        holds it); lease is None for an unreserved slot.  None when every slot is reserved (the
+        caller then keeps its flags in device memory)."""
         if not self._free:
-            raise L.NfdpfError("HostMapped: every slot is reserved by a captured graph")
+            return None
         k = self._free[self._next % len(self._free)]
+        lease = None
         if reserve:
             self._free.remove(k)
+            lease = _SlotLease(self, k)
         else:
             self._next += 1
-        return self._dev + k * self.slot_bytes, self._view[k]
+        return self._dev + k * self.slot_bytes, self._view[k], lease
+
+    def _release(self, k: int):
+        if k not in self._free:
+            self._free.append(k)
 
     def __del__(self):
         try:
             if getattr(self, "_host", None):
                 lib().nfdpf_host_mapped_free(self._host)
                 self._host = None
+        except Exception:  # interpreter shutdown
+            pass
+
+
+class _SlotLease:
+    """A reserved HostMapped slot; returned to its pool on release() or when dropped."""
+
+    def __init__(self, pool: HostMapped, k: int):
+        self._pool, self.k = pool, k
+
+    def release(self):
+        pool, self._pool = self._pool, None
+        if pool is not None:
+            pool._release(self.k)
+
+    def __del__(self):
+        try:
+            self.release()
         except Exception:  # interpreter shutdown
             pass
 

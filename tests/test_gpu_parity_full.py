@@ -308,6 +308,30 @@ def test_fullsize_ot_direct(name):
         assert torch.equal(idx.cpu(), ident)
 
 
+@pytest.mark.timeout(120)
+def test_ot_stop_at_c4_share():
+    """One Sinkhorn call at a C4 rank's share, 32 rows x N = 4000 (BASELINE configs[3]: B = 256
+    over 8 GPUs): the reference's stop rule ends the loop when ANY row of the batch has converged
+    (resamplers.py:126-129), so it is pinned at the batch the ranks actually run -- iteration
+    count exact, x' against the oracle's FP64 transport (tests/golden/ot_c4_share.npz, written by
+    tests/golden/gen_ot_share.py; the input is regenerated from its seed)."""
+    import sys
+    from nfdpf import ops
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from gen_ot_share import ot_share_input
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ot_c4_share.npz"))
+    x, w = ot_share_input(int(fx["seed"]))
+    xo, wo, idx, it = ops.ot_resample(torch.from_numpy(x).to(DEV), torch.from_numpy(w).to(DEV))
+    xr = torch.from_numpy(fx["xr"]).double()
+    e = (xo.cpu().double() - xr).abs()
+    rel = float((e / xr.abs().clamp_min(1.0)).max())
+    _table(f"C4 share OT (B={x.shape[0]}, N={x.shape[1]}): iterations {int(it.item())} (oracle {int(fx['iters'])}), "
+           f"max |x'| {float(xr.abs().max()):.1f}, max abs err {float(e.max()):.2e}, rel {rel:.2e}")
+    assert int(it.item()) == int(fx["iters"])
+    assert rel <= 5e-5
+    assert torch.all(wo.cpu() == 1.0 / x.shape[1])
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", list(F.CASES))
 def test_fullsize_free_running(name):
