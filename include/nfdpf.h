@@ -414,6 +414,11 @@ typedef struct nfdpf_filter_desc {
                                last with a system-scope release (a completion word: host-mapped
                                flags can be waited on without a stream operation)} */
   float *pass_obs;          /* optional [1] out: the obs-likelihood sum_t mean_{b,n} logw (DPFs.py:191) */
+  int32_t meas_mfma;        /* 1 = meas_params is the CRNVP measurement's MFMA fragment blob (encoder
+                               included, pe_params unused by the measurement; nfdpf.pack.
+                               crnvp_mfma_tensors, csrc/crnvp_mfma.hpp; n_flows <= 2): the features-
+                               by-particles layout of the f32-MFMA measurement, read by the no-flow
+                               one-launch pass (tiled_pass_cm_kernel); 0 = the pair layout above */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);

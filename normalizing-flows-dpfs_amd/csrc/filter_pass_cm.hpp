@@ -31,26 +31,21 @@
 //
 // Every wait is bounded (pass_spin: 200 ms, the workspace's abort word), as in filter_pass.hpp.
 
+#include "crnvp_mfma.hpp"
+
 namespace nfdpf {
 
 constexpr int kCmWaves = 8;  // 512 threads: two waves (two steps in flight) per particle group
-// experiment knob: the measurement's weights staged in LDS once per launch (ds_read broadcasts)
-// instead of streamed through the scalar cache every step
-#ifndef NFDPF_CM_STAGE
-#define NFDPF_CM_STAGE 0
-#endif
+constexpr int kCmMfmaFlows = 2;  // the MFMA measurement's LDS blob holds up to 2 flows (DPFs.py:46: n_sequence 2)
 
 struct PassCmLds {
   float xr[2][4][64][2];     // x_t by parity of t: the group's other wave reads it for step t + 1
   float nb[2][5][kTile];     // slot t's hand-over by parity: lr, raw lik, prior, x0, x1
-  float encq[kCmWaves][kE];  // each wave's copy of its step's frame encoding (crnvp_lik's encv)
+  alignas(16) float encq[kCmWaves][kE];  // each wave's copy of its step's frame encoding (crnvp_lik's encv)
   uint32_t rowc[kPassMaxTiles * 4 * kGC];
   RowNorm rn[2];
   int xf[4];                 // x_t of group g written (t + 1)
   int fR;                    // slot t's row normaliser in rn[t & 1] (t + 1)
-#if NFDPF_CM_STAGE
-  alignas(16) float wst[kCrnvpPe + kMaxFlows * kCrnvpFlow];  // [encoder | flows]
-#endif
 };
 
 // the row normaliser of slot s from its C(s) granules (tiles x 4 groups, each {max u, sum e,
@@ -133,21 +128,26 @@ __device__ __forceinline__ float pass_cm_norm(const nfdpf_filter_desc &d, const 
   return lp;
 }
 
-template <int MEAS>
+// MF (CRNVP with d.meas_mfma): the measurement on f32 MFMA (crnvp_mfma.hpp), 64 particles per
+// wave, its fragment blob staged in LDS once per launch; else crnvp_lik per lane (scalar-cache
+// weights, VALU)
+template <int MEAS, bool MF = false>
 __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const nfdpf_filter_desc d, PassWs ws) {
   static_assert(MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_COS || MEAS == NFDPF_MEAS_GAUSSIAN,
                 "the no-flow pass: the CRNVP, cosine or gaussian measurement");
+  static_assert(!MF || MEAS == NFDPF_MEAS_CRNVP, "MFMA: the CRNVP measurement");
   constexpr bool SHIFT = meas_shifted<MEAS>();  // CRNVP / gaussian: lik - the row max (model/models.py:276)
   __shared__ PassCmLds L;
+  __shared__ f4v wfr[MF ? crnvp_mfma_floats(kCmMfmaFlows) / 4 : 1];  // MF: the fragment blob
   int b, tile;
   pass_tile_row(b, tile);
   const uint32_t tag0 = __hip_atomic_load(&ws.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 12;
   if (threadIdx.x < 4) L.xf[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.fR = 0;
-#if NFDPF_CM_STAGE
-  for (int q = threadIdx.x; q < kCrnvpPe; q += blockDim.x) L.wst[q] = d.pe_params[q];
-  for (int q = threadIdx.x; q < d.n_flows * kCrnvpFlow; q += blockDim.x) L.wst[kCrnvpPe + q] = d.meas_params[q];
-#endif
+  if constexpr (MF) {  // (16-B aligned blob of whole float4s: checked on the host)
+    const f4v *src = reinterpret_cast<const f4v *>(d.meas_params);
+    for (int q = threadIdx.x; q < crnvp_mfma_floats(d.n_flows) / 4; q += blockDim.x) wfr[q] = src[q];
+  }
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = w & 3, k = w >> 2, slot = g * 64 + lane, N = d.N, tiles = n_tiles(N);
   const int i = tile * kTile + slot;
@@ -196,14 +196,13 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
       const float ve = lane < kE ? d.enc[((int64_t)b * d.T + t) * d.E + lane] : 0.f;
       vinv = 1.0 / fmax(sqrt(wave_sum((double)ve * ve)), 1e-12);
     }
-    if (valid) {
+    if constexpr (MF) {  // the whole wave: its 64 particles x_t are in xr[par][g]
+      const float r = crnvp_lik_mfma(reinterpret_cast<const float *>(wfr), d.n_flows, d.meas_prior_std, L.encq[w],
+                                     &L.xr[par][g][0][0]);
+      if (valid) raw = r;
+    } else if (valid) {
       if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
-#if NFDPF_CM_STAGE
-        const float *wl = L.wst;
-        raw = crnvp_lik(wl, wl + kCrnvpPe, d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
-#else
         raw = crnvp_lik(wptr(d.pe_params), wptr(d.meas_params), d.n_flows, d.meas_prior_std, L.encq[w], x0, x1);
-#endif
       } else if constexpr (MEAS == NFDPF_MEAS_COS) {  // model/models.py:206-219 (measure<COS>'s arithmetic)
         double ss, dot;
         encode_dot<kE>(wptr(d.pe_params), x0, x1, L.encq[w], ss, dot);
@@ -263,6 +262,7 @@ typedef void (*pass_cm_kernel_t)(const nfdpf_filter_desc, PassWs);
 static pass_cm_kernel_t pass_cm_kernel_of(const nfdpf_filter_desc &d) {
   return d.measurement == NFDPF_MEAS_COS        ? tiled_pass_cm_kernel<NFDPF_MEAS_COS>
          : d.measurement == NFDPF_MEAS_GAUSSIAN ? tiled_pass_cm_kernel<NFDPF_MEAS_GAUSSIAN>
+         : d.meas_mfma                          ? tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP, true>
                                                 : tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>;
 }
 
@@ -275,6 +275,7 @@ static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
       (d.measurement != NFDPF_MEAS_CRNVP && d.measurement != NFDPF_MEAS_COS && d.measurement != NFDPF_MEAS_GAUSSIAN))
     return false;
   if (d.rng_mode != NFDPF_RNG_DEVICE || d.phase != 0 || d.E != kE || d.force_resample || d.pass_gate) return false;
+  if (d.meas_mfma && (d.measurement != NFDPF_MEAS_CRNVP || d.n_flows > kCmMfmaFlows)) return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 0 || d.n_flows > kMaxFlows || d.T < 1 ||
       d.T > kPassMaxT || d.B < 1 || d.B > 256)
     return false;

@@ -233,6 +233,7 @@ extern "C" int nfdpf_filter_step(const nfdpf_filter_desc *dp, void *stream) {
                 "nfdpf_filter_step: bad sizes (B=%d N=%d T=%d t=%d); N >= 2 (std needs N-1)",
                 d.B, d.N, d.T, d.t);
   NFDPF_REQUIRE(d.phase >= 0 && d.phase <= 2, "nfdpf_filter_step: bad phase");
+  NFDPF_REQUIRE(!d.meas_mfma, "nfdpf_filter_step: the MFMA fragment blob (meas_mfma) is for the tiled launches");
   NFDPF_REQUIRE(d.n_flows >= 0 && d.n_flows <= kMaxFlows, "nfdpf_filter_step: n_flows <= %d",
                 kMaxFlows);
   NFDPF_REQUIRE(d.hidden == kH, "nfdpf_filter_step: FCNN hidden width must be %d", kH);

@@ -31,6 +31,7 @@ __device__ unsigned long long g_qtrace[1024][16][16];
 #endif
 
 #include "split.hpp"
+#include "crnvp_mfma.hpp"
 
 // front + dyn in one launch (tiled_fdyn_kernel) for rows up to this length (LDS)
 constexpr int kMergedMaxN_ = 4096;
@@ -1129,12 +1130,19 @@ __device__ __forceinline__ void store_softmax_fin(float u, bool valid, double *s
 // STAGE (CRNVP, use_stage, opt-in): the measurement's encoder and flow weights copied into LDS
 // once per workgroup and read from there (ds_read) instead of streamed through the scalar cache
 // (26 KB, more than it holds).  Measured slower: not the default.
+// MV (CRNVP): 0 = the measurement per lane with its weights through the scalar cache, 1 = the
+// same with the weights staged in LDS (STAGE), 2 = on f32 MFMA, 64 particles per wave with the
+// fragment blob (d.meas_mfma, csrc/crnvp_mfma.hpp) staged in LDS -- the step launch of the C3
+// shape when a gate fires (the no-flow pass reruns step by step with the Sinkhorn)
 constexpr int kCrnvpPe = pe_size(kE);                                  // encoder floats
 constexpr int kCrnvpFlow = 2 * 2 * net_size<kE / 2, kH>(kE);           // floats per flow
-template <bool NFD, bool NFC, int MEAS, bool STAGE = false>
+template <bool NFD, bool NFC, int MEAS, int MV = 0>
 __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_desc d, TiledWs ws) {
+  constexpr bool STAGE = MV == 1, MF = MV == 2;
+  static_assert(!MF || (MEAS == NFDPF_MEAS_CRNVP && !NFC), "MFMA measurement: CRNVP, bootstrap or nf_dyn proposal");
   __shared__ StepShared L;
-  extern __shared__ float4 wstage[];  // STAGE: [encoder | flows] weights
+  extern __shared__ float4 wstage[];  // STAGE: [encoder | flows] weights; MF: the fragment blob
+  __shared__ float xw[MF ? kTile : 1][2];  // MF: the proposals, per wave, for its MFMA measurement
   TRACE(2, 0)
   const int tiles = n_tiles(d.N);
   int b, tile;
@@ -1150,6 +1158,10 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
     const int nmp4 = d.n_flows * kCrnvpFlow / 4;
     for (int k = threadIdx.x; k < kCrnvpPe / 4; k += kTile) wstage[k] = pe4[k];
     for (int k = threadIdx.x; k < nmp4; k += kTile) wstage[kCrnvpPe / 4 + k] = mp4[k];
+  }
+  if constexpr (MF) {  // 16-B aligned blob of whole float4s (checked on the host)
+    const float4 *mp4 = reinterpret_cast<const float4 *>(d.meas_params);
+    for (int k = threadIdx.x; k < crnvp_mfma_floats(d.n_flows) / 4; k += kTile) wstage[k] = mp4[k];
   }
   if (valid) {  // issued before the row prologue so they overlap it
     in = load_prop_in<NFD>(S, i);
@@ -1172,7 +1184,24 @@ __global__ __launch_bounds__(kTile) void tiled_prop_kernel(const nfdpf_filter_de
     finish_prev(d, ws, b, tile, i, true, i < d.N ? load_prev_in(row_slot(d, b, d.t - 1), i) : PrevIn{}, L.d);
   TRACE(2, 1)
   float lk = -INFINITY, u = 0.f;
-  if (valid) {
+  if constexpr (MF) {  // the proposal per lane, then the wave's 64 likelihoods on MFMA
+    float q0x = 0.f, q1x = 0.f, propose = 0.f, prior = 0.f;
+    if (valid) {
+      const float jp = stage_propose_inverse<NFC>(d, in, L.cb_cond, q0x, q1x);
+      stage_prior<NFD, NFC>(d, S, i, in, L.cb_dyn, q0x, q1x, jp, propose, prior);
+    }
+    xw[threadIdx.x][0] = q0x;
+    xw[threadIdx.x][1] = q1x;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float r = crnvp_lik_mfma(reinterpret_cast<const float *>(wstage), d.n_flows, d.meas_prior_std, L.encv,
+                                   &xw[threadIdx.x & ~63][0]);
+    if (valid) {
+      lk = r;
+      S.hlik[i] = lk;
+      u = logw(lr, lk, prior, propose);
+    }
+  } else if (valid) {
     float q0x, q1x, propose, prior;
     if constexpr (STAGE) {
       static_assert(!STAGE || MEAS == NFDPF_MEAS_CRNVP, "staged weights: CRNVP only");
@@ -2092,7 +2121,7 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
     }
   }
   if constexpr (!NFC && MEAS == NFDPF_MEAS_CRNVP) {
-    if (use_cm(d)) {
+    if (use_cm(d) && !d.meas_mfma) {
       const size_t lds = cm_lds_bytes(d.n_flows);
       // the fold buffer exceeds the default 64 KB at 3-4 flows
       ensure_max_dynamic_lds((const void *)tiled_prop_cm_kernel<NFD>, (int)cm_lds_bytes(kMaxFlows));
@@ -2111,13 +2140,22 @@ static void launch_prop(const nfdpf_filter_desc &d, TiledWs ws, dim3 g, hipStrea
       tiled_prop2_kernel<NFD, NFC, MEAS, 2><<<g, 2 * kTile, 0, st>>>(d, ws);
   } else {
     if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
+      if (d.meas_mfma) {  // (NFC is false here: the tiled_prop2 branch above takes the conditional proposal)
+        const size_t lds = (size_t)crnvp_mfma_floats(d.n_flows) * sizeof(float);
+        if (ev)
+          hipExtLaunchKernelGGL(tiled_prop_kernel<NFD, NFC, MEAS, 2>, g, dim3(kTile), lds, st, ev[0], ev[1], 0, d,
+                                ws);
+        else
+          tiled_prop_kernel<NFD, NFC, MEAS, 2><<<g, kTile, lds, st>>>(d, ws);
+        return;
+      }
       if (use_stage(d)) {
         const size_t lds = (size_t)(kCrnvpPe + d.n_flows * kCrnvpFlow) * sizeof(float);
         if (ev)
-          hipExtLaunchKernelGGL(tiled_prop_kernel<NFD, NFC, MEAS, true>, g, dim3(kTile), lds, st, ev[0], ev[1], 0,
+          hipExtLaunchKernelGGL(tiled_prop_kernel<NFD, NFC, MEAS, 1>, g, dim3(kTile), lds, st, ev[0], ev[1], 0,
                                 d, ws);
         else
-          tiled_prop_kernel<NFD, NFC, MEAS, true><<<g, kTile, lds, st>>>(d, ws);
+          tiled_prop_kernel<NFD, NFC, MEAS, 1><<<g, kTile, lds, st>>>(d, ws);
         return;
       }
     }
@@ -2166,6 +2204,8 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   if (pass_cm_config_ok(d)) {  // the C3 / C1 shape: no flows on the particle path (CRNVP, cosine, gaussian)
     NFDPF_REQUIRE(d.pe_params && (d.meas_params || d.measurement != NFDPF_MEAS_CRNVP) && d.ess_all,
                   "nfdpf_filter_pass_tiled: parameters / ess_all missing");
+    NFDPF_REQUIRE(!d.meas_mfma || ((uintptr_t)d.meas_params & 15) == 0,
+                  "nfdpf_filter_pass_tiled: the MFMA fragment blob must be 16-B aligned");
     const int verify_cm = d.pass_gates && d.B_global == d.B;
     NFDPF_REQUIRE(!d.pass_gates || verify_cm, "nfdpf_filter_pass_tiled: pass_gates needs a pass of the whole batch");
     hipStream_t st = as_stream(stream);
@@ -2326,6 +2366,10 @@ extern "C" int nfdpf_filter_step_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_step_tiled: fused measurements need E == %d", kE);
   NFDPF_REQUIRE(!(d.measurement == NFDPF_MEAS_CRNVP || d.measurement == NFDPF_MEAS_NN) || d.meas_params,
                 "nfdpf_filter_step_tiled: measurement parameters missing");
+  NFDPF_REQUIRE(!d.meas_mfma || (d.measurement == NFDPF_MEAS_CRNVP && !d.nf_cond && d.n_flows <= 2 &&
+                                 ((uintptr_t)d.meas_params & 15) == 0),
+                "nfdpf_filter_step_tiled: meas_mfma needs the CRNVP measurement without --NF-cond, n_flows <= 2 "
+                "and a 16-B aligned fragment blob");
   NFDPF_REQUIRE(d.E + 4 <= kMaxCtx, "nfdpf_filter_step_tiled: E too large");
   NFDPF_REQUIRE(d.measurement != NFDPF_MEAS_EXTERNAL || d.phase != 0,
                 "nfdpf_filter_step_tiled: EXTERNAL measurement runs as phase 1 + phase 2");

@@ -17,7 +17,7 @@ struct StepShared {
   f2 cb_dyn[kMaxFlows * 2 * kH];   // folded bias pairs [flow][coupling half][j] of nf_dyn
   f2 cb_cond[kMaxFlows * 2 * kH];  // ... of the proposal flow
   float ctx[kMaxCtx];
-  float encv[kE];       // this row's frame encoding (raw)
+  alignas(16) float encv[kE];  // this row's frame encoding (raw; 16-B aligned: crnvp_lik_mfma's b128 reads)
   double vinv;          // cos: 1 / max(|encv|, 1e-12), fp64
   float nnrow[kNnH];    // NN: folded first layer of the obs half
   float f[16];

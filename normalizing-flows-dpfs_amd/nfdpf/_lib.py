@@ -48,6 +48,7 @@ class FilterDesc(Structure):
         ("prof_front", c_int32),
         ("pass_gate", c_int32),
         ("pass_gates", c_void_p), ("pass_flags", c_void_p), ("pass_obs", c_void_p),
+        ("meas_mfma", c_int32),
     ]
 
 

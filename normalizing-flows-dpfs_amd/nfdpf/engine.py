@@ -273,6 +273,7 @@ class FilterEngine:
         d.resampler = L.RESAMPLE[c.resampler]
         d.rng_mode, d.force_resample = L.RNG_DEVICE, int(c.force_resample)
         d.n_flows, d.hidden, d.split_nets = c.n_flows, c.hidden, int(split_nets)
+        d.meas_mfma = int(self._meas_mfma())
         ok = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
         self._gate_resident = False
         if ok and c.NF_dyn and c.NF_cond and not c.force_resample and shard.world == 1:
@@ -330,6 +331,22 @@ class FilterEngine:
         shared = len(set(ids)) < len(ids)
         self._shared_device = (key, shared)
         return shared
+
+    def _meas_mfma(self) -> bool:
+        """Does the no-flow pass (C3 shape) run the CRNVP measurement on f32 MFMA
+        (csrc/crnvp_mfma.hpp; NFDPF_CM_MFMA=0 keeps the per-lane VALU measurement)?"""
+        c, m = self.cfg, self.m
+        if c.measurement != "CRNVP" or c.NF_dyn or c.NF_cond or os.environ.get("NFDPF_CM_MFMA", "1") == "0":
+            return False
+        from .pack import crnvp_mfma_ok
+        return crnvp_mfma_ok(m.particle_encoder, list(m.cnf_measurement.flows))
+
+    def _mfma_blob(self, dev):
+        """The CRNVP measurement's MFMA fragment blob (nfdpf.pack.crnvp_mfma_tensors)."""
+        from .pack import crnvp_mfma_tensors
+        m = self.m
+        return blob(m, "meas_mfma", [m.particle_encoder, m.cnf_measurement],
+                    lambda: crnvp_mfma_tensors(m.particle_encoder, list(m.cnf_measurement.flows)), dev)
 
     def _pass_blobs(self, dev):
         """The dynamic / proposal stacks in the one-launch pass's layout (nfdpf.pack.pass_flow_tensors)."""
@@ -497,6 +514,9 @@ class FilterEngine:
         d.seed = int(c.seed) & (2 ** 64 - 1)
         d.dyn_params, d.cond_params = L.ptr(dyn), L.ptr(cond)
         d.pe_params, d.meas_params = L.ptr(pe), L.ptr(meas)
+        if tiled and self._meas_mfma():  # the C3 shape's CRNVP measurement on MFMA (pass and step launches)
+            mf = self._mfma_blob(dev)
+            d.meas_params, d.meas_mfma = mf.data_ptr(), 1  # (caching-allocator blocks: 512-B aligned)
         d.enc, d.lin = enc.data_ptr(), L.ptr(lin)
         d.hist_x, d.hist_p, d.hist_noise, d.hist_lik = hx.data_ptr(), hp.data_ptr(), hn.data_ptr(), hl.data_ptr()
         d.hist_jac, d.hist_prior, d.hist_idx = L.ptr(hj), L.ptr(hr), hi.data_ptr()

@@ -259,6 +259,86 @@ def pass_flow_tensors(flows):
     return out
 
 
+def mfma_frag(w: torch.Tensor) -> torch.Tensor:
+    """A matrix W [M, K] (M a multiple of 16, K of 4) as the A operands of a chain of
+    v_mfma_f32_16x16x4_f32 with features as rows and particles as columns (csrc/crnvp_mfma.hpp):
+    [M / 16][lane 64][K / 4] with entry (MT, l, s) = W[16 MT + (l & 15)][16 (s >> 2) + 4 (l >> 4) +
+    (s & 3)] -- K-step s reads, in lane group g, register s & 3 of the previous layer's M tile
+    s >> 2, so chained layers exchange no data."""
+    M, K = w.shape
+    lane = torch.arange(64)
+    s = torch.arange(K // 4)
+    rows = (16 * torch.arange(M // 16))[:, None, None] + (lane & 15)[None, :, None]
+    cols = 16 * (s >> 2)[None, None, :] + 4 * (lane >> 4)[None, :, None] + (s & 3)[None, None, :]
+    return w[rows, cols]
+
+
+def crnvp_mfma_tensors(encoder: nn.Module, flows):
+    """The CRNVP measurement (model/models.py:256-278: particle encoder Linear(2,16) ReLU
+    Linear(16,32) ReLU Linear(32,E), then RealNVP_cond flows of dim E with condition E) as the
+    fragment blob of csrc/crnvp_mfma.hpp (offsets kCmf*): the encoder's layer 1 plain (it runs on
+    VALU), layers 2 and 3 as mfma_frag; per flow and coupling half the nets t and s stacked as 16
+    hidden rows (t 0-7, s 8-15) -- the fold over the condition columns W1[:, HALF:], layer 1 over
+    u = W1[:, :HALF], layers 2 and 3 block-diagonal -- with the tanh algebra of
+    pass_coupling_tensors folded in (float64, rounded once)."""
+    l1, l2, l3 = _linears(encoder)
+    f64 = lambda t: t.detach().double().cpu()  # noqa: E731
+    out = [f64(l1.weight).reshape(-1), f64(l1.bias), mfma_frag(f64(l2.weight)).reshape(-1), f64(l2.bias),
+           mfma_frag(f64(l3.weight)).reshape(-1), f64(l3.bias)]
+    c = TANH_C
+    for f in flows:
+        half = f.dim // 2
+        for t_net, s_net in ((f.t1, f.s1), (f.t2, f.s2)):
+            nets = []
+            for net in (t_net, s_net):
+                (w1, b1), (w2, b2), (w3, b3) = [(f64(m.weight), f64(m.bias)) for m in _linears(net.network)]
+                nets.append(dict(w1u=c * w1[:, :half], w1c=c * w1[:, half:], b1=c * b1, w2=-2.0 * c * w2,
+                                 b2=c * (b2 + w2.sum(1)), w3=-2.0 * w3, b3=b3 + w3.sum(1)))
+            t, s_ = nets
+            H, O = t["w2"].shape[0], t["w3"].shape[0]
+            # hidden row p of the 16: t-net unit j at 4 (j >> 1) + (j & 1), s-net unit j at
+            # 4 (j >> 1) + 2 + (j & 1) -- the t units in registers 0-1 of every lane group, the s
+            # units in registers 2-3, so layer 3's t outputs read K-steps 0-1 only and its s
+            # outputs K-steps 2-3 (half of the block-diagonal layer's MFMAs skipped)
+            j = torch.arange(H)
+            pt, ps = 4 * (j >> 1) + (j & 1), 4 * (j >> 1) + 2 + (j & 1)
+
+            def rows(a, b):
+                o = torch.zeros((2 * H,) + tuple(a.shape[1:]), dtype=torch.float64)
+                o[pt], o[ps] = a, b
+                return o
+            w2 = torch.zeros(2 * H, 2 * H, dtype=torch.float64)
+            w2[pt[:, None], pt[None, :]] = t["w2"]
+            w2[ps[:, None], ps[None, :]] = s_["w2"]
+            w3 = torch.zeros(2 * O, 2 * H, dtype=torch.float64)
+            w3[:O, pt] = t["w3"]
+            w3[O:, ps] = s_["w3"]
+            out += [mfma_frag(rows(t["w1c"], s_["w1c"])).reshape(-1),
+                    mfma_frag(rows(t["w1u"], s_["w1u"])).reshape(-1),
+                    mfma_frag(w2).reshape(-1), mfma_frag(w3).reshape(-1),
+                    rows(t["b1"], s_["b1"]), rows(t["b2"], s_["b2"]), torch.cat([t["b3"], s_["b3"]])]
+    return [x.float() for x in out]
+
+
+def crnvp_mfma_ok(encoder: nn.Module, flows) -> bool:
+    """The shapes csrc/crnvp_mfma.hpp is written for: encoder 2 -> 16 -> 32 -> 32, one or two
+    RealNVP_cond flows of dim 32, condition 32, hidden 8."""
+    try:
+        l1, l2, l3 = _linears(encoder)
+    except ValueError:
+        return False
+    if (l1.weight.shape, l2.weight.shape, l3.weight.shape) != ((16, 2), (32, 16), (32, 32)):
+        return False
+    if not 1 <= len(flows) <= 2:
+        return False
+    for f in flows:
+        if hasattr(f, "initial_param") or getattr(f, "dim", None) != 32 or getattr(f, "obser_dim", None) != 32:
+            return False
+        if [tuple(m.weight.shape) for m in _linears(f.t1.network)] != [(8, 48), (8, 8), (16, 8)]:
+            return False
+    return True
+
+
 class BlobCache:
     """Flat fp32 copy of a parameter set on one device in a kernel layout, rebuilt only when
     a source parameter changes (storage, version counter)."""

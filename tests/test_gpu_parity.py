@@ -718,6 +718,7 @@ def test_crnvp_two_chain_matches_one_chain(N, nf_dyn, resampler, force, monkeypa
     wl = F.workload("c3_full", B=5, N=N, T=5)
     models = wl["models"].to(DEV)
     out = {}
+    monkeypatch.setenv("NFDPF_CM_MFMA", "0")  # (the per-lane measurement launches compared here)
     for single in ("1", "0"):
         monkeypatch.setenv("NFDPF_CM_TWO_CHAIN", "0" if single == "1" else "1")
         cfg = FilterConfig(N=N, NF_dyn=nf_dyn, NF_cond=False, measurement="CRNVP", resampler=resampler,
@@ -746,6 +747,7 @@ def test_crnvp_staged_weights_match_scalar(N, nf_dyn, resampler, force, monkeypa
     wl = F.workload("c3_full", B=5, N=N, T=5)
     models = wl["models"].to(DEV)
     out = {}
+    monkeypatch.setenv("NFDPF_CM_MFMA", "0")  # (the per-lane measurement launches compared here)
     for scalar in ("1", "0"):
         monkeypatch.setenv("NFDPF_CRNVP_STAGE", "0" if scalar == "1" else "1")
         cfg = FilterConfig(N=N, NF_dyn=nf_dyn, NF_cond=False, measurement="CRNVP", resampler=resampler,
@@ -758,3 +760,32 @@ def test_crnvp_staged_weights_match_scalar(N, nf_dyn, resampler, force, monkeypa
         assert (x is None) == (y is None), f
         assert x is None or torch.equal(x, y), f
     assert torch.isfinite(b.lik).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,nf_dyn,resampler,force", [(1000, False, "ot", True), (777, True, "soft", False),
+                                                      (65, False, "ot", False)])
+def test_crnvp_mfma_matches_valu(N, nf_dyn, resampler, force, monkeypatch):
+    """CRNVP without --NF-cond: the step launch's measurement on f32 MFMA (64 particles per wave,
+    csrc/crnvp_mfma.hpp, the default) against the per-lane VALU measurement (NFDPF_CM_MFMA=0) on
+    the same step: the same function with the tanh algebra folded into the weights and other
+    summation orders, so the likelihoods agree to rounding (1e-5 relative + 1e-4) at step 0, whose
+    inputs are identical (later steps follow the resampler, which these differences can tip).
+    Ragged N (65: one full wave and one particle) included."""
+    import _fullsize as F
+    from nfdpf.engine import FilterConfig, FilterEngine
+    wl = F.workload("c3_full", B=5, N=N, T=4)
+    models = wl["models"].to(DEV)
+    out = {}
+    for mf in ("1", "0"):
+        monkeypatch.setenv("NFDPF_CM_MFMA", mf)
+        monkeypatch.setenv("NFDPF_PASS", "0")  # the step launches
+        cfg = FilterConfig(N=N, NF_dyn=nf_dyn, NF_cond=False, measurement="CRNVP", resampler=resampler,
+                           force_resample=force, seed=7, kernel="tiled")
+        out[mf] = FilterEngine(cfg, models).run(wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+        torch.cuda.synchronize()
+    a, b = out["1"], out["0"]
+    assert torch.isfinite(a.lik).all()
+    assert torch.equal(a.noise[:, 0], b.noise[:, 0])
+    assert_close(a.lik[:, 0].cpu(), b.lik[:, 0].cpu(), 1e-5, 1e-4, "likelihood, step 0")
+    assert_close(a.probs[:, 0].cpu(), b.probs[:, 0].cpu(), 1e-4, 1e-9, "weights, step 0")
