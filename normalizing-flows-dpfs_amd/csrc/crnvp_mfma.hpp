@@ -59,6 +59,9 @@ __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f4v ld4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
+// relu as one v_max_i32 on the bit pattern (a negative float, -0 included, is a negative int):
+// fmaxf(x, 0) of an MFMA result compiles to a canonicalising v_max(x, x) plus the max
+__device__ __forceinline__ float relu_i(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 __device__ __forceinline__ float sig_r(float y) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(y) + 1.0f); }
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   const long long x = __double_as_longlong(v);
@@ -87,38 +90,37 @@ __device__ __forceinline__ float crnvp_lik_mfma(const float *W, int n_flows, flo
     for (int q = 0; q < 4; ++q) {
       const float x0 = xr[2 * (16 * q + col)], x1 = xr[2 * (16 * q + col) + 1];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h1[q][r] = relu(fmaf(w1[r], x1, fmaf(w0[r], x0, b1[r])));
+      for (int r = 0; r < 4; ++r) h1[q][r] = relu_i(fmaf(w1[r], x1, fmaf(w0[r], x0, b1[r])));
     }
   }
-  // ---- layer 2 (16 -> 32, relu)
-  f4v h2[2][4];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const f4v a = ld4(W + kCmfEW2 + (mt * 64 + l) * 4), bias = ld4(W + kCmfEB2 + 16 * mt + 4 * g);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f4v acc = bias;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma4(a[s], h1[q][s], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = relu(acc[r]);
-      h2[mt][q] = acc;
-    }
-  }
-  // ---- layer 3 (32 -> 32): e, the condition
+  // ---- layers 2 (16 -> 32, relu) and 3 (32 -> 32): e, the condition; one N tile at a time (its
+  // layer-2 output is all layer 3 needs: 8 live registers instead of 32)
   f4v e[2][4];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const f4v a0 = ld4(W + kCmfEW3 + (mt * 64 + l) * 8), a1 = ld4(W + kCmfEW3 + (mt * 64 + l) * 8 + 4);
-    const f4v bias = ld4(W + kCmfEB3 + 16 * mt + 4 * g);
+  {
+    const f4v a2[2] = {ld4(W + kCmfEW2 + l * 4), ld4(W + kCmfEW2 + (64 + l) * 4)};
+    const f4v bias2[2] = {ld4(W + kCmfEB2 + 4 * g), ld4(W + kCmfEB2 + 16 + 4 * g)};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      f4v acc = bias;
+      f4v h2[2];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma4(a0[s], h2[0][q][s], acc);
+      for (int mt = 0; mt < 2; ++mt) {
+        f4v acc = bias2[mt];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma4(a1[s], h2[1][q][s], acc);
-      e[mt][q] = acc;
+        for (int s = 0; s < 4; ++s) acc = mfma4(a2[mt][s], h1[q][s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = relu_i(acc[r]);
+        h2[mt] = acc;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const f4v a0 = ld4(W + kCmfEW3 + (mt * 64 + l) * 8), a1 = ld4(W + kCmfEW3 + (mt * 64 + l) * 8 + 4);
+        f4v acc = ld4(W + kCmfEB3 + 16 * mt + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(a0[s], h2[0][s], acc);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(a1[s], h2[1][s], acc);
+        e[mt][q] = acc;
+      }
     }
   }
   // ---- the flows: lo = encv[0:16], up = encv[16:32] (the same for every particle at the start)
@@ -131,7 +133,7 @@ __device__ __forceinline__ float crnvp_lik_mfma(const float *W, int n_flows, flo
       up[q] = up0;
     }
   }
-  f4v lds[4] = {};  // per column: this lane's share of sum(s) over every half
+  float lds[4] = {0.f, 0.f, 0.f, 0.f};  // per N tile: this lane's share of sum(s) over every half
   for (int f = 0; f < n_flows; ++f) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -183,8 +185,8 @@ __device__ __forceinline__ float crnvp_lik_mfma(const float *W, int n_flows, flo
         for (int r = 0; r < 4; ++r) {  // exp(s) as one v_exp_f32 of s log2(e): |s| is O(1) here, where
                                        // expf's range reduction (~10 VALU) buys nothing
           v[q][r] = t[r] + v[q][r] * __builtin_amdgcn_exp2f(s[r] * 1.4426950408889634f);
-          lds[q][r] += s[r];
         }
+        lds[q] += (s[0] + s[1]) + (s[2] + s[3]);
       }
     }
   }
@@ -205,7 +207,7 @@ __device__ __forceinline__ float crnvp_lik_mfma(const float *W, int n_flows, flo
     }
     m += shfl_xor_d(m, 16);
     mq[q] = m + shfl_xor_d(m, 32);
-    float ls = (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]);
+    float ls = lds[q];
     ls += __shfl_xor(ls, 16);
     ldq[q] = ls + __shfl_xor(ls, 32);
   }

@@ -15,10 +15,13 @@
 // the raw likelihood (the CRNVP shift, model/models.py:276).  That chain is short (a sweep and a
 // few VALU ops per particle); the likelihoods run ahead of it.
 //
-// Grid (tiles, B) of 512-thread workgroups, all resident (pass_cm_config_ok).  Wave w handles
-// particle group g = w & 3 (64 particles of the tile, one per lane; waves w and w + 4 share a
-// SIMD) on the steps of parity k = w >> 2: two steps of a group in flight per SIMD, each wave
-// with 256 VGPRs for the measurement's registers.  Per step t, wave (g, t & 1):
+// Grid (tiles, B) of 4 K-wave workgroups (K = 2: 512 threads; K = 3: 768, NFDPF_CM_K), all
+// resident (pass_cm_config_ok).  Wave w handles particle group g = w & 3 (64 particles of the
+// tile, one per lane; waves w, w + 4, ... share a SIMD) on the steps t = k mod K, k = w >> 2: K
+// steps of a group in flight per SIMD.  The step-indexed buffers stay double-buffered for any K:
+// the x hand-over is serialised by the xf flags, and nb / rn / the C granules of slot s are
+// reused by slot s + 2 only after the C(s + 1) sweep, which needs every wave that read them.
+// Per step t, wave (g, t mod K):
 //   1. x_t from x_{t-1} (LDS xr, from the group's other wave; flag xf[g]) + vel_t + eps_t ->
 //      xr, hist_x / noise / index;
 //   2. lik_t = crnvp_lik(x_t) (raw), the step's frame encoding in the wave's own LDS copy;
@@ -27,7 +30,7 @@
 //      the other wave's hand-over nb (finish_prev's arithmetic: hist_p, hist_lik shifted, the
 //      fin partials) -> log p_{t-1};
 //   4. u_t, the group's partials {max u, sum e, sum e^2, max lik} -> C(t) granules.
-// The waves of parity T & 1 normalise the last slot after their loop.
+// The waves of k = T mod K normalise the last slot after their loop.
 //
 // Every wait is bounded (pass_spin: 200 ms, the workspace's abort word), as in filter_pass.hpp.
 
@@ -35,13 +38,20 @@
 
 namespace nfdpf {
 
-constexpr int kCmWaves = 8;  // 512 threads: two waves (two steps in flight) per particle group
+// steps in flight per particle group (waves per group): 2 (512 threads, <= 256 VGPRs per wave) or
+// 3 (768 threads, <= 168 VGPRs: the MFMA measurement, whose MFMA and VALU phases then overlap
+// across three waves per SIMD)
+// (tiled_pass_cm_kernel<MEAS, MF, K>; pass_cm_k: NFDPF_CM_K, read per call)
+constexpr int kCmMaxK = 3;
 constexpr int kCmMfmaFlows = 2;  // the MFMA measurement's LDS blob holds up to 2 flows (DPFs.py:46: n_sequence 2)
 
 struct PassCmLds {
-  float xr[2][4][64][2];     // x_t by parity of t: the group's other wave reads it for step t + 1
+  // x_t in buffer t mod K: the group's next wave reads it for step t + 1, and the MFMA measurement
+  // of step t reads it back (its particles per N tile) while the next waves move on -- only the
+  // wave of step t + K, this same wave, overwrites it
+  float xr[kCmMaxK][4][64][2];
   float nb[2][5][kTile];     // slot t's hand-over by parity: lr, raw lik, prior, x0, x1
-  alignas(16) float encq[kCmWaves][kE];  // each wave's copy of its step's frame encoding (crnvp_lik's encv)
+  alignas(16) float encq[4 * kCmMaxK][kE];  // each wave's copy of its step's frame encoding (crnvp_lik's encv)
   uint32_t rowc[kPassMaxTiles * 4 * kGC];
   RowNorm rn[2];
   int xf[4];                 // x_t of group g written (t + 1)
@@ -131,8 +141,8 @@ __device__ __forceinline__ float pass_cm_norm(const nfdpf_filter_desc &d, const 
 // MF (CRNVP with d.meas_mfma): the measurement on f32 MFMA (crnvp_mfma.hpp), 64 particles per
 // wave, its fragment blob staged in LDS once per launch; else crnvp_lik per lane (scalar-cache
 // weights, VALU)
-template <int MEAS, bool MF = false>
-__global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const nfdpf_filter_desc d, PassWs ws) {
+template <int MEAS, bool MF = false, int K = 2>
+__global__ __launch_bounds__(4 * K * 64, 1) void tiled_pass_cm_kernel(const nfdpf_filter_desc d, PassWs ws) {
   static_assert(MEAS == NFDPF_MEAS_CRNVP || MEAS == NFDPF_MEAS_COS || MEAS == NFDPF_MEAS_GAUSSIAN,
                 "the no-flow pass: the CRNVP, cosine or gaussian measurement");
   static_assert(!MF || MEAS == NFDPF_MEAS_CRNVP, "MFMA: the CRNVP measurement");
@@ -149,7 +159,8 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
     for (int q = threadIdx.x; q < crnvp_mfma_floats(d.n_flows) / 4; q += blockDim.x) wfr[q] = src[q];
   }
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int g = w & 3, k = w >> 2, slot = g * 64 + lane, N = d.N, tiles = n_tiles(N);
+  const int g = w & 3, k = w >> 2, slot = g * 64 + lane, N = d.N, tiles = n_tiles(N);  // k: t mod K
+  const int km1 = k == 0 ? K - 1 : k - 1;  // (t - 1) mod K
   const int i = tile * kTile + slot;
   const bool valid = i < N;
   const int64_t grow = d.row_base + b;
@@ -157,12 +168,12 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
   float lr = 0.f;  // log p of this wave's particle in the slot before its next step
   if (k == 0) {  // x_0 = the initial particles (step 0 is parity 0's)
     if (valid) {
-      L.xr[1][g][lane][0] = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i];
-      L.xr[1][g][lane][1] = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i + 1];
+      L.xr[K - 1][g][lane][0] = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i];  // "x_{-1}": buffer -1 mod K
+      L.xr[K - 1][g][lane][1] = d.x_prev[(int64_t)b * d.x_prev_rs + 2 * i + 1];
       lr = logf(d.p_prev[(int64_t)b * d.p_prev_rs + i]);
     }
   }
-  for (int t = k; t < d.T; t += 2) {
+  for (int t = k; t < d.T; t += K) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
     const PassWs &ws = *(const PassWs *)kernarg_ws();
     const int par = t & 1;
@@ -175,10 +186,10 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
     wait_flag(&L.xf[g], t);  // x_{t-1} of the group
     float x0 = 0.f, x1 = 0.f, de = 0.f;
     if (valid) {
-      x0 = (L.xr[par ^ 1][g][lane][0] + v0) + e0;
-      x1 = (L.xr[par ^ 1][g][lane][1] + v1) + e1;
-      L.xr[par][g][lane][0] = x0;
-      L.xr[par][g][lane][1] = x1;
+      x0 = (L.xr[km1][g][lane][0] + v0) + e0;
+      x1 = (L.xr[km1][g][lane][1] + v1) + e1;
+      L.xr[k][g][lane][0] = x0;
+      L.xr[k][g][lane][1] = x1;
     }
     set_flag(&L.xf[g], t + 1);
     if (valid) {
@@ -196,9 +207,9 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
       const float ve = lane < kE ? d.enc[((int64_t)b * d.T + t) * d.E + lane] : 0.f;
       vinv = 1.0 / fmax(sqrt(wave_sum((double)ve * ve)), 1e-12);
     }
-    if constexpr (MF) {  // the whole wave: its 64 particles x_t are in xr[par][g]
+    if constexpr (MF) {  // the whole wave: its 64 particles x_t are in xr[t mod K][g]
       const float r = crnvp_lik_mfma(reinterpret_cast<const float *>(wfr), d.n_flows, d.meas_prior_std, L.encq[w],
-                                     &L.xr[par][g][0][0]);
+                                     &L.xr[k][g][0][0]);
       if (valid) raw = r;
     } else if (valid) {
       if constexpr (MEAS == NFDPF_MEAS_CRNVP) {
@@ -252,18 +263,31 @@ __global__ __launch_bounds__(kCmWaves * 64, 1) void tiled_pass_cm_kernel(const n
     }
   }
   // the last slot's normalisation: the waves of parity T & 1 (they would have run step T)
-  if (k == (d.T & 1)) {
+  if (k == d.T % K) {
     if (g == 0) pass_cm_poll_c<SHIFT>(d, ws, L, b, tile, tag0, d.T - 1);
     pass_cm_norm<SHIFT>(d, ws, L, b, tile, g, d.T - 1, slot, i, valid);
   }
 }
 
 typedef void (*pass_cm_kernel_t)(const nfdpf_filter_desc, PassWs);
+// steps in flight per particle group: 3 for the MFMA measurement (three waves per SIMD overlap its
+// MFMA and VALU phases: 0.594 -> 0.560 ms per C3 pass, A/B on one box), else 2 (the per-lane VALU
+// measurement spills at 168 VGPRs); NFDPF_CM_K=2|3 (read per call) overrides
+static int pass_cm_k(const nfdpf_filter_desc &d) {
+  const char *e = getenv("NFDPF_CM_K");
+  if (e && (e[0] == '2' || e[0] == '3')) return e[0] - '0';
+  return d.meas_mfma ? 3 : 2;
+}
+static int pass_cm_threads(const nfdpf_filter_desc &d) { return 4 * pass_cm_k(d) * 64; }
+template <int K>
+static pass_cm_kernel_t pass_cm_kernel_k(const nfdpf_filter_desc &d) {
+  return d.measurement == NFDPF_MEAS_COS        ? tiled_pass_cm_kernel<NFDPF_MEAS_COS, false, K>
+         : d.measurement == NFDPF_MEAS_GAUSSIAN ? tiled_pass_cm_kernel<NFDPF_MEAS_GAUSSIAN, false, K>
+         : d.meas_mfma                          ? tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP, true, K>
+                                                : tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP, false, K>;
+}
 static pass_cm_kernel_t pass_cm_kernel_of(const nfdpf_filter_desc &d) {
-  return d.measurement == NFDPF_MEAS_COS        ? tiled_pass_cm_kernel<NFDPF_MEAS_COS>
-         : d.measurement == NFDPF_MEAS_GAUSSIAN ? tiled_pass_cm_kernel<NFDPF_MEAS_GAUSSIAN>
-         : d.meas_mfma                          ? tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP, true>
-                                                : tiled_pass_cm_kernel<NFDPF_MEAS_CRNVP>;
+  return pass_cm_k(d) == 3 ? pass_cm_kernel_k<3>(d) : pass_cm_kernel_k<2>(d);
 }
 
 // The C3-shaped pass applies: the configuration, the speculative gate (not forced, not gated in
@@ -282,7 +306,7 @@ static bool pass_cm_config_ok(const nfdpf_filter_desc &d) {
   // every row resident in one launch: above that the step launches are faster for this shape
   // (C3 x 128 rows on one MI355X: 3.14e9 particle-steps/s step by step against 2.90e9 for two
   // resident chunks of the pass -- unlike the C2 shape, its step launches fill the device)
-  return pass_resident_rows(pass_cm_kernel_of(d), kCmWaves * 64, n_tiles(d.N)) >= d.B;
+  return pass_resident_rows(pass_cm_kernel_of(d), pass_cm_threads(d), n_tiles(d.N)) >= d.B;
 }
 
 }  // namespace nfdpf

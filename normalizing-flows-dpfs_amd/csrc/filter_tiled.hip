@@ -2214,9 +2214,9 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
     if (const char *e = getenv("NFDPF_PASS_WAIT_US"))  // read per call (tests force a timeout)
       ws.wait_ticks = (uint64_t)std::max(1L, atol(e)) * 100ull;
     const auto kern = pass_cm_kernel_of(d);
-    const int rows = pass_resident_rows(kern, kCmWaves * 64, n_tiles(d.N));
+    const int rows = pass_resident_rows(kern, pass_cm_threads(d), n_tiles(d.N));
     NFDPF_REQUIRE(rows >= 1, "nfdpf_filter_pass_tiled: no row of the pass fits on the device");
-    pass_launch_rows(kern, d, ws, kCmWaves * 64, std::min(rows, d.B), st);
+    pass_launch_rows(kern, d, ws, pass_cm_threads(d), std::min(rows, d.B), st);
     tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, verify_cm, 4);
     return launch_status("nfdpf_filter_pass_tiled");
   }
