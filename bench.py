@@ -333,7 +333,9 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
     graph = None
     # auto (engine.FilterEngine.run): speculative gates when sharded, for OT at any world size
     # unless the previous pass resampled, and wherever the whole pass runs as one launch
-    spec = eng.speculates(shard)  # the engine's own decision for the next pass (engine._decide_spec)
+    # the engine's own decision for the next pass (engine._decide_spec); a pass following a gate
+    # plan (engine._plan_select) is verified after it the same way
+    spec = eng.speculates(shard) or eng.plans(shard)
     # one GPU, a gated or forced one-launch pass (gates decided inside the launch): captured with
     # finish=False too, so that each replay's fault flags are checked (finish_pending) -- a replay
     # whose row hand-offs timed out is rerun, never taken for a result
@@ -700,7 +702,8 @@ def main():
                        "execution": ("hipGraph replay of the pass" if run_i["graph"] is not None else "Python launches")
                                     + (", the whole pass as one launch" if eng_i.last_pass else "")
                                     + (", ESS gate decided inside the launch" if eng_i.last_gate_pass else "")
-                                    + (", speculative ESS gate" if run_i["spec"] else ""),
+                                    + (", ESS gates following the last exact pass's plan, verified after the pass"
+                                       if eng_i.last_plan_pass else ", speculative ESS gate" if run_i["spec"] else ""),
                        "pass_kernel_avg_ms_live": run_i["kernel_ms"] if eng_i.last_pass else None}
 
     if rank == 0:
@@ -717,7 +720,8 @@ def main():
                          f"{'hipGraph replay of the pass' if graph is not None else 'Python launches'}"
                          + (", the whole pass as one launch" if eng.last_pass else "")
                          + (", ESS gate decided inside the launch" if eng.last_gate_pass else "")
-                         + (", speculative ESS gate verified once per pass" if spec else "")
+                         + (", ESS gates following the last exact pass's plan, verified once per pass"
+                            if eng.last_plan_pass else ", speculative ESS gate verified once per pass" if spec else "")
                          + (", frame encodings = particle encoder(true positions)" if args.enc_from_state else ""),
                        "global_batch": B * world, "num_particles": N, "seq_len": T,
                        "parallelism": f"batch-sharded x{world}"},

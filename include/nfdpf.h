@@ -419,6 +419,16 @@ typedef struct nfdpf_filter_desc {
                                crnvp_mfma_tensors, csrc/crnvp_mfma.hpp; n_flows <= 2): the features-
                                by-particles layout of the f32-MFMA measurement, read by the no-flow
                                one-launch pass (tiled_pass_cm_kernel); 0 = the pair layout above */
+  const int32_t *pass_plan; /* nfdpf_filter_pass_tiled with pass_gate = 1, optional [T]: the ESS gate
+                               decisions to follow instead of deciding them inside the launch (the
+                               "plan" pass: step t resamples iff pass_plan[t]; no batch-wide
+                               exchange, so a sharded batch (B_global != B) and a batch of more rows
+                               than the device holds at once run it too).  With pass_gates and the
+                               whole batch (B_global == B) the epilogue writes the ACTUAL gates of
+                               the trajectory (from the pass's own partials) to pass_gates and
+                               counts the steps where they differ from the plan in pass_flags[0];
+                               the caller reruns with a corrected plan -- the result is the
+                               reference's only when no step differs */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);

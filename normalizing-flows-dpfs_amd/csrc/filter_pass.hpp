@@ -817,9 +817,14 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     if (t == 0 && valid) pass_noise(d, 0, grow, i, en0, en1);
     // the step's input particles: own (x0, x1) or the row's resampling's
     float xs0 = x0, xs1 = x1;
+    // the step's motion noise: kept aside -- the first attempt draws step t + 1's into (en0, en1)
+    // while its A exchange is in flight, and a redone step (GATE) must move with step t's own
+    const float sn0 = en0, sn1 = en1;
     int src = i, variant = 0, fire = FORCE ? 1 : 0;
-    const int pred = GATE ? (t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
-    bool known = !GATE || t == 0;  // the step's decision is in hand (GATE: else speculated)
+    // (a plan pass follows d.pass_plan: the decision is known, never speculated)
+    const int32_t *plan = GATE ? d.pass_plan : nullptr;
+    const int pred = GATE ? (plan ? (plan[t] ? 1 : 0) : t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
+    bool known = !GATE || t == 0 || plan;  // the step's decision is in hand (GATE: else speculated)
     auto take_resampled = [&]() {
       if (valid) {
         xs0 = L.rs.xr_l[slot][0];
@@ -834,7 +839,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       }
       pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
       if (GATE) {
-        fire = wait_dec(L, t);
+        fire = plan ? pred : wait_dec(L, t);
         known = true;
       }
       if (fire) take_resampled();
@@ -857,8 +862,8 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
       } else {
         e0 = e1 = p0 = p1 = 0.f;
         if (valid) {
-          e0 = en0;
-          e1 = en1;
+          e0 = sn0;
+          e1 = sn1;
           p0 = (xs0 + v0) + e0;
           p1 = (xs1 + v1) + e1;
         }
@@ -1065,7 +1070,8 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     const float K = d.dens_const, two_var = 2.0f * (d.pos_noise * d.pos_noise);
     const int par = t & 1;
     const RowSlot S = row_slot(d, b, t);
-    const int pred = GATE ? (t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
+    const int32_t *plan = GATE ? d.pass_plan : nullptr;
+    const int pred = GATE ? (plan ? (plan[t] ? 1 : 0) : t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
     if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
     PT(t, 0);
     if (g == 0) {
@@ -1082,7 +1088,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
         set_flag(&L.fE, s + 1);
       }
     }
-    if (GATE && !pred && t > 0) {
+    if (GATE && !pred && t > 0 && !plan) {
       // the proposal, or the chain's call to resample the row after all (a dropped speculation;
       // rq is only ever raised before qf of the same step)
       Spin sp;
@@ -1192,9 +1198,16 @@ __device__ __forceinline__ float pass_poll_c(const nfdpf_filter_desc &d, const P
 // the mean follows ATen's cascade order over them.  Every workgroup decides alike, from the same
 // words.  The decision goes to dec[t & 1] / fD; workgroup (0, 0) also records it (pass_gates,
 // the epilogue's count).
+// With a plan (d.pass_plan) the decision is the plan's: no exchange, nothing recorded here (the
+// epilogue verifies the plan against the pass's own partials).
 __device__ __forceinline__ void pass_gate(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                           uint32_t tag0, int t, float inv) {
   const int tiles = n_tiles(d.N), lane = threadIdx.x & 63, B = d.B;
+  if (d.pass_plan) {
+    if (lane == 0) L.dec[t & 1] = d.pass_plan[t] ? 1 : 0;
+    set_flag(&L.fD, t + 1);
+    return;
+  }
   float s;
   if (t == 0) {
     const double *parts = reinterpret_cast<const double *>(d.ess_all);
@@ -1311,7 +1324,11 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       wait_flag(&L.qf[g], t + 1);
       // GATE: a resampling at step t (predicted, or the chain's redo) may still be summing its
       // gathered weights in the scratch the MFMA layers reuse -- until fS (qf implies fD >= t + 1)
-      if (GATE && (pdec || __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0)) wait_flag(&L.fS, t + 1);
+      // (a plan pass: the flow waves resampled at step t iff the plan's gate fired -- nothing is
+      // speculated from step t - 1's decision there)
+      if (GATE && (d.pass_plan ? d.pass_plan[t] != 0
+                               : (pdec || __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0)))
+        wait_flag(&L.fS, t + 1);
       PT(t, 4);
 #ifndef NFDPF_EXP_NOENC
       encode_dot_mfma_half<kE>(ef, role, L.qbuf[par] + g * 64, L.qbuf[par] + kTile + g * 64, L.encq[we], ss, dot,
@@ -1356,7 +1373,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       if (grp) lk = encode();
       // step t is committed (qf): its decision is known; a fired gate resampled the row and
       // this particle's log-weight is its source's (the chain's resampling left it in lr_l)
-      pdec = __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]);
+      pdec = d.pass_plan ? (d.pass_plan[t] ? 1 : 0) : __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]);
       if (pdec != 0) lr = valid_e ? L.lr_l[slot_e] : 0.f;
     }
     // the log-weight (DPFs.py:187)
@@ -1531,7 +1548,8 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     int nf = 0;
     for (int t = 0; t < T; ++t) {
       acc += eq_l[t];
-      nf += eg_l[t];
+      // a plan pass: the steps whose actual gate differs from the plan's
+      nf += d.pass_plan ? (eg_l[t] != (d.pass_plan[t] ? 1 : 0)) : eg_l[t];
     }
     if (d.pass_obs) d.pass_obs[0] = (float)acc;
     if (d.pass_flags) {  // (system scope: the caller may map them from pinned host memory)
@@ -1565,15 +1583,17 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   // a forced pass resamples every step inside the launch (soft resampler only); otherwise the
   // caller takes every gate as off and verifies them afterwards
   if (d.force_resample && d.resampler != NFDPF_RESAMPLE_SOFT) return false;
-  // the in-launch gate: the whole batch in this launch, the soft resampler (its lin markers)
-  if (d.pass_gate && !d.force_resample && (d.B_global != d.B || d.resampler != NFDPF_RESAMPLE_SOFT)) return false;
+  // the in-launch gate: the whole batch in this launch (unless it follows a plan), the soft resampler
+  if (d.pass_gate && !d.force_resample &&
+      ((d.B_global != d.B && !d.pass_plan) || d.resampler != NFDPF_RESAMPLE_SOFT))
+    return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
       d.B < 1 || d.B > 256)  // (the epilogue stages a step's B row sums in LDS)
     return false;
-  // every workgroup resident at once; a speculative or forced pass may also run its rows in
+  // every workgroup resident at once; a speculative, forced or plan pass may also run its rows in
   // resident chunks (pass_launch_rows), the gated one not (its rows wait for the batch decision)
   const int rows = pass_resident_rows(pass_kernel_of(d), 4 * kTile, n_tiles(d.N));
-  return rows >= d.B || (rows >= 1 && pass_mode_of(d) != kModeGate);
+  return rows >= d.B || (rows >= 1 && (pass_mode_of(d) != kModeGate || d.pass_plan));
 }
 
 }  // namespace nfdpf

@@ -2231,8 +2231,9 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   // the epilogue's gates: those of a speculative pass of the whole batch (a sharded one is
   // verified by the caller over the gathered partials, nfdpf_ess_gate_tiled_batch), or the
   // decisions the gated pass took itself
-  const int verify = mode == kModeSpec && d.pass_gates && d.B_global == d.B;
-  NFDPF_REQUIRE(!d.pass_gates || verify || mode == kModeGate,
+  // (a plan pass's epilogue verifies the plan from the partials, as a speculative pass's)
+  const int verify = (mode == kModeSpec || (mode == kModeGate && d.pass_plan)) && d.pass_gates && d.B_global == d.B;
+  NFDPF_REQUIRE(!d.pass_gates || verify || (mode == kModeGate && !d.pass_plan),
                 "nfdpf_filter_pass_tiled: pass_gates needs a pass of the whole batch (B_global == B) that is not forced");
   hipStream_t st = as_stream(stream);
   PassWs ws = pass_carve(workspace, d.B, d.N, d.T);
@@ -2242,10 +2243,10 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
   const auto kern = pass_kernel_of(d);
   const int rows = pass_resident_rows(kern, 4 * kTile, n_tiles(d.N));
   // (pass_config_ok: the gated pass has all its rows resident in one launch)
-  NFDPF_REQUIRE(rows >= d.B || (rows >= 1 && mode != kModeGate),
+  NFDPF_REQUIRE(rows >= d.B || (rows >= 1 && (mode != kModeGate || d.pass_plan)),
                 "nfdpf_filter_pass_tiled: the pass's rows do not fit on the device");
   pass_launch_rows(kern, d, ws, 4 * kTile, std::min(rows, d.B), st);
-  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate ? 2 : verify, 8);
+  tiled_pass_epilogue_kernel<<<d.T, 64, 0, st>>>(d, ws, mode == kModeGate && !d.pass_plan ? 2 : verify, 8);
   return launch_status("nfdpf_filter_pass_tiled");
 }
 

@@ -49,6 +49,7 @@ class FilterDesc(Structure):
         ("pass_gate", c_int32),
         ("pass_gates", c_void_p), ("pass_flags", c_void_p), ("pass_obs", c_void_p),
         ("meas_mfma", c_int32),
+        ("pass_plan", c_void_p),
     ]
 
 

@@ -70,6 +70,12 @@ class FilterConfig:
     # resampler: nfdpf_filter_pass_tiled with pass_gate = 1); None / True = wherever it applies
     # and the pass is not speculated explicitly, False = never
     pass_gate: Optional[bool] = None
+    # the one-launch pass following a gate PLAN -- the last exact pass's T gates, taken in advance
+    # and verified after the pass from its own partials (a differing gate reruns it exactly): no
+    # batch-wide exchange inside the launch, so it also runs sharded and with more rows than the
+    # device holds at once.  None = where the gated pass does not apply (a sharded batch, rows
+    # beyond the resident grid), True = also on one GPU in place of the gated pass, False = never
+    pass_plan: Optional[bool] = None
 
 
 @dataclass
@@ -175,6 +181,14 @@ class FilterEngine:
         self.last_gate_pass = False  # the last run was the gated one-launch pass (gates decided in the launch)
         self.last_gates = None       # one shard's one-launch pass: its T gates (decided, or verified) [T] int32
         self.last_verify = None      # finish_pending's outcome: "ok", "fired" (a gate miss) or "fault"
+        # gate plans (cfg.pass_plan): the T gates the next auto pass follows (np.int32, the last exact
+        # or verified pass's), their device copy (one buffer, rewritten in place: a captured pass
+        # reads the current plan), plan passes run / missed
+        self._plan = None
+        self._plan_buf, self._plan_buf_val = None, None
+        self.last_plan_pass = False
+        self.plan_passes = 0
+        self.plan_misses = 0
 
     def __getstate__(self):
         # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
@@ -186,6 +200,7 @@ class FilterEngine:
         st["_shared_device"] = None
         st["step_events"] = None
         st["_hmapped"] = None  # (pinned host memory of this process)
+        st["_plan_buf"], st["_plan_buf_val"] = None, None
         return st
 
     def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False,
@@ -246,6 +261,60 @@ class FilterEngine:
         return bool(pass_ok and shard.world == 1 and c.resampler == "soft" and not c.force_resample
                     and c.pass_gate is not False and c.NF_dyn and c.NF_cond
                     and getattr(self, "_gate_resident", False))
+
+    def _plan_capable(self, pass_ok) -> bool:
+        """Can the one-launch pass follow a gate plan (the C2 shape's gated kernel with
+        d.pass_plan: soft resampler, not forced; any world size, rows in resident chunks)?"""
+        c = self.cfg
+        return bool(pass_ok and c.resampler == "soft" and not c.force_resample and c.NF_dyn and c.NF_cond
+                    and c.pass_gate is not False and c.pass_plan is not False
+                    and os.environ.get("NFDPF_PASS_PLAN", "1") != "0")
+
+    def _plan_wanted(self, pass_ok, gate_ok) -> bool:
+        """Auto mode: do gate plans replace the other gate strategies for these shapes?  Where the
+        gated pass does not apply (a sharded batch: its alternative is one exchange per step; rows
+        beyond the resident grid), or everywhere with cfg.pass_plan True (or NFDPF_PASS_PLAN=1)."""
+        return self._plan_capable(pass_ok) and (not gate_ok or self.cfg.pass_plan is True
+                                                or os.environ.get("NFDPF_PASS_PLAN") == "1")
+
+    def _plan_select(self, pass_ok, gate_ok, T, auto, plan, finish, dev):
+        """The next pass's plan (np.int32 [T]) and its device buffer, or (None, None).  Explicit
+        ``plan`` (run(plan=...)), else auto: the engine's plan when gate plans are wanted and it
+        fires some gate (with none, the speculative pass is the same launch with less to do)."""
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if plan is not None:
+            if not self._plan_capable(pass_ok):
+                raise L.NfdpfError("FilterEngine.run: plan= needs the C2-shaped one-launch pass (soft resampler, "
+                                   "NF_dyn and NF_cond, not forced; cfg.pass_plan not False)")
+            p = np.asarray(plan).astype(np.int32).reshape(-1)
+            if p.shape[0] != T:
+                raise L.NfdpfError(f"FilterEngine.run: plan= has {p.shape[0]} gates for T={T} steps")
+        else:
+            p = self._plan
+            if not (auto and p is not None and p.shape[0] == T and p.any() and self._plan_wanted(pass_ok, gate_ok)):
+                return None, None
+            if finish and capturing:  # (nothing could verify it after the replay)
+                return None, None
+        buf = self._plan_buf
+        if buf is None or buf.device != dev or buf.numel() != T:
+            if capturing:
+                return None, None
+            buf = self._plan_buf = torch.empty(T, device=dev, dtype=torch.int32)
+            self._plan_buf_val = None
+        if self._plan_buf_val is None or not np.array_equal(self._plan_buf_val, p):
+            if capturing:  # (a captured pass reads the buffer as it stands)
+                return None, None
+            buf.copy_(torch.from_numpy(p))  # (stream-ordered: passes already queued read the old plan)
+            self._plan_buf_val = p.copy()
+        return p, buf
+
+    def plans(self, shard=None) -> bool:
+        """Whether run() (auto arguments) will follow a gate plan in its next pass (same shapes as
+        the last run): like a speculative pass, its gates are verified after the pass."""
+        shard = shard or ShardInfo()
+        p = self._plan
+        return bool(self.cfg.speculate_gate is None and p is not None and p.any()
+                    and self._plan_wanted(self.last_pass_ok, self._gate_ok(shard, self.last_pass_ok)))
 
     def _pass_supported(self, B, N, T, E, split_nets, shard) -> bool:
         """Can this configuration run its whole pass as one launch (nfdpf_filter_pass_supported:
@@ -376,7 +445,7 @@ class FilterEngine:
     @torch.no_grad()
     def run(self, enc: torch.Tensor, start_state: torch.Tensor, vel_input: torch.Tensor,
             shard: Optional[ShardInfo] = None, host: Optional[HostDraws] = None, init=None,
-            teacher=None, finish: bool = True, speculate: Optional[bool] = None) -> FilterResult:
+            teacher=None, finish: bool = True, speculate: Optional[bool] = None, plan=None) -> FilterResult:
         """``teacher`` (tests only): dict with the reference's own history ``x`` (B,T,N,2) and
         ``p`` (B,T,N); step t then starts from the reference's step t-1 state and its gate
         is the reference's own torch expression (one-step parity).
@@ -386,7 +455,14 @@ class FilterEngine:
         verified from all steps' gathered partials (one all-gather) and a fired gate reruns
         the pass with the per-step exchange -- the result is the reference's either way.
         ``finish=False`` leaves the verification to ``finish_pending()`` (the pass itself is
-        then free of collectives and host syncs: capturable in a graph)."""
+        then free of collectives and host syncs: capturable in a graph).
+
+        Gate plans (cfg.pass_plan; ``plan``: T gates given explicitly): the one-launch pass
+        follows the plan's gates, with no batch-wide exchange inside the launch, and its actual
+        gates are verified after it like a speculative pass's (one shard: its epilogue; sharded:
+        the gathered partials).  A differing gate reruns the pass exactly (one GPU: gated; sharded:
+        once more with the corrected plan, then the per-step exchange) and the engine's plan
+        becomes the actual gates."""
         c = self.cfg
         dev = enc.device
         L.require_device(enc, "FilterEngine.run")
@@ -420,14 +496,25 @@ class FilterEngine:
                    and self._pass_supported(B, N, T, E, split_nets, shard))
         self.last_pass_ok = pass_ok
         gate_ok = self._gate_ok(shard, pass_ok)
-        spec = self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish,
-                                 pass_ok=pass_ok, gate_ok=gate_ok)
+        plan_arr, plan_buf = self._plan_select(pass_ok, gate_ok, T, auto, plan, finish, dev)
+        plan_pass = plan_arr is not None
+        spec = False if plan_pass else \
+            self._decide_spec(shard, speculate, host_mode, teacher is not None, consume=True, finish=finish,
+                              pass_ok=pass_ok, gate_ok=gate_ok)
         # the one-launch pass: gates speculated (verified after it), decided inside the launch
-        # (one GPU, soft resampler), or every step resampling (--force-resample: no gate to
-        # decide, the row's resampling runs inside the launch)
-        gate_pass = gate_ok and not spec
+        # (one GPU, soft resampler), following a plan (verified after it), or every step
+        # resampling (--force-resample: no gate to decide, the row's resampling runs inside the launch)
+        gate_pass = (gate_ok and not spec) or plan_pass
         use_pass = pass_ok and (spec or c.force_resample or gate_pass)
-        self.last_gate_pass = gate_pass
+        self.last_gate_pass = gate_pass and not plan_pass
+        self.last_plan_pass = plan_pass
+        checked = spec or plan_pass  # the gates are verified after the pass
+        # an exact run by the step launches where gate plans apply (sharded; rows beyond the
+        # resident grid): keep every step's (gathered) input partials, so that the run's gates
+        # become the engine's plan (the next passes follow it)
+        record = (tiled and not checked and not use_pass and not host_mode and teacher is None
+                  and self._plan_capable(pass_ok))
+        hist1 = record and shard.world == 1  # (one shard: its partials history is the record)
         self.last_gates = None  # (set below by a one-shard one-launch pass; never a previous run's)
 
         f32 = dict(device=dev, dtype=torch.float32)
@@ -446,7 +533,7 @@ class FilterEngine:
             tiles = ops.tiled_tiles(N)
             # per-(row, tile) softmax partials {max u, sum e, sum e^2, max lik} of each step:
             # the next step's gate and (deferred) normalisation derive from them
-            if spec or use_pass:  # every step's partials kept for the verification
+            if spec or use_pass or hist1:  # every step's partials kept for the verification
                 ess_hist = torch.empty((T + 1, B, tiles, 4), device=dev, dtype=torch.float64)
                 ess_bufs = [ess_hist[t] for t in range(1, T + 1)]
                 ess0 = ess_hist[0]
@@ -477,12 +564,15 @@ class FilterEngine:
         if tiled:
             ws = ops.tiled_workspace(B, N, T, dev)
             gather_buf = torch.empty((shard.B_global, tiles, 4), device=dev, dtype=torch.float64) \
-                if shard.world > 1 and not spec else None
+                if shard.world > 1 and not checked else None
         else:
             ess_bufs = [torch.empty(B, **f32), torch.empty(B, **f32)]
             ess0 = ie0
             gather_buf = torch.empty(shard.B_global, **f32) if shard.world > 1 else None
-        ess_all = ess0 if spec else self._gather(ess0, shard, gather_buf)
+        # (record: step t's gathered input partials at gather_hist[t]; one shard, its own at ess_hist[t])
+        gather_hist = torch.empty((T, shard.B_global, tiles, 4), device=dev, dtype=torch.float64) \
+            if record and shard.world > 1 else None
+        ess_all = ess0 if checked else self._gather(ess0, shard, gather_hist[0] if gather_hist is not None else gather_buf)
         gate_buf = torch.empty(1, device=dev, dtype=torch.int32)
         # (the step launches' speculative gate word; the one-launch pass reads none)
         spec_gate = torch.zeros(1, device=dev, dtype=torch.int32) if spec and not use_pass else None
@@ -521,7 +611,7 @@ class FilterEngine:
         d.hist_x, d.hist_p, d.hist_noise, d.hist_lik = hx.data_ptr(), hp.data_ptr(), hn.data_ptr(), hl.data_ptr()
         d.hist_jac, d.hist_prior, d.hist_idx = L.ptr(hj), L.ptr(hr), hi.data_ptr()
         d.lw_sum, d.pred, d.scratch = lw_sum.data_ptr(), pred.data_ptr(), scratch.data_ptr()
-        d.ess_local = int(spec)
+        d.ess_local = int(checked)
 
         fired = [] if host_mode else None
         self.last_ot_calls = 0
@@ -558,6 +648,8 @@ class FilterEngine:
                 pdyn, pcond = self._pass_blobs(dev)
                 d.dyn_params, d.cond_params = pdyn.data_ptr(), pcond.data_ptr()
             d.pass_gate = int(gate_pass)
+            d.pass_plan = plan_buf.data_ptr() if plan_pass else None
+            self.plan_passes += int(plan_pass)
             if shard.world == 1:  # the epilogue verifies the gates / reads the fault counter on the device
                 i32 = dict(device=dev, dtype=torch.int32)
                 pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(3, **i32),
@@ -565,7 +657,7 @@ class FilterEngine:
                 self.last_gates = pass_out[0]  # the T gates: decided in the launch, or verified
                 d.pass_gates, d.pass_flags, d.pass_obs = L.ptr(pass_out[0]), L.ptr(pass_out[1]), L.ptr(pass_out[2])
                 capturing = torch.cuda.is_current_stream_capturing()
-                if spec or capturing or not finish:
+                if checked or capturing or not finish:
                     # the pass's {fired, faults, done} straight into pinned, device-mapped host memory
                     # (ops.HostMapped): read without a copy launch once the pass is complete -- the
                     # speculative pass's verification, and the fault check of a gated / forced pass
@@ -604,7 +696,7 @@ class FilterEngine:
                 d.ess_all, d.ess_out, d.gate = ess_in_p[t], ess_out_p[t], spec_gate_p
             else:
                 d.ess_all = ess_all.data_ptr()
-                d.ess_out = ess_out_p[t & 1]
+                d.ess_out = ess_out_p[t if hist1 else t & 1]
                 d.gate = None
             d.host_noise = d.host_offsets = None
             if host_mode:
@@ -692,9 +784,10 @@ class FilterEngine:
             if spec:
                 pass
             elif shard.world > 1:
-                ess_all = self._gather(ess_bufs[t & 1], shard, gather_buf)
+                ess_all = self._gather(ess_bufs[t & 1], shard,
+                                       gather_hist[t + 1] if gather_hist is not None and t + 1 < T else gather_buf)
             else:
-                ess_all = ess_bufs[t & 1]
+                ess_all = ess_bufs[t if hist1 else t & 1]
         # a wave-pair hand-off that timed out leaves stale data (csrc/split.hpp): fail loudly
         # (a stream-ordered read and a sync: deferred to finish_pending when the caller asked
         # for a pass free of host syncs)
@@ -705,7 +798,10 @@ class FilterEngine:
                                     and os.environ.get("NFDPF_CM_TWO_CHAIN", "0") == "1")
         capturing = torch.cuda.is_current_stream_capturing()
         check_split = tiled and handoffs and not capturing
-        if use_pass and not spec:
+        if record:  # the exact run's gates: the plan of the next passes
+            self._plan = ops.ess_gate_tiled_batch(gather_hist if gather_hist is not None else ess_hist[:T], N, 0,
+                                                  False).cpu().numpy()
+        if use_pass and not checked:
             # a forced or gated pass: one shard's epilogue read the fault counter and reduced the
             # obs-likelihood (one host read here); sharded, every rank's count is summed so that all
             # ranks fall back together.  Captured in a graph, or run(finish=False): the flags are
@@ -720,6 +816,8 @@ class FilterEngine:
             if not capturing:
                 if pass_out is not None:
                     n_fired, faults = pass_out[1].tolist()[:2]
+                    if gate_pass and not faults and self._plan_wanted(pass_ok, gate_ok):
+                        self._plan = pass_out[0].cpu().numpy()  # the gates it decided: the next passes' plan
                 else:
                     n_fired, faults = 0, self._faults_all(shard, dev)
                 if faults:  # the grid was not all resident: the step launches instead
@@ -735,7 +833,7 @@ class FilterEngine:
         # one-shard speculative pass: the gates and the fault counter are verified on the device
         # (the one-launch pass's epilogue, or ops.pass_verify after the step launches -- both
         # capturable) and read once in finish_pending
-        verify_dev = spec and tiled and shard.world == 1
+        verify_dev = checked and tiled and shard.world == 1
         if check_split and (finish or not spec) and not verify_dev and not use_pass:
             L.check_split_fault("nfdpf_filter_step_tiled", dev)
             check_split = False
@@ -743,14 +841,16 @@ class FilterEngine:
             self._ot_fired = self.last_ot_calls > 0
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
         tot = None if verify_dev else lw_sum.double().sum(0)  # (verified on the device: reduced there)
-        if spec:
+        if checked:
             res = FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, None, pred, fired)
             verify = None
             if verify_dev:
                 verify = [pass_out[1] if flags_host is None else None, pass_out[2], flags_host, flags_lease] \
                     if pass_out is not None else list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None, None]
                 check_split = False
-            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass, False)
+            # (+ the plan followed, and one shard's actual gates: a miss's new plan)
+            self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass, False,
+                             plan_arr, pass_out[0] if pass_out is not None else None)
             if not finish:
                 return res  # the caller verifies (finish_pending, e.g. after each graph replay)
             ok = self.finish_pending()
@@ -763,6 +863,13 @@ class FilterEngine:
                 # the pass's grid was not resident (not a gate miss): the one-launch pass is now off
                 # for this engine and the step launches rerun it; the speculation state is left alone
                 return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, speculate=speculate)
+            if plan_pass:
+                # a gate differed from the plan: the pass again, exactly -- one GPU with every row
+                # resident, gated; else the step launches with the batch gate per step -- and the
+                # gates it takes become the plan (a plan of a pass that missed is exact only up to
+                # its first differing gate: following it again would fix one more gate per pass)
+                self.plan_misses += 1
+                return self.run(enc, start_state, vel_input, shard=shard, host=host, init=init, speculate=False)
             # a gate fired: the pass again, gated (one GPU, the one-launch pass: the gates decided in
             # the launch; the next passes stay gated while gates keep firing) or with the per-step
             # exchange
@@ -852,6 +959,8 @@ class FilterEngine:
         pend = pending if pending is not None else self._pending
         parts, tot, shard, N, res, split_dev, verify, was_pass = pend[:8]
         decided = len(pend) > 8 and pend[8]  # the gates were decided inside the launch
+        # a plan pass: the plan it followed, and one shard's actual gates (its epilogue's)
+        plan, gates_dev = (pend[9], pend[10]) if len(pend) > 10 else (None, None)
         self.last_verify = "ok"
         if verify is not None:  # the device verification's flags: the one host synchronisation
             if verify[0] is None:  # mapped from host memory: complete once the stream is
@@ -869,8 +978,10 @@ class FilterEngine:
                 self._pass_fault(faults)  # the one-launch pass's grid was not resident: rerun step by step
                 self.last_verify = "fault"
                 return False
-            if fired and not decided:
+            if fired and not decided:  # (a plan pass: `fired` counts the gates that differ from the plan)
                 self.last_verify = "fired"
+                if plan is not None:
+                    self._plan = gates_dev.cpu().numpy()  # exact up to its first differing gate
                 return False
             res.obs_likelihood = verify[1]
             return True
@@ -888,7 +999,13 @@ class FilterEngine:
         if shard.world > 1:
             dist.all_reduce(tot, group=shard.group)
         gates = ops.ess_gate_tiled_batch(parts, N, 0, False)
-        if bool(gates.any()):
+        if plan is not None:  # the pass followed a plan: its actual gates must be the plan's
+            g = gates.cpu().numpy()
+            if not np.array_equal(g, plan):
+                self.last_verify = "fired"
+                self._plan = g
+                return False
+        elif bool(gates.any()):
             self.last_verify = "fired"
             return False
         res.obs_likelihood = (tot / (shard.B_global * N)).sum().float()

@@ -219,3 +219,77 @@ def test_sharded_pass_matches_unsharded(kind, tmp_path):
                 assert torch.equal(part[f], full[f][r * h:(r + 1) * h]), (kind, f, r)
         a, b = float(part["obs_likelihood"]), float(full["obs_likelihood"])
         assert abs(a - b) <= 1e-6 * abs(b), (a, b)
+
+
+# ---- gate plans, sharded: the exact run (per-step exchange) records the batch's gates, the next
+# pass follows them as one launch per rank (no exchange inside it) and one all-gather verifies it
+def _plan_run(rows, shard=None, rank=0, world=1):
+    import torch.distributed as dist
+    from nfdpf.engine import FilterConfig, FilterEngine
+    B, N, T = PASS_CASES["firing"]
+    models, enc, start, vel = _pass_inputs("firing", rows)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321,
+                       kernel="tiled", pass_plan=True)  # (unsharded: the gated pass's decisions, then plans)
+    eng = FilterEngine(cfg, models)
+    eng.run(enc, start, vel, shard=shard, speculate=False)  # exact; its gates become the plan
+    plan = None if eng._plan is None else eng._plan.copy()
+    for r in range(world):  # (the ranks share the one GPU: each pass's grid resident by itself)
+        if r == rank:
+            res = eng.run(enc, start, vel, shard=shard, finish=False)
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+    planned = eng.last_plan_pass
+    verified = eng.finish_pending()
+    eng._pending = None
+    torch.cuda.synchronize()
+    out = {f: getattr(res, f).cpu() for f in FIELDS if getattr(res, f) is not None}
+    out["obs_likelihood"] = res.obs_likelihood.cpu() if verified else torch.tensor(float("nan"))
+    out["planned"], out["verified"], out["plan"] = planned, verified, torch.from_numpy(plan)
+    return out
+
+
+def _worker_plan(rank, world, port, path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root, os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NFDPF_PASS_SHARED_OK="1")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf import _lib
+        from nfdpf.engine import ShardInfo
+        _lib.load()
+        B = PASS_CASES["firing"][0] // world
+        out = _plan_run((rank * B, (rank + 1) * B), ShardInfo.from_env(B), rank, world)
+        torch.save(out, f"{path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_plan_pass_matches_unsharded(tmp_path):
+    """The firing case on two ranks: the exact sharded run (step launches, one all-gather per
+    step) records the same batch gates as the unsharded gated pass decides; the next pass on each
+    rank follows them as ONE launch with no exchange inside (d.pass_plan) and the one all-gather
+    after it verifies them -- bit for bit the unsharded plan pass (every history; obs to 1e-6)."""
+    import torch.multiprocessing as mp
+    from nfdpf import _lib
+    _lib.load()
+    B = PASS_CASES["firing"][0]
+    full = _plan_run((0, B))
+    assert full["planned"] and full["verified"] and int(full["plan"].sum()) > 0
+    world = 2
+    path = str(tmp_path / "plan")
+    mp.start_processes(_worker_plan, args=(world, _free_port(), path), nprocs=world, start_method="spawn")
+    parts = [torch.load(f"{path}.{r}", weights_only=True) for r in range(world)]
+    h = B // world
+    for r, part in enumerate(parts):
+        assert torch.equal(part["plan"], full["plan"]), (r, part["plan"], full["plan"])
+        assert part["planned"] and part["verified"], (r, part["planned"], part["verified"])
+        for f in FIELDS:
+            if f in full:
+                assert torch.equal(part[f], full[f][r * h:(r + 1) * h]), (f, r)
+        a, b = float(part["obs_likelihood"]), float(full["obs_likelihood"])
+        assert abs(a - b) <= 1e-6 * abs(b), (a, b)

@@ -682,3 +682,119 @@ def test_auto_mode_switches_between_speculative_and_gated():
         assert eng.last_gate_pass and int(eng.last_gates.sum()) == 0
     eng.run(*quiet)
     assert eng.last_pass and not eng.last_gate_pass, "two quiet gated passes: speculation again"
+
+
+def _c2_full(B, N, T, **kw):
+    import _fullsize as F
+    from nfdpf.engine import FilterConfig, FilterEngine
+    wl = F.workload("c2_full", B=B, N=N, T=T)
+    models = wl["models"].to(DEV)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=5, kernel="tiled", **kw)
+    return FilterEngine(cfg, models), (wl["enc"].to(DEV), wl["start"].to(DEV), wl["vel"].to(DEV))
+
+
+PLAN_FIELDS = ("particles", "probs", "noise", "lik", "index", "jac", "prior", "pred", "obs_likelihood")
+
+
+@pytest.mark.parametrize("B,N,T", [(8, 1000, 16), (64, 1000, 50), (5, 777, 9)])
+def test_plan_pass_equals_gated(B, N, T, monkeypatch):
+    """The pass following a gate plan (d.pass_plan: no batch-wide exchange inside the launch) given
+    the gated pass's own decisions == the gated pass, bit for bit (histories, decisions, obs); its
+    epilogue verifies the plan against the pass's own partials: no rerun.  The gated pass's motion
+    noise is the step launches' (Philox keyed on step, row, particle) at every step -- also at the
+    steps whose speculated attempt it dropped and redid after the gate fired."""
+    eng_g, inp = _c2_full(B, N, T, speculate_gate=False)
+    g = eng_g.run(*inp)
+    assert eng_g.last_gate_pass
+    gates = eng_g.last_gates.cpu().numpy()
+    monkeypatch.setenv("NFDPF_PASS", "0")
+    eng_s, _ = _c2_full(B, N, T, speculate_gate=False)
+    s = eng_s.run(*inp)
+    monkeypatch.delenv("NFDPF_PASS")
+    assert not eng_s.last_pass
+    assert torch.equal(s.noise, g.noise), "the gated pass's motion noise differs from the step launches'"
+    if T >= 16:
+        assert 0 < gates.sum() < T, "the case should mix fired and quiet steps"
+    eng_p, _ = _c2_full(B, N, T)
+    p = eng_p.run(*inp, plan=gates)
+    assert eng_p.last_plan_pass and eng_p.pass_launches == 1 and eng_p.last_verify == "ok" and eng_p.plan_misses == 0
+    assert np.array_equal(eng_p.last_gates.cpu().numpy(), gates)
+    for f in PLAN_FIELDS:
+        assert torch.equal(getattr(p, f), getattr(g, f)), f
+
+
+@pytest.mark.parametrize("flip", ["drop", "add"])
+def test_plan_pass_wrong_plan_reruns(flip):
+    """A plan that differs from the actual gates (a fired gate dropped, or a quiet step resampled):
+    the verification catches it, the pass reruns exactly (the gated pass) and the engine's plan
+    becomes that pass's gates; the result is the gated pass's, bit for bit."""
+    B, N, T = 8, 1000, 16
+    eng_g, inp = _c2_full(B, N, T, speculate_gate=False)
+    g = eng_g.run(*inp)
+    gates = eng_g.last_gates.cpu().numpy()
+    wrong = gates.copy()
+    k = int(np.flatnonzero(gates)[-1]) if flip == "drop" else int(np.flatnonzero(gates == 0)[-1])
+    wrong[k] ^= 1
+    eng, _ = _c2_full(B, N, T, pass_plan=True)
+    r = eng.run(*inp, plan=wrong)
+    assert eng.plan_misses == 1 and eng.pass_launches == 2 and eng.last_gate_pass and not eng.last_plan_pass
+    assert np.array_equal(eng._plan, gates)
+    for f in PLAN_FIELDS:
+        assert torch.equal(getattr(r, f), getattr(g, f)), f
+
+
+def test_auto_plan_mode_one_gpu():
+    """cfg.pass_plan = True on one GPU: the first pass speculates and misses, the gated rerun's
+    decisions become the plan, and the next passes follow it (verified, no rerun) -- the gated
+    pass's result each time; a hipGraph-captured plan pass (run(finish=False), finish_pending
+    after the replay) too."""
+    B, N, T = 8, 1000, 16
+    eng, inp = _c2_full(B, N, T, pass_plan=True)
+    g = eng.run(*inp)
+    assert eng.pass_launches == 2 and eng.last_gate_pass and eng._plan is not None and eng._plan.any()
+    assert eng.plans()
+    for _ in range(2):
+        p = eng.run(*inp)
+        assert eng.last_plan_pass and eng.last_verify == "ok" and eng.plan_misses == 0
+        for f in PLAN_FIELDS:
+            assert torch.equal(getattr(p, f), getattr(g, f)), f
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        cap = eng.run(*inp, finish=False)
+    pend = eng.take_pending()
+    assert eng.last_plan_pass
+    for _ in range(2):
+        eng.arm_flags(pend)
+        graph.replay()
+        assert eng.finish_pending(pend), eng.last_verify
+        for f in PLAN_FIELDS:
+            assert torch.equal(getattr(cap, f), getattr(g, f)), f
+
+
+def test_plan_pass_rows_beyond_resident():
+    """More rows than the device holds at once (the gated pass does not apply): auto mode's
+    speculative pass misses, the exact rerun (step launches, the batch gate per step) records its
+    gates as the plan, and the next pass follows it in resident chunks of rows -- verified (its
+    gates are the step launches') and, row for row, bit-equal to a resident plan pass of the first
+    rows given the same plan (rows depend on the batch only through the gates)."""
+    from nfdpf import _lib as L
+    N, T = 1000, 12
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    B = min(256, 2 * (cus // 4) + 8)  # (4 workgroups a row at N = 1000: more rows than CUs / 4)
+    eng, inp = _c2_full(B, N, T)
+    eng.run(*inp)
+    assert eng.last_pass_ok and not eng._gate_resident, "the gated pass should not fit this many rows"
+    assert eng._plan is not None and eng._plan.any(), "the exact rerun recorded no firing plan"
+    plan = eng._plan.copy()
+    p = eng.run(*inp)
+    assert eng.last_plan_pass and eng.last_verify == "ok" and eng.plan_misses == 0
+    assert np.array_equal(eng.last_gates.cpu().numpy(), plan)
+    b = min(8, B)
+    eng_s, _ = _c2_full(b, N, T)
+    sub = eng_s.run(*(x[:b] for x in inp), plan=plan, finish=False)
+    eng_s.take_pending()
+    torch.cuda.synchronize()
+    for f in PLAN_FIELDS[:-1]:
+        assert torch.equal(getattr(sub, f), getattr(p, f)[:b]), f
+    assert L.lib().nfdpf_split_fault(1, torch.cuda.current_stream().cuda_stream) == 0
