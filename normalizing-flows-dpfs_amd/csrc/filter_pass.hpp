@@ -73,7 +73,7 @@ struct PassHdr {
 
 #ifdef NFDPF_EXP_PTRACE
 // experiment-only: per-step phase timestamps (s_memrealtime, 100 MHz) of waves 0, 1 and 8 of
-// every workgroup, steps < 64 (scripts/exp_ptrace.py)
+// every workgroup, steps < 64 (scripts/archive/exp_ptrace.py)
 __device__ unsigned long long g_ptrace[256][16][64][20];
 #define PT(t, k)                                                                                   \
   do {                                                                                             \

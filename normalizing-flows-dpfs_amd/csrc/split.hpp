@@ -332,7 +332,7 @@ __device__ __forceinline__ float net_split(cf2 *w, float u, const f2 *cb) {
 // RealNVP_cond flow, forward (nf/flows.py:215-226) / inverse (:228-239), split over a wave
 // pair.  fw = the flow's split block (kSplitFlow floats, wave-uniform), cbs = its folded
 // biases in split order (16 pairs).  Both waves end with identical lo, up and log-det.
-// NFDPF_EXP_SAMEW (experiment builds only, scripts/exp_build.sh; wrong results): every net of
+// NFDPF_EXP_SAMEW (experiment builds only, scripts/archive/exp_build.sh; wrong results): every net of
 // a stack reads the first net's weights -- the scalar-cache footprint of the coupling nets
 // shrinks from 16 nets to 2, which prices their weight misses.
 #ifdef NFDPF_EXP_SAMEW

@@ -156,7 +156,7 @@ def load(path: str = LIB_PATH):
         raise NfdpfError(f"libnfdpf.so not found at {path}: build it with "
                          f"`python -c 'import __graft_entry__ as g; g.build()'` or `make -C {PKG_DIR}/csrc`")
     lib = ctypes.CDLL(path)
-    # NFDPF_LIB_PARTIAL=1 (experiment builds of older sources, scripts/exp_run.sh only): skip
+    # NFDPF_LIB_PARTIAL=1 (experiment builds of older sources, scripts/archive/exp_run.sh only): skip
     # entry points the library lacks; otherwise a missing symbol is an error
     partial = os.environ.get("NFDPF_LIB_PARTIAL") == "1"
     for name, (res, args) in SIGNATURES.items():

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of experiment libraries on the C2 bench line: scripts/exp_ab.sh base W8 W32 ...
+# A/B of experiment libraries on the C2 bench line: scripts/archive/exp_ab.sh base W8 W32 ...
 # (base = the in-tree libnfdpf.so); one bench run per lib, ms_per_step printed
 export TMPDIR=/tmp
 mkdir -p gpurun_out

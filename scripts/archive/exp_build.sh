@@ -1,6 +1,6 @@
 #!/bin/bash
 # Experiment builds of libnfdpf.so with -D flags (never shipped): exp/lib_<TAG>.so
-#   scripts/exp_build.sh TRACE -DNFDPF_EXP_TRACE
+#   scripts/archive/exp_build.sh TRACE -DNFDPF_EXP_TRACE
 set -e
 TAG=$1; shift
 cd "$(dirname "$0")/../normalizing-flows-dpfs_amd/csrc"

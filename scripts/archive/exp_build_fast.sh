@@ -2,8 +2,8 @@
 # Experiment build of libnfdpf.so with -D flags applied to one source only (SRC, default
 # filter_tiled: the pass and the step launches); the other objects are the in-tree build's:
 # exp/lib_<TAG>.so (never shipped)
-#   scripts/exp_build_fast.sh S3B -DNFDPF_SWEEP_WE=3 -DNFDPF_SWEEP_PRIO=3
-#   SRC=cglow scripts/exp_build_fast.sh CGD -DNFDPF_EXP_CGDUMP -DNFDPF_CG_TARGET=68339
+#   scripts/archive/exp_build_fast.sh S3B -DNFDPF_SWEEP_WE=3 -DNFDPF_SWEEP_PRIO=3
+#   SRC=cglow scripts/archive/exp_build_fast.sh CGD -DNFDPF_EXP_CGDUMP -DNFDPF_CG_TARGET=68339
 set -e
 TAG=$1; shift
 SRC=${SRC:-filter_tiled}

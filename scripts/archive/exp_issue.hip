@@ -1,6 +1,6 @@
 // Issue-cost microbenchmark (experiment only): cycles per instruction of one wave's stream of
 // independent / dependent v_pk_fma_f32, v_fma_f32, v_exp_f32, v_rcp_f32 on gfx950, with W waves
-// per SIMD.  Built by hand: hipcc --offload-arch=gfx950 -O3 scripts/exp_issue.hip -o exp/issue_bench
+// per SIMD.  Built by hand: hipcc --offload-arch=gfx950 -O3 scripts/archive/exp_issue.hip -o exp/issue_bench
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef float f2 __attribute__((ext_vector_type(2)));

@@ -1,5 +1,5 @@
 """Experiment: per-step phase timestamps of the one-launch pass (lib built with
--DNFDPF_EXP_PTRACE, loaded through NFDPF_LIB; scripts/exp_build.sh PTRACE -DNFDPF_EXP_PTRACE).
+-DNFDPF_EXP_PTRACE, loaded through NFDPF_LIB; scripts/archive/exp_build.sh PTRACE -DNFDPF_EXP_PTRACE).
 C2 bench workload, the last of 3 passes; durations in us, median over the 256 workgroups and
 steps 4..45.
 Chain waves 0-3: 0 step start, 1 A published, 2 nf_dyn context folded (fA), 3 nf_dyn inverse

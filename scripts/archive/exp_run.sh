@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing of experiment builds (exp/lib_<V>.so, scripts/exp_build.sh) on one box: the default
+# Timing of experiment builds (exp/lib_<V>.so, scripts/archive/exp_build.sh) on one box: the default
 # bench per variant, alternating rounds; prints value, live proposal-launch and front-launch ms.
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 """Experiment: phases of the merged front launch (tiled_fdyn_kernel) of the last step of a C2
-pass, lib built with -DNFDPF_EXP_TRACE (scripts/exp_build.sh TRACE -DNFDPF_EXP_TRACE), loaded
+pass, lib built with -DNFDPF_EXP_TRACE (scripts/archive/exp_build.sh TRACE -DNFDPF_EXP_TRACE), loaded
 through NFDPF_LIB.  Slots (us from the workgroup's start, median / max over 256 workgroups):
 4 gate wave: partials loaded + per-row terms staged; 5 gate decided; 6 wave 1: its sources
 landed; 7 wave 1: speculative row motion summed; 1 barrier; 2 row context + folds; 3 end."""

@@ -10,7 +10,7 @@ if [ -n "$TESTS" ]; then
   rc=$?; tail -3 gpurun_out/r03_ab_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -f exp/lib_TRACE.so ]; then
-  NFDPF_LIB_PARTIAL=1 NFDPF_LIB=$PWD/exp/lib_TRACE.so timeout -k 10 200 python -u scripts/exp_trace_fdyn.py > gpurun_out/r03_trace_fdyn.log 2>&1
+  NFDPF_LIB_PARTIAL=1 NFDPF_LIB=$PWD/exp/lib_TRACE.so timeout -k 10 200 python -u scripts/archive/exp_trace_fdyn.py > gpurun_out/r03_trace_fdyn.log 2>&1
   rc=$?; tail -8 gpurun_out/r03_trace_fdyn.log; [ $rc -eq 0 ] || exit $rc
 fi
 for round in 1 2; do

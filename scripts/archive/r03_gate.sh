@@ -8,4 +8,4 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method threa
   tests/test_gpu_parity_full.py tests/test_gpu_dist.py tests/test_gpu_ot_speculate.py -k "c2 or gate or spec or shard or rows" \
   > gpurun_out/r03_gate_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r03_gate_tests.log; [ $rc -eq 0 ] || exit $rc
-VARIANTS="BASE NEW" bash scripts/r03_ab.sh
+VARIANTS="BASE NEW" bash scripts/archive/r03_ab.sh

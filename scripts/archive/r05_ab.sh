@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of experiment libraries on the C2 bench (quiet line + informative line), one box:
-#   [BENCH_EXTRA="--config c3"] scripts/r05_ab.sh OUTTAG base S3 S3B ...   (base = the in-tree library)
+#   [BENCH_EXTRA="--config c3"] scripts/archive/r05_ab.sh OUTTAG base S3 S3B ...   (base = the in-tree library)
 OUT=$1; shift
 mkdir -p gpurun_out
 for tag in "$@"; do

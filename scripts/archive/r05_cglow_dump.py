@@ -3,7 +3,7 @@ workload (tests/_fullsize.py: the oracle's teacher-forced run, CPU), evaluates O
 the reference's own particles of every step (the kernel-alone comparison of
 test_fullsize_teacher_forced) and saves the raw (unshifted) kernel likelihoods with the
 particles, encodings and the oracle float32 likelihoods, for a layer-by-layer analysis on the CPU
-(scripts/r05_cglow_layers.py).  GPU box: python scripts/r05_cglow_dump.py gpurun_out/r05_cglow.npz"""
+(scripts/r05_cglow_layers.py).  GPU box: python scripts/archive/r05_cglow_dump.py gpurun_out/r05_cglow.npz"""
 import os
 import sys
 

@@ -1,9 +1,9 @@
 """Experiment: dump OUR CGLOW kernel's per-particle 1x1-conv W, its
 log|det W| (the in-kernel LU's) and the actnorm outputs for the outlier particle
-(NFDPF_CG_TARGET of the exp build: SRC=cglow scripts/exp_build_fast.sh CGD -DNFDPF_EXP_CGDUMP
+(NFDPF_CG_TARGET of the exp build: SRC=cglow scripts/archive/exp_build_fast.sh CGD -DNFDPF_EXP_CGDUMP
 -DNFDPF_CG_TARGET=68339), on the c5_n10000 workload's step-2 reference particles (exp/cg_in.npz,
-cut from scripts/r05_cglow_dump.py's output).  GPU box:
-NFDPF_LIB=exp/lib_CGD.so python scripts/r05_cglow_w.py gpurun_out/r05_cgw.npz"""
+cut from scripts/archive/r05_cglow_dump.py's output).  GPU box:
+NFDPF_LIB=exp/lib_CGD.so python scripts/archive/r05_cglow_w.py gpurun_out/r05_cgw.npz"""
 import ctypes
 import os
 import sys

@@ -1,7 +1,7 @@
 """Experiment: where the wall time of the timed bench loop goes between the pass kernels -- reads
 a rocprofv3 --kernel-trace CSV (of `bench.py --no-forced --no-informative --no-cpu-baseline`) and
 prints, over the last K tiled_pass_kernel<0> launches, each kernel's mean duration and the mean
-idle gap before it (the GPU doing nothing).  python scripts/r05_gaps.py <kernel_trace.csv> [K]"""
+idle gap before it (the GPU doing nothing).  python scripts/archive/r05_gaps.py <kernel_trace.csv> [K]"""
 import csv
 import sys
 from collections import defaultdict

@@ -1,6 +1,6 @@
 """Experiment: where a step of the GATED one-launch pass (kModeGate; --spec: the speculative pass,
 --force: the forced pass) waits -- per-step phase
-timestamps (lib built with -DNFDPF_EXP_PTRACE: scripts/exp_build.sh PTRACE -DNFDPF_EXP_PTRACE,
+timestamps (lib built with -DNFDPF_EXP_PTRACE: scripts/archive/exp_build.sh PTRACE -DNFDPF_EXP_PTRACE,
 loaded through NFDPF_LIB).  C2 bench workload ([--informative]: frame encodings = the particle
 encoder at the true positions, the gate fires), the last of 3 passes; medians over the 256
 workgroups and steps 4..45, us.  Times are relative to the chain's hand-over of step t-1 (qf)."""

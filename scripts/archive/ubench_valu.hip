@@ -1,6 +1,6 @@
 // Experiment: issue cost per wave-instruction of the VALU ops the coupling nets use
 // (v_exp_f32, v_rcp_f32, v_fma_f32, v_pk_fma_f32, v_pk_mul_f32) at 1, 2, 4 waves per SIMD.
-// Build: hipcc -O3 -w --offload-arch=gfx950 scripts/ubench_valu.hip -o exp/ubench
+// Build: hipcc -O3 -w --offload-arch=gfx950 scripts/archive/ubench_valu.hip -o exp/ubench
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 

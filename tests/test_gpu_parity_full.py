@@ -171,7 +171,7 @@ def test_fullsize_teacher_forced(name):
     cglow = w["cfg"]["measurement"] == "CGLOW"
     if cglow:
         # The CGLOW likelihood is steep in the particle position (|d lik / d x| up to ~2e3 at
-        # C5, scripts/diag_c5.py), so a particle's own fp32 rounding (checked under "particles")
+        # C5, scripts/archive/diag_c5.py), so a particle's own fp32 rounding (checked under "particles")
         # moves it by ~1e-2 in any float32 evaluation.  The measurement is therefore asserted on
         # IDENTICAL particles: our CGLOW kernel on the reference's own teacher-forced proposals
         # against the float64 measurement there, next to the reference's float32 likelihood
@@ -192,7 +192,7 @@ def test_fullsize_teacher_forced(name):
         # W has cond 5.9e6, our W is within 1.2 ulp of the float64 W (rms error 9.2e-9, the
         # reference float32's 8.5e-9) and our LU's log|det| within 7e-3 of float64 slogdet of OUR
         # W, yet log|det W| moves 0.18 -- random W errors of that rms move it 0.044 median, 0.155
-        # at p99 (scripts/r05_cglow_w.py).  No layer is worse than the
+        # at p99 (scripts/archive/r05_cglow_w.py).  No layer is worse than the
         # reference's float32; the element is the tail of the conditioning amplification.
         qk, qr = np.quantile(e_k, 0.999), np.quantile(e_r, 0.999)
         sig = _cglow_w_sigma(w, ref[0])
