@@ -429,6 +429,19 @@ typedef struct nfdpf_filter_desc {
                                counts the steps where they differ from the plan in pass_flags[0];
                                the caller reruns with a corrected plan -- the result is the
                                reference's only when no step differs */
+  void **gate_peers;        /* nfdpf_filter_pass_tiled with pass_gate = 1 on a sharded batch
+                               (B_global != B, B_global <= 512), optional [gate_world] device array:
+                               every rank's gate-exchange buffer (nfdpf_gate_xchg_alloc, the peers'
+                               mapped by nfdpf_gate_xchg_open; entry gate_rank is this rank's own).
+                               Each step, each row's 1 / sum p^2 goes to every rank's buffer (one
+                               tagged 8-byte granule, system scope) and each rank sweeps its own
+                               buffer's B_global granules in global row order: the batch-global
+                               gate decided inside every rank's launch, identically (DPFs.py:163-165)
+                               -- the gated pass sharded.  Every rank's pass must run concurrently
+                               (the sweeps wait for each other; a wait that times out counts a
+                               hand-off fault as a non-resident grid does) */
+  int32_t gate_world;       /* ranks in gate_peers */
+  int32_t gate_rank;        /* this rank's index in gate_peers */
 } nfdpf_filter_desc;
 
 NFDPF_API int nfdpf_filter_step(const nfdpf_filter_desc *d, void *stream);
@@ -503,6 +516,18 @@ NFDPF_API int nfdpf_filter_init(const float *start, int start_rs, const float *v
  * launch).  No reference counterpart. */
 NFDPF_API int nfdpf_host_mapped_alloc(int64_t bytes, void **host, void **dev);
 NFDPF_API int nfdpf_host_mapped_free(void *host);
+/* The cross-rank gate exchange of the sharded gated pass (nfdpf_filter_desc.gate_peers): each rank
+ * allocates one buffer of nfdpf_gate_xchg_bytes(B_global) bytes in uncached device memory
+ * (zeroed; a 256-B header whose first word is the exchange's pass epoch, then [2][B_global]
+ * tagged granules), exports it as a 64-byte IPC handle, and maps every peer's buffer from its
+ * handle (hipIpcOpenMemHandle; over xGMI on one node).  close unmaps a peer's buffer, free
+ * releases this rank's own.  Replaces the per-step all-gather of the gate partials (DPFs.py:163:
+ * the batch-global mean) for the one-launch pass.  No reference counterpart. */
+NFDPF_API int64_t nfdpf_gate_xchg_bytes(int B_global);
+NFDPF_API int nfdpf_gate_xchg_alloc(int64_t bytes, void **dev, void *ipc_handle);
+NFDPF_API int nfdpf_gate_xchg_open(const void *ipc_handle, void **dev);
+NFDPF_API int nfdpf_gate_xchg_close(void *dev);
+NFDPF_API int nfdpf_gate_xchg_free(void *dev);
 NFDPF_API int nfdpf_filter_step_tiled(const nfdpf_filter_desc *d, void *workspace, void *stream);
 /* the ESS gate (DPFs.py:163-165) of step t from the [B][tiles][4] partials of step t-1
  * -> int32 [1] (OT path) */

@@ -56,6 +56,10 @@ namespace nfdpf {
 constexpr int kPassMaxTiles = 4;   // N <= 1024: one poll sweep of <= 192 granules per exchange
 constexpr int kPassMaxT = 4000;    // tag = (epoch << 12) + t + 1
 constexpr uint32_t kPassEpochMask = (1u << 20) - 1;  // the epoch's 20 bits of the 32-bit tag
+// the sharded gated pass's cross-rank gate exchange (d.gate_peers, nfdpf_gate_xchg_alloc): a
+// 256-B header (word 0: the exchange's pass epoch), then [2][B_global] tagged granules
+constexpr int kXgMaxRows = 512;
+constexpr int kXgHdr = 32;  // header, in granules
 constexpr int kGA = 8;             // granules per flow-wave publish: 4 doubles
 constexpr int kGC = 6;             // per encoder-wave publish: max (f32), sum e, sum e^2 (f64), pad
 
@@ -205,7 +209,7 @@ struct PassLds {
   int fD, rq;
   int dec[2];
   int hxf[4];
-  uint32_t rowe[256];
+  uint32_t rowe[kXgMaxRows];       // (B_global rows: the sharded gated pass's sweep of every rank's rows)
 };
 
 // A loop-invariant lane value made opaque inside a persistent step loop: the compiler would
@@ -308,7 +312,7 @@ struct NoWork {
 struct NoStop {
   __device__ bool operator()() const { return false; }
 };
-template <int NC = 3, class Work = NoWork, class Stop = NoStop>
+template <int NC = 3, class Work = NoWork, class Stop = NoStop, int SCOPE = __HIP_MEMORY_SCOPE_AGENT>
 __device__ int poll_rowx(const uint64_t *g, int n, uint32_t tag, uint32_t *dst, Work work = Work(),
                          Stop stop = Stop()) {
   const int l = threadIdx.x & 63;
@@ -323,7 +327,7 @@ __device__ int poll_rowx(const uint64_t *g, int n, uint32_t tag, uint32_t *dst, 
   auto sweep = [&]() {
 #pragma unroll
     for (int c = 0; c < NC; ++c)
-      if (!ok[c]) v[c] = __hip_atomic_load(g + 64 * c + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!ok[c]) v[c] = __hip_atomic_load(g + 64 * c + l, __ATOMIC_RELAXED, SCOPE);
   };
   sweep();
   work();
@@ -1191,6 +1195,34 @@ __device__ __forceinline__ float pass_poll_c(const nfdpf_filter_desc &d, const P
   return inv;
 }
 
+// kModeGate on a sharded batch (d.gate_peers): this row's term goes to every rank's exchange buffer
+// (one granule per rank, system scope: over xGMI to the peers), then this rank's own buffer is
+// swept for all B_global terms -- in global row order, so every rank sums the same words in the
+// same order and takes the same decision.  The slot parity follows the exchange's running step
+// count (epoch x T + t): a rank may run one step ahead of the slowest, also across passes.
+// (t = 0: the row's term from its initial partials, as the unsharded t = 0 sum.)  -> the decision
+__device__ __forceinline__ int pass_gate_xrank(const nfdpf_filter_desc &d, PassLds &L, int b, int tile, int t,
+                                               float inv) {
+  const int tiles = n_tiles(d.N), lane = threadIdx.x & 63, Bg = d.B_global;
+  uint64_t *const *peers = reinterpret_cast<uint64_t *const *>(d.gate_peers);
+  const uint64_t *own = peers[d.gate_rank];
+  const uint32_t xep =
+      __hip_atomic_load(reinterpret_cast<const uint32_t *>(own), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t tag = (xep << 12) + (uint32_t)t + 1u;
+  const int64_t slot = kXgHdr + (int64_t)(((uint64_t)xep * (uint64_t)d.T + (uint64_t)t) & 1u) * Bg;
+  const float r = t == 0 ? row_inv_ess(reinterpret_cast<const double *>(d.ess_all) + (int64_t)b * tiles * kSm,
+                                       tiles, d.N, false)
+                         : inv;
+  if (tile == 0 && lane < d.gate_world)
+    __hip_atomic_store(peers[lane] + slot + d.row_base + b, ((uint64_t)tag << 32) | __float_as_uint(r),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int h = 0; h < Bg; h += 256)  // (256 granules a sweep)
+    if (poll_rowx<4, NoWork, NoStop, __HIP_MEMORY_SCOPE_SYSTEM>(own + slot + h, min(256, Bg - h), tag, L.rowe + h))
+      break;  // (timed out: the pass drains)
+  const float s = cascade_row_sum([&](int q) { return __uint_as_float(L.rowe[q]); }, Bg);
+  return (s / (float)Bg) < 0.5f * (float)d.N ? 1 : 0;
+}
+
 // kModeGate, wave 8 of every workgroup: the batch-global ESS gate of step t (DPFs.py:163-165:
 // torch.mean over the rows of 1 / sum p^2 of slot t - 1, < 0.5 N), tiled_gate_batch_kernel's
 // arithmetic.  t = 0: from the initial partials (ess_all).  t > 0: this row's term `inv` (from the
@@ -1200,6 +1232,7 @@ __device__ __forceinline__ float pass_poll_c(const nfdpf_filter_desc &d, const P
 // the epilogue's count).
 // With a plan (d.pass_plan) the decision is the plan's: no exchange, nothing recorded here (the
 // epilogue verifies the plan against the pass's own partials).
+template <bool XR>
 __device__ __forceinline__ void pass_gate(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                           uint32_t tag0, int t, float inv) {
   const int tiles = n_tiles(d.N), lane = threadIdx.x & 63, B = d.B;
@@ -1209,6 +1242,16 @@ __device__ __forceinline__ void pass_gate(const nfdpf_filter_desc &d, const Pass
     return;
   }
   float s;
+  if constexpr (XR) {  // sharded: every rank's rows (its own kernel instance: the registers of the step loop)
+    const int fire = pass_gate_xrank(d, L, b, tile, t, inv);
+    if (lane == 0) L.dec[t & 1] = fire;
+    set_flag(&L.fD, t + 1);
+    if (b == 0 && tile == 0 && lane == 0) {
+      ws.eg[t] = fire;
+      if (d.pass_gates) d.pass_gates[t] = fire;
+    }
+    return;
+  }
   if (t == 0) {
     const double *parts = reinterpret_cast<const double *>(d.ess_all);
     s = cascade_row_sum([&](int r) { return row_inv_ess(parts + (int64_t)r * tiles * kSm, tiles, d.N, false); }, B);
@@ -1287,7 +1330,7 @@ __device__ __forceinline__ void sweep_prio(bool on) {
   }
 }
 
-template <int MODE>
+template <int MODE, bool XR = false>
 __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const PassWs &ws, PassLds &L, int b, int tile,
                                              uint32_t tag0) {
   constexpr bool FORCE = MODE == kModeForce, GATE = MODE == kModeGate;
@@ -1303,7 +1346,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
   int pdec = 0;  // GATE: step t - 1's decision (the flow waves resampled at step t iff it or step t's fired)
-  if (GATE && we == sweeper) pass_gate(d, ws, L, b, tile, tag0, 0, 0.f);
+  if (GATE && we == sweeper) pass_gate<XR>(d, ws, L, b, tile, tag0, 0, 0.f);
   const int slot_e_ = slot_e, i_e_ = i_e;
   for (int t = 0; t < d.T; ++t) {
     // (opaque_int where the VGPR pressure spilled their addresses: FORCE / GATE)
@@ -1365,7 +1408,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
         sweep_prio<MODE>(true);
         const float inv = pass_poll_c(d, ws, L, b, tile, tag0, t - 1);
         PT(t, 10);
-        pass_gate(d, ws, L, b, tile, tag0, t, inv);
+        pass_gate<XR>(d, ws, L, b, tile, tag0, t, inv);
         sweep_prio<MODE>(false);
       }
       PT(t, 2);
@@ -1418,7 +1461,8 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   pass_norm(d, ws, L, b, tile, d.T - 1, i_e, valid_e, u, qx0, qx1);
 }
 
-template <int MODE>
+// XR: kModeGate on a sharded batch (d.gate_peers: the cross-rank gate exchange, pass_gate_xrank)
+template <int MODE, bool XR = false>
 __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_filter_desc d, PassWs ws) {
   __shared__ PassLds L;
   int b, tile;
@@ -1445,7 +1489,7 @@ __global__ __launch_bounds__(4 * kTile, 1) void tiled_pass_kernel(const nfdpf_fi
     pass_prior<MODE>(d, ws, L, b, tile, tag0);
   } else {
     __builtin_amdgcn_s_setprio(NFDPF_PRIO_ENC);
-    pass_encoder<MODE>(d, ws, L, b, tile, tag0);
+    pass_encoder<MODE, XR>(d, ws, L, b, tile, tag0);
   }
 }
 
@@ -1560,6 +1604,11 @@ __global__ __launch_bounds__(64) void tiled_pass_epilogue_kernel(const nfdpf_fil
     ws.hdr->abort = 0;
     ws.hdr->done = 0;
     ws.hdr->epoch = ep > kPassEpochMask ? 0u : ep;
+    if (d.gate_peers) {  // the cross-rank exchange's epoch (every rank's pass bumps its own alike)
+      uint32_t *xe = reinterpret_cast<uint32_t *const *>(d.gate_peers)[d.gate_rank];
+      __hip_atomic_store(xe, (__hip_atomic_load(xe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & kPassEpochMask,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1569,6 +1618,7 @@ static int pass_mode_of(const nfdpf_filter_desc &d) {
 typedef void (*pass_kernel_t)(const nfdpf_filter_desc, PassWs);
 static pass_kernel_t pass_kernel_of(const nfdpf_filter_desc &d) {
   const int m = pass_mode_of(d);
+  if (m == kModeGate && d.gate_peers) return tiled_pass_kernel<kModeGate, true>;
   return m == kModeForce ? tiled_pass_kernel<kModeForce> : m == kModeGate ? tiled_pass_kernel<kModeGate>
                                                                           : tiled_pass_kernel<kModeSpec>;
 }
@@ -1585,7 +1635,8 @@ static bool pass_config_ok(const nfdpf_filter_desc &d) {
   if (d.force_resample && d.resampler != NFDPF_RESAMPLE_SOFT) return false;
   // the in-launch gate: the whole batch in this launch (unless it follows a plan), the soft resampler
   if (d.pass_gate && !d.force_resample &&
-      ((d.B_global != d.B && !d.pass_plan) || d.resampler != NFDPF_RESAMPLE_SOFT))
+      ((d.B_global != d.B && !d.pass_plan && !(d.gate_peers && d.gate_world >= 1 && d.B_global <= kXgMaxRows)) ||
+       d.resampler != NFDPF_RESAMPLE_SOFT))
     return false;
   if (d.N < 2 || n_tiles(d.N) > kPassMaxTiles || d.n_flows < 1 || d.n_flows > 2 || d.T < 1 || d.T > kPassMaxT ||
       d.B < 1 || d.B > 256)  // (the epilogue stages a step's B row sums in LDS)

@@ -2228,6 +2228,10 @@ extern "C" int nfdpf_filter_pass_tiled(const nfdpf_filter_desc *dp, void *worksp
                 "nfdpf_filter_pass_tiled: configuration not supported here (nfdpf_filter_pass_supported == 0)");
   const int mode = pass_mode_of(d);
   NFDPF_REQUIRE(d.ess_all || mode == kModeForce, "nfdpf_filter_pass_tiled: ess_all (the initial partials) missing");
+  NFDPF_REQUIRE(!d.gate_peers || (mode == kModeGate && !d.pass_plan && d.gate_rank >= 0 && d.gate_rank < d.gate_world &&
+                                  d.gate_world <= 64 && d.B_global <= kXgMaxRows && d.row_base + d.B <= d.B_global),
+                "nfdpf_filter_pass_tiled: gate_peers needs a gated pass (no plan), 0 <= gate_rank < gate_world <= 64 "
+                "and B_global <= %d", kXgMaxRows);
   // the epilogue's gates: those of a speculative pass of the whole batch (a sharded one is
   // verified by the caller over the gathered partials, nfdpf_ess_gate_tiled_batch), or the
   // decisions the gated pass took itself

@@ -89,3 +89,59 @@ extern "C" int nfdpf_host_mapped_free(void *host) {
   return NFDPF_OK;
 }
 
+
+// The sharded gated pass's cross-rank gate exchange (include/nfdpf.h, filter_pass.hpp pass_gate):
+// uncached device memory, so that granules a peer GPU stores over xGMI are read from memory by
+// this GPU's polling loads, never from a stale L2 line.
+static int xchg_fail(const char *what, hipError_t e) {
+  (void)hipGetLastError();
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return NFDPF_ELAUNCH;
+}
+
+extern "C" int64_t nfdpf_gate_xchg_bytes(int B_global) {
+  return B_global <= 0 ? 0 : 256 + 2 * (int64_t)B_global * 8;
+}
+
+extern "C" int nfdpf_gate_xchg_alloc(int64_t bytes, void **dev, void *ipc_handle) {
+  NFDPF_REQUIRE(bytes > 0 && dev && ipc_handle, "nfdpf_gate_xchg_alloc: bad arguments");
+  *dev = nullptr;
+  hipError_t e = hipExtMallocWithFlags(dev, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) {
+    *dev = nullptr;
+    return xchg_fail("nfdpf_gate_xchg_alloc (hipExtMallocWithFlags)", e);
+  }
+  hipIpcMemHandle_t h;
+  if ((e = hipMemset(*dev, 0, (size_t)bytes)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess ||
+      (e = hipIpcGetMemHandle(&h, *dev)) != hipSuccess) {
+    (void)hipFree(*dev);
+    *dev = nullptr;
+    return xchg_fail("nfdpf_gate_xchg_alloc (hipIpcGetMemHandle)", e);
+  }
+  static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
+  memcpy(ipc_handle, &h, sizeof(h));
+  return NFDPF_OK;
+}
+
+extern "C" int nfdpf_gate_xchg_open(const void *ipc_handle, void **dev) {
+  NFDPF_REQUIRE(ipc_handle && dev, "nfdpf_gate_xchg_open: bad arguments");
+  hipIpcMemHandle_t h;
+  memcpy(&h, ipc_handle, sizeof(h));
+  *dev = nullptr;
+  const hipError_t e = hipIpcOpenMemHandle(dev, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) {
+    *dev = nullptr;
+    return xchg_fail("nfdpf_gate_xchg_open (hipIpcOpenMemHandle)", e);
+  }
+  return NFDPF_OK;
+}
+
+extern "C" int nfdpf_gate_xchg_close(void *dev) {
+  if (dev) NFDPF_REQUIRE(hipIpcCloseMemHandle(dev) == hipSuccess, "nfdpf_gate_xchg_close: hipIpcCloseMemHandle failed");
+  return NFDPF_OK;
+}
+
+extern "C" int nfdpf_gate_xchg_free(void *dev) {
+  if (dev) NFDPF_REQUIRE(hipFree(dev) == hipSuccess, "nfdpf_gate_xchg_free: hipFree failed");
+  return NFDPF_OK;
+}

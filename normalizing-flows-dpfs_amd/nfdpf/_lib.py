@@ -50,6 +50,7 @@ class FilterDesc(Structure):
         ("pass_gates", c_void_p), ("pass_flags", c_void_p), ("pass_obs", c_void_p),
         ("meas_mfma", c_int32),
         ("pass_plan", c_void_p),
+        ("gate_peers", c_void_p), ("gate_world", c_int32), ("gate_rank", c_int32),
     ]
 
 
@@ -128,6 +129,11 @@ SIGNATURES = {
     "nfdpf_filter_tiled_init": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_host_mapped_alloc": (c_int, [c_int64, c_void_p, c_void_p]),
     "nfdpf_host_mapped_free": (c_int, [c_void_p]),
+    "nfdpf_gate_xchg_bytes": (c_int64, [c_int]),
+    "nfdpf_gate_xchg_alloc": (c_int, [c_int64, c_void_p, c_void_p]),
+    "nfdpf_gate_xchg_open": (c_int, [c_void_p, c_void_p]),
+    "nfdpf_gate_xchg_close": (c_int, [c_void_p]),
+    "nfdpf_gate_xchg_free": (c_int, [c_void_p]),
     "nfdpf_filter_init": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_uint64,
                                   c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nfdpf_filter_pass_supported": (c_int, [POINTER(FilterDesc)]),

@@ -189,6 +189,9 @@ class FilterEngine:
         self.last_plan_pass = False
         self.plan_passes = 0
         self.plan_misses = 0
+        # sharded: the cross-rank gate exchange of the gated pass (ops.GateExchange), keyed by the
+        # process group, B_global and device; None inside when a rank could not set it up
+        self._xg = None
 
     def __getstate__(self):
         # DPF keeps its engine, and main.py pickles the whole DPF (main.py:57): the last pass's
@@ -200,7 +203,7 @@ class FilterEngine:
         st["_shared_device"] = None
         st["step_events"] = None
         st["_hmapped"] = None  # (pinned host memory of this process)
-        st["_plan_buf"], st["_plan_buf_val"] = None, None
+        st["_plan_buf"], st["_plan_buf_val"], st["_xg"] = None, None, None
         return st
 
     def _decide_spec(self, shard, speculate=None, host_mode=False, teacher=False, consume=False,
@@ -231,7 +234,7 @@ class FilterEngine:
         auto = speculate is None and c.speculate_gate is None
         if speculate is None:
             speculate = c.speculate_gate if c.speculate_gate is not None else \
-                (tiled and (shard.world > 1 or c.resampler == "ot" or (pass_ok and not (gate_ok and self._gate_mode))))
+                (tiled and (c.resampler == "ot" or ((shard.world > 1 or pass_ok) and not (gate_ok and self._gate_mode))))
             if auto and finish and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 speculate = False
         if auto and tiled and c.resampler == "ot" and self._ot_fired:
@@ -258,9 +261,33 @@ class FilterEngine:
         # shapes -- only speculates)
         # (and every row resident at once: the gated pass's rows wait for the batch's decision;
         # a speculative pass of more rows runs them in resident chunks)
-        return bool(pass_ok and shard.world == 1 and c.resampler == "soft" and not c.force_resample
+        # (sharded: with the cross-rank gate exchange set up for this group -- _xgate)
+        xg = getattr(self, "_xg", None)
+        xg_ok = shard.world == 1 or (xg is not None and xg[0] == self._xg_key(shard) and xg[1] is not None)
+        return bool(pass_ok and xg_ok and c.resampler == "soft" and not c.force_resample
                     and c.pass_gate is not False and c.NF_dyn and c.NF_cond
                     and getattr(self, "_gate_resident", False))
+
+    @staticmethod
+    def _xg_key(shard):
+        return (id(shard.group), shard.world, shard.rank, shard.B_global)
+
+    def _xgate(self, shard, pass_ok, finish, dev):
+        """Sharded: set up (once per group and B_global) the cross-rank gate exchange that lets the
+        gated pass decide the batch-global gate inside every rank's launch (ops.GateExchange; a
+        collective: every rank reaches this call with the same arguments).  Not for a pass captured
+        into a graph or left unfinished (its fault and obs reductions are collectives after the
+        launch), nor above 512 global rows; NFDPF_XGATE=0 turns it off."""
+        c = self.cfg
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if not (shard.world > 1 and pass_ok and finish and not capturing and c.resampler == "soft"
+                and not c.force_resample and c.NF_dyn and c.NF_cond and c.pass_gate is not False
+                and self._gate_resident and shard.B_global <= 512 and os.environ.get("NFDPF_XGATE", "1") != "0"):
+            return None
+        key = self._xg_key(shard)
+        if self._xg is None or self._xg[0] != key:
+            self._xg = (key, ops.GateExchange.create(shard.B_global, shard.rank, shard.world, shard.group, dev))
+        return self._xg[1]
 
     def _plan_capable(self, pass_ok) -> bool:
         """Can the one-launch pass follow a gate plan (the C2 shape's gated kernel with
@@ -345,8 +372,8 @@ class FilterEngine:
         d.meas_mfma = int(self._meas_mfma())
         ok = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
         self._gate_resident = False
-        if ok and c.NF_dyn and c.NF_cond and not c.force_resample and shard.world == 1:
-            d.pass_gate = 1
+        if ok and c.NF_dyn and c.NF_cond and not c.force_resample:
+            d.pass_gate, d.B_global = 1, B  # (this rank's rows all resident: sharded, the exchange is per step)
             self._gate_resident = bool(L.lib().nfdpf_filter_pass_supported(ctypes.byref(d)))
         self.pass_fallback_reason = None if ok else self._shape_limit(B, N)
         warn = self.pass_fallback_reason and not getattr(self, "_fallback_warned", False)
@@ -495,7 +522,8 @@ class FilterEngine:
         pass_ok = (not external and teacher is None and not host_mode
                    and self._pass_supported(B, N, T, E, split_nets, shard))
         self.last_pass_ok = pass_ok
-        gate_ok = self._gate_ok(shard, pass_ok)
+        xg = self._xgate(shard, pass_ok, finish, dev) if shard.world > 1 else None
+        gate_ok = self._gate_ok(shard, pass_ok) and (shard.world == 1 or xg is not None)
         plan_arr, plan_buf = self._plan_select(pass_ok, gate_ok, T, auto, plan, finish, dev)
         plan_pass = plan_arr is not None
         spec = False if plan_pass else \
@@ -650,6 +678,13 @@ class FilterEngine:
             d.pass_gate = int(gate_pass)
             d.pass_plan = plan_buf.data_ptr() if plan_pass else None
             self.plan_passes += int(plan_pass)
+            xg_pass = gate_pass and not plan_pass and shard.world > 1
+            if xg_pass:  # the batch-global gate through every rank's exchange buffer, per step
+                d.gate_peers, d.gate_world, d.gate_rank = xg.peers.data_ptr(), shard.world, shard.rank
+                i32 = dict(device=dev, dtype=torch.int32)
+                xg_out = (torch.empty(T, **i32), torch.empty(3, **i32))  # the decisions; {fired, faults, done}
+                self.last_gates = xg_out[0]
+                d.pass_gates, d.pass_flags = xg_out[0].data_ptr(), xg_out[1].data_ptr()
             if shard.world == 1:  # the epilogue verifies the gates / reads the fault counter on the device
                 i32 = dict(device=dev, dtype=torch.int32)
                 pass_out = (torch.empty(T, **i32) if (spec or gate_pass) else None, torch.empty(3, **i32),
@@ -814,7 +849,14 @@ class FilterEngine:
                 self._pending = (None, None, shard, N, res, None, verify, True, True)
                 return res
             if not capturing:
-                if pass_out is not None:
+                if xg_pass:  # (the epilogue read and cleared this rank's fault counter)
+                    n_fired, faults = xg_out[1].tolist()[:2]
+                    ft = torch.tensor([faults], device=dev, dtype=torch.int64)
+                    dist.all_reduce(ft, group=shard.group)  # every rank falls back together
+                    faults = int(ft.item())
+                    if not faults and self._plan_wanted(pass_ok, gate_ok):
+                        self._plan = xg_out[0].cpu().numpy()  # the decisions: the next passes' plan
+                elif pass_out is not None:
                     n_fired, faults = pass_out[1].tolist()[:2]
                     if gate_pass and not faults and self._plan_wanted(pass_ok, gate_ok):
                         self._plan = pass_out[0].cpu().numpy()  # the gates it decided: the next passes' plan

@@ -622,6 +622,61 @@ class HostMapped:
             pass
 
 
+class GateExchange:
+    """The sharded gated pass's cross-rank gate exchange (include/nfdpf.h nfdpf_gate_xchg_*): this
+    rank's buffer of uncached device memory and every peer's, mapped from its IPC handle --
+    ``peers`` (int64 [world] on the device) is the pass's d.gate_peers.  Set up collectively over
+    the shard's process group (every rank allocates and exports, then maps the others); ``create``
+    returns None on EVERY rank when any rank could not (the caller then keeps the exchange-free
+    modes).  Unmapped / freed when dropped."""
+
+    def __init__(self, own, opened, peers):
+        self._own, self._opened, self.peers = own, opened, peers
+
+    @staticmethod
+    def create(B_global: int, rank: int, world: int, group, device) -> "Optional[GateExchange]":
+        import ctypes
+        import torch.distributed as dist
+        lb = lib()
+        own, h = ctypes.c_void_p(), ctypes.create_string_buffer(64)
+        ok = lb.nfdpf_gate_xchg_alloc(int(lb.nfdpf_gate_xchg_bytes(B_global)), ctypes.byref(own),
+                                      ctypes.cast(h, ctypes.c_void_p)) == L.NFDPF_OK
+        hs = [None] * world
+        dist.all_gather_object(hs, h.raw if ok else None, group=group)
+        ptrs, opened = [], []
+        ok = ok and all(x is not None for x in hs)
+        if ok:
+            for r, hb in enumerate(hs):
+                if r == rank:
+                    ptrs.append(own.value)
+                    continue
+                p = ctypes.c_void_p()
+                hbuf = ctypes.create_string_buffer(hb, 64)
+                if lb.nfdpf_gate_xchg_open(ctypes.cast(hbuf, ctypes.c_void_p), ctypes.byref(p)) != L.NFDPF_OK:
+                    ok = False
+                    break
+                ptrs.append(p.value)
+                opened.append(p.value)
+        oks = [None] * world
+        dist.all_gather_object(oks, bool(ok), group=group)
+        if not all(oks):
+            for p in opened:
+                lb.nfdpf_gate_xchg_close(p)
+            if own.value:
+                lb.nfdpf_gate_xchg_free(own.value)
+            return None
+        return GateExchange(own.value, opened, torch.tensor(ptrs, dtype=torch.int64, device=device))
+
+    def __del__(self):
+        try:
+            lb = lib()
+            for p in self._opened:
+                lb.nfdpf_gate_xchg_close(p)
+            lb.nfdpf_gate_xchg_free(self._own)
+        except Exception:  # interpreter shutdown
+            pass
+
+
 class _SlotLease:
     """A reserved HostMapped slot; returned to its pool on release() or when dropped."""
 

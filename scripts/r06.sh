@@ -29,9 +29,11 @@ for step in $STEPS; do
   kind=${step%%:*}; arg=${step#*:}
   n=$((n + 1))
   case "$kind" in
-  tests)
+  tests)  # (pytest args comma-separated; "+" in a -k expression reads " or ")
+    IFS=',' read -ra TA <<< "$arg"
+    for i in "${!TA[@]}"; do TA[$i]="${TA[$i]//+/ or }"; done
     timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest -x -v --timeout ${TEST_ONE:-300} --timeout-method thread \
-      -p no:cacheprovider ${arg//,/ } > $O/t_$n.log 2>&1
+      -p no:cacheprovider "${TA[@]}" > $O/t_$n.log 2>&1
     rc=$?; echo "tests $arg rc=$rc"; tail -3 $O/t_$n.log; [ $rc -eq 0 ] || exit $rc ;;
   bench)
     for s in ${arg//,/ }; do

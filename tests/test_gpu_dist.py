@@ -253,7 +253,9 @@ def _worker_plan(rank, world, port, path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root, os.path.join(root, "tests")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NFDPF_PASS_SHARED_OK="1")
+    # (NFDPF_XGATE=0: the exact sharded run is the step launches' per-step exchange, not the gated
+    # pass through the cross-rank exchange -- test_sharded_gated_pass_matches_unsharded covers that)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NFDPF_PASS_SHARED_OK="1", NFDPF_XGATE="0")
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -293,3 +295,76 @@ def test_sharded_plan_pass_matches_unsharded(tmp_path):
                 assert torch.equal(part[f], full[f][r * h:(r + 1) * h]), (f, r)
         a, b = float(part["obs_likelihood"]), float(full["obs_likelihood"])
         assert abs(a - b) <= 1e-6 * abs(b), (a, b)
+
+
+# ---- the gated pass, sharded: the batch-global gate through the cross-rank exchange (IPC-mapped
+# buffers, ops.GateExchange) inside every rank's launch
+def _xgate_run(rows, shard=None, world=1):
+    from nfdpf.engine import FilterConfig, FilterEngine
+    B, N, T = PASS_CASES["firing"]
+    models, enc, start, vel = _pass_inputs("firing", rows)
+    cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321, kernel="tiled")
+    eng = FilterEngine(cfg, models)
+    outs = []
+    for _ in range(2):  # (twice: the exchange's epoch carries from pass to pass)
+        res = eng.run(enc, start, vel, shard=shard, speculate=False)
+        torch.cuda.synchronize()
+        out = {f: getattr(res, f).cpu() for f in FIELDS if getattr(res, f) is not None}
+        out["obs_likelihood"] = res.obs_likelihood.cpu()
+        out["gated"], out["launches"] = eng.last_gate_pass, eng.pass_launches
+        out["gates"] = eng.last_gates.cpu() if eng.last_gates is not None else None
+        outs.append(out)
+    return outs
+
+
+def _worker_xgate(rank, world, port, path):
+    import sys
+    import warnings
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root, os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NFDPF_PASS_SHARED_OK="1")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf import _lib
+        from nfdpf.engine import ShardInfo
+        _lib.load()
+        B = PASS_CASES["firing"][0] // world
+        with warnings.catch_warnings(record=True) as wl:
+            warnings.simplefilter("always")
+            outs = _xgate_run((rank * B, (rank + 1) * B), ShardInfo.from_env(B), world)
+        outs[0]["warnings"] = [str(w.message) for w in wl]
+        torch.save(outs, f"{path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_gated_pass_matches_unsharded(tmp_path):
+    """The firing case on two ranks, their gated one-launch passes running CONCURRENTLY on the one
+    GPU (each grid of 4 rows x 4 tiles; NFDPF_PASS_SHARED_OK): every step's batch-global gate is
+    decided inside both launches from the 8 rows' terms swept through the IPC-mapped exchange
+    buffers (d.gate_peers) -- no fallback, no per-step all-gather.  Both passes of each rank equal
+    the unsharded gated pass bit for bit (every history and every decision; obs to 1e-6)."""
+    import torch.multiprocessing as mp
+    from nfdpf import _lib
+    _lib.load()
+    B = PASS_CASES["firing"][0]
+    full = _xgate_run((0, B))
+    assert full[0]["gated"] and full[0]["launches"] == 1 and int(full[0]["gates"].sum()) > 0
+    world = 2
+    path = str(tmp_path / "xgate")
+    mp.start_processes(_worker_xgate, args=(world, _free_port(), path), nprocs=world, start_method="spawn")
+    parts = [torch.load(f"{path}.{r}", weights_only=True) for r in range(world)]
+    h = B // world
+    for r, outs in enumerate(parts):
+        assert not outs[0]["warnings"], (r, outs[0]["warnings"])
+        for k, (o, f) in enumerate(zip(outs, full)):
+            assert o["gated"] and o["launches"] == k + 1, (r, k, o["gated"], o["launches"])
+            assert torch.equal(o["gates"], f["gates"]), (r, k, o["gates"], f["gates"])
+            for fld in FIELDS:
+                if fld in f:
+                    assert torch.equal(o[fld], f[fld][r * h:(r + 1) * h]), (fld, r, k)
+            a, b = float(o["obs_likelihood"]), float(f["obs_likelihood"])
+            assert abs(a - b) <= 1e-6 * abs(b), (a, b)
