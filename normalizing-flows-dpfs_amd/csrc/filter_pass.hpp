@@ -734,6 +734,24 @@ __device__ __forceinline__ float pass_forward(cf2 *fw, int ns, float &lo, float 
   return l1 + ts.y;
 }
 
+// kModeGate: the prediction of step t's decision from the decisions so far -- a 2-bit saturating
+// counter per history of the last two decisions (bits 0-1: the history, last decision in bit 0;
+// bits 2 + 2h: counter h).  The chain, prior and encoder waves each keep a copy, updated with the
+// same committed decisions, so all predict alike (the row's resampling barriers match).  It starts
+// as "the previous step's decision" and learns e.g. the alternation of a filter whose resampling
+// restores the ESS for a step (c2_full: 17 of 50 steps fire, every other one).
+struct GatePred {
+  int s = (1 << 2) | (2 << 4) | (1 << 6) | (2 << 8);
+  __device__ __forceinline__ int get() const { return ((s >> (2 + 2 * (s & 3))) & 3) >= 2 ? 1 : 0; }
+  __device__ __forceinline__ void update(int d) {
+    const int h = s & 3, sh = 2 + 2 * h;
+    int c = (s >> sh) & 3;
+    c = d ? min(c + 1, 3) : max(c - 1, 0);
+    s = (s & ~(3 << sh)) | (c << sh);
+    s = (s & ~3) | (((h << 1) | (d ? 1 : 0)) & 3);
+  }
+};
+
 // kModeGate: step t's decision once wave 8 has taken it (fD >= t + 1): 1 = the batch-global ESS
 // gate fired (DPFs.py:163-165); the same value in every workgroup of the grid
 __device__ __forceinline__ int wait_dec(PassLds &L, int t) {
@@ -799,7 +817,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
   constexpr int nsd = kNsDyn, nsc = net_size<1, kH>(kE + 4);
   const double inv_n = 1.0 / N, inv_n1 = 1.0 / (N - 1);  // the row contexts' (ctx_from_sums)
   int round = 0;  // flow_barrier rounds (FORCE / GATE)
-  int prev_dec = 0;  // GATE: the decision of step t - 1 (the prediction for step t)
+  GatePred gp;  // GATE: the prediction of step t's decision
   float en0 = 0.f, en1 = 0.f;  // the next step's motion noise
   // the step's velocity, loaded one step ahead (beside the next step's noise): no scalar-load
   // latency at the head of the step
@@ -827,7 +845,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     int src = i, variant = 0, fire = FORCE ? 1 : 0;
     // (a plan pass follows d.pass_plan: the decision is known, never speculated)
     const int32_t *plan = GATE ? d.pass_plan : nullptr;
-    const int pred = GATE ? (plan ? (plan[t] ? 1 : 0) : t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
+    const int pred = GATE ? (plan ? (plan[t] ? 1 : 0) : t == 0 ? wait_dec(L, 0) : gp.get()) : 0;
     bool known = !GATE || t == 0 || plan;  // the step's decision is in hand (GATE: else speculated)
     auto take_resampled = [&]() {
       if (valid) {
@@ -1039,7 +1057,7 @@ __device__ __forceinline__ void pass_chain(const nfdpf_filter_desc &d, const Pas
     PT(t, 5);
     x0 = q0;
     x1 = q1;
-    prev_dec = fire;
+    if (GATE) gp.update(fire);
     pre = PRE;
   }
   if (GATE) {  // the last slot's stores (the encoder pair's C(T - 1) waits for them)
@@ -1064,7 +1082,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
   const bool valid = i < N;
   constexpr int nsd = kNsDyn;
   int round = 0;
-  int prev_dec = 0;
+  GatePred gp;  // GATE: the prediction of step t's decision (pass_chain's, from the same decisions)
   const int i_ = i, slot_ = slot;
   for (int t = 0; t < d.T; ++t) {
     const nfdpf_filter_desc &d = *(const nfdpf_filter_desc *)kernarg_desc();  // (kernarg_desc)
@@ -1075,7 +1093,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     const int par = t & 1;
     const RowSlot S = row_slot(d, b, t);
     const int32_t *plan = GATE ? d.pass_plan : nullptr;
-    const int pred = GATE ? (plan ? (plan[t] ? 1 : 0) : t == 0 ? wait_dec(L, 0) : prev_dec) : 0;
+    const int pred = GATE ? (plan ? (plan[t] ? 1 : 0) : t == 0 ? wait_dec(L, 0) : gp.get()) : 0;
     if (FORCE || pred) pass_resample(d, ws, L, b, tile, tag0, t, round, FORCE || NFDPF_GATE_LATE);
     PT(t, 0);
     if (g == 0) {
@@ -1132,7 +1150,7 @@ __device__ __forceinline__ void pass_prior(const nfdpf_filter_desc &d, const Pas
     }
     set_flag(&L.rf[g], t + 1);
     set_flag(&L.pf[g], t + 1);
-    if (GATE) prev_dec = __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]);  // committed: known
+    if (GATE) gp.update(__builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]));  // committed: known
     PT(t, 2);
   }
 }
@@ -1345,7 +1363,8 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
   const EncFrag2 ef = enc_frag2_load(d.pe_params);  // the encoder's weight fragments, once
   float lr = valid_e ? logf(d.p_prev[(int64_t)b * d.p_prev_rs + i_e]) : 0.f;
   float u = 0.f, qx0 = 0.f, qx1 = 0.f;
-  int pdec = 0;  // GATE: step t - 1's decision (the flow waves resampled at step t iff it or step t's fired)
+  int pdec = 0;  // GATE: step t's decision, once committed
+  GatePred gp;   // GATE: the flow waves' prediction (they resampled at step t iff it or step t's decision fired)
   if (GATE && we == sweeper) pass_gate<XR>(d, ws, L, b, tile, tag0, 0, 0.f);
   const int slot_e_ = slot_e, i_e_ = i_e;
   for (int t = 0; t < d.T; ++t) {
@@ -1370,7 +1389,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       // (a plan pass: the flow waves resampled at step t iff the plan's gate fired -- nothing is
       // speculated from step t - 1's decision there)
       if (GATE && (d.pass_plan ? d.pass_plan[t] != 0
-                               : (pdec || __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0)))
+                               : ((t > 0 && gp.get()) || __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]) != 0)))
         wait_flag(&L.fS, t + 1);
       PT(t, 4);
 #ifndef NFDPF_EXP_NOENC
@@ -1418,6 +1437,7 @@ __device__ __forceinline__ void pass_encoder(const nfdpf_filter_desc &d, const P
       // this particle's log-weight is its source's (the chain's resampling left it in lr_l)
       pdec = d.pass_plan ? (d.pass_plan[t] ? 1 : 0) : __builtin_amdgcn_readfirstlane(*(lds_vint *)&L.dec[par]);
       if (pdec != 0) lr = valid_e ? L.lr_l[slot_e] : 0.f;
+      gp.update(pdec);
     }
     // the log-weight (DPFs.py:187)
     PT(t, 3);
