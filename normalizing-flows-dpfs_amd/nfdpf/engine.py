@@ -322,7 +322,7 @@ class FilterEngine:
                 return None, None
             if finish and capturing:  # (nothing could verify it after the replay)
                 return None, None
-        buf = self._plan_buf
+        buf, dev = self._plan_buf, torch.device(dev)
         if buf is None or buf.device != dev or buf.numel() != T:
             if capturing:
                 return None, None
