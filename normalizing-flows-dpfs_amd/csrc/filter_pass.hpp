@@ -714,9 +714,11 @@ __device__ __forceinline__ f2 ts_half(cf2 *w, float u, const f2 *cb) {
 // RealNVP_cond flow inverse (nf/flows.py:228-239) / forward (:215-226) on one wave: fw = the
 // flow's pair-layout block (half 1 at fw, half 2 at fw + ns), cb = its 16 folded bias pairs
 // (half 2 at cb + kH); the update arithmetic of split.hpp's coupling_*_split
-// exp(s) of the coupling update as one v_exp_f32 of s log2(e) (|s| = O(1): expf's range reduction,
-// ~10 VALU on the chain's critical path per coupling half, buys nothing there)
-__device__ __forceinline__ float exp_s(float s) { return __builtin_amdgcn_exp2f(s * 1.4426950408889634f); }
+// exp(s) of the coupling update: expf, as split.hpp's step launches.  (One v_exp_f32 of s log2(e)
+// measured neutral on the pass's time, and its extra rounding of s log2(e) took the forced pass's
+// indices against the step launches' from > 99 % to 94 % agreement over 8 steps of resampling --
+// test_split_nets_match_pair_layout: not worth it.)
+__device__ __forceinline__ float exp_s(float s) { return expf(s); }
 __device__ __forceinline__ float pass_inverse(cf2 *fw, int ns, float &lo, float &up, const f2 *cb) {
   f2 ts = ts_half(fw + ns, up, cb + kH);
   lo = (lo - ts.x) * exp_s(-ts.y);
