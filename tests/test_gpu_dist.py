@@ -114,7 +114,10 @@ def test_sharded_engine_matches_unsharded(case, tmp_path):
 # fires: the sharded passes ARE the result), "firing" = the c2_full workload (aligned encodings:
 # the gathered verification catches the fired gate and every rank reruns with the per-step
 # exchange)
-PASS_CASES = {"quiet": (8, 1000, 12), "firing": (8, 1000, 12), "quiet_c3": (8, 1000, 12)}
+# (firing_gated: the same, with the gated pass allowed -- the rerun after the missed speculation is
+# then the gated pass on every rank, the batch gate exchanged inside the launches, round 6)
+PASS_CASES = {"quiet": (8, 1000, 12), "firing": (8, 1000, 12), "firing_gated": (8, 1000, 12),
+              "quiet_c3": (8, 1000, 12)}
 
 
 def _pass_inputs(kind, rows):
@@ -130,7 +133,7 @@ def _pass_inputs(kind, rows):
         g = torch.Generator().manual_seed(31)
         enc, start, vel = torch.randn(B, T, 32, generator=g), torch.randn(B, 4, generator=g) * 10, \
             torch.randn(B, T, 2, generator=g) * 3
-    else:
+    else:  # firing, firing_gated
         import _fullsize as F
         wl = F.workload("c2_full", B=B, N=N, T=T)
         models, enc, start, vel = wl["models"].to(DEV), wl["enc"], wl["start"], wl["vel"]
@@ -151,7 +154,8 @@ def _pass_run(kind, rows, shard=None, rank=0, world=1):
                            kernel="tiled")
     else:
         cfg = FilterConfig(N=N, NF_dyn=True, NF_cond=True, measurement="cos", resampler="soft", seed=321,
-                           kernel="tiled", pass_gate=False)  # (the unsharded rerun: the step launches, as the ranks')
+                           kernel="tiled",  # (firing: the unsharded rerun by the step launches, as the ranks')
+                           pass_gate=None if kind == "firing_gated" else False)
     eng = FilterEngine(cfg, models)
     for r in range(world):
         if r == rank:
@@ -167,7 +171,7 @@ def _pass_run(kind, rows, shard=None, rank=0, world=1):
     torch.cuda.synchronize()
     out = {f: getattr(res, f).cpu() for f in FIELDS if getattr(res, f) is not None}
     out["obs_likelihood"] = res.obs_likelihood.cpu()
-    out["launched"], out["verified"] = launched, verified
+    out["launched"], out["verified"], out["gated"] = launched, verified, eng.last_gate_pass
     return out
 
 
@@ -205,7 +209,8 @@ def test_sharded_pass_matches_unsharded(kind, tmp_path):
     B = PASS_CASES[kind][0]
     full = _pass_run(kind, (0, B))
     assert full["launched"], "the unsharded one-launch pass did not run"
-    assert full["verified"] == (kind != "firing")
+    assert full["verified"] == (kind not in ("firing", "firing_gated"))
+    assert full["gated"] == (kind == "firing_gated")
     world = 2
     path = str(tmp_path / "pass")
     mp.start_processes(_worker_pass, args=(world, _free_port(), kind, path), nprocs=world, start_method="spawn")
@@ -214,6 +219,7 @@ def test_sharded_pass_matches_unsharded(kind, tmp_path):
     for r, part in enumerate(parts):
         assert part["launched"], f"rank {r}: the sharded one-launch pass did not run"
         assert part["verified"] == full["verified"], (r, part["verified"])
+        assert part["gated"] == full["gated"], (r, part["gated"])  # firing_gated: the sharded GATED pass
         for f in FIELDS:
             if f in full:
                 assert torch.equal(part[f], full[f][r * h:(r + 1) * h]), (kind, f, r)
