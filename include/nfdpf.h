@@ -547,6 +547,16 @@ NFDPF_API int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int 
  * each gate as it goes, DPFs.py:163-165). */
 NFDPF_API int nfdpf_pass_verify(const double *parts, const float *lw_sum, int T, int B, int N, int t0,
                                 int32_t *gates, int32_t *flags, float *obs, void *stream);
+/* The verification of a SHARDED speculative pass from one small all-gather: each rank reduces its
+ * [T][B][tiles][4] step partials to the rows' gate terms terms[t * B + b] = 1 / sum p^2 of row b at
+ * step t (tiled_gate_batch_kernel's per-row arithmetic; the +1e-12 terms iff t0 + t > 0) and puts
+ * its hand-off fault counter (read and cleared, as an int32) in terms[T * B]; after the ranks'
+ * term arrays are gathered in global row order, nfdpf_ess_gate_terms takes the T batch-global
+ * gates (DPFs.py:163-165: ATen's cascade mean over the B_global rows) from terms [T][B_global].
+ * Bit-identical to nfdpf_ess_gate_tiled_batch on the gathered partials, at 1 / (4 tiles x 4)
+ * of the gathered bytes.  No reference counterpart. */
+NFDPF_API int nfdpf_ess_row_terms(const double *parts, int T, int B, int N, int t0, float *terms, void *stream);
+NFDPF_API int nfdpf_ess_gate_terms(const float *terms, int T, int B, int N, int force, int32_t *gates, void *stream);
 
 #ifdef __cplusplus
 }

@@ -2278,6 +2278,41 @@ extern "C" int nfdpf_ess_gate_tiled_batch(const double *parts, int T, int B, int
   return launch_status("nfdpf_ess_gate_tiled_batch");
 }
 
+namespace nfdpf {
+// row b's gate term of step t (block = step, lanes over rows); the last block also reads and
+// clears the hand-off fault counter into terms[T * B]
+__global__ __launch_bounds__(64) void ess_row_terms_kernel(const double *__restrict__ parts, int B, int tiles, int N,
+                                                           int t0, float *terms) {
+  const int k = blockIdx.x;
+  const double *p = parts + (int64_t)k * B * tiles * kSm;
+  for (int r = threadIdx.x; r < B; r += 64)
+    terms[(int64_t)k * B + r] = row_inv_ess(p + (int64_t)r * tiles * kSm, tiles, N, t0 + k > 0);
+  if (k == (int)gridDim.x - 1 && threadIdx.x == 0)
+    reinterpret_cast<int32_t *>(terms)[(int64_t)gridDim.x * B] = atomicExch(&g_split_fault, 0);
+}
+// tiled_gate_batch_kernel's cascade over the gathered rows' terms (one wave per step)
+__global__ __launch_bounds__(64) void ess_gate_terms_kernel(const float *__restrict__ terms, int B, int N, int force,
+                                                            int32_t *gates) {
+  const int k = blockIdx.x;
+  const float *p = terms + (int64_t)k * B;
+  const float s = cascade_row_sum([&](int r) { return p[r]; }, force ? 0 : B);
+  if (threadIdx.x == 0) gates[k] = (force || (s / (float)B) < 0.5f * (float)N) ? 1 : 0;
+}
+}  // namespace nfdpf
+
+extern "C" int nfdpf_ess_row_terms(const double *parts, int T, int B, int N, int t0, float *terms, void *stream) {
+  NFDPF_REQUIRE(parts && terms && T >= 1 && B >= 1 && N >= 1 && t0 >= 0, "nfdpf_ess_row_terms: bad arguments");
+  ess_row_terms_kernel<<<T, 64, 0, as_stream(stream)>>>(parts, B, n_tiles(N), N, t0, terms);
+  return launch_status("nfdpf_ess_row_terms");
+}
+
+extern "C" int nfdpf_ess_gate_terms(const float *terms, int T, int B, int N, int force, int32_t *gates, void *stream) {
+  NFDPF_REQUIRE(gates && (force || terms) && T >= 0 && B >= 1 && N >= 1, "nfdpf_ess_gate_terms: bad arguments");
+  if (T == 0) return NFDPF_OK;
+  ess_gate_terms_kernel<<<T, 64, 0, as_stream(stream)>>>(terms, B, N, force, gates);
+  return launch_status("nfdpf_ess_gate_terms");
+}
+
 extern "C" int nfdpf_pass_verify(const double *parts, const float *lw_sum, int T, int B, int N, int t0,
                                  int32_t *gates, int32_t *flags, float *obs, void *stream) {
   NFDPF_REQUIRE(parts && lw_sum && gates && flags && obs && T >= 1 && B >= 1 && N >= 1 && t0 >= 0,

@@ -129,6 +129,8 @@ SIGNATURES = {
     "nfdpf_filter_tiled_init": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_host_mapped_alloc": (c_int, [c_int64, c_void_p, c_void_p]),
     "nfdpf_host_mapped_free": (c_int, [c_void_p]),
+    "nfdpf_ess_row_terms": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "nfdpf_ess_gate_terms": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "nfdpf_gate_xchg_bytes": (c_int64, [c_int]),
     "nfdpf_gate_xchg_alloc": (c_int, [c_int64, c_void_p, c_void_p]),
     "nfdpf_gate_xchg_open": (c_int, [c_void_p, c_void_p]),

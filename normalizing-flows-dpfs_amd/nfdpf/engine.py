@@ -1027,20 +1027,43 @@ class FilterEngine:
                 return False
             res.obs_likelihood = verify[1]
             return True
-        if split_dev is not None:
-            if was_pass:
-                faults = self._faults_all(shard, split_dev)
-                if faults:
-                    self._pass_fault(faults)
-                    self.last_verify = "fault"
-                    return False
-            else:
-                L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
-        tot = tot.clone()
-        parts = self._gather_steps(parts, shard)
         if shard.world > 1:
-            dist.all_reduce(tot, group=shard.group)
-        gates = ops.ess_gate_tiled_batch(parts, N, 0, False)
+            # ONE all-gather of each rank's summary: its rows' gate terms of every step (the per-row
+            # half of the batch gate's arithmetic, nfdpf_ess_row_terms: T x B floats instead of the
+            # T x B x tiles x 4 doubles of partials), its hand-off fault counter and its per-step
+            # log-weight sums; then the gates over the gathered rows (nfdpf_ess_gate_terms), and
+            # ONE host read of {gates, faults}
+            T, B = parts.shape[0], parts.shape[1]
+            summ = torch.cat([tot.view(torch.float32), ops.ess_row_terms(parts, N)])  # (the fp64 words first)
+            S = summ.numel()
+            g = torch.empty(shard.world * S, device=summ.device, dtype=torch.float32)
+            dist.all_gather_into_tensor(g, summ, group=shard.group)
+            g = g.view(shard.world, S)
+            terms = g[:, 2 * T:2 * T + T * B].reshape(shard.world, T, B).permute(1, 0, 2).reshape(T, shard.world * B)
+            gates = ops.ess_gate_terms(terms, N)
+            faults = g[:, 2 * T + T * B].view(torch.int32).to(torch.int64).sum()
+            host = torch.cat([gates.to(torch.int64), faults.view(1)]).cpu()
+            faults = int(host[T])
+            if faults:
+                if not was_pass:
+                    raise L.NfdpfError(f"nfdpf_filter_step_tiled: {faults} wave hand-off(s) timed out on the device "
+                                       f"(outputs invalid)")
+                self._pass_fault(faults)
+                self.last_verify = "fault"
+                return False
+            tot = g[:, :2 * T].contiguous().view(torch.float64).sum(0)  # (rank order)
+            gates = host[:T].to(torch.int32)
+        else:
+            if split_dev is not None:
+                if was_pass:
+                    faults = self._faults_all(shard, split_dev)
+                    if faults:
+                        self._pass_fault(faults)
+                        self.last_verify = "fault"
+                        return False
+                else:
+                    L.check_split_fault("nfdpf_filter_step_tiled", split_dev)
+            gates = ops.ess_gate_tiled_batch(parts, N, 0, False)
         if plan is not None:  # the pass followed a plan: its actual gates must be the plan's
             g = gates.cpu().numpy()
             if not np.array_equal(g, plan):

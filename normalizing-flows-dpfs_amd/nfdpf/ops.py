@@ -721,6 +721,29 @@ def ess_gate_tiled_batch(parts, N, t0=0, force=False, out=None):
     return g
 
 
+def ess_row_terms(parts, N, t0=0, out=None):
+    """[T, B, tiles, 4] step partials -> float32 [T * B + 1]: the rows' gate terms (1 / sum p^2,
+    t-major), then this device's hand-off fault counter (read and cleared) as int32 bits
+    (include/nfdpf.h nfdpf_ess_row_terms)."""
+    T, B = parts.shape[0], parts.shape[1]
+    parts = parts.to(torch.float64).contiguous()
+    terms = out if out is not None else torch.empty(T * B + 1, device=parts.device, dtype=torch.float32)
+    check(lib().nfdpf_ess_row_terms(ptr(parts), T, B, N, int(t0), ptr(terms), stream_ptr(parts.device)),
+          "nfdpf_ess_row_terms")
+    return terms
+
+
+def ess_gate_terms(terms, N, force=False, out=None):
+    """float32 [T, B_global] gathered gate terms -> the T batch-global gates int32 [T]
+    (nfdpf_ess_gate_terms: ATen's cascade mean over the rows, as nfdpf_ess_gate_tiled_batch)."""
+    T, B = terms.shape
+    terms = terms.contiguous()
+    g = out if out is not None else torch.empty(T, device=terms.device, dtype=torch.int32)
+    check(lib().nfdpf_ess_gate_terms(ptr(terms), T, B, N, int(bool(force)), ptr(g), stream_ptr(terms.device)),
+          "nfdpf_ess_gate_terms")
+    return g
+
+
 def pass_verify(parts, lw_sum, N, t0=0):
     """[T, B, tiles, 4] step partials and [B, T] lw_sum of a one-shard speculative pass ->
     (gates int32 [T], flags int32 [2] = {gates fired, hand-off faults since the last read},

@@ -274,6 +274,30 @@ def test_pass_verify_matches_gate_batch(T, B, N):
         assert 0 < int(ref.sum()) < T, "the case should mix fired and quiet steps"
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_terms_gates_match_gate_batch(world):
+    """The sharded verification's two halves (each rank: nfdpf_ess_row_terms of its rows; after
+    the gather: nfdpf_ess_gate_terms over B_global rows) == the batch gate kernel on the gathered
+    partials, bit for bit, with fired and quiet steps; the fault word rides at the end."""
+    from nfdpf import ops
+    T, B, N = 12, 8, 1000
+    tiles = (N + 255) // 256
+    g = torch.Generator().manual_seed(world)
+    odd = (torch.arange(T)[:, None, None] % 2 == 1).double()
+    m = torch.randn(T, world * B, tiles, generator=g, dtype=torch.float64) * odd
+    e = torch.rand(T, world * B, tiles, generator=g, dtype=torch.float64) * 250 + 1
+    sq = e * e / 256 * (1 + 0.01 + 30.0 * odd)
+    parts = torch.stack([m, e, sq, torch.zeros_like(m)], -1).to(DEV)
+    ref = ops.ess_gate_tiled_batch(parts, N, 0, False)
+    per_rank = [ops.ess_row_terms(parts[:, r * B:(r + 1) * B], N) for r in range(world)]
+    assert all(int(t[T * B:].view(torch.int32)) == 0 for t in per_rank)  # no hand-off fault
+    terms = torch.stack([t[:T * B].view(T, B) for t in per_rank], 1).reshape(T, world * B)
+    gates = ops.ess_gate_terms(terms, N)
+    torch.cuda.synchronize()
+    assert torch.equal(gates, ref), (gates.tolist(), ref.tolist())
+    assert 0 < int(ref.sum()) < T
+
+
 def test_pass_disabled_by_env(monkeypatch):
     """NFDPF_PASS=0 keeps the step-by-step launches (the library reads it per call)."""
     fx = load("e2e_c2.npz")
