@@ -353,7 +353,9 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
         # runs: the host round trip no longer leaves the GPU idle between passes.  A fired gate
         # reruns pass k (gated) before the next replay; the last pass is verified inside the
         # timing.
-        pipelined = (spec or decided) and world == 1
+        # (sharded, round 6: the same, the verification's small all-gather and gate kernels staged
+        # on the stream behind each replay and its result copied to pinned host memory)
+        pipelined = spec or decided
         graphs, caps, pends = [], [], []
         try:
             for _ in range(2 if pipelined else 1):
@@ -396,8 +398,8 @@ def timed_passes(fcfg, dpf, enc, start, vel_in, shard, args, world, dev):
             i = pipe["k"] & 1
             eng.arm_flags(pends[i])
             graphs[i].replay()
-            if pends[i][6] is not None and pends[i][6][0] is not None:  # flags on the device: stage a copy
-                eng.stage_flags(pends[i])
+            if world > 1 or (pends[i][6] is not None and pends[i][6][0] is not None):
+                eng.stage_flags(pends[i])  # flags on the device (or sharded: the gather): stage a copy
                 evs_done[i].record()
             out = verify_prev()
             pipe["prev"], pipe["k"] = i, pipe["k"] + 1

@@ -891,8 +891,10 @@ class FilterEngine:
                     if pass_out is not None else list(ops.pass_verify(ess_hist[:T], lw_sum, N)[1:]) + [None, None]
                 check_split = False
             # (+ the plan followed, and one shard's actual gates: a miss's new plan)
+            # (+ the plan followed, one shard's actual gates, and -- sharded -- the staged verification,
+            # stage_flags)
             self._pending = (ess_hist[:T], tot, shard, N, res, dev if check_split else None, verify, use_pass, False,
-                             plan_arr, pass_out[0] if pass_out is not None else None)
+                             plan_arr, pass_out[0] if pass_out is not None else None, [])
             if not finish:
                 return res  # the caller verifies (finish_pending, e.g. after each graph replay)
             ok = self.finish_pending()
@@ -929,6 +931,26 @@ class FilterEngine:
         return FilterResult(hx, hp, hn, hl, logw0, hi, hj, hr, obs, pred, fired)
 
     @staticmethod
+    def _sharded_verify(parts, tot, shard, N):
+        """The verification of a sharded speculative / plan pass, enqueued on the current stream:
+        ONE all-gather of each rank's summary -- its per-step log-weight sums (fp64), its rows' gate
+        terms of every step (nfdpf_ess_row_terms: the per-row half of the batch gate's arithmetic,
+        T x B floats instead of the T x B x tiles x 4 doubles of partials) and its hand-off fault
+        counter -- then the T gates over the gathered rows (nfdpf_ess_gate_terms).  -> (int64
+        [T + 1] on the device: the gates, then the faults summed over the ranks; fp64 [T]: the
+        step sums summed over the ranks, in rank order)."""
+        T, B = parts.shape[0], parts.shape[1]
+        summ = torch.cat([tot.view(torch.float32), ops.ess_row_terms(parts, N)])  # (the fp64 words first)
+        S = summ.numel()
+        g = torch.empty(shard.world * S, device=summ.device, dtype=torch.float32)
+        dist.all_gather_into_tensor(g, summ, group=shard.group)
+        g = g.view(shard.world, S)
+        terms = g[:, 2 * T:2 * T + T * B].reshape(shard.world, T, B).permute(1, 0, 2).reshape(T, shard.world * B)
+        gates = ops.ess_gate_terms(terms, N)
+        faults = g[:, 2 * T + T * B].view(torch.int32).to(torch.int64).sum()
+        return torch.cat([gates.to(torch.int64), faults.view(1)]), g[:, :2 * T].contiguous().view(torch.float64).sum(0)
+
+    @staticmethod
     def stage_flags(pending):
         """Enqueue (current stream) the copy of a one-shard speculative pass's device flags
         {fired, faults} into pinned host memory; after an event recorded behind it has completed,
@@ -936,6 +958,15 @@ class FilterEngine:
         later pass already queued keeps running (pipelined passes, bench.py).  Not while
         capturing a graph (the pinned allocation is not capturable): after the replay."""
         verify = pending[6]
+        parts, tot, shard, N = pending[:4]
+        if verify is None and shard is not None and shard.world > 1 and len(pending) > 11:
+            # sharded: the all-gather and the gates enqueued now, their small result copied to
+            # pinned host memory behind them (every rank stages the same sequence of collectives)
+            dev_small, tot_all = FilterEngine._sharded_verify(parts, tot, shard, N)
+            host = torch.empty(dev_small.shape, dtype=dev_small.dtype, pin_memory=True)
+            host.copy_(dev_small, non_blocking=True)
+            pending[11][:] = [host, tot_all]
+            return
         if verify is None or verify[0] is None:  # (flags already mapped from host memory)
             return
         if verify[2] is None:
@@ -1033,16 +1064,15 @@ class FilterEngine:
             # T x B x tiles x 4 doubles of partials), its hand-off fault counter and its per-step
             # log-weight sums; then the gates over the gathered rows (nfdpf_ess_gate_terms), and
             # ONE host read of {gates, faults}
-            T, B = parts.shape[0], parts.shape[1]
-            summ = torch.cat([tot.view(torch.float32), ops.ess_row_terms(parts, N)])  # (the fp64 words first)
-            S = summ.numel()
-            g = torch.empty(shard.world * S, device=summ.device, dtype=torch.float32)
-            dist.all_gather_into_tensor(g, summ, group=shard.group)
-            g = g.view(shard.world, S)
-            terms = g[:, 2 * T:2 * T + T * B].reshape(shard.world, T, B).permute(1, 0, 2).reshape(T, shard.world * B)
-            gates = ops.ess_gate_terms(terms, N)
-            faults = g[:, 2 * T + T * B].view(torch.int32).to(torch.int64).sum()
-            host = torch.cat([gates.to(torch.int64), faults.view(1)]).cpu()
+            T = parts.shape[0]
+            stage = pend[11] if len(pend) > 11 else []
+            if stage:  # staged (stage_flags): read with no stream operation once known complete
+                if not synced:
+                    torch.cuda.current_stream().synchronize()
+                host, tot = stage[0], stage[1]
+            else:
+                dev_small, tot = self._sharded_verify(parts, tot, shard, N)
+                host = dev_small.cpu()
             faults = int(host[T])
             if faults:
                 if not was_pass:
@@ -1051,7 +1081,6 @@ class FilterEngine:
                 self._pass_fault(faults)
                 self.last_verify = "fault"
                 return False
-            tot = g[:, :2 * T].contiguous().view(torch.float64).sum(0)  # (rank order)
             gates = host[:T].to(torch.int32)
         else:
             if split_dev is not None:
