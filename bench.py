@@ -259,15 +259,21 @@ def ot_call_ms(res, T, iters=10):
     return best
 
 
-def rocprof_avg_ms(tag, kname):
+def rocprof_avg_ms(tag, kname, instance=None):
     """Average duration (ms) of ``kname`` in the committed rocprofv3 --kernel-trace --stats
-    summary of this workload's bench command (scripts/r03_measure.sh -> profiles/rocprof_<tag>.csv,
-    tag = config [+ _force]), and the file; (None, None) when there is none."""
+    summary of this workload's bench command (scripts/r06.sh prof -> profiles/rocprof_<tag>.csv,
+    tag = config [+ _force]), and the file; (None, None) when there is none.  ``instance``: the
+    template instance's name prefix (e.g. "tiled_pass_kernel<0,": the speculative pass) -- the
+    summary of one bench command holds its forced and informative lines' instances too."""
     path = os.path.join(ROOT, "profiles", f"rocprof_{tag}.csv")
     if not os.path.exists(path):
         return None, None
     import csv
     rows = list(csv.DictReader(open(path)))
+    if instance is not None:
+        for row in rows:
+            if row["Name"].split("::", 1)[-1].startswith(instance):
+                return float(row["AverageNs"]) * 1e-6, os.path.relpath(path, ROOT)
     # "<kernel>[full]" (scripts/rocprof_ot_split.py): the Sinkhorn launches that ran an iteration,
     # without the early-exit tail the plain row averages in
     for want in (kname + "[full]", kname):
@@ -518,7 +524,21 @@ def dominant(cfg_name, flags, kernel, B, N, T, fcfg, run, force):
             nbytes = 44.0 * B * N
     tag = cfg_name + ("_force" if force else "")
     traffic, traffic_src = pmc_traffic(tag, kname)
-    rp_ms, rp_src = rocprof_avg_ms(tag, kname)
+    # the pass kernel's template instance that ran: the mode (0 speculative, 1 forced, 2 gated /
+    # plan; sharded gated: the cross-rank instance), or the no-flow pass's <MEAS, MFMA, K>
+    instance = None
+    if kname == "tiled_pass_kernel":
+        mode = 1 if force else (2 if (eng.last_gate_pass or eng.last_plan_pass) else 0)
+        xr = "true" if (mode == 2 and eng.last_gate_pass and B * (dist.get_world_size() if dist.is_initialized()
+                                                                   else 1) != B) else "false"
+        instance = f"tiled_pass_kernel<{mode}, {xr}>"
+    elif kname == "tiled_pass_cm_kernel":
+        meas = {"CRNVP": 1, "cos": 0, "gaussian": 3}.get(flags["measurement"])
+        mf = flags["measurement"] == "CRNVP" and os.environ.get("NFDPF_CM_MFMA", "1") != "0"
+        k = os.environ.get("NFDPF_CM_K") or ("3" if mf else "2")
+        if meas is not None:
+            instance = f"tiled_pass_cm_kernel<{meas}, {'true' if mf else 'false'}, {k}>"
+    rp_ms, rp_src = rocprof_avg_ms(tag, kname, instance)
     achieved_tf = F_ALG * units / (kernel_ms * 1e-3) / 1e12
     hbm_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
     # bound: the FP32 issue rate of the CU -- VALU for the coupling nets / Sinkhorn
