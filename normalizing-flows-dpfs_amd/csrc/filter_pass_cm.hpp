@@ -53,6 +53,9 @@ struct PassCmLds {
   float nb[2][5][kTile];     // slot t's hand-over by parity: lr, raw lik, prior, x0, x1
   alignas(16) float encq[4 * kCmMaxK][kE];  // each wave's copy of its step's frame encoding (crnvp_lik's encv)
   uint32_t rowc[kPassMaxTiles * 4 * kGC];
+  // a one-tile row (N <= 256, C1): exchange C stays in the workgroup -- the 4 groups' tagged
+  // granules by slot parity in LDS instead of the global granules (one LDS round trip, not an L2 one)
+  uint64_t cx[2][4 * kGC];
   RowNorm rn[2];
   int xf[4];                 // x_t of group g written (t + 1)
   int fR;                    // slot t's row normaliser in rn[t & 1] (t + 1)
@@ -61,12 +64,36 @@ struct PassCmLds {
 // the row normaliser of slot s from its C(s) granules (tiles x 4 groups, each {max u, sum e,
 // sum e^2, max raw lik}): the tile's merge over its groups in order (ess_out[s], the gate's
 // input), then row_norm's arithmetic over the tiles in order with the CRNVP shift.  One wave.
-template <bool SHIFT>
+// LDSC: the LDS exchange may apply (one-tile rows; compiled out of the MFMA measurement's kernel,
+// whose C3 rows have 4 tiles and whose registers are tight)
+template <bool SHIFT, bool LDSC>
 __device__ __forceinline__ void pass_cm_poll_c(const nfdpf_filter_desc &d, const PassWs &ws, PassCmLds &L, int b,
                                                int tile, uint32_t tag0, int s) {
   const int tiles = n_tiles(d.N), lane = threadIdx.x & 63;
   const int64_t row0 = (((int64_t)(s & 1) * d.B + b) * tiles) * 4;
-  if (poll_row(ws.gc + row0 * kGC, tiles * 4 * kGC, tag0 + (uint32_t)s + 1u, L.rowc)) {
+  bool got;
+  if (LDSC && tiles == 1) {  // the row's four groups in this workgroup: their granules in LDS
+    const uint32_t tag = tag0 + (uint32_t)s + 1u;
+    volatile uint64_t *cx = L.cx[s & 1];
+    uint64_t v = 0;
+    bool ok = lane >= 4 * kGC;
+    Spin sp;
+    for (;;) {
+      if (!ok) {
+        v = cx[lane];
+        ok = (uint32_t)(v >> 32) == tag;
+      }
+      if (__all(ok)) break;
+      if (!pass_spin(sp)) break;
+    }
+    got = __all(ok);
+    if (got && lane < 4 * kGC) L.rowc[lane] = (uint32_t)v;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  } else {
+    got = poll_row(ws.gc + row0 * kGC, tiles * 4 * kGC, tag0 + (uint32_t)s + 1u, L.rowc);
+  }
+  if (got) {
     const int k = lane < tiles ? lane : 0;
     float m = -INFINITY, lm = -INFINITY;
 #pragma unroll
@@ -154,6 +181,7 @@ __global__ __launch_bounds__(4 * K * 64, 1) void tiled_pass_cm_kernel(const nfdp
   const uint32_t tag0 = __hip_atomic_load(&ws.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 12;
   if (threadIdx.x < 4) L.xf[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.fR = 0;
+  if (threadIdx.x < 2 * 4 * kGC) (&L.cx[0][0])[threadIdx.x] = 0;  // (no tag: never a match)
   if constexpr (MF) {  // (16-B aligned blob of whole float4s: checked on the host)
     const f4v *src = reinterpret_cast<const f4v *>(d.meas_params);
     for (int q = threadIdx.x; q < crnvp_mfma_floats(d.n_flows) / 4; q += blockDim.x) wfr[q] = src[q];
@@ -232,7 +260,7 @@ __global__ __launch_bounds__(4 * K * 64, 1) void tiled_pass_cm_kernel(const nfdp
     }
     // 3. slot t - 1: its row normaliser (group 0's wave sweeps C(t - 1)), its normalisation
     if (t > 0) {
-      if (g == 0) pass_cm_poll_c<SHIFT>(d, ws, L, b, tile, tag0, t - 1);
+      if (g == 0) pass_cm_poll_c<SHIFT, !MF>(d, ws, L, b, tile, tag0, t - 1);
       lr = pass_cm_norm<SHIFT>(d, ws, L, b, tile, g, t - 1, slot, i, valid);
     }
     // 4. the log-weight (DPFs.py:187) and exchange C(t): this group's softmax partials
@@ -259,12 +287,15 @@ __global__ __launch_bounds__(4 * K * 64, 1) void tiled_pass_cm_kernel(const nfdp
                             : lane == 4 ? (uint32_t)(qb >> 32)
                                         : __float_as_uint(lmw);
       const int64_t gslot = (((int64_t)par * d.B + b) * tiles + tile) * 4 + g;
-      gran_store(ws.gc + gslot * kGC + lane, word, tag0 + (uint32_t)t + 1u);
+      if (!MF && tiles == 1)
+        *(volatile uint64_t *)&L.cx[par][g * kGC + lane] = ((uint64_t)(tag0 + (uint32_t)t + 1u) << 32) | word;
+      else
+        gran_store(ws.gc + gslot * kGC + lane, word, tag0 + (uint32_t)t + 1u);
     }
   }
   // the last slot's normalisation: the waves of parity T & 1 (they would have run step T)
   if (k == d.T % K) {
-    if (g == 0) pass_cm_poll_c<SHIFT>(d, ws, L, b, tile, tag0, d.T - 1);
+    if (g == 0) pass_cm_poll_c<SHIFT, !MF>(d, ws, L, b, tile, tag0, d.T - 1);
     pass_cm_norm<SHIFT>(d, ws, L, b, tile, g, d.T - 1, slot, i, valid);
   }
 }
