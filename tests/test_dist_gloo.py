@@ -262,3 +262,56 @@ def test_ot_stop_exchange_in_autograd_loop_world2():
     for rank, calls, x0 in res:
         assert calls == ["local", 20], calls
         assert x0 == 20.0
+
+
+def _worker_verify(rank, world, port, q):
+    """FilterEngine._sharded_verify's plumbing (the summary layout, the rank-major row order of the
+    gathered terms, the fault and step-sum reductions) on CPU tensors, with the two kernels
+    restated in torch (their arithmetic is pinned on the GPU: test_row_terms_gates_match_gate_batch)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "normalizing-flows-dpfs_amd"), root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nfdpf import ops
+        from nfdpf.engine import FilterEngine, ShardInfo
+        T, B, N = 5, 3, 50
+
+        def row_terms(parts, N, t0=0, out=None):  # terms [T*B] (t-major) then the fault word
+            terms = parts[..., 1].sum(-1).float().reshape(-1)
+            fault = torch.tensor([rank + 2], dtype=torch.int32).view(torch.float32)
+            return torch.cat([terms, fault])
+
+        def gate_terms(terms, N, force=False, out=None):
+            return (terms.mean(1) < 0.5 * N).to(torch.int32)
+        ops.ess_row_terms, ops.ess_gate_terms = row_terms, gate_terms
+        sh = ShardInfo.from_env(B)
+        g = torch.Generator().manual_seed(3)
+        parts_all = torch.rand(T, world * B, 2, 4, generator=g, dtype=torch.float64) * 40
+        tot_all = torch.rand(world, T, generator=g, dtype=torch.float64)
+        parts = parts_all[:, rank * B:(rank + 1) * B].contiguous()
+        small, tot = FilterEngine._sharded_verify(parts, tot_all[rank].clone(), sh, N)
+        q.put((rank, small.numpy(), tot.numpy(), parts_all.numpy(), tot_all.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_verify_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_verify, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    T, N = 5, 50
+    for rank, small, tot, parts_all, tot_all in out:
+        terms = parts_all[..., 1].sum(-1).astype(np.float32)  # [T, world * B], global row order
+        gates = (terms.mean(1) < 0.5 * N).astype(np.int64)
+        assert np.array_equal(small[:T], gates), (rank, small[:T], gates)
+        assert small[T] == sum(r + 2 for r in range(world))  # the fault words, summed over the ranks
+        np.testing.assert_allclose(tot, tot_all.sum(0), rtol=0, atol=1e-12)
