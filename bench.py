@@ -704,10 +704,14 @@ def main():
     if not args.force_resample and not args.enc_from_state and not args.no_informative and cheap and \
             flags["measurement"] in ("cos", "CRNVP"):
         dpf_i, enc_i, enc_note = dpf, enc_inf, "particle encoder at the true positions (--enc-from-state)"
+        rmse_note = None
         if flags["measurement"] == "CRNVP":  # C3: the reference init's likelihood is flat -- a trained-like model
             dpf_i, enc_i = trained_like(dpf, state)
             enc_note = ("trained-like CRNVP model (particle encoder ~ N(0, 0.5^2), flows ~ N(0, 0.1^2), seeded: the "
                         "c3_full parity case's) and its encoder at the true positions + 30 % noise")
+            rmse_note = ("random weights at trained scales, not a trained model: its sharp likelihood does not peak "
+                         "at the truth, so the filter drifts (the line times the OT-firing regime; parity of its "
+                         "Sinkhorn calls: scripts/r06_c3_trained_diag.py, test_fullsize_ot_direct)")
         run_i = timed_passes(fcfg, dpf_i, enc_i, start, vel_in, shard, args, world, dev)
         res_i = run_i["res"]
         ident = (torch.arange(N, device=dev) + N * (shard.row_base + torch.arange(B, device=dev))[:, None])
@@ -720,6 +724,7 @@ def main():
         informative = {"value": B * world * N * T * args.steps / run_i["elapsed"], "unit": "particle-steps/s",
                        "ms_per_step": run_i["elapsed"] / args.steps * 1e3, "steps": args.steps,
                        "resampled_steps": fired_i, "of_steps": T, "rmse": float(torch.sqrt(se_i / cnt)),
+                       **({"rmse_note": rmse_note} if rmse_note else {}),
                        "encodings": enc_note,
                        "execution": ("hipGraph replay of the pass" if run_i["graph"] is not None else "Python launches")
                                     + (", the whole pass as one launch" if eng_i.last_pass else "")

@@ -643,6 +643,7 @@ class FilterEngine:
 
         fired = [] if host_mode else None
         self.last_ot_calls = 0
+        ot_its = []  # the device-gated Sinkhorn calls' iteration counts (0: the gate was off)
         self.last_fused = False  # the step ran as one launch (tiled_step_fused_kernel), set at t = 0
         keep = []  # host uploads must outlive their kernels
         # per-step pointers precomputed as integers: the loop below is the launch path of every
@@ -768,13 +769,20 @@ class FilterEngine:
                     xin, pin = xp, pp
                 else:
                     xin, pin = hx[:, t - 1].contiguous(), hp[:, t - 1].contiguous()
-                # The Sinkhorn loop is max_iter launches; when the gate is off they would all be
-                # no-ops, so read the gate (one sync, as the reference's `if ESS < ...` does,
-                # DPFs.py:165) and skip the call.  The gate is batch-global: same on every rank.
-                # (--force-resample: the gate is on by construction -- no read, no sync)
-                fire = fired[-1] if host_mode else (True if c.force_resample else bool(gate_buf.item()))
-                if fire:
-                    self.last_ot_calls += 1
+                # The Sinkhorn call reads the device gate itself (every launch of a call whose gate
+                # is off returns at once, and the host's poll stops enqueueing iterations after the
+                # first), so the host does not wait for the gate before enqueueing the call: the
+                # reference's `if ESS < ...` (DPFs.py:165) is a host sync per step, which left the
+                # device idle while the call's launches went out.  The steps that resampled are
+                # counted from the calls' iteration counts after the pass (0: the gate was off).
+                # The gate is batch-global: same on every rank.  (--force-resample: on by
+                # construction; host draws / teacher forcing: the host's own decision.)
+                device_gate = not host_mode and teacher is None and not c.force_resample
+                fire = fired[-1] if host_mode else (True if c.force_resample else
+                                                    (None if device_gate else bool(gate_buf.item())))
+                if fire is None or fire:
+                    if fire:
+                        self.last_ot_calls += 1
                     if shard.world > 1:
                         # batch-coupled stop over every rank's rows (resamplers.py:126-129): the
                         # local loop, the MIN of the stop count, the tail at that state
@@ -784,7 +792,9 @@ class FilterEngine:
                         xo, _, _, it = ops.ot_resample(xin, pin, c.eps, c.scaling, c.threshold, c.max_iter,
                                                        shard.row_base, gate=gate_buf)
                     keep.append(xo)
-                    d.ot_x = xo.data_ptr()
+                    if fire is None:
+                        ot_its.append(it)
+                    d.ot_x = xo.data_ptr()  # (read by the step only where the gate fired)
                 else:
                     d.ot_x = xin.data_ptr()  # not read: the motion stage keeps the previous particles
             if t == 0 and tiled and not external:
@@ -879,6 +889,8 @@ class FilterEngine:
         if check_split and (finish or not spec) and not verify_dev and not use_pass:
             L.check_split_fault("nfdpf_filter_step_tiled", dev)
             check_split = False
+        if ot_its:  # (one read for the pass: the device-gated calls that ran)
+            self.last_ot_calls += int(torch.cat(ot_its).gt(0).sum())
         if c.resampler == "ot" and not spec:
             self._ot_fired = self.last_ot_calls > 0
         # obs_likelihood = sum_t mean_{b,n} logw_t (DPFs.py:191)
