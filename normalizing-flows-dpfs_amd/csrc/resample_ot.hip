@@ -957,7 +957,7 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
 
 __device__ __forceinline__ int ot_total_iter(const OtParams &P, const OtWs &ws) {
   // the caller's count (a sharded batch's global stop, the MIN over ranks of their own)
-  if (P.stop_at) return min(*P.stop_at - 2, max(P.max_iter - 1, 0));
+  if (P.stop_at) return max(min(*P.stop_at - 2, P.max_iter - 1), 0);  // (a stop_at < 2 reads state 0)
   return ws.st->stopped ? ws.st->K : max(P.max_iter - 1, 0);
 }
 
