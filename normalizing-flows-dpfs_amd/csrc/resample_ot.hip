@@ -89,6 +89,15 @@ __device__ __forceinline__ f2 pfma2(f2 a, f2 b, f2 c) { return __builtin_element
 #ifdef NFDPF_OT_RISKSTAT  // experiment builds: share of wave-slices on the two-exp path, per call
 __device__ unsigned int g_ot_risky, g_ot_wslices;
 #endif
+#ifdef NFDPF_EXP_OTTRACE  // experiment builds: per-phase timestamps of every iteration launch, lane 0 of wave 0
+__device__ uint64_t g_ot_tr[1024][64][8], g_ot_loopend[1024];
+#define OTT_WG (blockIdx.y * gridDim.x + blockIdx.x)
+#define OTTRACE(k, slot)                                         \
+  if (threadIdx.x == 0 && OTT_WG < 1024)                         \
+    g_ot_tr[OTT_WG][(k) & 63][slot] = __builtin_amdgcn_s_memrealtime();
+#else
+#define OTTRACE(k, slot)
+#endif
 struct OtState {
   int32_t stopped;    // set by the iteration that observes a converged row
   int32_t K;          // total_iter of the reference
@@ -621,6 +630,9 @@ __device__ __forceinline__ void wg_iter_sums(const float *tab, const double *msh
     }
 #undef OT_SLICE_LOOP
   }
+#ifdef NFDPF_EXP_OTTRACE
+  if (threadIdx.x == 0 && OTT_WG < 1024) g_ot_loopend[OTT_WG] = __builtin_amdgcn_s_memrealtime();
+#endif
   float mine[KR][2], out[2];
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
@@ -895,6 +907,7 @@ template <int W>
 __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) void ot_iter_kernel(
     OtParams P, OtWs ws, int k) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+  OTTRACE(k, 0)
   if (ot_off(P)) {
     if (lead && P.host) host_flag(P.host, 0, P.seq);  // nothing to iterate: stop enqueueing
     return;
@@ -919,6 +932,7 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
   }
   __syncthreads();
   if (s_stop) return;
+  OTTRACE(k, 1)
   const int b = blockIdx.y, N = P.N;
   const int i = blockIdx.x * kOtThreads + threadIdx.x;
   const bool v = i < N && threadIdx.x < kOtThreads;
@@ -943,6 +957,10 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
       },
       [&](int j) { return ((double)lw[j] + bx[j] * inv) * kLog2ed; },
       [&](int j) { return (logu + ay[j] * inv) * kLog2ed; }, lds, A, Bv, &ws.st->fallbacks);
+  OTTRACE(k, 3)
+#ifdef NFDPF_EXP_OTTRACE
+  if (threadIdx.x == 0 && OTT_WG < 1024) g_ot_tr[OTT_WG][k & 63][2] = g_ot_loopend[OTT_WG];
+#endif
   double na = 0.0, nb = 0.0, dmax = 0.0;
   if (v) {
     na = 0.5 * (oa + A);
@@ -951,7 +969,9 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
     pot_ptr(ws, P, k + 1, 1, b)[i] = nb;
     dmax = fmax(fabs(na - oa), fabs(nb - ob));
   }
+  OTTRACE(k, 4)
   emit_state_tables(P, ws, b, k + 1, v, xi, yi, v ? lw[i] : 0.f, logu, na, nb, shd, &dmax);
+  OTTRACE(k, 5)
   if (threadIdx.x == 0) ws.res[((int64_t)(k & 1) * P.B + b) * P.splits + blockIdx.x] = dmax;
 }
 
@@ -1232,6 +1252,12 @@ static int ot_iter_waves(int /*wgs*/) {
   const char *e = getenv("NFDPF_OT_ITER_WAVES");  // read per call (tests switch it)
   return (e && atoi(e) == 2 * kWaves) ? 2 * kWaves : kWaves;
 }
+
+#ifdef NFDPF_EXP_OTTRACE
+extern "C" __attribute__((visibility("default"))) int nfdpf_exp_ottrace(uint64_t *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ot_tr), sizeof(g_ot_tr)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int64_t nfdpf_ot_workspace_bytes(int B, int N) {
   return (B <= 0 || N <= 0) ? 256 : ws_bytes(B, N);

@@ -7,7 +7,7 @@
 set -e
 TAG=$1; shift
 SRC=${SRC:-filter_tiled}
-cd "$(dirname "$0")/../normalizing-flows-dpfs_amd/csrc"
+cd "$(dirname "$0")/../../normalizing-flows-dpfs_amd/csrc"
 mkdir -p ../../exp /tmp/nfdpf_exp
 FLAGS="-O3 -std=c++17 -fPIC -fvisibility=hidden --offload-arch=gfx950 -w"
 /opt/rocm/bin/hipcc $FLAGS "$@" -c $SRC.hip -o /tmp/nfdpf_exp/${SRC}_${TAG}.o
