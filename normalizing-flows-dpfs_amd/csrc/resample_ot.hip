@@ -972,6 +972,12 @@ __global__ __launch_bounds__(64 * W, W == 2 * kWaves ? 4 : NFDPF_OT_ITER_WPS) vo
   OTTRACE(k, 4)
   emit_state_tables(P, ws, b, k + 1, v, xi, yi, v ? lw[i] : 0.f, logu, na, nb, shd, &dmax);
   OTTRACE(k, 5)
+#ifdef NFDPF_EXP_OTTRACE
+  if (threadIdx.x == 0 && OTT_WG < 1024) {
+    g_ot_tr[OTT_WG][k & 63][6] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID (CU, SIMD, SE)
+    g_ot_tr[OTT_WG][k & 63][7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+  }
+#endif
   if (threadIdx.x == 0) ws.res[((int64_t)(k & 1) * P.B + b) * P.splits + blockIdx.x] = dmax;
 }
 

@@ -54,3 +54,29 @@ for k in range(min(K, 64)):
 print(f"median first-start -> last-end {np.median(tot):.2f} us")
 print("ot_stats (iterations, exact fallbacks -- per-mille of wave-slices on the two-exp path in an "
       "-DNFDPF_OT_RISKSTAT build):", ops.ot_stats())
+# per-workgroup spread at one iteration: total time vs placement (HW_ID / XCC_ID of wave 0)
+k = min(K, 64) // 2
+t = tr[:, k, :]
+tot_wg = (t[:, 5] - t[:, 0]) * 0.01
+loop_wg = (t[:, 2] - t[:, 1]) * 0.01
+hw = t[:, 6].astype(np.int64)
+xcc = t[:, 7].astype(np.int64) & 0xF
+cu = (hw >> 8) & 0xF
+se = (hw >> 13) & 0x7
+S = (N + 255) // 256
+print(f"iteration {k}: per-WG total us p10/p50/p90/max {np.percentile(tot_wg, [10, 50, 90, 100]).round(2)}; "
+      f"loop p10/p50/p90/max {np.percentile(loop_wg, [10, 50, 90, 100]).round(2)}")
+for x in range(8):
+    sel = xcc == x
+    if sel.any():
+        print(f"  XCC {x}: {sel.sum()} WGs, total p50 {np.median(tot_wg[sel]):.2f} max {tot_wg[sel].max():.2f}")
+key = xcc * 1000 + se * 100 + cu
+u, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+share = cnt[inv]
+for c in sorted(set(share)):
+    sel = share == c
+    print(f"  WGs sharing a CU with {c - 1} other(s): {sel.sum()}, total p50 {np.median(tot_wg[sel]):.2f}")
+rows = np.arange(len(tot_wg)) // S
+slices = np.arange(len(tot_wg)) % S
+print("  total p50 by slice index:", [round(float(np.median(tot_wg[slices == q])), 1) for q in range(S)])
+print("  end stamp spread (us) first/last WG end:", (t[:, 5].min() - t[:, 0].min()) * 0.01, (t[:, 5].max() - t[:, 0].min()) * 0.01)
