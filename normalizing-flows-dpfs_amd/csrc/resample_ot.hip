@@ -717,16 +717,20 @@ __device__ __forceinline__ void write_col(float *tab, double *msh, int64_t Np, b
 }
 
 // ------------------------------------------------------------------------------------------
-// setup: centre/scale (transport_function :218-222), eps0 = max_min^2 (:87-91, :117), logw
+// setup + the initial table, one launch of (splits, B) workgroups: every workgroup of row b
+// reduces the whole row itself -- centre/scale (transport_function :218-222), eps0 = max_min^2
+// (:87-91, :117), the largest log weight -- in the same order as its row's other workgroups
+// (identical results), writes the scaled points / log weights of its own slice and, slice 0,
+// the row's constants; then its slice of the table of the initial softmins at eps0
+// (:120-121): h_a = logw, h_b = logu (base 2).  (Round 1-6: a row launch of up to 1024
+// threads, then the table launch: 15 + 5 us at C3.)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict__ x,
-                                                        const float *__restrict__ w, int N,
-                                                        OtWs ws, const int32_t *gate, double sf,
-                                                        double eps) {
-  if (gate && *gate == 0) return;
+__global__ __launch_bounds__(kOtBlock) void ot_setup_kernel(const float *__restrict__ x, const float *__restrict__ w,
+                                                            OtParams P, OtWs ws) {
+  if (ot_off(P)) return;
   __shared__ double shd[32];
   __shared__ float shf[16];
-  const int b = blockIdx.x;
+  const int b = blockIdx.y, N = P.N, s0i = blockIdx.x * kOtThreads, s1i = min(s0i + kOtThreads, N);
   const float *xr = x + (int64_t)b * N * 2;
   double s0 = 0, s1 = 0;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
@@ -749,30 +753,34 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
   const float dm = fmaxf(d0, d1);
   const double diam = dm == 0.0f ? 1.0 : (double)dm;
   const double scale = diam * (double)sqrtf(2.0f);
+  auto sx = [&](int i) { return (float)((double)(xr[2 * i] - m0) / scale); };
+  auto sy = [&](int i) { return (float)((double)(xr[2 * i + 1] - m1) / scale); };
+  auto lwf = [&](int i) { return logf(w[(int64_t)b * N + i]); };
   float mx = -INFINITY, mn = INFINITY, lwmax = -INFINITY;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
-    const float a = (float)((double)(xr[2 * i] - m0) / scale);
-    const float c = (float)((double)(xr[2 * i + 1] - m1) / scale);
-    ws.xs[((int64_t)b * N + i) * 2] = a;
-    ws.xs[((int64_t)b * N + i) * 2 + 1] = c;
+    const float a = sx(i), c = sy(i), lw = lwf(i);
+    if (i >= s0i && i < s1i) {  // this workgroup's slice
+      ws.xs[((int64_t)b * N + i) * 2] = a;
+      ws.xs[((int64_t)b * N + i) * 2 + 1] = c;
+      ws.logw[(int64_t)b * N + i] = lw;
+    }
     mx = fmaxf(mx, fmaxf(a, c));
     mn = fminf(mn, fminf(a, c));
-    const float lw = logf(w[(int64_t)b * N + i]);
-    ws.logw[(int64_t)b * N + i] = lw;
     lwmax = fmaxf(lwmax, lw);
   }
   mx = block_max(mx, shf);
   mn = -block_max(-mn, shf);
   lwmax = block_max(lwmax, shf);
-  if (threadIdx.x == 0) {
-    const double mm = (double)mx - (double)mn;
-    ws.rowc[b * 4 + 0] = mm * mm;                        // epsilon_0 = diameter^2 (:117)
-    ws.rowc[b * 4 + 1] = -(double)logf((float)N);       // uniform log weight (:214-215)
-    ws.rowc[b * 4 + 2] = (double)lwmax;                 // shift of the first a-softmin
-    double e = mm * mm;                                 // eps_k, k = 0 .. kEpsTab-1 (:158)
+  const double mm = (double)mx - (double)mn;
+  const double eps0 = mm * mm, logu = -(double)logf((float)N);
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    ws.rowc[b * 4 + 0] = eps0;           // epsilon_0 = diameter^2 (:117)
+    ws.rowc[b * 4 + 1] = logu;           // uniform log weight (:214-215)
+    ws.rowc[b * 4 + 2] = (double)lwmax;  // shift of the first a-softmin
+    double e = eps0;                     // eps_k, k = 0 .. kEpsTab-1 (:158)
     for (int k = 0; k < kEpsTab; ++k) {
       ws.epsk[(int64_t)b * kEpsTab + k] = e;
-      e = fmax(e * sf, eps);
+      e = fmax(e * P.sf, P.eps);
     }
     if (b == 0) {
 #ifdef NFDPF_OT_RISKSTAT
@@ -784,19 +792,13 @@ __global__ __launch_bounds__(1024) void ot_setup_kernel(const float *__restrict_
       ws.st->fallbacks = 0;
     }
   }
-}
-
-// table of the initial softmins at eps0 (:120-121): h_a = logw, h_b = logu (base 2)
-__global__ __launch_bounds__(kOtBlock) void ot_prep_kernel(OtParams P, OtWs ws) {
-  if (ot_off(P)) return;
-  __shared__ double shd[32];
-  const int b = blockIdx.y, N = P.N, i = blockIdx.x * kOtThreads + threadIdx.x;
+  // the slice's table columns (thread t: i = s0i + t), from the same expressions
+  const int i = s0i + threadIdx.x;
   const bool v = i < N && threadIdx.x < kOtThreads;
-  const float *xs = ws.xs + (int64_t)b * N * 2;
-  const double h[2] = {v ? (double)ws.logw[(int64_t)b * N + i] * kLog2ed : 0.0, ws.rowc[b * 4 + 1] * kLog2ed};
-  const float s = kPrescale ? pscale(cost_scale(1.0 / ws.rowc[b * 4])) : 1.f;  // ot_init's epsilon
-  write_col<2, 0, true>(tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), np_of(P), v, v ? xs[2 * i] * s : 0.f,
-                        v ? xs[2 * i + 1] * s : 0.f, h, nullptr, shd);
+  const double h[2] = {v ? (double)lwf(i) * kLog2ed : 0.0, logu * kLog2ed};
+  const float sc = kPrescale ? pscale(cost_scale(1.0 / eps0)) : 1.f;  // ot_init's epsilon
+  write_col<2, 0, true>(tabI_row(ws, P, 1, b), mI_row(ws, P, 1, b), np_of(P), v, v ? sx(i) * sc : 0.f,
+                        v ? sy(i) * sc : 0.f, h, nullptr, shd);
 }
 
 // Table columns of state `ks` (the potentials a_y, b_x of thread i just produced): for the
@@ -1095,7 +1097,11 @@ __global__ __launch_bounds__(kOtBlock) void ot_apply_kernel(OtParams P, OtWs ws,
                                                              int64_t row_base,
                                                              float *__restrict__ x_out,
                                                              float *__restrict__ w_out,
-                                                             int64_t *__restrict__ idx_out) {
+                                                             int64_t *__restrict__ idx_out,
+                                                             int32_t *__restrict__ iters_out) {
+  // the call's iteration count (iters_out encoding; 0: the gate was off), from the first lane
+  if (iters_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    iters_out[0] = ot_off(P) ? 0 : ot_total_iter(P, ws) + 2;
   if (ot_off(P)) return;
   __shared__ __attribute__((aligned(16))) float lds[kLdsAll];
   const int b = blockIdx.y, N = P.N;
@@ -1309,8 +1315,7 @@ static bool poll_flags(volatile int32_t **host, int32_t **dev) {
 // The Sinkhorn loop (setup, the initial potentials, the iterations under the batch-coupled stop
 // rule or to *stop_at) -- the first half of nfdpf_ot_resample.
 static int ot_loop(const float *x, const float *w, OtParams &P, const OtWs &ws, int poll, hipStream_t st) {
-  const int B = P.B, N = P.N, max_iter = P.max_iter, splits = P.splits;
-  const int32_t *gate = P.gate;
+  const int B = P.B, max_iter = P.max_iter, splits = P.splits;
   std::unique_lock<std::mutex> lock;
   volatile int32_t *hf = nullptr;
   if (poll) {
@@ -1318,9 +1323,8 @@ static int ot_loop(const float *x, const float *w, OtParams &P, const OtWs &ws, 
     if (!poll_flags(&hf, &P.host)) return launch_status("nfdpf_ot_resample (poll flags)");
     P.seq = (g_poll_seq = (g_poll_seq + 1) & 0x7ffff);
   }
-  ot_setup_kernel<<<B, row_threads(N), 0, st>>>(x, w, N, ws, gate, P.sf, P.eps);
   const dim3 g(splits, B);
-  ot_prep_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
+  ot_setup_kernel<<<g, kOtBlock, 0, st>>>(x, w, P, ws);
   ot_init_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   const bool w8 = ot_iter_waves(B * splits) == 2 * kWaves;
   auto iter = [&](int k) {
@@ -1366,8 +1370,7 @@ static void ot_tail(const float *x, const OtParams &P, const OtWs &ws, int64_t r
   if (P.hist) ot_restore_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   ot_final_kernel<<<g, kOtBlock, 0, st>>>(P, ws);
   ot_col_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x);
-  ot_apply_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out);
-  if (iters_out) ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
+  ot_apply_kernel<<<g, kOtBlock, 0, st>>>(P, ws, x, row_base, x_out, w_out, idx_out, iters_out);
 }
 
 #define NFDPF_OT_CHECK_ARGS(name)                                                          \

@@ -1,11 +1,10 @@
-"""Experiment (round 6; NFDPF_OT_PERSIST selected a one-launch build of the Sinkhorn call with grid
-barriers, measured slower and not kept -- profiles/r06/r06_exp_ot_one_launch.txt): wall time of one Sinkhorn call at the C3 shape (64 rows x 1000, gate on) against
+"""Experiment (round 6): wall time of one Sinkhorn call at the C3 shape (64 rows x 1000, gate on) against
 its kernels (run under rocprofv3 --kernel-trace for the per-kernel timeline)."""
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "normalizing-flows-dpfs_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "normalizing-flows-dpfs_amd"))
 import torch  # noqa: E402
 
 from nfdpf import ops  # noqa: E402
@@ -16,8 +15,7 @@ x = (torch.randn(B, N, 2, generator=g) * 3.0).cuda()
 w = torch.rand(B, N, generator=g) + 0.05
 w = (w / w.sum(1, keepdim=True)).cuda()
 gate = torch.ones(1, dtype=torch.int32, device="cuda")
-for mode, poll in (("0", 1), ("0", 0), ("1", 1)):
-    os.environ["NFDPF_OT_PERSIST"] = mode
+for poll in (1, 0):
     for _ in range(3):
         ops.ot_resample(x, w, 0.1, 0.75, 1e-3, 100, 0, gate=gate, poll=bool(poll))
     torch.cuda.synchronize()
@@ -30,6 +28,6 @@ for mode, poll in (("0", 1), ("0", 0), ("1", 1)):
     b.record()
     torch.cuda.synchronize()
     it = out[3]
-    print(f"B {B} N {N} one-launch {ops.ot_one_launch(B, N)} poll {poll}: {1000 * a.elapsed_time(b) / reps:.1f} us per call (events), "
+    print(f"B {B} N {N} poll {poll}: {1000 * a.elapsed_time(b) / reps:.1f} us per call (events), "
           f"{1e6 * (time.perf_counter() - t0) / reps:.1f} us host, iters {int(it.item()) if it is not None else None}",
           flush=True)
