@@ -151,6 +151,14 @@ NFDPF_API int nfdpf_ot_resample(const float *x, const float *w, int B, int N, fl
                       float threshold, int max_iter, int64_t row_base, float *x_out,
                       float *w_out, int64_t *idx_out, int32_t *iters_out, void *workspace,
                       const int32_t *gate, const int32_t *stop_at, int poll, void *stream);
+/* The same with row strides (in floats) for x and w: row b of the particles starts at
+ * x + b * x_rs (x_rs >= 2N, its N points contiguous), of the weights at w + b * w_rs (w_rs >= N)
+ * -- one time step of a [B, T, N, 2] history read in place (the outputs stay contiguous). */
+NFDPF_API int nfdpf_ot_resample_rs(const float *x, int64_t x_rs, const float *w, int64_t w_rs, int B, int N,
+                                   float eps, float scaling, float threshold, int max_iter, int64_t row_base,
+                                   float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
+                                   void *workspace, const int32_t *gate, const int32_t *stop_at, int poll,
+                                   void *stream);
 
 /* Backward of nfdpf_ot_resample for training: the reference's gradient
  * reaches the particles only through x' = bmm(T, x) with T treated as a constant (its

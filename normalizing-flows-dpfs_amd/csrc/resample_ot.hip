@@ -183,6 +183,7 @@ struct OtParams {
   int32_t *host;           // optional (poll mode): mapped host flags {stop seq, seq * 4096 + k}
   int32_t seq;             // call sequence number for the host flags
   double *hist;            // optional (sharded batches): every state's potentials [max_iter][2][B][N]
+  int64_t x_rs = 0, w_rs = 0;  // row strides (floats) of the input particles / weights
 };
 
 // progress of the Sinkhorn loop to the polling host thread (system-scope stores into
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_setup_kernel(const float *__restr
   __shared__ double shd[32];
   __shared__ float shf[16];
   const int b = blockIdx.y, N = P.N, s0i = blockIdx.x * kOtThreads, s1i = min(s0i + kOtThreads, N);
-  const float *xr = x + (int64_t)b * N * 2;
+  const float *xr = x + (int64_t)b * P.x_rs;
   double s0 = 0, s1 = 0;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     s0 += xr[2 * i];
@@ -755,7 +756,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_setup_kernel(const float *__restr
   const double scale = diam * (double)sqrtf(2.0f);
   auto sx = [&](int i) { return (float)((double)(xr[2 * i] - m0) / scale); };
   auto sy = [&](int i) { return (float)((double)(xr[2 * i + 1] - m1) / scale); };
-  auto lwf = [&](int i) { return logf(w[(int64_t)b * N + i]); };
+  auto lwf = [&](int i) { return logf(w[(int64_t)b * P.w_rs + i]); };
   float mx = -INFINITY, mn = INFINITY, lwmax = -INFINITY;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     const float a = sx(i), c = sy(i), lw = lwf(i);
@@ -1086,7 +1087,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_col_kernel(OtParams P, OtWs ws, c
     rj = -logu + (double)ws.logw[(int64_t)b * N + j] - L * kLn2d;
   }
   const double h[1] = {rj * kLog2ed};
-  const float vals[2] = {v ? x[((int64_t)b * N + j) * 2] : 0.f, v ? x[((int64_t)b * N + j) * 2 + 1] : 0.f};
+  const float vals[2] = {v ? x[(int64_t)b * P.x_rs + 2 * j] : 0.f, v ? x[(int64_t)b * P.x_rs + 2 * j + 1] : 0.f};
   write_col<1, 2, false>(ws.tabA + (int64_t)b * 5 * Np, ws.mA + (int64_t)b * P.splits, Np, v, xj, yj, h, vals, shd);
 }
 
@@ -1127,7 +1128,7 @@ __global__ __launch_bounds__(kOtBlock) void ot_apply_kernel(OtParams P, OtWs ws,
     atomicAdd(&ws.st->fallbacks, 1);
     const float xi = xs[2 * i], yi = xs[2 * i + 1];
     const double fi = fg[i] * fsh;
-    const float *xr = x + (int64_t)b * N * 2;
+    const float *xr = x + (int64_t)b * P.x_rs;
     const float *E = ws.tabA + (int64_t)b * 5 * Np + 2 * Np;  // r_j - M_s
     const double *ms = ws.mA + (int64_t)b * P.splits;
     auto expo = [&](int j) {
@@ -1379,23 +1380,35 @@ static void ot_tail(const float *x, const OtParams &P, const OtWs &ws, int64_t r
   NFDPF_REQUIRE(((uintptr_t)workspace & 255) == 0, name ": workspace not 256-B aligned"); \
   NFDPF_REQUIRE(max_iter <= 4096, name ": max_iter <= 4096")
 
-extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
-                                 float scaling, float threshold, int max_iter, int64_t row_base,
-                                 float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
-                                 void *workspace, const int32_t *gate, const int32_t *stop_at,
-                                 int poll, void *stream) {
+extern "C" int nfdpf_ot_resample_rs(const float *x, int64_t x_rs, const float *w, int64_t w_rs, int B, int N,
+                                    float eps, float scaling, float threshold, int max_iter, int64_t row_base,
+                                    float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
+                                    void *workspace, const int32_t *gate, const int32_t *stop_at, int poll,
+                                    void *stream) {
   NFDPF_REQUIRE(x && w && x_out && w_out && idx_out && workspace,
                 "nfdpf_ot_resample: null pointer");
   NFDPF_OT_CHECK_ARGS("nfdpf_ot_resample");
+  NFDPF_REQUIRE(x_rs >= 2 * (int64_t)N && w_rs >= N, "nfdpf_ot_resample: row strides below the row length");
   if (B == 0) return NFDPF_OK;
   hipStream_t st = as_stream(stream);
   OtWs ws = carve(workspace, B, N);
   OtParams P{B, N, ot_splits(N), max_iter, (double)eps, (double)scaling * (double)scaling,
              (double)threshold, gate, stop_at, nullptr, 0, nullptr};
+  P.x_rs = x_rs;
+  P.w_rs = w_rs;
   const int rc = ot_loop(x, w, P, ws, poll, st);
   if (rc != NFDPF_OK) return rc;
   ot_tail(x, P, ws, row_base, x_out, w_out, idx_out, iters_out, st);
   return launch_status("nfdpf_ot_resample");
+}
+
+extern "C" int nfdpf_ot_resample(const float *x, const float *w, int B, int N, float eps,
+                                 float scaling, float threshold, int max_iter, int64_t row_base,
+                                 float *x_out, float *w_out, int64_t *idx_out, int32_t *iters_out,
+                                 void *workspace, const int32_t *gate, const int32_t *stop_at,
+                                 int poll, void *stream) {
+  return nfdpf_ot_resample_rs(x, 2 * (int64_t)N, w, N, B, N, eps, scaling, threshold, max_iter, row_base, x_out,
+                              w_out, idx_out, iters_out, workspace, gate, stop_at, poll, stream);
 }
 
 extern "C" int64_t nfdpf_ot_history_bytes(int B, int N, int max_iter) {
@@ -1412,6 +1425,8 @@ extern "C" int nfdpf_ot_sinkhorn_local(const float *x, const float *w, int B, in
   OtWs ws = carve(workspace, B, N);
   OtParams P{B, N, ot_splits(N), max_iter, (double)eps, (double)scaling * (double)scaling,
              (double)threshold, gate, nullptr, nullptr, 0, (double *)history};
+  P.x_rs = 2 * (int64_t)N;
+  P.w_rs = N;
   const int rc = ot_loop(x, w, P, ws, poll, st);
   if (rc != NFDPF_OK) return rc;
   ot_iters_kernel<<<1, 1, 0, st>>>(P, ws, iters_out);
@@ -1430,6 +1445,8 @@ extern "C" int nfdpf_ot_sinkhorn_finish(const float *x, int B, int N, float eps,
   OtWs ws = carve(workspace, B, N);
   OtParams P{B, N, ot_splits(N), max_iter, (double)eps, (double)scaling * (double)scaling,
              (double)threshold, gate, stop_at, nullptr, 0, (double *)history};
+  P.x_rs = 2 * (int64_t)N;
+  P.w_rs = N;
   ot_tail(x, P, ws, row_base, x_out, w_out, idx_out, iters_out, st);
   return launch_status("nfdpf_ot_sinkhorn_finish");
 }

@@ -86,6 +86,9 @@ SIGNATURES = {
     "nfdpf_ot_resample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int, c_void_p]),
+    "nfdpf_ot_resample_rs": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_float,
+                                     c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_int, c_void_p]),
     "nfdpf_ot_history_bytes": (c_int64, [c_int, c_int, c_int]),
     "nfdpf_ot_sinkhorn_local": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_int, c_void_p]),

@@ -767,8 +767,10 @@ class FilterEngine:
                     xin, pin = x0, p0
                 elif teacher is not None:
                     xin, pin = xp, pp
-                else:
+                elif shard.world > 1:
                     xin, pin = hx[:, t - 1].contiguous(), hp[:, t - 1].contiguous()
+                else:  # (read in place: nfdpf_ot_resample_rs)
+                    xin, pin = hx[:, t - 1], hp[:, t - 1]
                 # The Sinkhorn call reads the device gate itself (every launch of a call whose gate
                 # is off returns at once, and the host's poll stops enqueueing iterations after the
                 # first), so the host does not wait for the gate before enqueueing the call: the

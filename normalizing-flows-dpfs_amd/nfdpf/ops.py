@@ -271,19 +271,24 @@ def ot_resample(x, w, eps=0.1, scaling=0.75, threshold=1e-3, max_iter=100, row_b
     B, N, D = x.shape
     if D != 2:
         raise L.NfdpfError("ot_resample: the HIP Sinkhorn is built for 2-D particles (state_dim = 2)")
-    x, w = _c(x), _c(w)
-    xo = torch.empty_like(x)
-    wo = torch.empty_like(w)
+    # rows read in place when each row is contiguous (one step of a [B, T, N, 2] history:
+    # nfdpf_ot_resample_rs), else a contiguous copy
+    if not (x.dtype == torch.float32 and x.stride(2) == 1 and x.stride(1) == 2 and x.stride(0) >= 2 * N):
+        x = _c(x)
+    if not (w.dtype == torch.float32 and w.stride(1) == 1 and w.stride(0) >= N):
+        w = _c(w)
+    xo = torch.empty((B, N, 2), device=x.device, dtype=torch.float32)
+    wo = torch.empty((B, N), device=x.device, dtype=torch.float32)
     idx = torch.empty((B, N), device=x.device, dtype=torch.int64)
-    it = torch.zeros(1, device=x.device, dtype=torch.int32)
+    it = torch.empty(1, device=x.device, dtype=torch.int32)  # (the apply launch writes it, gate off included)
     if poll is None:
         poll = not torch.cuda.is_current_stream_capturing()
     nb = int(lib().nfdpf_ot_workspace_bytes(B, N))
     ws = workspace(nb, x.device) if keep is None else keep
-    check(lib().nfdpf_ot_resample(ptr(x), ptr(w), B, N, float(eps), float(scaling), float(threshold),
-                                  int(max_iter), int(row_base), ptr(xo), ptr(wo), ptr(idx), ptr(it),
-                                  _aligned_ptr(ws), ptr(gate), ptr(stop_at), int(bool(poll)),
-                                  stream_ptr(x.device)),
+    check(lib().nfdpf_ot_resample_rs(ptr(x), int(x.stride(0)), ptr(w), int(w.stride(0)), B, N, float(eps),
+                                     float(scaling), float(threshold), int(max_iter), int(row_base), ptr(xo),
+                                     ptr(wo), ptr(idx), ptr(it), _aligned_ptr(ws), ptr(gate), ptr(stop_at),
+                                     int(bool(poll)), stream_ptr(x.device)),
           "nfdpf_ot_resample")
     return xo, wo, idx, it
 

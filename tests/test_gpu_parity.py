@@ -223,6 +223,24 @@ def test_ot_iter_waves_bit_identical(B, N, kind, monkeypatch):
         assert torch.equal(u, v)
 
 
+def test_ot_strided_rows_match_contiguous():
+    """One step of a [B, T, N, 2] history read in place (nfdpf_ot_resample_rs, the engine's OT
+    input) gives the contiguous call's outputs bit for bit, gate on and off."""
+    from nfdpf import ops
+    g = torch.Generator().manual_seed(23)
+    B, T, N = 6, 3, 777
+    hx = (torch.randn(B, T, N, 2, generator=g) * 20).to(DEV)
+    hp = torch.softmax(torch.randn(B, T, N, generator=g) * 3, -1).to(DEV)
+    xs, ps = hx[:, 1], hp[:, 1]
+    assert not xs.is_contiguous() and not ps.is_contiguous()
+    a = ops.ot_resample(xs, ps, row_base=5)
+    b = ops.ot_resample(xs.contiguous(), ps.contiguous(), row_base=5)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+    off = torch.zeros(1, dtype=torch.int32, device=DEV)
+    assert int(ops.ot_resample(xs, ps, gate=off)[3].item()) == 0
+
+
 def test_ot_poll_matches_enqueue_all():
     """poll=1 (host follows the loop and stops enqueueing) gives the bit-identical result of
     poll=0 (all max_iter - 1 launches enqueued, graph-capturable), gate on and off."""
