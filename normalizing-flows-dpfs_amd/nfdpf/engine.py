@@ -755,7 +755,10 @@ class FilterEngine:
                 keep.append(nz)
                 d.host_noise = nz.data_ptr()
             elif c.resampler == "ot" and not spec:
-                if tiled:
+                if c.force_resample:  # the gate word is constant: set once, no gate launch per step
+                    if t == 0:
+                        gate_buf.fill_(1)
+                elif tiled:
                     ops.ess_gate_tiled(ess_all, N, t, c.force_resample, out=gate_buf)
                 else:
                     ops.ess_gate(ess_all, N, c.force_resample, out=gate_buf)
